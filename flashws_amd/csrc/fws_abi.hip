@@ -1,0 +1,135 @@
+// fws_abi.hip -- the extern "C" entry points of libfws_gpu.so (include/fws_gpu.h).
+// Host code: argument checks, workspace ownership, kernel launch sequencing.
+#include <stdlib.h>
+#include <string.h>
+
+#include "fws_internal.h"
+
+namespace {
+
+template <typename T>
+int dev_alloc(T **p, uint64_t count) {
+    *p = nullptr;
+    if (count == 0) count = 1;
+    return fws_hip_status(hipMalloc((void **)p, count * sizeof(T)));
+}
+
+template <typename T>
+void dev_free(T *&p) {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+}
+
+void free_plan(fws_plan_ws &w) {
+    dev_free(w.block_sums);
+    dev_free(w.cbase);
+    dev_free(w.unit_first);
+    dev_free(w.total);
+}
+
+}  // namespace
+
+int fws_ctx_ensure_plan(fws_gpu_ctx *ctx, uint64_t frames, uint64_t units) {
+    if (frames <= ctx->cap_frames && units <= ctx->cap_units && ctx->plan.cbase) return 0;
+    if (frames < ctx->cap_frames) frames = ctx->cap_frames;
+    if (units < ctx->cap_units) units = ctx->cap_units;
+    free_plan(ctx->plan);
+    int r;
+    if ((r = dev_alloc(&ctx->plan.block_sums, frames / 1024 + 2))) return r;
+    if ((r = dev_alloc(&ctx->plan.cbase, frames + 2))) return r;
+    if ((r = dev_alloc(&ctx->plan.unit_first, units + 2))) return r;
+    if ((r = dev_alloc(&ctx->plan.total, 2))) return r;
+    ctx->cap_frames = frames;
+    ctx->cap_units = units;
+    ctx->plan.unit_cap = units + 1;
+    return 0;
+}
+
+extern "C" {
+
+int fws_gpu_abi_version(void) { return FWS_GPU_ABI_VERSION; }
+
+int fws_gpu_device_count(int *count) {
+    if (!count) return FWS_ERR_INVALID;
+    *count = 0;
+    hipError_t e = hipGetDeviceCount(count);
+    if (e == hipErrorNoDevice) { *count = 0; return 0; }
+    return fws_hip_status(e);
+}
+
+int fws_gpu_ctx_create(int device, fws_gpu_ctx **out) {
+    if (!out) return FWS_ERR_INVALID;
+    *out = nullptr;
+    int n = 0;
+    int r = fws_gpu_device_count(&n);
+    if (r) return r;
+    if (device < 0 || device >= n) return FWS_ERR_NO_DEVICE;
+    hipDeviceProp_t prop;
+    if ((r = fws_hip_status(hipGetDeviceProperties(&prop, device)))) return r;
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return FWS_ERR_NO_DEVICE;
+    if ((r = fws_hip_status(hipSetDevice(device)))) return r;
+    fws_gpu_ctx *c = new fws_gpu_ctx();
+    c->device = device;
+    *out = c;
+    return 0;
+}
+
+void fws_gpu_ctx_destroy(fws_gpu_ctx *ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    free_plan(ctx->plan);
+    fws_decode_ws &d = ctx->dec;
+    dev_free(d.tile_count);
+    dev_free(d.tile_base);
+    dev_free(d.surv_pos);
+    dev_free(d.surv_next);
+    dev_free(d.jump);
+    dev_free(d.mark);
+    dev_free(d.mark_base);
+    dev_free(d.counters);
+    dev_free(d.descs);
+    delete ctx;
+}
+
+int fws_gpu_ctx_reserve(fws_gpu_ctx *ctx, uint64_t max_frames, uint64_t max_stream_bytes) {
+    if (!ctx) return FWS_ERR_INVALID;
+    int r = fws_hip_status(hipSetDevice(ctx->device));
+    if (r) return r;
+    // chunks <= bytes / 16 + 2 per frame; units = chunks / 256
+    const uint64_t units = (max_stream_bytes / 16 + 2 * max_frames) / 256 + 2;
+    if ((r = fws_ctx_ensure_plan(ctx, max_frames, units))) return r;
+    if (max_stream_bytes > ctx->cap_stream) ctx->cap_stream = max_stream_bytes;
+    return 0;
+}
+
+int fws_gpu_mask(void *dev_ptr, uint64_t n, uint32_t key, void *stream) {
+    if (n && !dev_ptr) return FWS_ERR_INVALID;
+    return fws_launch_mask_single(dev_ptr, n, key, 0u, (hipStream_t)stream);
+}
+
+int fws_gpu_unmask_plan(fws_gpu_ctx *ctx, const void *dev_base, const fws_frame_desc *dev_descs,
+                        uint32_t n, void *stream) {
+    if (!ctx || (n && (!dev_base || !dev_descs))) return FWS_ERR_INVALID;
+    if (n == 0) return 0;
+    if (ctx->cap_stream == 0 || n > ctx->cap_frames) return FWS_ERR_CAPACITY;
+    return fws_launch_plan((const uint8_t *)dev_base, dev_descs, n, ctx->plan, (hipStream_t)stream);
+}
+
+int fws_gpu_unmask_run(fws_gpu_ctx *ctx, void *dev_base, const fws_frame_desc *dev_descs,
+                       uint32_t n, void *stream) {
+    if (!ctx || (n && (!dev_base || !dev_descs))) return FWS_ERR_INVALID;
+    if (n == 0) return 0;
+    if (ctx->cap_stream == 0 || n > ctx->cap_frames) return FWS_ERR_CAPACITY;
+    const uint64_t max_chunks = ctx->cap_stream / 16 + 2ull * n;
+    return fws_launch_unmask((uint8_t *)dev_base, dev_descs, n, ctx->plan, max_chunks,
+                             (hipStream_t)stream);
+}
+
+int fws_gpu_unmask_batch(fws_gpu_ctx *ctx, void *dev_base, const fws_frame_desc *dev_descs,
+                         uint32_t n, void *stream) {
+    int r = fws_gpu_unmask_plan(ctx, dev_base, dev_descs, n, stream);
+    if (r) return r;
+    return fws_gpu_unmask_run(ctx, dev_base, dev_descs, n, stream);
+}
+
+}  // extern "C"

@@ -1,0 +1,119 @@
+// fws_device.h -- device-side helpers shared by the flashws_amd HIP kernels
+// (gfx950 only). Integer/byte work: no MFMA anywhere on this path.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "fws_gpu.h"
+
+namespace fwsk {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kWave = 64;           // CDNA wavefront width
+constexpr int kBlock = 256;         // 4 waves per workgroup
+constexpr int kUnmaskU = 4;         // 16-B chunks per lane per work unit
+constexpr uint64_t kUnitChunks = uint64_t(kWave) * kUnmaskU;   // 256 chunks = 4 KiB per wave unit
+
+// base/constexpr_math.h:67-82 RotateR, 32-bit.
+__device__ __forceinline__ uint32_t rotr32(uint32_t v, uint32_t b) {
+    b &= 31u;
+    return (v >> b) | (v << ((32u - b) & 31u));
+}
+
+// Rotated key for any 4-aligned address inside the region starting at
+// `region_addr` with key phase `phase`: byte at address x uses key byte
+// (x - region_addr + phase) & 3 (ws_mask.h:20,27 + w_socket.h:758).
+__device__ __forceinline__ uint32_t aligned_key(uint32_t key, uint32_t phase, uintptr_t region_addr) {
+    return rotr32(key, 8u * ((phase - (uint32_t)region_addr) & 3u));
+}
+
+// Number of 16-B aligned chunks touched by [addr, addr + len).
+__device__ __forceinline__ uint64_t chunks_of(uintptr_t addr, uint64_t len) {
+    if (len == 0) return 0;
+    return ((addr + len + 15u) >> 4) - (addr >> 4);
+}
+
+// XOR only the bytes of chunk [ca, ca+16) that lie inside [lo, hi); rk is the
+// key rotated for 4-aligned addresses. Never touches bytes outside [lo, hi).
+__device__ __forceinline__ void xor_partial_chunk(uintptr_t ca, uintptr_t lo, uintptr_t hi, uint32_t rk) {
+    uintptr_t b = ca > lo ? ca : lo;
+    uintptr_t e = (ca + 16u) < hi ? (ca + 16u) : hi;
+    while (b < e) {
+        if ((b & 3u) == 0 && b + 4u <= e) {
+            uint32_t *w = reinterpret_cast<uint32_t *>(b);
+            *w = *w ^ rk;
+            b += 4u;
+        } else {
+            uint8_t *p = reinterpret_cast<uint8_t *>(b);
+            *p = (uint8_t)(*p ^ (uint8_t)(rk >> (8u * (b & 3u))));
+            b += 1u;
+        }
+    }
+}
+
+// Largest f in [lo, hi] with cbase[f] <= g (cbase non-decreasing).
+__device__ __forceinline__ uint32_t find_frame(const uint64_t *__restrict__ cbase, uint32_t lo,
+                                               uint32_t hi, uint64_t g) {
+    while (lo < hi) {
+        uint32_t mid = lo + ((hi - lo + 1u) >> 1);
+        if (cbase[mid] <= g) lo = mid; else hi = mid - 1u;
+    }
+    return lo;
+}
+
+// RFC 6455 §5.2 header parse with the reference's exact semantics
+// (w_socket.h:435-524), for `avail` readable bytes at p (avail may exceed 14).
+// Returns header length (>0), 0 = incomplete, or a negative FWS_ERR_* code.
+struct Hdr {
+    uint64_t plen;
+    uint32_t key;
+    uint32_t opcode;
+    uint32_t fin;
+};
+
+__device__ __forceinline__ bool valid_opcode(uint32_t op) {   // w_socket.h:526-528
+    return (op <= 2u) | ((op >= 8u) & (op <= 10u));
+}
+
+template <typename ByteAt>
+__device__ __forceinline__ int parse_hdr(ByteAt at, uint64_t avail, bool is_server, Hdr &h) {
+    if (avail < 2) return 0;                                   // :443-445
+    uint32_t b0 = at(0);
+    h.opcode = b0 & 15u;                                       // :448
+    if (!valid_opcode(h.opcode)) return FWS_ERR_OPCODE;        // :451-454
+    h.fin = b0 >> 7;                                           // :465
+    if (b0 & 112u) return FWS_ERR_RSV;                         // :466-470
+    uint32_t b1 = at(1);
+    uint32_t masked = b1 >> 7;                                 // :472
+    uint64_t plen = b1 & 127u;                                 // :473
+    int n = 2;
+    if (plen == 126u) {                                        // :476-482
+        if (avail < 4) return 0;
+        plen = (uint64_t(at(2)) << 8) | at(3);
+        n = 4;
+    } else if (plen == 127u) {                                 // :483-492
+        if (avail < 10) return 0;
+        uint64_t v = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v = (v << 8) | at(2 + i);
+        plen = v;
+        n = 10;
+    }
+    if (plen > (1ull << 32)) return FWS_ERR_TOO_LARGE;         // :493-498
+    h.plen = plen;
+    if (is_server) {                                           // :502-516
+        if (!masked) return FWS_ERR_NOT_MASKED;
+        if (avail < (uint64_t)n + 4u) return 0;
+        h.key = uint32_t(at(n)) | (uint32_t(at(n + 1)) << 8) | (uint32_t(at(n + 2)) << 16) |
+                (uint32_t(at(n + 3)) << 24);
+        n += 4;
+    } else {
+        if (masked) return FWS_ERR_MASKED;                     // :518-521
+        h.key = 0;
+    }
+    return n;
+}
+
+}  // namespace fwsk

@@ -1,0 +1,190 @@
+"""Python face of the MI355X decode path, mirroring the reference's interface
+for this path (names and argument meaning of crypto/ws_mask.h and
+net/w_socket.h, error codes of ParseFrameHdr). Device memory, streams and
+events come from torch; all compute runs in libfws_gpu.so's HIP kernels.
+"""
+import ctypes as C
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import FRAME_DESC, FRAME_INFO, DECODE_RESULT, RX_EVENT, GenParams, check, lib
+
+
+def _stream_handle(stream=None):
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return C.c_void_p(s.cuda_stream)
+
+
+def _ptr(t):
+    return C.c_void_p(t.data_ptr())
+
+
+def device_count():
+    n = C.c_int(0)
+    check("fws_gpu_device_count", lib().fws_gpu_device_count(C.byref(n)))
+    return n.value
+
+
+class Ctx:
+    """fws_gpu_ctx: device workspace for one device / one host thread."""
+
+    def __init__(self, device=0, max_frames=0, max_stream_bytes=0):
+        self.device = device
+        h = C.c_void_p()
+        check("fws_gpu_ctx_create", lib().fws_gpu_ctx_create(device, C.byref(h)))
+        self.h = h
+        if max_frames or max_stream_bytes:
+            self.reserve(max_frames, max_stream_bytes)
+
+    def reserve(self, max_frames, max_stream_bytes):
+        check("fws_gpu_ctx_reserve", lib().fws_gpu_ctx_reserve(self.h, max_frames, max_stream_bytes))
+
+    def close(self):
+        if self.h:
+            lib().fws_gpu_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def ws_mask_bytes_fast(buf, key, offset=0, n=None, stream=None):
+    """Device twin of fws::WSMaskBytesFast(src, size, mask) (ws_mask.h:175):
+    XOR buf[offset:offset+n] (a uint8 CUDA tensor) with the 4-byte key in place."""
+    n = buf.numel() - offset if n is None else n
+    check("fws_gpu_mask", lib().fws_gpu_mask(C.c_void_p(buf.data_ptr() + offset), n, key & 0xFFFFFFFF,
+                                             _stream_handle(stream)))
+
+
+def descs_to_device(descs, device="cuda"):
+    """numpy FRAME_DESC array -> uint8 device tensor holding the structs."""
+    a = np.ascontiguousarray(descs, dtype=FRAME_DESC)
+    return torch.from_numpy(a.view(np.uint8)).to(device)
+
+
+def unmask_batch(ctx, base, dev_descs, n, stream=None):
+    """fws_gpu_unmask_batch: unmask every payload region in place."""
+    check("fws_gpu_unmask_batch", lib().fws_gpu_unmask_batch(ctx.h, _ptr(base), _ptr(dev_descs), n,
+                                                             _stream_handle(stream)))
+
+
+def unmask_plan(ctx, base, dev_descs, n, stream=None):
+    check("fws_gpu_unmask_plan", lib().fws_gpu_unmask_plan(ctx.h, _ptr(base), _ptr(dev_descs), n,
+                                                           _stream_handle(stream)))
+
+
+def unmask_run(ctx, base, dev_descs, n, stream=None):
+    check("fws_gpu_unmask_run", lib().fws_gpu_unmask_run(ctx.h, _ptr(base), _ptr(dev_descs), n,
+                                                         _stream_handle(stream)))
+
+
+def unmask_gather(ctx, dst, src, dev_descs, n, stream=None):
+    check("fws_gpu_unmask_gather", lib().fws_gpu_unmask_gather(ctx.h, _ptr(dst), _ptr(src), _ptr(dev_descs),
+                                                               n, _stream_handle(stream)))
+
+
+def decode_stream(ctx, wire, cap, frames=None, result=None, utf8_ok=None, stream=None, n=None):
+    """fws_gpu_decode_stream on a device uint8 tensor. Returns (status, frames
+    tensor, result tensor, utf8 tensor) -- device tensors, nothing synchronised."""
+    dev = wire.device
+    if frames is None:
+        frames = torch.empty(max(cap, 1) * FRAME_INFO.itemsize, dtype=torch.uint8, device=dev)
+    if result is None:
+        result = torch.empty(DECODE_RESULT.itemsize, dtype=torch.uint8, device=dev)
+    n = wire.numel() if n is None else n
+    u = C.c_void_p(utf8_ok.data_ptr()) if utf8_ok is not None else None
+    rc = lib().fws_gpu_decode_stream(ctx.h, _ptr(wire), n, _ptr(frames), cap, _ptr(result), u,
+                                     _stream_handle(stream))
+    return rc, frames, result, utf8_ok
+
+
+def read_result(result):
+    return np.frombuffer(result.cpu().numpy().tobytes(), dtype=DECODE_RESULT)[0]
+
+
+def read_frames(frames, count):
+    raw = frames[:count * FRAME_INFO.itemsize].cpu().numpy()
+    return np.frombuffer(raw.tobytes(), dtype=FRAME_INFO).copy()
+
+
+def validate_utf8(ctx, base, dev_descs, n, ok, stream=None):
+    check("fws_gpu_validate_utf8", lib().fws_gpu_validate_utf8(ctx.h, _ptr(base), _ptr(dev_descs), n,
+                                                               _ptr(ok), _stream_handle(stream)))
+
+
+# ------------------------------------------------------------ workloads
+GEN_FIXED, GEN_MIXED, GEN_FRAGMENTED, GEN_UTF8 = 0, 1, 2, 3
+
+
+def gen_batch(kind, seed=42, opcode=2, n_frames=0, payload_min=0, payload_max=0, target_bytes=0,
+              invalid_permille=0):
+    """Synthetic client-masked frames (fws_gen_batch). Returns (wire uint8
+    numpy array, FRAME_DESC array of payload regions, utf8_ok uint8 array)."""
+    p = GenParams(seed=seed, kind=kind, opcode=opcode, n_frames=n_frames, payload_min=payload_min,
+                  payload_max=payload_max, target_bytes=target_bytes,
+                  invalid_permille=invalid_permille)
+    wl, nf = C.c_uint64(0), C.c_uint64(0)
+    check("fws_gen_batch", lib().fws_gen_batch(C.byref(p), None, 0, C.byref(wl), None, 0, C.byref(nf),
+                                               None))
+    wire = np.empty(wl.value, dtype=np.uint8)
+    descs = np.zeros(nf.value, dtype=FRAME_DESC)
+    ok = np.zeros(nf.value, dtype=np.uint8)
+    check("fws_gen_batch", lib().fws_gen_batch(C.byref(p), wire.ctypes.data, wl.value, C.byref(wl),
+                                               descs.ctypes.data, nf.value, C.byref(nf), ok.ctypes.data))
+    return wire, descs, ok
+
+
+# BASELINE.json configs as generator calls
+def config_c2(seed=42, n_frames=65536, payload=4096):
+    return gen_batch(GEN_FIXED, seed=seed, opcode=2, n_frames=n_frames, payload_min=payload)
+
+
+def config_c3(seed=42, target=256 << 20):
+    return gen_batch(GEN_MIXED, seed=seed, opcode=2, payload_min=64, payload_max=65536,
+                     target_bytes=target)
+
+
+def config_c4(seed=42, target=256 << 20):
+    return gen_batch(GEN_FRAGMENTED, seed=seed, opcode=2, payload_min=4096, payload_max=1 << 20,
+                     target_bytes=target)
+
+
+def config_c5(seed=42, n_frames=262144, payload=16384, invalid_permille=10):
+    return gen_batch(GEN_UTF8, seed=seed, n_frames=n_frames, payload_min=payload,
+                     invalid_permille=invalid_permille)
+
+
+# ------------------------------------------------------------ RX session
+class RxSession:
+    """fws_rx_session: OnRecvData (w_socket.h:543-769) over the GPU for host reads."""
+
+    def __init__(self, ctx, is_server=True):
+        h = C.c_void_p()
+        check("fws_rx_session_create", lib().fws_rx_session_create(ctx.h, 1 if is_server else 0, C.byref(h)))
+        self.h = h
+
+    def feed(self, data, extra_cap=0, ev_cap=1 << 16, ctl_cap=1 << 20):
+        buf = np.frombuffer(bytes(data), dtype=np.uint8).copy()
+        ev = np.zeros(ev_cap, dtype=RX_EVENT)
+        ctl = np.zeros(ctl_cap, dtype=np.uint8)
+        n_ev, ctl_used = C.c_uint64(0), C.c_uint64(0)
+        ret = lib().fws_rx_session_feed(self.h, buf.ctypes.data if len(buf) else None, len(buf),
+                                        len(buf) + extra_cap, ev.ctypes.data, ev_cap, C.byref(n_ev),
+                                        ctl.ctypes.data, ctl_cap, C.byref(ctl_used))
+        return ret, buf, ev[:n_ev.value].copy(), ctl[:ctl_used.value].copy()
+
+    def close(self):
+        if self.h:
+            lib().fws_rx_session_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,198 @@
+/*
+ * fws_gpu.h -- C ABI of flashws_amd: the MI355X (gfx950) receive-path frame
+ * decode of flashws (RFC 6455 §5.2 header parse + 4-byte-key XOR unmask).
+ *
+ * Pure C. No HIP or torch types in the signatures: device memory is `void *`,
+ * streams are `void *` (a hipStream_t, NULL = the null stream). Every entry
+ * point returns an int status (0 = ok, negative = error, table below); none
+ * throws, none frees caller memory, none synchronises the stream unless its
+ * comment says so.
+ *
+ * Reference interfaces replaced (paths relative to flashws include/flashws/):
+ *   seam 1  fws::WSMaskBytesFast(uint8_t*, size_t, uint32_t)  crypto/ws_mask.h:175-197
+ *           -> fws_gpu_mask / fws_gpu_unmask_batch
+ *   seam 2  WSocket<D, is_server, tls>::OnRecvData(IOBuffer&) net/w_socket.h:543-769
+ *           (its ParseFrameHdr net/w_socket.h:435-524 and RX state :223-245)
+ *           -> fws_gpu_decode_stream (device-resident batch)
+ *           -> fws_rx_session_* (host buffers, same on_read() event contract)
+ * The reference-side binding a maintainer adds is in INTEGRATION.md.
+ */
+#ifndef FWS_GPU_H
+#define FWS_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FWS_GPU_ABI_VERSION 1
+
+/* ---- status codes ------------------------------------------------------
+ * Protocol errors keep the reference's ParseFrameHdr return values
+ * (w_socket.h:451-521) so callers can forward them unchanged to
+ * WSServerSocket's Close(WS_ABNORMAL_CLOSE, ...) (ws_server_socket.h:176-181). */
+enum {
+    FWS_OK = 0,
+    FWS_ERR_RSV = -1,           /* RSV1-3 set                 w_socket.h:466-470 */
+    FWS_ERR_TOO_LARGE = -2,     /* payload_len > 2^32         w_socket.h:493-498 */
+    FWS_ERR_NOT_MASKED = -3,    /* server RX, MASK bit clear  w_socket.h:513-515 */
+    FWS_ERR_MASKED = -4,        /* client RX, MASK bit set    w_socket.h:518-521 */
+    FWS_ERR_OPCODE = -9,        /* opcode not 0-2/8-10        w_socket.h:451-454 */
+    FWS_ERR_CAPACITY = -20,     /* an output array is too small (count still reported) */
+    FWS_ERR_INVALID = -21,      /* bad argument / not initialised */
+    FWS_ERR_NO_DEVICE = -22,    /* no gfx950 device visible */
+    FWS_ERR_HIP_BASE = -1000    /* -1000 - hipError_t */
+};
+
+/* ---- descriptor-mode unmask --------------------------------------------
+ * One payload region to unmask in place. Byte i of the region is XORed with
+ * key byte ((phase + i) & 3), key = the 4 wire key bytes loaded as a native
+ * little-endian uint32 (w_socket.h:504; ws_mask.h:17-28). Continuing a frame
+ * at payload offset k is phase = k & 3, the same as the reference's
+ * RotateR(key, 8 * (k & 3)) (w_socket.h:756-759). Regions of one batch must
+ * not overlap; they may be in any order and any alignment. */
+typedef struct fws_frame_desc {
+    uint64_t payload_off;   /* byte offset from the batch's device base */
+    uint64_t payload_len;   /* bytes to unmask (0 allowed) */
+    uint32_t key;
+    uint32_t phase;         /* 0..3 */
+} fws_frame_desc;           /* 24 bytes */
+
+/* ---- stream decode output ------------------------------------------------
+ * One parsed frame of a server-side (client-masked) byte stream. */
+typedef struct fws_frame_info {
+    uint64_t hdr_off;       /* offset of the frame's first header byte */
+    uint64_t payload_len;   /* length field from the header (w_socket.h:473-492) */
+    uint32_t key;           /* mask key, native LE u32 of the wire bytes */
+    uint8_t opcode;         /* raw opcode of this frame (0 = continuation) */
+    uint8_t fin;
+    uint8_t hdr_len;        /* 6, 8 or 14 */
+    uint8_t flags;          /* FWS_FRAME_TRUNCATED: payload runs past the stream end */
+} fws_frame_info;           /* 24 bytes */
+
+#define FWS_FRAME_TRUNCATED 1u
+
+/* Result of one fws_gpu_decode_stream call (written to device memory). */
+typedef struct fws_decode_result {
+    int32_t status;         /* FWS_OK or the first protocol error on the stream */
+    uint32_t n_frames;      /* frames parsed (complete headers), also past capacity */
+    uint64_t consumed;      /* bytes consumed: end of last frame part (== len unless a
+                               partial header remains, or an error stopped the decode) */
+    uint64_t err_off;       /* offset of the failing header when status < 0 */
+    uint64_t carry_unread;  /* payload bytes of the last frame still to come */
+    uint32_t carry_hdr_len; /* bytes of an incomplete trailing header (<= 13) */
+    uint32_t n_survivors;   /* diagnostics: speculative header candidates kept */
+} fws_decode_result;        /* 40 bytes */
+
+typedef struct fws_gpu_ctx fws_gpu_ctx;
+
+int fws_gpu_abi_version(void);
+int fws_gpu_device_count(int *count);
+
+/* A context owns the device workspace of one device and is used from one
+ * host thread at a time (one context per stream/thread; the reference is one
+ * FLoop per thread, floop.h:331-345). */
+int fws_gpu_ctx_create(int device, fws_gpu_ctx **out);
+void fws_gpu_ctx_destroy(fws_gpu_ctx *ctx);
+/* Pre-size the workspace so later calls never allocate (hipGraph-capturable). */
+int fws_gpu_ctx_reserve(fws_gpu_ctx *ctx, uint64_t max_frames, uint64_t max_stream_bytes);
+
+/* seam 1 -- device twin of WSMaskBytesFast (ws_mask.h:175): XOR n bytes at
+ * dev_ptr with key, in place, on `stream`. Any alignment, any n. */
+int fws_gpu_mask(void *dev_ptr, uint64_t n, uint32_t key, void *stream);
+
+/* Descriptor-mode batch unmask: every region of dev_descs[0..n) (device
+ * memory) inside dev_base is unmasked in place. Load-balanced over 16-byte
+ * chunks, so one launch covers any mix of frame sizes. */
+int fws_gpu_unmask_batch(fws_gpu_ctx *ctx, void *dev_base, const fws_frame_desc *dev_descs,
+                         uint32_t n, void *stream);
+
+/* The two halves of fws_gpu_unmask_batch, for callers that reuse one plan
+ * (same descriptors) across buffers: _plan builds the chunk plan of the
+ * descriptors in ctx, _run unmasks with the last plan built in ctx. */
+int fws_gpu_unmask_plan(fws_gpu_ctx *ctx, const void *dev_base, const fws_frame_desc *dev_descs,
+                        uint32_t n, void *stream);
+int fws_gpu_unmask_run(fws_gpu_ctx *ctx, void *dev_base, const fws_frame_desc *dev_descs,
+                       uint32_t n, void *stream);
+
+/* Same, out of place: dst[dst_off_i ..] = src[payload_off_i ..] ^ key, with
+ * dst_off = exclusive prefix sum of payload_len (message reassembly, C4). */
+int fws_gpu_unmask_gather(fws_gpu_ctx *ctx, void *dev_dst, const void *dev_src,
+                          const fws_frame_desc *dev_descs, uint32_t n, void *stream);
+
+/* seam 2 (device-resident) -- fused header parse + unmask of a server-side
+ * wire stream dev_wire[0..len) that starts at a frame header. Payloads are
+ * unmasked in place; frames are listed in dev_frames (capacity cap) and the
+ * outcome in *dev_result (device memory). Semantics are OnRecvData's on one
+ * buffer: decoding stops at the first protocol error (frames before it are
+ * still unmasked), a truncated last payload is unmasked as far as present, an
+ * incomplete trailing header is left for the next call. If dev_utf8_ok is
+ * non-NULL, byte i of it is set to 1 iff frame i is TEXT (opcode 1), FIN,
+ * complete, and its unmasked payload is well-formed UTF-8 (else 0). */
+int fws_gpu_decode_stream(fws_gpu_ctx *ctx, void *dev_wire, uint64_t len,
+                          fws_frame_info *dev_frames, uint32_t cap,
+                          fws_decode_result *dev_result, uint8_t *dev_utf8_ok, void *stream);
+
+/* Per-frame UTF-8 validation of already-unmasked payloads (Unicode Table
+ * 3-7): ok[i] = 1 iff region i is well-formed UTF-8. */
+int fws_gpu_validate_utf8(fws_gpu_ctx *ctx, const void *dev_base, const fws_frame_desc *dev_descs,
+                          uint32_t n, uint8_t *dev_ok, void *stream);
+
+/* ---- host-buffer RX session: OnRecvData over the GPU ----------------------
+ * Mirrors WSocket::OnRecvData (w_socket.h:543-769) for one server
+ * connection: reads are host buffers, decode runs on the device, and the
+ * on_read() contract (opcode, part, is_frame_end, is_msg_end, is_control) is
+ * reported as an event array whose order and values match the reference.
+ * Control frames: PING -> a PONG event (the caller sends the reply), CLOSE ->
+ * a CLOSE event with status code; their payload bytes are copied to ctl_out. */
+typedef struct fws_rx_event {
+    uint32_t kind;          /* 0 ON_READ, 1 PONG_TO_SEND, 2 CLOSE_RECEIVED */
+    uint32_t opcode;        /* reported opcode (continuations report the first frame's, w_socket.h:626) */
+    uint8_t is_ctl;
+    uint8_t frame_end;
+    uint8_t msg_end;
+    uint8_t fin;
+    uint32_t code;          /* CLOSE status code (1005 if absent) */
+    uint64_t size;          /* bytes in this part */
+    uint64_t data_off;      /* ON_READ data part: offset of the part in the read buffer */
+    uint64_t ctl_off;       /* control payload copy offset in ctl_out */
+    uint64_t capacity;      /* IOBuffer capacity of the view, relative to the read start */
+} fws_rx_event;             /* 48 bytes */
+
+typedef struct fws_rx_session fws_rx_session;
+
+int fws_rx_session_create(fws_gpu_ctx *ctx, int is_server, fws_rx_session **out);
+void fws_rx_session_destroy(fws_rx_session *s);
+/* Decode one read in place (buf is host memory, unmasked on return). Returns
+ * 0 or the reference's negative ParseFrameHdr code. buf_capacity: the view's
+ * capacity measured from buf (the last part's IOBuffer capacity). */
+int fws_rx_session_feed(fws_rx_session *s, uint8_t *buf, uint64_t size, uint64_t buf_capacity,
+                        fws_rx_event *events, uint64_t ev_cap, uint64_t *n_events,
+                        uint8_t *ctl_out, uint64_t ctl_cap, uint64_t *ctl_used);
+
+/* ---- synthetic workloads (BASELINE configs, not test oracles) ------------ */
+typedef struct fws_gen_params {
+    uint64_t seed;
+    uint32_t kind;          /* 0 fixed-size frames, 1 log-uniform sizes, 2 fragmented message, 3 UTF-8 text */
+    uint32_t opcode;        /* data opcode for kinds 0/1 (1 TEXT, 2 BIN) */
+    uint64_t n_frames;      /* kinds 0/3: frame count */
+    uint64_t payload_min;   /* kind 0/3: the payload size; kinds 1/2: minimum */
+    uint64_t payload_max;   /* kinds 1/2: maximum (log-uniform in [min, max]) */
+    uint64_t target_bytes;  /* kinds 1/2: stop once the payload total reaches this */
+    uint32_t invalid_permille; /* kind 3: frames carrying one invalid UTF-8 sequence */
+    uint32_t pad_;
+} fws_gen_params;
+
+/* Two-call protocol: with wire == NULL only *wire_len and *n_frames are
+ * computed. Otherwise fills wire (cap bytes, host memory) with client-masked
+ * frames and descs (payload regions, phase 0) and, for kind 3, utf8_ok
+ * (expected per-frame validity). */
+int fws_gen_batch(const fws_gen_params *p, uint8_t *wire, uint64_t cap, uint64_t *wire_len,
+                  fws_frame_desc *descs, uint64_t descs_cap, uint64_t *n_frames, uint8_t *utf8_ok);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FWS_GPU_H */

@@ -1,0 +1,131 @@
+"""GPU parity: device XOR unmask (fws_gpu_mask / fws_gpu_unmask_batch) vs the
+oracle's restatement of WSMaskBytesFast (crypto/ws_mask.h:175-197), bit-exact.
+Sweeps the alignment/length/phase space the reference's own test_mask.cpp
+(tests/test-utils/test_mask.cpp:148-177) only samples at offset 1."""
+import numpy as np
+import pytest
+import torch
+
+import orc
+from flashws_amd import gpu
+
+pytestmark = pytest.mark.gpu
+
+ALIGN = 256
+
+
+def aligned_host(n):
+    raw = np.zeros(n + ALIGN, dtype=np.uint8)
+    off = (-raw.ctypes.data) % ALIGN
+    return raw[off:off + n]
+
+
+def oracle_unmask_regions(buf, descs):
+    out = buf.copy()
+    for d in descs:
+        o, n, k, ph = int(d["payload_off"]), int(d["payload_len"]), int(d["key"]), int(d["phase"])
+        key = orc.orc().orc_rotr32(k, 8 * ph)   # phase == RotateR(key, 8*phase) (w_socket.h:758)
+        orc.orc_mask("ws_mask_fast", out, key, o, n)
+    return out
+
+
+def run_batch(ctx, host, descs, cuda):
+    dev = torch.from_numpy(host.copy()).to(cuda)
+    dd = gpu.descs_to_device(descs, cuda)
+    gpu.unmask_batch(ctx, dev, dd, len(descs))
+    torch.cuda.synchronize()
+    return dev.cpu().numpy()
+
+
+def test_mask_single_sweep(cuda):
+    """fws_gpu_mask over offsets 0..63 x lens 0..300 (+ big) x 2 keys."""
+    rng = np.random.default_rng(1)
+    base = rng.integers(0, 256, 70000, dtype=np.uint8)
+    dev = torch.from_numpy(base).to(cuda)
+    ptr_mod = dev.data_ptr() % 256
+    assert ptr_mod == 0
+    lens = list(range(0, 301, 7)) + [511, 512, 513, 2047, 2048, 2049, 4093, 4096, 16384, 65535]
+    for key in (0xA1B2C3D4, 0x00000001):
+        for off in range(0, 64, 3):
+            for n in lens:
+                d = dev.clone()
+                gpu.ws_mask_bytes_fast(d, key, off, n)
+                got = d.cpu().numpy()
+                exp = base.copy()
+                orc.orc_mask("ws_mask_fast", exp, key, off, n)
+                assert np.array_equal(got, exp), (hex(key), off, n)
+
+
+def test_unmask_batch_alignment_sweep(ctx, cuda):
+    """One batch: every (offset mod 64, len 0..600, phase) region, packed with gaps."""
+    rng = np.random.default_rng(2)
+    regions = []
+    pos = 0
+    for ln in range(0, 601):
+        for sh in (0, 1, 5, 13, 31, 47, 63):
+            pos = (pos + 63) // 64 * 64 + sh
+            regions.append((pos, ln, int(rng.integers(0, 2**32)), int(rng.integers(0, 4))))
+            pos += ln + int(rng.integers(0, 9))
+    host = aligned_host(pos + 64)
+    host[:] = rng.integers(0, 256, len(host), dtype=np.uint8)
+    descs = np.array(regions, dtype=gpu.FRAME_DESC)
+    order = rng.permutation(len(descs))          # any order is allowed
+    descs = descs[order]
+    got = run_batch(ctx, host, descs, cuda)
+    exp = oracle_unmask_regions(host, descs)
+    assert np.array_equal(got, exp)
+
+
+def test_unmask_batch_adjacent_regions(ctx, cuda):
+    """Regions sharing 16-B chunks (1..15-byte gaps and zero gaps)."""
+    rng = np.random.default_rng(3)
+    regions, pos = [], 3
+    for i in range(5000):
+        ln = int(rng.integers(0, 40))
+        regions.append((pos, ln, int(rng.integers(0, 2**32)), int(rng.integers(0, 4))))
+        pos += ln + int(rng.integers(0, 3))
+    host = aligned_host(pos + 32)
+    host[:] = rng.integers(0, 256, len(host), dtype=np.uint8)
+    descs = np.array(regions, dtype=gpu.FRAME_DESC)
+    got = run_batch(ctx, host, descs, cuda)
+    assert np.array_equal(got, oracle_unmask_regions(host, descs))
+
+
+@pytest.mark.parametrize("n_frames", [1, 7, 4096])
+def test_unmask_batch_c2_shape(ctx, cuda, n_frames):
+    wire, descs, _ = gpu.config_c2(seed=7, n_frames=n_frames)
+    got = run_batch(ctx, wire, descs, cuda)
+    exp = wire.copy()
+    ret, frames, _, consumed = orc.orc_decode_stream(exp)
+    assert ret == 0 and consumed == len(wire) and len(frames) == n_frames
+    assert np.array_equal(got, exp)
+
+
+def test_unmask_batch_c2_full(ctx, cuda):
+    """BASELINE config 2 at full size: 65 536 x 4 KiB, seed 42, bit-exact."""
+    wire, descs, _ = gpu.config_c2()
+    got = run_batch(ctx, wire, descs, cuda)
+    exp = wire.copy()
+    ret, frames, _, consumed = orc.orc_decode_stream(exp)
+    assert ret == 0 and len(frames) == 65536
+    assert np.array_equal(got, exp)
+
+
+def test_unmask_batch_mixed(ctx, cuda):
+    wire, descs, _ = gpu.config_c3(seed=5, target=16 << 20)
+    got = run_batch(ctx, wire, descs, cuda)
+    exp = wire.copy()
+    ret, frames, _, _ = orc.orc_decode_stream(exp)
+    assert ret == 0 and len(frames) == len(descs)
+    assert np.array_equal(got, exp)
+
+
+def test_unmask_batch_involution(ctx, cuda):
+    """Size-independent property at full C2 size: two passes restore the input."""
+    wire, descs, _ = gpu.config_c2(seed=11)
+    dev = torch.from_numpy(wire).to(cuda)
+    dd = gpu.descs_to_device(descs, cuda)
+    gpu.unmask_batch(ctx, dev, dd, len(descs))
+    gpu.unmask_batch(ctx, dev, dd, len(descs))
+    torch.cuda.synchronize()
+    assert torch.equal(dev.cpu(), torch.from_numpy(wire))

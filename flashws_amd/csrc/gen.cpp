@@ -115,8 +115,8 @@ void fill_utf8(std::mt19937_64 &r, uint8_t *p, uint64_t n) {
 // Overwrite with one always-invalid pattern (Unicode Table 3-7 violations).
 void inject_invalid(Gen &g, uint8_t *p, uint64_t n) {
     static const uint8_t pats[6][4] = {{0xFF, 0, 0, 0}, {0xC0, 0x80, 0, 0}, {0xED, 0xA0, 0x80, 0},
-                                       {0x80, 0, 0, 0}, {0xF4, 0x90, 0x80, 0x80}, {0xE2, 0x82, 0, 0}};
-    static const int lens[6] = {1, 2, 3, 1, 4, 2};
+                                       {0xC1, 0xBF, 0, 0}, {0xF4, 0x90, 0x80, 0x80}, {0xE2, 0x82, 0, 0}};
+    static const int lens[6] = {1, 2, 3, 2, 4, 2};
     int k = (int)(g.meta() % 6);
     if (k == 5) {                      // truncated 3-byte sequence at the very end
         if (n >= 2) { p[n - 2] = 0xE2; p[n - 1] = 0x82; }

@@ -46,6 +46,14 @@ assert FRAME_DESC.itemsize == 24 and FRAME_INFO.itemsize == 24
 assert DECODE_RESULT.itemsize == 40 and RX_EVENT.itemsize == 48
 
 
+class RxState(C.Structure):
+    """fws_rx_state (field names of the reference's members, w_socket.h:223-245)."""
+    _fields_ = [("recv_status", C.c_int32), ("last_rx_mask_key", C.c_uint32),
+                ("unread_pl_len", C.c_uint64), ("last_rx_opcode", C.c_uint8),
+                ("last_rx_control_opcode", C.c_uint8), ("last_rx_fin_flag", C.c_uint8),
+                ("is_rx_control_frame", C.c_uint8), ("last_rx_hdr_part_len", C.c_uint32)]
+
+
 class GenParams(C.Structure):
     _fields_ = [("seed", C.c_uint64), ("kind", C.c_uint32), ("opcode", C.c_uint32),
                 ("n_frames", C.c_uint64), ("payload_min", C.c_uint64), ("payload_max", C.c_uint64),
@@ -72,6 +80,7 @@ SIGNATURES = [
     ("fws_rx_session_create", _I, [_P, _I, C.POINTER(C.c_void_p)]),
     ("fws_rx_session_destroy", None, [_P]),
     ("fws_rx_session_feed", _I, [_P, _P, _U64, _U64, _P, _U64, _PU64, _P, _U64, _PU64]),
+    ("fws_rx_session_state", _I, [_P, _P]),
     ("fws_gen_batch", _I, [C.POINTER(GenParams), _P, _U64, _PU64, _P, _U64, _PU64, _P]),
 ]
 

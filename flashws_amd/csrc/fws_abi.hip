@@ -81,11 +81,14 @@ void fws_gpu_ctx_destroy(fws_gpu_ctx *ctx) {
     fws_decode_ws &d = ctx->dec;
     dev_free(d.tile_count);
     dev_free(d.tile_base);
-    dev_free(d.surv_pos);
-    dev_free(d.surv_next);
+    dev_free(d.tile_entry);
+    dev_free(d.tile_frames);
+    dev_free(d.fbase);
+    dev_free(d.surv_info);
+    dev_free(d.surv_leaf);
     dev_free(d.jump);
-    dev_free(d.mark);
-    dev_free(d.mark_base);
+    dev_free(d.on_path);
+    dev_free(d.path);
     dev_free(d.counters);
     dev_free(d.descs);
     delete ctx;
@@ -112,7 +115,7 @@ int fws_gpu_unmask_plan(fws_gpu_ctx *ctx, const void *dev_base, const fws_frame_
     if (!ctx || (n && (!dev_base || !dev_descs))) return FWS_ERR_INVALID;
     if (n == 0) return 0;
     if (ctx->cap_stream == 0 || n > ctx->cap_frames) return FWS_ERR_CAPACITY;
-    return fws_launch_plan((const uint8_t *)dev_base, dev_descs, n, ctx->plan, (hipStream_t)stream);
+    return fws_launch_plan((const uint8_t *)dev_base, dev_descs, n, nullptr, ctx->plan, (hipStream_t)stream);
 }
 
 int fws_gpu_unmask_run(fws_gpu_ctx *ctx, void *dev_base, const fws_frame_desc *dev_descs,
@@ -121,7 +124,7 @@ int fws_gpu_unmask_run(fws_gpu_ctx *ctx, void *dev_base, const fws_frame_desc *d
     if (n == 0) return 0;
     if (ctx->cap_stream == 0 || n > ctx->cap_frames) return FWS_ERR_CAPACITY;
     const uint64_t max_chunks = ctx->cap_stream / 16 + 2ull * n;
-    return fws_launch_unmask((uint8_t *)dev_base, dev_descs, n, ctx->plan, max_chunks,
+    return fws_launch_unmask((uint8_t *)dev_base, dev_descs, n, nullptr, ctx->plan, max_chunks,
                              (hipStream_t)stream);
 }
 
@@ -130,6 +133,44 @@ int fws_gpu_unmask_batch(fws_gpu_ctx *ctx, void *dev_base, const fws_frame_desc 
     int r = fws_gpu_unmask_plan(ctx, dev_base, dev_descs, n, stream);
     if (r) return r;
     return fws_gpu_unmask_run(ctx, dev_base, dev_descs, n, stream);
+}
+
+int fws_gpu_unmask_gather(fws_gpu_ctx *ctx, void *dev_dst, const void *dev_src, const fws_frame_desc *dev_descs,
+                          uint32_t n, void *stream) {
+    if (!ctx || (n && (!dev_dst || !dev_src || !dev_descs))) return FWS_ERR_INVALID;
+    if (((uintptr_t)dev_dst & 15u) != 0) return FWS_ERR_INVALID;
+    if (n == 0) return 0;
+    if (ctx->cap_stream == 0 || n > ctx->cap_frames) return FWS_ERR_CAPACITY;
+    return fws_launch_gather((uint8_t *)dev_dst, (const uint8_t *)dev_src, dev_descs, n, ctx->plan, ctx->cap_stream,
+                             (hipStream_t)stream);
+}
+
+int fws_gpu_validate_utf8(fws_gpu_ctx *ctx, const void *dev_base, const fws_frame_desc *dev_descs, uint32_t n,
+                          uint8_t *dev_ok, void *stream) {
+    if (!ctx || (n && (!dev_base || !dev_descs || !dev_ok))) return FWS_ERR_INVALID;
+    return fws_launch_utf8_descs((const uint8_t *)dev_base, dev_descs, n, dev_ok, (hipStream_t)stream);
+}
+
+int fws_gpu_decode_stream(fws_gpu_ctx *ctx, void *dev_wire, uint64_t len, fws_frame_info *dev_frames,
+                          uint32_t cap, fws_decode_result *dev_result, uint8_t *dev_utf8_ok, void *stream) {
+    if (!ctx || !dev_result || (len && !dev_wire) || (cap && !dev_frames)) return FWS_ERR_INVALID;
+    if (((uintptr_t)dev_wire & 15u) != 0) return FWS_ERR_INVALID;   // tiles are staged with 16-B loads
+    hipStream_t s = (hipStream_t)stream;
+    int r;
+    if ((r = fws_hip_status(hipSetDevice(ctx->device)))) return r;
+    if ((r = fws_decode_ensure(ctx, len, cap))) return r;
+    const uint64_t units = (len / 16 + 2ull * cap) / 256 + 2;
+    if ((r = fws_ctx_ensure_plan(ctx, cap, units))) return r;
+    if ((r = fws_launch_decode(ctx, (uint8_t *)dev_wire, len, dev_frames, cap, dev_result, s))) return r;
+    if (cap == 0 || len == 0) return 0;
+    const uint32_t *n_dev = ctx->dec.counters + kDecodeFramesCounter;
+    if ((r = fws_launch_plan((const uint8_t *)dev_wire, ctx->dec.descs, cap, n_dev, ctx->plan, s))) return r;
+    if ((r = fws_launch_unmask((uint8_t *)dev_wire, ctx->dec.descs, cap, n_dev, ctx->plan,
+                               len / 16 + 2ull * cap, s)))
+        return r;
+    if (dev_utf8_ok) return fws_launch_utf8_frames((const uint8_t *)dev_wire, len, dev_frames, cap, n_dev,
+                                                   dev_utf8_ok, s);
+    return 0;
 }
 
 }  // extern "C"

@@ -20,20 +20,23 @@ struct fws_plan_ws {
     uint64_t unit_cap = 0;            // capacity of unit_first (writes are clamped)
 };
 
-// Stream-decode workspace (see decode_kernels.hip).
+// Stream-decode workspace (decode_kernels.hip).
 struct fws_decode_ws {
-    uint64_t tile_bytes = 0;          // bytes per scan tile
     uint64_t max_tiles = 0;
     uint64_t max_surv = 0;            // capacity of the survivor arrays
+    uint64_t max_descs = 0;
+    uint32_t levels = 0;              // pointer-doubling tables allocated
     uint32_t *tile_count = nullptr;   // survivors per tile
-    uint64_t *tile_base = nullptr;    // exclusive prefix of tile_count
-    uint64_t *surv_pos = nullptr;     // survivor header offsets, sorted
-    uint64_t *surv_next = nullptr;    // next header offset of each survivor
+    uint32_t *tile_base = nullptr;    // first survivor index of each tile
+    uint32_t *tile_entry = nullptr;   // survivor index of the tile's first true header
+    uint32_t *tile_frames = nullptr;  // true frames per tile
+    uint32_t *fbase = nullptr;        // exclusive prefix of tile_frames
+    fws_frame_info *surv_info = nullptr;
+    uint32_t *surv_leaf = nullptr;    // leaf (last in-tile header) of each survivor's chain
     uint32_t *jump = nullptr;         // [levels][max_surv] pointer-doubling tables
-    uint32_t levels = 0;
-    uint8_t *mark = nullptr;          // on-path flags
-    uint64_t *mark_base = nullptr;    // exclusive prefix of marks
-    uint32_t *counters = nullptr;     // misc device counters
+    uint8_t *on_path = nullptr;       // survivor is a true frame header
+    uint32_t *path = nullptr;         // path nodes (k_mark)
+    uint32_t *counters = nullptr;     // see decode_kernels.hip Counter
     fws_frame_desc *descs = nullptr;  // payload regions of the decoded frames
 };
 
@@ -51,7 +54,22 @@ int fws_ctx_ensure_plan(fws_gpu_ctx *ctx, uint64_t frames, uint64_t units);
 
 // unmask_kernels.hip
 int fws_launch_mask_single(void *dev_ptr, uint64_t n, uint32_t key, uint32_t phase, hipStream_t s);
-int fws_launch_plan(const uint8_t *base, const fws_frame_desc *d, uint32_t n, fws_plan_ws &ws,
-                    hipStream_t s);
-int fws_launch_unmask(uint8_t *base, const fws_frame_desc *d, uint32_t n, const fws_plan_ws &ws,
-                      uint64_t max_chunks, hipStream_t s);
+// n_dev (optional, device memory): the actual count, <= n (n is the host-side bound).
+int fws_launch_plan(const uint8_t *base, const fws_frame_desc *d, uint32_t n, const uint32_t *n_dev,
+                    fws_plan_ws &ws, hipStream_t s);
+int fws_launch_unmask(uint8_t *base, const fws_frame_desc *d, uint32_t n, const uint32_t *n_dev,
+                      const fws_plan_ws &ws, uint64_t max_chunks, hipStream_t s);
+
+// text_kernels.hip
+int fws_launch_utf8_frames(const uint8_t *base, uint64_t N, const fws_frame_info *frames, uint32_t n,
+                           const uint32_t *n_dev, uint8_t *ok, hipStream_t s);
+int fws_launch_utf8_descs(const uint8_t *base, const fws_frame_desc *descs, uint32_t n, uint8_t *ok,
+                          hipStream_t s);
+int fws_launch_gather(uint8_t *dst, const uint8_t *src, const fws_frame_desc *d, uint32_t n, fws_plan_ws &ws,
+                      uint64_t max_bytes, hipStream_t s);
+
+// decode_kernels.hip
+constexpr int kDecodeFramesCounter = 3;   // index of the device frame count in dec.counters
+int fws_decode_ensure(fws_gpu_ctx *ctx, uint64_t N, uint32_t cap);
+int fws_launch_decode(fws_gpu_ctx *ctx, uint8_t *wire, uint64_t N, fws_frame_info *frames, uint32_t cap,
+                      fws_decode_result *res, hipStream_t s);

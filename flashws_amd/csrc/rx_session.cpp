@@ -1,0 +1,316 @@
+// rx_session.cpp -- fws_rx_session: WSocket::OnRecvData (net/w_socket.h:543-769)
+// for host read buffers, with the byte work on the GPU.
+//
+// Per read: the continuation of a frame in progress is unmasked with the
+// carried (rotated) key (fws_gpu_mask), the rest of the read -- prefixed with
+// any header bytes staged from the previous read -- goes through
+// fws_gpu_decode_stream (parallel header parse + unmask), the unmasked bytes
+// come back into the caller's buffer, and the host replays the reference's
+// per-part bookkeeping over the decoded frame list (no byte parsing, no XOR on
+// the host) to produce the exact on_read() / PONG / CLOSE event sequence and
+// carried RX state (w_socket.h:223-245). Host code only; server side only
+// (client RX has no unmask and is out of scope).
+#include <string.h>
+
+#include <vector>
+
+#include "fws_internal.h"
+
+namespace {
+
+constexpr int kWaitHead = 0, kWaitPayload = 1;   // w_socket.h:225-228
+
+inline uint32_t rotr(uint32_t v, uint32_t b) {     // base/constexpr_math.h:67-82
+    b &= 31u;
+    return (v >> b) | (v << ((32u - b) & 31u));
+}
+
+}  // namespace
+
+struct fws_rx_session {
+    fws_gpu_ctx *ctx = nullptr;
+    hipStream_t stream = nullptr;
+    // carried RX state, w_socket.h:223-245
+    int recv_status = kWaitHead;
+    uint64_t unread = 0;
+    uint32_t key = 0;
+    uint8_t last_op = 0, last_ctl_op = 0, last_fin = 0;
+    bool is_ctl = false;
+    uint32_t part_len = 0;
+    uint8_t hdr[14] = {};
+    // control payload staging (buf_), w_socket.h:637-658
+    uint8_t ctl[128] = {};
+    uint32_t ctl_size = 0;
+    bool ctl_alloc = false;
+    // device side
+    uint8_t *dA = nullptr, *dB = nullptr;
+    uint64_t capA = 0, capB = 0;
+    fws_frame_info *dframes = nullptr;
+    uint32_t fcap = 0;
+    fws_decode_result *dres = nullptr;
+    std::vector<fws_frame_info> frames;
+    std::vector<uint8_t> stream_host;
+    // event sinks of the current feed
+    fws_rx_event *ev = nullptr;
+    uint64_t ev_cap = 0, n_ev = 0;
+    uint8_t *ctl_out = nullptr;
+    uint64_t ctl_cap = 0, ctl_used = 0;
+
+    void push(const fws_rx_event &e) {
+        if (n_ev < ev_cap) ev[n_ev] = e;
+        ++n_ev;
+    }
+    uint64_t push_ctl(const uint8_t *p, uint64_t n) {
+        const uint64_t off = ctl_used;
+        if (ctl_used + n <= ctl_cap) memcpy(ctl_out + ctl_used, p, n);
+        ctl_used += n;
+        return off;
+    }
+
+    // ParseFrameHdr's state side effects and result on <= 14 staged bytes
+    // (w_socket.h:443-521); used only for a header left incomplete at the end
+    // of a read and for the failing header of a protocol error.
+    int host_parse(const uint8_t *d, uint64_t avail) {
+        if (avail < 2) return 0;
+        const uint32_t b0 = d[0], op = b0 & 15u;
+        const bool valid = (op <= 2u) || (op >= 8u && op <= 10u);
+        if (!valid) return FWS_ERR_OPCODE;
+        if (op >> 3) { is_ctl = true; last_ctl_op = (uint8_t)op; }
+        else if (op != 0u) last_op = (uint8_t)op;
+        if (b0 & 112u) return FWS_ERR_RSV;
+        const uint32_t b1 = d[1];
+        const bool masked = b1 >> 7;
+        uint64_t plen = b1 & 127u, n = 2;
+        if (plen == 126u) {
+            if (avail < 4) return 0;
+            plen = ((uint64_t)d[2] << 8) | d[3];
+            n = 4;
+        } else if (plen == 127u) {
+            if (avail < 10) return 0;
+            plen = 0;
+            for (int i = 0; i < 8; ++i) plen = (plen << 8) | d[2 + i];
+            n = 10;
+        }
+        if (plen > (1ull << 32)) return FWS_ERR_TOO_LARGE;
+        if (!masked) return FWS_ERR_NOT_MASKED;
+        if (avail < n + 4) return 0;
+        memcpy(&key, d + n, 4);
+        return (int)(n + 4);
+    }
+
+    // The per-part tail of OnRecvData's loop body, w_socket.h:623-764.
+    void part(uint8_t *buf, uint64_t size, uint64_t cap, uint64_t data, uint64_t avail, uint64_t remain,
+              int status_at_part) {
+        const bool frame_end = unread <= remain;
+        const bool msg_end = last_fin && frame_end;
+        const uint32_t opcode = is_ctl ? last_ctl_op : last_op;
+        if (is_ctl && avail > 0) {                                    // :629-659
+            if (status_at_part == kWaitHead || !ctl_alloc) { ctl_alloc = true; ctl_size = 0; }
+            const uint64_t room = sizeof(ctl) - ctl_size;
+            memcpy(ctl + ctl_size, buf + data, avail < room ? avail : room);
+            ctl_size += (uint32_t)avail;
+        }
+        if (frame_end && is_ctl) {                                   // :661-711
+            const uint32_t n = ctl_alloc ? ctl_size : 0u;
+            if (opcode == 9u) {
+                fws_rx_event e{};
+                e.kind = 1; e.opcode = 10; e.is_ctl = 1; e.frame_end = 1; e.msg_end = 1; e.fin = 1;
+                e.size = n; e.data_off = data; e.ctl_off = push_ctl(ctl, n);
+                push(e);
+                ctl_alloc = false; ctl_size = 0;
+            } else if (opcode == 8u) {
+                fws_rx_event e{};
+                e.kind = 2; e.opcode = 8; e.is_ctl = 1; e.frame_end = 1; e.msg_end = 1; e.fin = 1;
+                e.code = n >= 2 ? ((uint32_t)ctl[0] << 8 | ctl[1]) : 1005u;
+                e.size = n; e.data_off = data; e.ctl_off = push_ctl(ctl, n);
+                push(e);
+                ctl_alloc = false; ctl_size = 0;
+            }
+        }
+        if (!is_ctl || opcode == 10u) {                               // :713-747
+            fws_rx_event e{};
+            e.kind = 0; e.opcode = opcode; e.is_ctl = is_ctl; e.frame_end = frame_end; e.msg_end = msg_end;
+            if (!is_ctl) {
+                e.size = avail;
+                e.data_off = data;
+                e.capacity = (data + avail == size) ? cap : data + avail;
+            } else {
+                const uint32_t n = ctl_alloc ? ctl_size : 0u;
+                e.size = n; e.data_off = data; e.ctl_off = push_ctl(ctl, n);
+                ctl_alloc = false; ctl_size = 0;
+            }
+            push(e);
+        }
+        unread -= avail;                                              // :750-764
+        if (unread == 0 && is_ctl) is_ctl = false;
+        if (!frame_end) {
+            key = rotr(key, (uint32_t)(avail & 3u) * 8u);
+            recv_status = kWaitPayload;
+        } else {
+            recv_status = kWaitHead;
+        }
+    }
+
+    int ensure(uint64_t bytes, uint32_t nframes) {
+        hipError_t e = hipSuccess;
+        if (bytes + 32 > capA) {
+            if (dA) (void)hipFree(dA);
+            if (dB) (void)hipFree(dB);
+            capA = capB = (bytes + 32 + 4095) & ~4095ull;
+            if ((e = hipMalloc((void **)&dA, capA)) != hipSuccess) return fws_hip_status(e);
+            if ((e = hipMalloc((void **)&dB, capB)) != hipSuccess) return fws_hip_status(e);
+        }
+        if (nframes > fcap) {
+            if (dframes) (void)hipFree(dframes);
+            fcap = nframes;
+            if ((e = hipMalloc((void **)&dframes, (uint64_t)fcap * sizeof(fws_frame_info))) != hipSuccess)
+                return fws_hip_status(e);
+        }
+        if (!dres && (e = hipMalloc((void **)&dres, sizeof(fws_decode_result))) != hipSuccess)
+            return fws_hip_status(e);
+        return 0;
+    }
+};
+
+extern "C" {
+
+int fws_rx_session_create(fws_gpu_ctx *ctx, int is_server, fws_rx_session **out) {
+    if (!ctx || !out) return FWS_ERR_INVALID;
+    *out = nullptr;
+    if (!is_server) return FWS_ERR_INVALID;      // client RX (no unmask) is not on this path
+    int r = fws_hip_status(hipSetDevice(ctx->device));
+    if (r) return r;
+    fws_rx_session *s = new fws_rx_session();
+    s->ctx = ctx;
+    if ((r = fws_hip_status(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking)))) {
+        delete s;
+        return r;
+    }
+    *out = s;
+    return 0;
+}
+
+void fws_rx_session_destroy(fws_rx_session *s) {
+    if (!s) return;
+    if (s->stream) (void)hipStreamSynchronize(s->stream);
+    if (s->dA) (void)hipFree(s->dA);
+    if (s->dB) (void)hipFree(s->dB);
+    if (s->dframes) (void)hipFree(s->dframes);
+    if (s->dres) (void)hipFree(s->dres);
+    if (s->stream) (void)hipStreamDestroy(s->stream);
+    delete s;
+}
+
+int fws_rx_session_state(const fws_rx_session *s, fws_rx_state *out) {
+    if (!s || !out) return FWS_ERR_INVALID;
+    out->recv_status = s->recv_status;
+    out->mask_key = s->key;
+    out->unread_pl_len = s->unread;
+    out->last_rx_opcode = s->last_op;
+    out->last_rx_control_opcode = s->last_ctl_op;
+    out->last_rx_fin_flag = s->last_fin;
+    out->is_rx_control_frame = s->is_ctl ? 1 : 0;
+    out->last_rx_hdr_part_len = s->part_len;
+    return 0;
+}
+
+static int feed_impl(fws_rx_session *s, uint8_t *buf, uint64_t size, uint64_t buf_capacity);
+
+int fws_rx_session_feed(fws_rx_session *s, uint8_t *buf, uint64_t size, uint64_t buf_capacity,
+                        fws_rx_event *events, uint64_t ev_cap, uint64_t *n_events,
+                        uint8_t *ctl_out, uint64_t ctl_cap, uint64_t *ctl_used) {
+    if (!s || (size && !buf) || !n_events || !ctl_used) return FWS_ERR_INVALID;
+    s->ev = events; s->ev_cap = events ? ev_cap : 0; s->n_ev = 0;
+    s->ctl_out = ctl_out; s->ctl_cap = ctl_out ? ctl_cap : 0; s->ctl_used = 0;
+    const int r = feed_impl(s, buf, size, buf_capacity);
+    *n_events = s->n_ev;
+    *ctl_used = s->ctl_used;
+    if (r == 0 && (s->n_ev > ev_cap || s->ctl_used > ctl_cap)) return FWS_ERR_CAPACITY;
+    return r;
+}
+
+static int feed_impl(fws_rx_session *s, uint8_t *buf, uint64_t size, uint64_t buf_capacity) {
+    if (size == 0) return 0;
+    int r;
+    hipError_t e;
+    hipStream_t st = s->stream;
+    const uint32_t fcap = (uint32_t)((size + s->part_len) / 6 + 2);
+    if ((r = s->ensure(size + 16, fcap))) return r;
+
+    // 1. continuation of the frame in progress (WAIT_FRAME_PAYLOAD, w_socket.h:607-617)
+    uint64_t u = 0;
+    if (s->recv_status == kWaitPayload) {
+        u = size < s->unread ? size : s->unread;
+        if (u) {
+            if ((e = hipMemcpyAsync(s->dA, buf, u, hipMemcpyHostToDevice, st)) != hipSuccess) return fws_hip_status(e);
+            if ((r = fws_gpu_mask(s->dA, u, s->key, st))) return r;
+            if ((e = hipMemcpyAsync(buf, s->dA, u, hipMemcpyDeviceToHost, st)) != hipSuccess) return fws_hip_status(e);
+        }
+    }
+    // 2. header stream: staged header bytes + the rest of the read
+    const uint32_t part0 = s->part_len;
+    const uint64_t rest = size - u;
+    const uint64_t L = part0 + rest;
+    fws_decode_result res{};
+    if (rest) {
+        if (part0 && (e = hipMemcpyAsync(s->dB, s->hdr, part0, hipMemcpyHostToDevice, st)) != hipSuccess)
+            return fws_hip_status(e);
+        if ((e = hipMemcpyAsync(s->dB + part0, buf + u, rest, hipMemcpyHostToDevice, st)) != hipSuccess)
+            return fws_hip_status(e);
+        if ((r = fws_gpu_decode_stream(s->ctx, s->dB, L, s->dframes, fcap, s->dres, nullptr, st))) return r;
+        if ((e = hipMemcpyAsync(&res, s->dres, sizeof(res), hipMemcpyDeviceToHost, st)) != hipSuccess)
+            return fws_hip_status(e);
+        if ((e = hipMemcpyAsync(buf + u, s->dB + part0, rest, hipMemcpyDeviceToHost, st)) != hipSuccess)
+            return fws_hip_status(e);
+    }
+    if ((e = hipStreamSynchronize(st)) != hipSuccess) return fws_hip_status(e);
+    if (res.status == FWS_ERR_CAPACITY) return FWS_ERR_CAPACITY;
+    s->frames.resize(res.n_frames);
+    if (res.n_frames) {
+        if ((e = hipMemcpy(s->frames.data(), s->dframes, (uint64_t)res.n_frames * sizeof(fws_frame_info),
+                           hipMemcpyDeviceToHost)) != hipSuccess)
+            return fws_hip_status(e);
+    }
+
+    // 3. replay OnRecvData's loop over the decoded parts
+    if (u) {
+        s->part(buf, size, buf_capacity, 0, u, size, kWaitPayload);
+    }
+    if (!rest) return 0;   // the whole read was payload of the frame in progress
+    // header stream coordinate x <-> read coordinate x - part0 + u
+    for (uint32_t i = 0; i < res.n_frames; ++i) {
+        const fws_frame_info &fi = s->frames[i];
+        const uint32_t op = fi.opcode;
+        if (op >> 3) { s->is_ctl = true; s->last_ctl_op = (uint8_t)op; }      // :455-464
+        else if (op != 0u) s->last_op = (uint8_t)op;
+        s->key = fi.key;
+        s->part_len = 0;
+        const uint64_t data = fi.hdr_off + fi.hdr_len - part0 + u;
+        s->unread = fi.payload_len;
+        s->last_fin = fi.fin;
+        const uint64_t remain = size - data;
+        const uint64_t avail = remain < fi.payload_len ? remain : fi.payload_len;
+        s->part(buf, size, buf_capacity, data, avail, remain, kWaitHead);
+    }
+    // 4. the read ends inside a header, or at a protocol error (bookkeeping of
+    //    the staged parse, w_socket.h:566-603)
+    if (res.status < 0 || res.carry_hdr_len) {
+        const uint64_t at = res.status < 0 ? res.err_off : L - res.carry_hdr_len;
+        uint8_t win[14];
+        uint64_t have = 0;
+        for (; have < 14 && at + have < L; ++have) {
+            const uint64_t x = at + have;
+            win[have] = x < part0 ? s->hdr[x] : buf[x - part0 + u];
+        }
+        const int pr = s->host_parse(win, have);
+        if (res.status < 0) return pr < 0 ? pr : res.status;
+        // incomplete: reference stages min(14 - part_len, bytes left) (:567-569, 592)
+        const uint64_t staged_before = at < part0 ? part0 - at : 0;   // bytes of it from earlier reads
+        const uint64_t from_read = L - at - staged_before;
+        memmove(s->hdr, win, have);
+        s->part_len = (uint32_t)(staged_before + from_read);
+    }
+    return 0;
+}
+
+}  // extern "C"

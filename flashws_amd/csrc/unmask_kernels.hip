@@ -53,7 +53,9 @@ __device__ __forceinline__ uint64_t desc_chunks(const uint8_t *base, const fws_f
 
 __global__ __launch_bounds__(kBlock) void k_plan_count(const uint8_t *base,
                                                        const fws_frame_desc *__restrict__ d,
-                                                       uint32_t n, uint64_t *__restrict__ block_sums) {
+                                                       uint32_t n, const uint32_t *__restrict__ n_dev,
+                                                       uint64_t *__restrict__ block_sums) {
+    if (n_dev && *n_dev < n) n = *n_dev;
     const uint64_t f0 = uint64_t(blockIdx.x) * kPlanTile + uint64_t(threadIdx.x) * kPlanItems;
     uint64_t s = 0;
 #pragma unroll
@@ -68,11 +70,13 @@ __global__ __launch_bounds__(kBlock) void k_plan_count(const uint8_t *base,
 // holding chunk u * kUnitChunks; *total_out = total chunks.
 __global__ __launch_bounds__(kBlock) void k_plan_scan(const uint8_t *base,
                                                       const fws_frame_desc *__restrict__ d, uint32_t n,
+                                                      const uint32_t *__restrict__ n_dev,
                                                       const uint64_t *__restrict__ block_sums,
                                                       uint64_t *__restrict__ cbase,
                                                       uint32_t *__restrict__ unit_first,
                                                       uint64_t *__restrict__ total_out,
                                                       uint64_t unit_cap) {
+    if (n_dev && *n_dev < n) n = *n_dev;
     __shared__ uint64_t s_prefix;
     // prefix of earlier blocks (n_blocks is small: n / 1024)
     uint64_t p = 0;
@@ -105,11 +109,15 @@ __global__ __launch_bounds__(kBlock) void k_plan_scan(const uint8_t *base,
                 for (; u < ue; ++u) unit_first[u] = (uint32_t)f;
             }
             run += c[i];
+            if (f == n - 1) {   // the thread holding the last frame has the grand total
+                cbase[n] = run;
+                *total_out = run;
+            }
         }
     }
-    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == kBlock - 1) {
-        cbase[n] = run;        // last thread of the last block holds the grand total
-        *total_out = run;
+    if (n == 0 && blockIdx.x == 0 && threadIdx.x == 0) {
+        cbase[0] = 0;
+        *total_out = 0;
     }
 }
 
@@ -118,10 +126,13 @@ __global__ __launch_bounds__(kBlock) void k_plan_scan(const uint8_t *base,
 // are issued before any XOR/store so each lane keeps 64 B in flight.
 template <bool kSingle>
 __global__ __launch_bounds__(kBlock) void k_unmask(uint8_t *base, const fws_frame_desc *__restrict__ d,
-                                                   uint32_t n, const uint64_t *__restrict__ cbase,
+                                                   uint32_t n, const uint32_t *__restrict__ n_dev,
+                                                   const uint64_t *__restrict__ cbase,
                                                    const uint32_t *__restrict__ unit_first,
                                                    const uint64_t *__restrict__ total_ptr,
                                                    uint64_t unit_cap, fws_frame_desc single) {
+    if (!kSingle && n_dev && *n_dev < n) n = *n_dev;
+    if (n == 0) return;
     const uint64_t total = kSingle ? chunks_of((uintptr_t)(base + single.payload_off), single.payload_len)
                                    : *total_ptr;
     uint64_t n_units = (total + kUnitChunks - 1) / kUnitChunks;
@@ -192,24 +203,24 @@ int fws_launch_mask_single(void *dev_ptr, uint64_t n, uint32_t key, uint32_t pha
     const uint64_t chunks = ((((uintptr_t)dev_ptr) + n + 15u) >> 4) - (((uintptr_t)dev_ptr) >> 4);
     const uint64_t units = (chunks + kUnitChunks - 1) / kUnitChunks;
     hipLaunchKernelGGL(k_unmask<true>, dim3(grid_for_units(units)), dim3(kBlock), 0, s,
-                       (uint8_t *)dev_ptr, nullptr, 1u, nullptr, nullptr, nullptr, 0ull, one);
+                       (uint8_t *)dev_ptr, nullptr, 1u, nullptr, nullptr, nullptr, nullptr, 0ull, one);
     return fws_hip_status(hipGetLastError());
 }
 
-int fws_launch_plan(const uint8_t *base, const fws_frame_desc *d, uint32_t n, fws_plan_ws &ws,
-                    hipStream_t s) {
+int fws_launch_plan(const uint8_t *base, const fws_frame_desc *d, uint32_t n, const uint32_t *n_dev,
+                    fws_plan_ws &ws, hipStream_t s) {
     const uint32_t nb = (n + kPlanTile - 1) / kPlanTile;
-    hipLaunchKernelGGL(k_plan_count, dim3(nb), dim3(kBlock), 0, s, base, d, n, ws.block_sums);
-    hipLaunchKernelGGL(k_plan_scan, dim3(nb), dim3(kBlock), 0, s, base, d, n, ws.block_sums, ws.cbase,
+    hipLaunchKernelGGL(k_plan_count, dim3(nb), dim3(kBlock), 0, s, base, d, n, n_dev, ws.block_sums);
+    hipLaunchKernelGGL(k_plan_scan, dim3(nb), dim3(kBlock), 0, s, base, d, n, n_dev, ws.block_sums, ws.cbase,
                        ws.unit_first, ws.total, ws.unit_cap);
     return fws_hip_status(hipGetLastError());
 }
 
-int fws_launch_unmask(uint8_t *base, const fws_frame_desc *d, uint32_t n, const fws_plan_ws &ws,
-                      uint64_t max_chunks, hipStream_t s) {
+int fws_launch_unmask(uint8_t *base, const fws_frame_desc *d, uint32_t n, const uint32_t *n_dev,
+                      const fws_plan_ws &ws, uint64_t max_chunks, hipStream_t s) {
     const uint64_t units = (max_chunks + kUnitChunks - 1) / kUnitChunks;
     fws_frame_desc none{0, 0, 0, 0};
     hipLaunchKernelGGL(k_unmask<false>, dim3(grid_for_units(units)), dim3(kBlock), 0, s, base, d, n,
-                       ws.cbase, ws.unit_first, ws.total, ws.unit_cap, none);
+                       n_dev, ws.cbase, ws.unit_first, ws.total, ws.unit_cap, none);
     return fws_hip_status(hipGetLastError());
 }

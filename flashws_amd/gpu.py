@@ -178,6 +178,11 @@ class RxSession:
                                         ctl.ctypes.data, ctl_cap, C.byref(ctl_used))
         return ret, buf, ev[:n_ev.value].copy(), ctl[:ctl_used.value].copy()
 
+    def state(self):
+        st = _lib.RxState()
+        check("fws_rx_session_state", lib().fws_rx_session_state(self.h, C.byref(st)))
+        return st
+
     def close(self):
         if self.h:
             lib().fws_rx_session_destroy(self.h)

@@ -161,6 +161,18 @@ typedef struct fws_rx_event {
     uint64_t capacity;      /* IOBuffer capacity of the view, relative to the read start */
 } fws_rx_event;             /* 48 bytes */
 
+/* Carried RX state of a session (w_socket.h:223-245), for inspection. */
+typedef struct fws_rx_state {
+    int32_t recv_status;    /* 0 WAIT_FRAME_HEAD, 1 WAIT_FRAME_PAYLOAD */
+    uint32_t mask_key;      /* last_rx_mask_key_, rotated for the next payload byte */
+    uint64_t unread_pl_len;
+    uint8_t last_rx_opcode;
+    uint8_t last_rx_control_opcode;
+    uint8_t last_rx_fin_flag;
+    uint8_t is_rx_control_frame;
+    uint32_t last_rx_hdr_part_len;
+} fws_rx_state;             /* 24 bytes */
+
 typedef struct fws_rx_session fws_rx_session;
 
 int fws_rx_session_create(fws_gpu_ctx *ctx, int is_server, fws_rx_session **out);
@@ -171,6 +183,7 @@ void fws_rx_session_destroy(fws_rx_session *s);
 int fws_rx_session_feed(fws_rx_session *s, uint8_t *buf, uint64_t size, uint64_t buf_capacity,
                         fws_rx_event *events, uint64_t ev_cap, uint64_t *n_events,
                         uint8_t *ctl_out, uint64_t ctl_cap, uint64_t *ctl_used);
+int fws_rx_session_state(const fws_rx_session *s, fws_rx_state *out);
 
 /* ---- synthetic workloads (BASELINE configs, not test oracles) ------------ */
 typedef struct fws_gen_params {

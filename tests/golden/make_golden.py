@@ -26,31 +26,11 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(HERE))
 sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
 import orc  # noqa: E402
+from wsframes import frame  # noqa: E402
 
 MASK_LENS = list(range(0, 601)) + [1023, 1024, 1025, 2047, 2048, 2049, 4093, 4096, 16384, 65535, 65536]
 MASK_KEYS = [0x3D21FA37, 0x00000001, 0xFFFFFFFF]
 MASK_BASE_LEN = 65536 + 64 + 64
-
-
-def frame(opcode, payload, fin=1, key=0x3D21FA37, rsv=0, masked=True, len_form=None):
-    """Client frame bytes (RFC 6455 §5.2). len_form forces 126/127 encodings."""
-    n = len(payload)
-    b = bytearray([(fin << 7) | (rsv << 4) | opcode])
-    m = 0x80 if masked else 0
-    form = len_form if len_form else (n if n < 126 else (126 if n <= 65535 else 127))
-    if form == 126:
-        b += bytes([m | 126]) + struct.pack(">H", n)
-    elif form == 127:
-        b += bytes([m | 127]) + struct.pack(">Q", n)
-    else:
-        b += bytes([m | n])
-    if masked:
-        kb = struct.pack("<I", key)
-        b += kb
-        b += bytes(c ^ kb[i & 3] for i, c in enumerate(payload))
-    else:
-        b += payload
-    return bytes(b)
 
 
 def raw_header(b0, b1, ext=b"", key=b"\x01\x02\x03\x04"):

@@ -1,0 +1,252 @@
+"""GPU parity of the fused header parse + unmask (fws_gpu_decode_stream) against
+the oracle's restatement of OnRecvData / ParseFrameHdr (net/w_socket.h:435-769),
+bit-exact: unmasked bytes, frame list (offset, length, key, opcode, FIN,
+header length), status / error offset / carry-out.
+
+Sizes the oracle finishes in seconds are compared byte-for-byte; full
+BASELINE sizes additionally through size-independent properties.
+"""
+import numpy as np
+import pytest
+import torch
+
+import orc
+from flashws_amd import gpu
+from wsframes import frame
+
+pytestmark = pytest.mark.gpu
+
+
+def decode(ctx, wire, cuda, cap=None):
+    dev = torch.from_numpy(np.ascontiguousarray(wire)).to(cuda)
+    cap = cap if cap is not None else len(wire) // 6 + 16
+    rc, fr, res, _ = gpu.decode_stream(ctx, dev, cap=cap)
+    assert rc == 0, rc
+    r = gpu.read_result(res)
+    n = min(int(r["n_frames"]), cap)
+    return dev.cpu().numpy(), gpu.read_frames(fr, n), r
+
+
+def expect(wire):
+    buf = np.array(wire, dtype=np.uint8, copy=True)
+    ret, frames, err_off, consumed = orc.orc_decode_stream(buf)
+    return buf, frames, ret, err_off, consumed
+
+
+def check(ctx, cuda, wire):
+    wire = np.frombuffer(bytes(wire), dtype=np.uint8) if not isinstance(wire, np.ndarray) else wire
+    got, gframes, r = decode(ctx, wire, cuda)
+    buf, frames, ret, err_off, consumed = expect(wire)
+    assert int(r["status"]) == ret
+    assert int(r["n_frames"]) == len(frames)
+    for k in ("hdr_off", "payload_len", "key", "opcode", "fin", "hdr_len"):
+        assert np.array_equal(gframes[k], frames[k]), k
+    assert np.array_equal(got, buf)
+    if ret < 0:
+        assert int(r["err_off"]) == err_off
+    else:
+        assert int(r["consumed"]) == consumed
+    return r
+
+
+def test_rfc_hello(ctx, cuda):
+    r = check(ctx, cuda, bytes.fromhex("818537fa213d7f9f4d5158"))
+    assert int(r["n_frames"]) == 1 and int(r["consumed"]) == 11
+
+
+def test_empty_stream(ctx, cuda):
+    dev = torch.zeros(16, dtype=torch.uint8, device=cuda)
+    rc, fr, res, _ = gpu.decode_stream(ctx, dev, cap=4, n=0)
+    assert rc == 0
+    r = gpu.read_result(res)
+    assert int(r["status"]) == 0 and int(r["n_frames"]) == 0
+
+
+@pytest.mark.parametrize("tail", [b"", b"\x82", b"\x82\xfe\x01", bytes([0x82, 0xFF]) + b"\0" * 5])
+def test_incomplete_trailing_header(ctx, cuda, tail):
+    wire = frame(2, b"abc" * 100) + frame(1, b"x") + tail
+    r = check(ctx, cuda, wire)
+    assert int(r["carry_hdr_len"]) == len(tail)
+
+
+def test_truncated_payload(ctx, cuda):
+    wire = frame(2, b"p" * 5000) + frame(2, bytes(range(256)) * 100)
+    wire = wire[:-777]
+    r = check(ctx, cuda, wire)
+    assert int(r["carry_unread"]) == 777
+
+
+@pytest.mark.parametrize("bad,code", [(bytes([0xC2, 0x80]), -1), (bytes([0x83, 0x80]), -9),
+                                      (bytes([0x82, 0x05]), -3),
+                                      (bytes([0x82, 0xFF]) + (2**32 + 1).to_bytes(8, "big"), -2)])
+@pytest.mark.parametrize("lead", [0, 1, 40, 20000, 40000])
+def test_protocol_errors(ctx, cuda, bad, code, lead):
+    rng = np.random.default_rng(lead)
+    pre = b"".join(frame(2, rng.integers(0, 256, int(rng.integers(0, 3000)), dtype=np.uint8).tobytes())
+                   for _ in range(lead // 1000 + (1 if lead else 0)))
+    wire = pre + bad + b"\0" * 64 + frame(2, b"never")
+    r = check(ctx, cuda, wire)
+    assert int(r["status"]) == code and int(r["err_off"]) == len(pre)
+
+
+def test_first_header_invalid(ctx, cuda):
+    r = check(ctx, cuda, bytes([0x80 | 3, 0x80]) + b"\0" * 100)
+    assert int(r["status"]) == -9 and int(r["n_frames"]) == 0
+
+
+def test_zero_length_and_control_frames(ctx, cuda):
+    parts = [frame(2, b""), frame(9, b"ping"), frame(1, b"t", fin=0), frame(10, b"pong"),
+             frame(0, b"", fin=0), frame(0, b"end"), frame(8, b"\x03\xe8")]
+    check(ctx, cuda, b"".join(parts) * 50)
+
+
+def test_length_forms(ctx, cuda):
+    parts = [frame(2, b"hello", len_form=126), frame(2, b"hello", len_form=127),
+             frame(2, b"q" * 65535), frame(2, b"r" * 65536), frame(2, b"s" * 125), frame(2, b"t" * 126)]
+    check(ctx, cuda, b"".join(parts))
+
+
+def test_len_2p32_header_only(ctx, cuda):
+    wire = bytes([0x82, 0xFF]) + (1 << 32).to_bytes(8, "big") + b"\1\2\3\4" + b"\x55" * 300
+    r = check(ctx, cuda, wire)
+    assert int(r["carry_unread"]) == (1 << 32) - 300
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_random_small_frames(ctx, cuda, seed):
+    """Dense frames (0..300 B) so every 16 KiB tile holds many true headers."""
+    rng = np.random.default_rng(100 + seed)
+    out = []
+    total = 0
+    while total < 200_000:
+        n = int(rng.integers(0, 300))
+        op = int(rng.choice([1, 2, 0, 9, 10])) if n <= 125 else int(rng.choice([1, 2, 0]))
+        out.append(frame(op, rng.integers(0, 256, n, dtype=np.uint8).tobytes(),
+                         fin=int(rng.random() < 0.7), key=int(rng.integers(0, 2**32))))
+        total += len(out[-1])
+    check(ctx, cuda, b"".join(out))
+
+
+@pytest.mark.parametrize("size", [1, 15, 16, 16383, 16384, 16385, 16390, 32768 + 7])
+def test_single_frame_tile_boundaries(ctx, cuda, size):
+    for lead in (0, 1, 7, 16370):
+        wire = frame(2, b"a" * lead) + frame(1, bytes(range(256)) * (size // 256) + b"z" * (size % 256))
+        check(ctx, cuda, wire)
+
+
+def test_c3_mixed_parity(ctx, cuda):
+    """BASELINE config 3 shape (log-uniform 64 B..64 KiB) at 64 MiB, bit-exact."""
+    wire, descs, _ = gpu.config_c3(seed=9, target=64 << 20)
+    r = check(ctx, cuda, wire)
+    assert int(r["n_frames"]) == len(descs)
+
+
+def test_c2_full_parity(ctx, cuda):
+    wire, descs, _ = gpu.config_c2()
+    r = check(ctx, cuda, wire)
+    assert int(r["n_frames"]) == 65536
+
+
+def test_c3_full_roundtrip(ctx, cuda):
+    """Full C3 (256 MiB): frames equal the generator's, payload regions equal
+    the descriptor-mode unmask of the same input (size-independent check)."""
+    wire, descs, _ = gpu.config_c3()
+    got, gframes, r = decode(ctx, wire, cuda, cap=len(descs) + 16)
+    assert int(r["status"]) == 0 and int(r["n_frames"]) == len(descs)
+    assert np.array_equal(gframes["hdr_off"] + gframes["hdr_len"], descs["payload_off"])
+    assert np.array_equal(gframes["key"], descs["key"])
+    dev = torch.from_numpy(wire).to(cuda)
+    gpu.unmask_batch(ctx, dev, gpu.descs_to_device(descs, cuda), len(descs))
+    assert np.array_equal(dev.cpu().numpy(), got)
+
+
+def test_adversarial_all_valid_positions(ctx, cuda):
+    """Every offset parses as a valid empty frame (0x80 0x80 ...): 6-byte frames."""
+    wire = (bytes([0x80, 0x80]) + b"\x80" * 4) * 10000
+    check(ctx, cuda, wire)
+
+
+def test_utf8_flags_c5_shape(ctx, cuda):
+    wire, descs, ok = gpu.config_c5(seed=5, n_frames=512, payload=16384, invalid_permille=100)
+    dev = torch.from_numpy(wire).to(cuda)
+    flags = torch.zeros(len(descs), dtype=torch.uint8, device=cuda)
+    rc, fr, res, _ = gpu.decode_stream(ctx, dev, cap=len(descs) + 4, utf8_ok=flags)
+    assert rc == 0
+    got = flags.cpu().numpy()
+    assert np.array_equal(got, ok), (got.sum(), ok.sum())
+    unm = dev.cpu().numpy()
+    exp = [orc.orc_utf8_valid(unm[o:o + n]) for o, n in zip(descs["payload_off"], descs["payload_len"])]
+    assert np.array_equal(got.astype(bool), np.array(exp))
+
+
+def test_validate_utf8_edge_cases(ctx, cuda):
+    cases = [b"", b"a", b"\xc2\x80", b"\xc2", b"\xe0\xa0\x80", b"\xe0\x9f\x80", b"\xed\x9f\xbf", b"\xed\xa0\x80",
+             b"\xf0\x90\x80\x80", b"\xf0\x8f\xbf\xbf", b"\xf4\x8f\xbf\xbf", b"\xf4\x90\x80\x80", b"\xf5\x80\x80\x80",
+             b"\xc0\x80", b"\xc1\xbf", b"\x80", b"a\xe2\x82", "héllo wörld €𝄞".encode(), b"\xff", b"ab\xe2\x82\xacd"]
+    rng = np.random.default_rng(3)
+    for _ in range(300):
+        cases.append(rng.integers(0, 256, int(rng.integers(0, 40)), dtype=np.uint8).tobytes())
+        s = "".join(chr(int(c)) for c in rng.integers(0x20, 0x2FFF, 20) if not 0xD800 <= int(c) <= 0xDFFF)
+        b = bytearray(s.encode())
+        if len(b) and rng.random() < 0.5:
+            b[int(rng.integers(0, len(b)))] = int(rng.integers(0x80, 0x100))
+        cases.append(bytes(b))
+    blob, regions, pos = bytearray(), [], 0
+    for c in cases:
+        pad = int(rng.integers(0, 20))
+        blob += b"\0" * pad
+        pos += pad
+        regions.append((pos, len(c), 0, 0))
+        blob += c
+        pos += len(c)
+    dev = torch.frombuffer(bytearray(blob) + b"\0" * 32, dtype=torch.uint8).to(cuda)
+    descs = np.array(regions, dtype=gpu.FRAME_DESC)
+    ok = torch.zeros(len(descs), dtype=torch.uint8, device=cuda)
+    gpu.validate_utf8(ctx, dev, gpu.descs_to_device(descs, cuda), len(descs), ok)
+    got = ok.cpu().numpy().astype(bool)
+    for c, g in zip(cases, got):
+        try:
+            c.decode("utf-8")
+            exp = True
+        except UnicodeDecodeError:
+            exp = False
+        assert g == exp, c
+        assert orc.orc_utf8_valid(c) == exp, c
+
+
+def test_gather_reassembly_c4_shape(ctx, cuda):
+    wire, descs, _ = gpu.config_c4(seed=3, target=32 << 20)
+    src = torch.from_numpy(wire).to(cuda)
+    total = int(descs["payload_len"].sum())
+    dst = torch.zeros(total + 64, dtype=torch.uint8, device=cuda)
+    gpu.unmask_gather(ctx, dst, src, gpu.descs_to_device(descs, cuda), len(descs))
+    buf = wire.copy()
+    ret, frames, _, _ = orc.orc_decode_stream(buf)
+    assert ret == 0
+    exp = np.zeros(total, dtype=np.uint8)
+    w = orc.orc().orc_reassemble(buf.ctypes.data, frames.ctypes.data, len(frames), exp.ctypes.data)
+    assert w == total
+    assert np.array_equal(dst[:total].cpu().numpy(), exp)
+    assert int(dst[total:].sum()) == 0
+    assert torch.equal(src.cpu(), torch.from_numpy(wire))          # source untouched
+
+
+def test_gather_small_regions(ctx, cuda):
+    rng = np.random.default_rng(8)
+    regions, pos = [], 5
+    for _ in range(3000):
+        n = int(rng.integers(0, 40))
+        regions.append((pos, n, int(rng.integers(0, 2**32)), int(rng.integers(0, 4))))
+        pos += n + int(rng.integers(0, 5))
+    host = rng.integers(0, 256, pos + 64, dtype=np.uint8)
+    descs = np.array(regions, dtype=gpu.FRAME_DESC)
+    total = int(descs["payload_len"].sum())
+    dst = torch.zeros(total + 16, dtype=torch.uint8, device=cuda)
+    gpu.unmask_gather(ctx, dst, torch.from_numpy(host).to(cuda), gpu.descs_to_device(descs, cuda), len(descs))
+    exp, w = np.zeros(total, dtype=np.uint8), 0
+    for o, n, k, ph in regions:
+        seg = host[o:o + n].copy()
+        orc.orc_mask("mask1", seg, orc.orc().orc_rotr32(k, 8 * ph))
+        exp[w:w + n] = seg
+        w += n
+    assert np.array_equal(dst[:total].cpu().numpy(), exp)

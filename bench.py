@@ -45,7 +45,9 @@ def parse():
     ap.add_argument("--nbuf", type=int, default=4)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--extra", action="store_true", help="also time the fused stream decode")
+    ap.add_argument("--extra", action="store_true",
+                    help="also time C2 stream decode, C3, C4, e2e (PCIe) -> 'extra'")
+    ap.add_argument("--c5", action="store_true", help="with --extra: the 4 GiB C5 UTF-8 config")
     return ap.parse_args()
 
 
@@ -67,11 +69,24 @@ def barrier(world):
 
 
 def max_over_ranks(world, x):
+    """Slowest rank's value (the timed region ends when every rank is done)."""
     if world == 1:
         return x
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def shard_seed(rank):
+    """Each rank decodes its own independent batch: frames shard trivially
+    (SURVEY §8e), so there is no collective on the data path."""
+    return 42 + rank
+
+
+def aggregate_gib_s(world, payload_bytes_per_rank, step_s):
+    """Whole-job throughput: all ranks' payload / the slowest rank's step."""
+    return world * payload_bytes_per_rank / step_s / GIB
 
 
 def cpu_baseline(wire, seconds):
@@ -138,7 +153,7 @@ def main():
     world, rank, local = setup_dist(args)
     dev = torch.device("cuda", torch.cuda.current_device())
 
-    wire, descs, _ = gpu.config_c2(seed=42 + rank, n_frames=args.frames, payload=args.payload)
+    wire, descs, _ = gpu.config_c2(seed=shard_seed(rank), n_frames=args.frames, payload=args.payload)
     n = len(descs)
     payload_bytes = int(descs["payload_len"].sum())
     wire_bytes = len(wire)
@@ -182,7 +197,7 @@ def main():
     if args.extra:
         extra = stream_decode_extra(ctx, wire, dev, args)
 
-    value = world * payload_bytes / step_s / GIB
+    value = aggregate_gib_s(world, payload_bytes, step_s)
     achieved = alg_bytes / kern_s / 1e9
     traffic = pmc_traffic()
     out = {
@@ -219,8 +234,86 @@ def main():
         dist.destroy_process_group()
 
 
-def stream_decode_extra(ctx, wire, dev, args):
-    return {}
+def _time(fn, steps, stream):
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn(0)
+    torch.cuda.synchronize()
+    ev0.record(stream)
+    for i in range(steps):
+        fn(i)
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    return ev0.elapsed_time(ev1) / 1e3 / steps
+
+
+def stream_decode_extra(ctx, wire_c2, dev, args):
+    """The other BASELINE configs and the
+    PCIe-inclusive end-to-end rate; reported as `extra`, not as `value`."""
+    stream = torch.cuda.current_stream()
+    steps = max(4, min(args.steps, 50)) // 2 * 2         # even: in-place XOR restores the input
+    out = {}
+
+    def decode_cfg(name, wire, n_frames, utf8=False, nbuf=4):
+        c = gpu.Ctx(dev.index or 0, max_frames=n_frames + 64, max_stream_bytes=len(wire))
+        bufs = [torch.from_numpy(wire).to(dev) for _ in range(nbuf)]
+        cap = n_frames + 64
+        frames = torch.empty(cap * gpu.FRAME_INFO.itemsize, dtype=torch.uint8, device=dev)
+        res = torch.empty(gpu.DECODE_RESULT.itemsize, dtype=torch.uint8, device=dev)
+        ok = torch.zeros(cap, dtype=torch.uint8, device=dev) if utf8 else None
+        def step(i):
+            rc, _, _, _ = gpu.decode_stream(c, bufs[i % nbuf], cap, frames=frames, result=res, utf8_ok=ok)
+            assert rc == 0, rc
+        t = _time(step, steps, stream)
+        r = gpu.read_result(res)
+        assert int(r["status"]) == 0 and int(r["n_frames"]) == n_frames, (name, r)
+        payload = int(gpu.read_frames(frames, n_frames)["payload_len"].sum())
+        rec = {"GiB_per_s": round(payload / t / GIB, 1), "ms_per_step": round(t * 1e3, 4), "frames": n_frames,
+               "wire_bytes": len(wire), "alg_GB_per_s": round((len(wire) + payload) / t / 1e9, 1)}
+        if utf8:
+            rec["utf8_invalid_frames"] = int((ok[:n_frames] == 0).sum().item())
+        del bufs
+        c.close()
+        return rec
+
+    out["C2_stream_decode"] = decode_cfg("C2", wire_c2, args.frames)
+    w3, d3, _ = gpu.config_c3()
+    out["C3_mixed_stream_decode"] = decode_cfg("C3", w3, len(d3))
+    del w3
+    # C4: one 256 MiB fragmented message, unmask + reassemble out of place
+    w4, d4, _ = gpu.config_c4()
+    c = gpu.Ctx(dev.index or 0, max_frames=len(d4) + 8, max_stream_bytes=len(w4))
+    src = torch.from_numpy(w4).to(dev)
+    total = int(d4["payload_len"].sum())
+    dsts = [torch.empty(total + 64, dtype=torch.uint8, device=dev) for _ in range(4)]
+    dd4 = gpu.descs_to_device(d4, dev)
+    t = _time(lambda i: gpu.unmask_gather(c, dsts[i % 4], src, dd4, len(d4)), steps, stream)
+    out["C4_fragmented_reassemble"] = {"GiB_per_s": round(total / t / GIB, 1), "ms_per_step": round(t * 1e3, 4),
+                                       "fragments": len(d4), "alg_GB_per_s": round((len(w4) + total) / t / 1e9, 1)}
+    c.close()
+    del src, dsts, w4
+    # C5 per-GPU share: 262 144 x 16 KiB TEXT frames (4 GiB), decode + fused-launch UTF-8 flags
+    if args.c5:
+        w5, d5, ok5 = gpu.config_c5()
+        rec = decode_cfg("C5", w5, len(d5), utf8=True, nbuf=1)
+        rec["utf8_invalid_frames_expected"] = int((ok5 == 0).sum())
+        out["C5_utf8_text_decode"] = rec
+        del w5
+    # end-to-end: pinned host -> HBM -> unmask -> host (PCIe-inclusive), C2
+    n = args.frames
+    host_in = torch.from_numpy(wire_c2).pin_memory()
+    host_out = torch.empty_like(host_in).pin_memory()
+    dbuf = torch.empty(len(wire_c2), dtype=torch.uint8, device=dev)
+    _, descs, _ = gpu.config_c2(seed=42, n_frames=n, payload=args.payload)
+    dd = gpu.descs_to_device(descs, dev)
+    def e2e(i):
+        dbuf.copy_(host_in, non_blocking=True)
+        gpu.unmask_batch(ctx, dbuf, dd, n)
+        host_out.copy_(dbuf, non_blocking=True)
+    t = _time(e2e, 10, stream)
+    out["C2_end_to_end_pcie"] = {"GiB_per_s": round(int(descs["payload_len"].sum()) / t / GIB, 1),
+                                 "ms_per_step": round(t * 1e3, 3),
+                                 "path": "pinned H2D + fws_gpu_unmask_batch + D2H, one stream"}
+    return {"extra": out}
 
 
 if __name__ == "__main__":

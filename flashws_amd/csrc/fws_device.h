@@ -16,6 +16,25 @@ constexpr int kBlock = 256;         // 4 waves per workgroup
 constexpr int kUnmaskU = 4;         // 16-B chunks per lane per work unit
 constexpr uint64_t kUnitChunks = uint64_t(kWave) * kUnmaskU;   // 256 chunks = 4 KiB per wave unit
 
+// 16-B accesses through the global address space. Addresses are computed as
+// integers (chunk arithmetic), which would otherwise make hipcc emit flat_*
+// loads (counted on both vmcnt and lgkmcnt) and serialise them.
+typedef __attribute__((address_space(1))) u32x4 g_u32x4;
+
+template <bool kNT = false>
+__device__ __forceinline__ u32x4 gload16(uintptr_t a) {
+    const g_u32x4 *p = (const g_u32x4 *)a;
+    if constexpr (kNT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+
+template <bool kNT = false>
+__device__ __forceinline__ void gstore16(uintptr_t a, u32x4 v) {
+    g_u32x4 *p = (g_u32x4 *)a;
+    if constexpr (kNT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
 // base/constexpr_math.h:67-82 RotateR, 32-bit.
 __device__ __forceinline__ uint32_t rotr32(uint32_t v, uint32_t b) {
     b &= 31u;

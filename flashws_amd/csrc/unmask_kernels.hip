@@ -146,6 +146,8 @@ __global__ __launch_bounds__(kBlock) void k_unmask(uint8_t *base, const fws_fram
             flo = unit_first[u];
             fhi = (u + 1 < n_units) ? unit_first[u + 1] : n - 1;
         }
+        const uintptr_t safe =
+            (uintptr_t)(base + (kSingle ? single.payload_off : d[flo].payload_off)) & ~uintptr_t(15);
         uintptr_t ca[kUnmaskU], lo[kUnmaskU], hi[kUnmaskU];
         uint32_t rk[kUnmaskU];
         bool live[kUnmaskU];
@@ -171,15 +173,152 @@ __global__ __launch_bounds__(kBlock) void k_unmask(uint8_t *base, const fws_fram
 #pragma unroll
         for (int j = 0; j < kUnmaskU; ++j) {
             full[j] = live[j] && ca[j] >= lo[j] && ca[j] + 16u <= hi[j];
-            if (full[j]) v[j] = *reinterpret_cast<const u32x4 *>(ca[j]);
+            // unconditional load so every lane's loads issue back to back before
+            // any wait; non-full lanes read the chunk holding the first byte of
+            // the unit's first frame (non-empty, inside the caller's buffer)
+            v[j] = gload16(full[j] ? ca[j] : safe);
         }
 #pragma unroll
         for (int j = 0; j < kUnmaskU; ++j) {
             if (full[j]) {
-                *reinterpret_cast<u32x4 *>(ca[j]) = v[j] ^ rk[j];
+                gstore16(ca[j], v[j] ^ rk[j]);
             } else if (live[j]) {
                 xor_partial_chunk(ca[j], lo[j], hi[j], rk[j]);
             }
+        }
+    }
+}
+
+// Fast variant. A wave owns G consecutive plan units (G x 4 KiB). When those
+// units touch at most 4 frames (every frame >= ~4 KiB, e.g. BASELINE C2) the
+// frame metadata is wave-uniform: it is fetched with scalar loads (lgkmcnt, so
+// it never queues behind the payload loads on vmcnt), the lane's frame is
+// picked by three compares, and all G*4 16-B loads of a lane are in flight
+// before the first XOR. Units with more frames take the per-lane search path.
+// One chunk by the generic path: per-lane search of its frame, then a full
+// 16-B XOR or a byte-exact partial one (region heads/tails).
+__device__ __forceinline__ void unmask_one_chunk(uint8_t *base, const fws_frame_desc *__restrict__ d,
+                                              const uint64_t *__restrict__ cbase, uint32_t flo, uint32_t fhi,
+                                              uint64_t g) {
+    const uint32_t f = find_frame(cbase, flo, fhi, g);
+    const fws_frame_desc fd = d[f];
+    const uintptr_t a0 = (uintptr_t)(base + fd.payload_off);
+    const uintptr_t ca = (a0 & ~uintptr_t(15)) + (uintptr_t)((g - cbase[f]) << 4);
+    const uint32_t rk = aligned_key(fd.key, fd.phase, a0);
+    if (ca >= a0 && ca + 16u <= a0 + fd.payload_len) {
+        gstore16(ca, gload16(ca) ^ rk);
+    } else {
+        xor_partial_chunk(ca, a0, a0 + fd.payload_len, rk);
+    }
+}
+
+// XOR the in-region bytes [lo, hi) of the loaded chunk v at ca and store only
+// those (dword stores where a whole dword is inside, byte stores at the edges).
+__device__ __forceinline__ void store_partial(uintptr_t ca, u32x4 v, uint32_t rk, uintptr_t lo, uintptr_t hi) {
+    const uint32_t w4[4] = {v.x ^ rk, v.y ^ rk, v.z ^ rk, v.w ^ rk};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uintptr_t w = ca + 4u * i;
+        if (w >= lo && w + 4u <= hi) {
+            *(__attribute__((address_space(1))) uint32_t *)w = w4[i];
+        } else if (w + 4u > lo && w < hi) {
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+                if (w + b >= lo && w + b < hi)
+                    *(__attribute__((address_space(1))) uint8_t *)(w + b) = (uint8_t)(w4[i] >> (8 * b));
+        }
+    }
+}
+
+// Scalar (wave-uniform) metadata of one plan unit: its first frame and
+// whether the unit touches at most 2 frames.
+struct UnitMeta {
+    uint32_t flo, fhi;
+};
+
+__device__ __forceinline__ UnitMeta unit_meta(const uint32_t *__restrict__ unit_first, uint64_t u, uint64_t n_units,
+                                              uint32_t n) {
+    UnitMeta m{0u, 0u};
+    if (u < n_units) {
+        m.flo = unit_first[u];
+        m.fhi = (u + 1 < n_units) ? unit_first[u + 1] : n - 1;
+    }
+    return m;
+}
+
+// Fast variant, one 4 KiB plan unit per wave step. When the unit touches at
+// most 2 frames (every frame >= 4 KiB, e.g. BASELINE C2) the frame metadata is
+// wave-uniform: fetched with scalar loads (lgkmcnt, never queued behind the
+// payload loads on vmcnt), the lane's frame is one 64-bit compare, all 4
+// loads of a lane issue back to back, region heads/tails are stored byte-exact
+// from the same loaded chunk, and the next unit's metadata is fetched while
+// this unit's payload is in flight. Units with more frames take the per-lane
+// search path.
+template <bool kNT>
+__global__ __launch_bounds__(kBlock) void k_unmask_fast(uint8_t *base, const fws_frame_desc *__restrict__ d,
+                                                        uint32_t n, const uint32_t *__restrict__ n_dev,
+                                                        const uint64_t *__restrict__ cbase,
+                                                        const uint32_t *__restrict__ unit_first,
+                                                        const uint64_t *__restrict__ total_ptr, uint64_t unit_cap) {
+    constexpr int J = kUnmaskU;
+    if (n_dev && *n_dev < n) n = *n_dev;
+    if (n == 0) return;
+    const uint64_t total = *total_ptr;
+    uint64_t n_units = (total + kUnitChunks - 1) / kUnitChunks;
+    if (n_units > unit_cap) n_units = unit_cap;
+    const int lane = threadIdx.x & (kWave - 1);
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const uint64_t nwaves = uint64_t(gridDim.x) * (kBlock / kWave);
+    uint64_t u = uint64_t(blockIdx.x) * (kBlock / kWave) + wave;
+    UnitMeta m = unit_meta(unit_first, u, n_units, n);
+    for (; u < n_units; u += nwaves) {
+        const uint32_t flo = m.flo, fhi = m.fhi;
+        const uint64_t g0 = u * kUnitChunks + lane;
+        if (fhi - flo >= 2u) {                          // many small frames: generic path
+            m = unit_meta(unit_first, u + nwaves, n_units, n);
+#pragma unroll 1
+            for (int j = 0; j < J; ++j) {
+                const uint64_t g = g0 + uint64_t(j) * kWave;
+                if (g < total) unmask_one_chunk(base, d, cbase, flo, fhi, g);
+            }
+            continue;
+        }
+        uint64_t A[2], L[2], H[2];
+        uint32_t R[2];
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const uint32_t f = (flo + (uint32_t)k <= fhi) ? flo + (uint32_t)k : fhi;
+            const fws_frame_desc fd = d[f];
+            const uint64_t c = cbase[f];
+            const uintptr_t a0 = (uintptr_t)(base + fd.payload_off);
+            A[k] = (uint64_t)(a0 & ~uintptr_t(15)) - (c << 4);          // chunk g lives at A + 16 g
+            L[k] = a0;
+            H[k] = a0 + fd.payload_len;
+            R[k] = aligned_key(fd.key, fd.phase, a0);
+        }
+        const uint64_t CB1 = (fhi > flo) ? cbase[flo + 1] : ~0ull;
+        uintptr_t ca[J];
+        uint32_t rk[J];
+        bool live[J], s1[J];
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+            const uint64_t g = g0 + uint64_t(j) * kWave;
+            s1[j] = g >= CB1;
+            rk[j] = s1[j] ? R[1] : R[0];
+            ca[j] = (uintptr_t)((s1[j] ? A[1] : A[0]) + (g << 4));
+            live[j] = g < total;
+        }
+        const uintptr_t safe = (uintptr_t)L[0] & ~uintptr_t(15);   // holds a byte of frame flo
+        u32x4 v[J];
+#pragma unroll
+        for (int j = 0; j < J; ++j) v[j] = gload16<kNT>(live[j] ? ca[j] : safe);
+        m = unit_meta(unit_first, u + nwaves, n_units, n);        // next unit, overlapped
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+            if (!live[j]) continue;
+            const uintptr_t lo = s1[j] ? L[1] : L[0], hi = s1[j] ? H[1] : H[0];
+            if (ca[j] >= lo && ca[j] + 16u <= hi) gstore16<kNT>(ca[j], v[j] ^ rk[j]);
+            else store_partial(ca[j], v[j], rk[j], lo, hi);
         }
     }
 }
@@ -189,10 +328,26 @@ __global__ __launch_bounds__(kBlock) void k_unmask(uint8_t *base, const fws_fram
 // ---------------------------------------------------------------- launchers
 using namespace fwsk;
 
+// Kernel variant used by fws_launch_unmask (tuning hook, not part of the ABI):
+// 0 = k_unmask (per-lane search), 1 = k_unmask_fast, 5 = k_unmask_fast nontemporal.
+static int g_unmask_variant = 5;
+extern "C" __attribute__((visibility("default"))) int fws_internal_set_unmask_variant(int v) {
+    const int old = g_unmask_variant;
+    if (v >= 0 && v <= 7) g_unmask_variant = v;
+    return old;
+}
+
+static int g_grid_cap = 8192;   // tuning hook: max workgroups of the streaming kernels
+extern "C" __attribute__((visibility("default"))) int fws_internal_set_grid_cap(int blocks) {
+    const int old = g_grid_cap;
+    if (blocks > 0) g_grid_cap = blocks;
+    return old;
+}
+
 static int grid_for_units(uint64_t units) {
     // memory-bound: cap near 256 CUs x 8 blocks and grid-stride the rest
     uint64_t blocks = (units + (kBlock / kWave) - 1) / (kBlock / kWave);
-    if (blocks > 2048) blocks = 2048;
+    if (blocks > (uint64_t)g_grid_cap) blocks = (uint64_t)g_grid_cap;
     if (blocks < 1) blocks = 1;
     return (int)blocks;
 }
@@ -220,7 +375,16 @@ int fws_launch_unmask(uint8_t *base, const fws_frame_desc *d, uint32_t n, const 
                       const fws_plan_ws &ws, uint64_t max_chunks, hipStream_t s) {
     const uint64_t units = (max_chunks + kUnitChunks - 1) / kUnitChunks;
     fws_frame_desc none{0, 0, 0, 0};
-    hipLaunchKernelGGL(k_unmask<false>, dim3(grid_for_units(units)), dim3(kBlock), 0, s, base, d, n,
-                       n_dev, ws.cbase, ws.unit_first, ws.total, ws.unit_cap, none);
+    const int v = g_unmask_variant;
+    const dim3 grid(grid_for_units(units)), blk(kBlock);
+    if (v == 0 || v == 4)
+        hipLaunchKernelGGL(k_unmask<false>, grid, blk, 0, s, base, d, n, n_dev, ws.cbase, ws.unit_first, ws.total,
+                           ws.unit_cap, none);
+    else if (v < 4)
+        hipLaunchKernelGGL(k_unmask_fast<false>, grid, blk, 0, s, base, d, n, n_dev, ws.cbase, ws.unit_first,
+                           ws.total, ws.unit_cap);
+    else
+        hipLaunchKernelGGL(k_unmask_fast<true>, grid, blk, 0, s, base, d, n, n_dev, ws.cbase, ws.unit_first,
+                           ws.total, ws.unit_cap);
     return fws_hip_status(hipGetLastError());
 }

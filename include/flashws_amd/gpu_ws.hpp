@@ -1,0 +1,114 @@
+// flashws_amd/gpu_ws.hpp -- header-only C++ adapter that drops the MI355X
+// decode path (libfws_gpu.so, include/fws_gpu.h) into flashws's own frame and
+// buffer API. It does not include flashws.h (that header links in only one
+// TU, SURVEY §0 finding 2): the reference types are template parameters.
+//
+//   seam 1  fws::WSMaskBytesFast(src, size, mask)         crypto/ws_mask.h:175
+//           -> fws_amd::WSMaskBytesFastDevice(dev_src, size, mask, stream)
+//   seam 2  WSocket<...>::OnRecvData(IOBuffer&)            net/w_socket.h:543-769
+//           -> fws_amd::GpuRxDecoder::OnRecvData(io_buf, sink)
+//
+// GpuRxDecoder keeps the reference's on_read() contract (w_socket.h:82-84):
+// the sink receives (opcode, IOBuffer view aliasing io_buf, is_frame_end,
+// is_msg_end, is_control) in the reference's order; PING payloads are handed
+// back for the PONG reply and CLOSE frames with their status code, exactly
+// where the reference calls SendControlMsg / on_close (w_socket.h:661-711).
+// Return values are the reference's ParseFrameHdr codes (0 or negative).
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+#include <stdexcept>
+#include <string_view>
+#include <utility>
+#include <vector>
+
+#include "../fws_gpu.h"
+
+namespace fws_amd {
+
+// seam 1: in-place XOR unmask of device memory (any alignment, any size).
+inline int WSMaskBytesFastDevice(void *dev_src, size_t size, uint32_t mask, void *hip_stream = nullptr) {
+    return fws_gpu_mask(dev_src, size, mask, hip_stream);
+}
+
+// RAII device context (one per host thread / FLoop, floop.h:331-345).
+class GpuContext {
+public:
+    explicit GpuContext(int device = 0, uint64_t max_frames = 0, uint64_t max_stream_bytes = 0) {
+        if (fws_gpu_ctx_create(device, &ctx_) != 0) throw std::runtime_error("fws_gpu_ctx_create failed");
+        if ((max_frames || max_stream_bytes) && fws_gpu_ctx_reserve(ctx_, max_frames, max_stream_bytes) != 0)
+            throw std::runtime_error("fws_gpu_ctx_reserve failed");
+    }
+    ~GpuContext() { fws_gpu_ctx_destroy(ctx_); }
+    GpuContext(const GpuContext &) = delete;
+    GpuContext &operator=(const GpuContext &) = delete;
+    fws_gpu_ctx *get() const { return ctx_; }
+
+private:
+    fws_gpu_ctx *ctx_ = nullptr;
+};
+
+// seam 2: OnRecvData over the GPU. IOBuffer is fws::IOBuffer (or any type with
+// the same {data, size, start_pos, capacity} members and 4-arg constructor,
+// base/buffer_manager.h:36-52). Sink must provide:
+//   void on_read(uint32_t opcode, IOBuffer &&part, bool frame_end, bool msg_end, bool is_ctl);
+//   void on_ping(std::string_view payload);               // reply PONG (w_socket.h:662-666)
+//   void on_close(uint32_t code, std::string_view payload); // w_socket.h:667-710
+//   IOBuffer request_buf(size_t n);                         // e.g. fws::RequestBuf (buffer_manager.h:90)
+template <class IOBuffer>
+class GpuRxDecoder {
+public:
+    explicit GpuRxDecoder(GpuContext &ctx) {
+        if (fws_rx_session_create(ctx.get(), 1, &s_) != 0) throw std::runtime_error("fws_rx_session_create failed");
+        events_.resize(1024);
+        ctl_.resize(4096);
+    }
+    ~GpuRxDecoder() { fws_rx_session_destroy(s_); }
+    GpuRxDecoder(const GpuRxDecoder &) = delete;
+    GpuRxDecoder &operator=(const GpuRxDecoder &) = delete;
+
+    template <class Sink>
+    int OnRecvData(IOBuffer &io_buf, Sink &&sink) {
+        uint8_t *data = io_buf.data + io_buf.start_pos;
+        const uint64_t size = (uint64_t)io_buf.size;
+        const uint64_t cap = io_buf.capacity - io_buf.start_pos;
+        // bounds: every part / control event needs >= 6 wire bytes, except the
+        // first (a continuation) and the last; control payloads fit the read
+        if (events_.size() < size / 3 + 8) events_.resize(size / 3 + 8);
+        if (ctl_.size() < size + 256) ctl_.resize(size + 256);
+        uint64_t n_ev = 0, ctl_used = 0;
+        const int ret = fws_rx_session_feed(s_, data, size, cap, events_.data(), events_.size(), &n_ev,
+                                            ctl_.data(), ctl_.size(), &ctl_used);
+        for (uint64_t i = 0; i < n_ev && i < events_.size(); ++i) {
+            const fws_rx_event &e = events_[i];
+            const std::string_view ctl((const char *)ctl_.data() + e.ctl_off, e.size);
+            if (e.kind == 1) {
+                sink.on_ping(ctl);
+            } else if (e.kind == 2) {
+                sink.on_close(e.code, ctl);
+            } else if (!e.is_ctl) {
+                // aliasing view of the (now unmasked) read buffer, w_socket.h:715-728
+                sink.on_read(e.opcode,
+                             IOBuffer(io_buf.data, (ssize_t)e.size, io_buf.start_pos + e.data_off,
+                                      io_buf.start_pos + e.capacity),
+                             e.frame_end != 0, e.msg_end != 0, false);
+            } else {
+                // PONG payload: copied into a fresh buffer (the reference hands over
+                // its control buffer buf_, w_socket.h:729-731)
+                IOBuffer b = sink.request_buf(ctl.size());
+                for (size_t k = 0; k < ctl.size(); ++k) b.data[b.start_pos + k] = (uint8_t)ctl[k];
+                b.size = (ssize_t)ctl.size();
+                sink.on_read(e.opcode, std::move(b), e.frame_end != 0, e.msg_end != 0, true);
+            }
+        }
+        return ret;
+    }
+
+private:
+    fws_rx_session *s_ = nullptr;
+    std::vector<fws_rx_event> events_;
+    std::vector<uint8_t> ctl_;
+};
+
+}  // namespace fws_amd

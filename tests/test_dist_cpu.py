@@ -1,0 +1,64 @@
+"""CPU, world_size 2 over gloo: the multi-GPU path of bench.py (one process
+per GPU, independent shards, barrier + max-over-ranks timing, aggregate =
+sum of shards / slowest rank) with the oracle standing in for the device
+decode. No collective touches frame data."""
+import os
+import socket
+
+import numpy as np
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    sys.path.insert(0, os.path.join(root, "tests"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    import orc
+    from flashws_amd import gpu
+    wire, descs, _ = gpu.config_c2(seed=bench.shard_seed(rank), n_frames=512)
+    dist.barrier()
+    import time
+    t0 = time.perf_counter()
+    buf = wire.copy()
+    ret, frames, _, _ = orc.orc_decode_stream(buf)
+    t1 = time.perf_counter()
+    dist.barrier()
+    step = bench.max_over_ranks(world, t1 - t0)
+    payload = int(descs["payload_len"].sum())
+    agg = bench.aggregate_gib_s(world, payload, step)
+    digest = torch.tensor([int(buf[:4096].sum())], dtype=torch.int64)
+    gathered = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(gathered, digest)          # test-only check that shards differ
+    q.put((rank, ret, len(frames), step, t1 - t0, agg, payload, [int(g) for g in gathered]))
+    dist.destroy_process_group()
+
+
+def test_two_rank_batch_split_gloo():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    steps = [r[3] for r in res]
+    assert steps[0] == steps[1] == max(r[4] for r in res)        # both report the slowest rank
+    for rank, ret, nf, step, own, agg, payload, gathered in res:
+        assert ret == 0 and nf == 512
+        assert np.isclose(agg, world * payload / step / (1 << 30))
+    assert res[0][7][0] != res[0][7][1]                           # independent shards

@@ -337,7 +337,7 @@ extern "C" __attribute__((visibility("default"))) int fws_internal_set_unmask_va
     return old;
 }
 
-static int g_grid_cap = 8192;   // tuning hook: max workgroups of the streaming kernels
+static int g_grid_cap = 16384;  // tuning hook: max workgroups of the streaming kernels
 extern "C" __attribute__((visibility("default"))) int fws_internal_set_grid_cap(int blocks) {
     const int old = g_grid_cap;
     if (blocks > 0) g_grid_cap = blocks;

@@ -5,21 +5,22 @@
 // Frame boundaries are a serial dependency (header i+1's offset comes from
 // header i's length), so the stream is parsed speculatively and in parallel:
 //
-//  k_scan   one workgroup per 16 KiB tile staged in LDS. Every byte offset is
-//           parsed as a header (ParseFrameHdr semantics, w_socket.h:435-524);
-//           valid headers point at the next header offset. Pointer jumping in
-//           LDS resolves every chain to the last header before the tile end
-//           (its "leaf") or to DEAD (an invalid header). Offsets whose chain
-//           survives are "survivors": every true header is one, most random
-//           payload offsets are not (~2% pass one parse, few survive a chain).
+//  k_scan   one workgroup per 16 KiB tile staged in LDS. A two-byte test
+//           drops every offset that cannot start a masked header; the rest
+//           (~2% of random payload bytes) are parsed with ParseFrameHdr's
+//           semantics (w_socket.h:435-524) and point at the next header.
+//           Pointer jumping in LDS resolves every chain to the last header
+//           before the tile end (its "leaf") or to DEAD (an invalid header).
+//           Offsets whose chain survives are "survivors": every true header
+//           is one, few random offsets are.
 //  k_link   survivor graph: a non-leaf points at its leaf; a leaf points at
 //           the survivor at its exit offset in a later tile (binary search),
 //           or at a terminal (END, DEAD = invalid header, INCOMPLETE header).
 //  k_jump   pointer doubling tables J_k = J_{k-1} o J_{k-1} (K-1 launches,
 //           K = ceil(log2(path bound)); the path visits <= 2 nodes per tile).
-//  k_mark   one workgroup expands the root's path top-down through J_k and
-//           records each tile's entry header.
-//  k_walk / k_tile_scan / k_emit
+//  k_entry  one thread per tile: binary lifting through J_k from the root
+//           finds the tile's first true header (offsets increase along the path).
+//  k_walk / k_tile_sums / k_tile_scan / k_emit
 //           per tile: follow the true chain from its entry through the tile's
 //           survivors, then write frames (fws_frame_info) and payload regions
 //           (fws_frame_desc) in stream order.
@@ -36,7 +37,6 @@ constexpr uint32_t kTile = 16384;            // bytes per scan tile
 constexpr uint32_t kHalo = 16;               // header bytes past the tile end
 constexpr uint16_t kDead = 0xFFFF;
 constexpr uint16_t kLeaf = 0x8000;           // kLeaf | offset: chain ends at this header
-constexpr uint32_t kPerThread = kTile / kBlock;
 
 constexpr uint32_t kNone = 0xFFFFFFFFu;           // "no node" (memset 0xFF)
 constexpr uint32_t kTermEnd = 0xFFFFFFFEu;        // chain reaches / passes the stream end
@@ -52,146 +52,351 @@ enum Counter {
     kCntRoot = 4,        // survivor index of the header at offset 0 (kNone if absent)
     kCntTerm = 5,        // terminal code of the path
     kCntLast = 6,        // last path node
+    kCntSpill = 7,       // survivors spilled by dense tiles
     kCntCount = 8
 };
 
-__device__ __forceinline__ int parse_lds(const uint8_t *sbuf, uint32_t p, uint64_t avail, Hdr &h) {
-    return parse_hdr([&](int i) -> uint32_t { return sbuf[p + i]; }, avail, true, h);
+// ------------------------------------------------------------------ k_scan
+// Offsets whose first two bytes cannot start a server-side header (RSV set,
+// reserved opcode, MASK clear: w_socket.h:451-515) are dead on sight; only the
+// rest ("candidates", ~2% of random payload bytes) are parsed in full and
+// pointer-jumped. Candidate k is the k-th set bit of cbits (node index).
+//
+// Each thread owns kScanChunks 16-byte chunks of the tile and keeps a 32-byte
+// register window (its chunk + the next one) from which the candidate test
+// and every header parse read with constant byte indices: after the window
+// load, the tile bytes in LDS are dead and the node table reuses them.
+constexpr int kScanThreads = 512;
+constexpr int kScanChunks = int(kTile / 16u) / kScanThreads;
+constexpr int kScanWords = int(kTile / 64u);          // 64-offset bitmap words (256)
+
+template <int kT>
+__device__ __forceinline__ uint32_t block_excl_scan_u32(uint32_t c, uint32_t *swsum, uint32_t *total) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t inc = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t x = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += x;
+    }
+    if (lane == 63) swsum[w] = inc;
+    __syncthreads();
+    uint32_t off = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < kT / 64; ++i) {
+        off += (i < w) ? swsum[i] : 0u;
+        tot += swsum[i];
+    }
+    __syncthreads();
+    *total = tot;
+    return off + inc - c;
 }
 
-// ------------------------------------------------------------------ k_scan
-__global__ __launch_bounds__(kBlock) void k_scan(const uint8_t *__restrict__ wire, uint64_t N,
-                                                 fws_frame_info *__restrict__ surv_info,
-                                                 uint32_t *__restrict__ surv_leaf,
-                                                 uint32_t *__restrict__ tile_base,
-                                                 uint32_t *__restrict__ tile_count,
-                                                 uint32_t *__restrict__ counters, uint32_t s_cap) {
-    __shared__ __attribute__((aligned(16))) uint8_t sbuf[kTile + kHalo];
-    __shared__ uint16_t sptr[kTile];
-    __shared__ uint64_t sbits[kTile / 64];
-    __shared__ uint32_t spre[kTile / 64];
+// Bit i set <=> offset i of the chunk passes the two-byte header test
+// (RSV clear, opcode in {0,1,2,8,9,10}, MASK set), four offsets per dword:
+// rsv:  (b0 & 0x70) == 0      <=> bit 7 of (b0 & 0x70) + 0x7F is clear
+// op:   (b0 & 7) <= 2         <=> bit 3 of (b0 & 7) + 5 is clear
+// mask: bit 7 of b1 (= byte i+1, v_alignbyte by one)
+__device__ __forceinline__ uint32_t cand_bits16(const u32x4 &lo, uint32_t next_dword) {
+    const uint32_t W[5] = {lo.x, lo.y, lo.z, lo.w, next_dword};
+    uint32_t m = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t x = W[i];
+        const uint32_t b1 = __builtin_amdgcn_alignbyte(W[i + 1], x, 1u);
+        const uint32_t rsv_ok = ~((x & 0x70707070u) + 0x7F7F7F7Fu);
+        const uint32_t op_ok = (~((x & 0x07070707u) + 0x05050505u)) << 4;
+        const uint32_t f = rsv_ok & op_ok & b1 & 0x80808080u;
+        m |= (((f >> 7) & 1u) | ((f >> 14) & 2u) | ((f >> 21) & 4u) | ((f >> 28) & 8u)) << (4 * i);
+    }
+    return m;
+}
+
+// Bytes b..b+15 (b < 16) of the 32-byte window lo:hi as four dwords: shift by
+// 8 bytes, then 4, then v_alignbyte -- selects on named values, no indexing.
+__device__ __forceinline__ void window16(const u32x4 &lo, const u32x4 &hi, uint32_t b, uint32_t out[4]) {
+    const bool s8 = (b & 8u) != 0, s4 = (b & 4u) != 0;
+    const uint32_t a0 = s8 ? lo.z : lo.x, a1 = s8 ? lo.w : lo.y, a2 = s8 ? hi.x : lo.z;
+    const uint32_t a3 = s8 ? hi.y : lo.w, a4 = s8 ? hi.z : hi.x, a5 = s8 ? hi.w : hi.y;
+    const uint32_t c0 = s4 ? a1 : a0, c1 = s4 ? a2 : a1, c2 = s4 ? a3 : a2;
+    const uint32_t c3 = s4 ? a4 : a3, c4 = s4 ? a5 : a4;
+    const uint32_t sh = b & 3u;
+    out[0] = __builtin_amdgcn_alignbyte(c1, c0, sh);
+    out[1] = __builtin_amdgcn_alignbyte(c2, c1, sh);
+    out[2] = __builtin_amdgcn_alignbyte(c3, c2, sh);
+    out[3] = __builtin_amdgcn_alignbyte(c4, c3, sh);
+}
+
+// parse_hdr (server side) on a register window; same codes and order of checks
+// as ParseFrameHdr (w_socket.h:435-524), with the key picked by its length form
+// so no byte index is dynamic (a dynamic index would spill the window).
+__device__ __forceinline__ int parse_window(const u32x4 &lo, const u32x4 &hi, uint32_t b, uint64_t avail, Hdr &h) {
+    uint32_t d[4];
+    window16(lo, hi, b, d);
+    if (avail < 2) return 0;                                       // :443-445
+    const uint32_t b0 = d[0] & 0xFFu, b1 = (d[0] >> 8) & 0xFFu;
+    h.opcode = b0 & 15u;
+    if (!valid_opcode(h.opcode)) return FWS_ERR_OPCODE;            // :451-454
+    h.fin = b0 >> 7;
+    if (b0 & 112u) return FWS_ERR_RSV;                             // :466-470
+    uint64_t plen = b1 & 127u;
+    int n = 2;
+    uint32_t key = __builtin_amdgcn_alignbyte(d[1], d[0], 2u);     // bytes 2..5
+    if (plen == 126u) {                                            // :476-482
+        if (avail < 4) return 0;
+        plen = ((d[0] >> 8) & 0xFF00u) | (d[0] >> 24);
+        n = 4;
+        key = d[1];                                                // bytes 4..7
+    } else if (plen == 127u) {                                     // :483-492
+        if (avail < 10) return 0;
+        const uint32_t hi32 = __builtin_amdgcn_alignbyte(d[1], d[0], 2u);   // bytes 2..5
+        const uint32_t lo32 = __builtin_amdgcn_alignbyte(d[2], d[1], 2u);   // bytes 6..9
+        plen = (uint64_t(__builtin_bswap32(hi32)) << 32) | __builtin_bswap32(lo32);
+        n = 10;
+        key = __builtin_amdgcn_alignbyte(d[3], d[2], 2u);          // bytes 10..13
+    }
+    if (plen > (1ull << 32)) return FWS_ERR_TOO_LARGE;             // :493-498
+    h.plen = plen;
+    if (!(b1 >> 7)) return FWS_ERR_NOT_MASKED;                     // :502-507
+    if (avail < (uint64_t)n + 4u) return 0;                        // :508-511
+    h.key = key;
+    return n + 4;
+}
+
+constexpr uint32_t kSlots = 32;              // per-tile survivor slots before spilling
+
+__global__ __launch_bounds__(kScanThreads) void k_scan(const uint8_t *__restrict__ wire, uint64_t N,
+                                                       fws_frame_info *__restrict__ stage_info,
+                                                       uint32_t *__restrict__ stage_leaf,
+                                                       fws_frame_info *__restrict__ spill_info,
+                                                       uint32_t *__restrict__ spill_leaf,
+                                                       uint32_t *__restrict__ tile_spill,
+                                                       uint32_t *__restrict__ tile_count,
+                                                       uint32_t *__restrict__ counters, uint32_t s_cap) {
+    // tile bytes (phase 1) and node table (phase 2+) share the same LDS
+    __shared__ __attribute__((aligned(16))) union {
+        uint8_t bytes[kTile + kHalo];
+        uint16_t nval[kTile];                // per candidate: next candidate, kLeaf|self, kDead
+    } sm;
+    __shared__ uint64_t cbits[kScanWords];   // candidate offsets
+    __shared__ uint32_t cpre[kScanWords];
+    __shared__ uint64_t sbits[kScanWords];   // surviving candidates (by node index)
+    __shared__ uint32_t spre[kScanWords];
+    __shared__ uint32_t swsum[kScanThreads / 64];
     __shared__ uint32_t sbase, stotal;
 
     const uint32_t t = blockIdx.x;
     const uint64_t t0 = uint64_t(t) * kTile;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    uint8_t *sbuf = sm.bytes;
 
     // stage the tile + halo (wire is 16-B aligned, tiles are 16-B multiples)
-    for (uint32_t i = tid * 16u; i < kTile + kHalo; i += kBlock * 16u) {
-        const uint64_t q = t0 + i;
-        if (q + 16u <= N) {
-            *reinterpret_cast<u32x4 *>(sbuf + i) = *reinterpret_cast<const u32x4 *>(wire + q);
-        } else {
+    const bool interior = t0 + kTile + kHalo <= N;
+    if (interior) {
+        u32x4 v[kScanChunks];
 #pragma unroll
-            for (int b = 0; b < 16; ++b) sbuf[i + b] = (q + b < N) ? wire[q + b] : 0;
-        }
-    }
-    __syncthreads();
-
-    // parse every offset: next-header pointer, leaf, or dead
-    for (uint32_t k = 0; k < kPerThread; ++k) {
-        const uint32_t p = uint32_t(tid) + k * kBlock;
-        const uint64_t q = t0 + p;
-        uint16_t v = kDead;
-        if (q < N) {
-            Hdr h;
-            const int r = parse_lds(sbuf, p, N - q, h);
-            if (r == 0) {
-                v = kLeaf | p;                       // incomplete header at the stream end
-            } else if (r > 0) {
-                const uint64_t nx = q + (uint64_t)r + h.plen;
-                v = (nx < t0 + kTile) ? (uint16_t)(nx - t0) : (uint16_t)(kLeaf | p);
+        for (int j = 0; j < kScanChunks; ++j)
+            v[j] = gload16(reinterpret_cast<uintptr_t>(wire + t0 + (uint64_t)(j * kScanThreads + tid) * 16u));
+        u32x4 hv;
+        if (tid == 0) hv = gload16(reinterpret_cast<uintptr_t>(wire + t0 + kTile));
+#pragma unroll
+        for (int j = 0; j < kScanChunks; ++j)
+            *reinterpret_cast<u32x4 *>(sbuf + (j * kScanThreads + tid) * 16) = v[j];
+        if (tid == 0) *reinterpret_cast<u32x4 *>(sbuf + kTile) = hv;
+    } else {
+        for (uint32_t i = tid * 16u; i < kTile + kHalo; i += kScanThreads * 16u) {
+            const uint64_t q = t0 + i;
+            if (q + 16u <= N) {
+                *reinterpret_cast<u32x4 *>(sbuf + i) = gload16(reinterpret_cast<uintptr_t>(wire + q));
+            } else {
+#pragma unroll
+                for (int b = 0; b < 16; ++b) sbuf[i + b] = (q + b < N) ? wire[q + b] : 0;
             }
         }
-        sptr[p] = v;
+    }
+    if (tid < kScanWords) sbits[tid] = 0;
+    __syncthreads();
+
+    // register windows + candidate bitmap (16 bits per chunk)
+    u32x4 lo[kScanChunks], hi[kScanChunks];
+    uint32_t cm[kScanChunks];
+#pragma unroll
+    for (int j = 0; j < kScanChunks; ++j) {
+        const uint32_t c = uint32_t(j * kScanThreads + tid);
+        lo[j] = *reinterpret_cast<const u32x4 *>(sbuf + c * 16u);
+        hi[j] = *reinterpret_cast<const u32x4 *>(sbuf + c * 16u + 16u);
+        uint32_t m = cand_bits16(lo[j], hi[j].x);
+        if (!interior) {
+            // offsets at or past the end: zero bytes never pass; the last byte
+            // is a candidate on its own (an incomplete header, w_socket.h:443-445)
+            const uint64_t q = t0 + uint64_t(c) * 16u;
+            if (q >= N) m = 0;
+            else if (N - q <= 16u) m = (m & ((1u << (N - q)) - 1u)) | (1u << (N - q - 1u));
+        }
+        cm[j] = m;
+        reinterpret_cast<uint16_t *>(cbits)[c] = (uint16_t)m;
+    }
+    __syncthreads();
+    uint32_t nc;
+    {
+        const uint32_t pc = tid < kScanWords ? (uint32_t)__popcll(cbits[tid]) : 0u;
+        const uint32_t e = block_excl_scan_u32<kScanThreads>(pc, swsum, &nc);
+        if (tid < kScanWords) cpre[tid] = e;
+    }
+    __syncthreads();
+    auto crank = [&](uint32_t p) -> uint32_t {
+        return cpre[p >> 6] + (uint32_t)__popcll(cbits[p >> 6] & ((1ull << (p & 63u)) - 1ull));
+    };
+    auto chunk_rank = [&](uint32_t c) -> uint32_t {     // node index of the chunk's first candidate
+        return cpre[c >> 2] + (uint32_t)__popcll(cbits[c >> 2] & ((1ull << ((c & 3u) * 16u)) - 1ull));
+    };
+
+    // parse candidates from the register windows (LDS bytes are dead from here)
+    uint32_t kfirst[kScanChunks];
+#pragma unroll
+    for (int j = 0; j < kScanChunks; ++j) {
+        const uint32_t c = uint32_t(j * kScanThreads + tid);
+        uint32_t bits = cm[j];
+        uint32_t k = chunk_rank(c);
+        kfirst[j] = k;
+        while (bits) {
+            const uint32_t b = (uint32_t)__ffs(bits) - 1u;
+            bits &= bits - 1u;
+            const uint32_t p = c * 16u + b;
+            const uint64_t q = t0 + p;
+            Hdr h;
+            const int r = parse_window(lo[j], hi[j], b, N - q, h);
+            uint16_t v = kDead;
+            if (r == 0) {
+                v = (uint16_t)(kLeaf | k);                // incomplete header at the stream end
+            } else if (r > 0) {
+                const uint64_t nx = q + (uint64_t)r + h.plen;
+                if (nx < t0 + kTile) {
+                    const uint32_t pn = (uint32_t)(nx - t0);
+                    v = ((cbits[pn >> 6] >> (pn & 63u)) & 1ull) ? (uint16_t)crank(pn) : kDead;
+                } else {
+                    v = (uint16_t)(kLeaf | k);
+                }
+            }
+            sm.nval[k] = v;
+            ++k;
+        }
     }
     __syncthreads();
 
-    // pointer jumping: every live offset ends at its leaf or dies
+    // pointer jumping over candidate nodes: every chain ends at its leaf or dies
     for (;;) {
         int changed = 0;
-        for (uint32_t k = 0; k < kPerThread; ++k) {
-            const uint32_t p = uint32_t(tid) + k * kBlock;
-            const uint16_t v = sptr[p];
+        for (uint32_t k = tid; k < nc; k += kScanThreads) {
+            const uint16_t v = sm.nval[k];
             if (v < kTile) {
-                sptr[p] = sptr[v];
+                sm.nval[k] = sm.nval[v];
                 changed = 1;
             }
         }
         if (!__syncthreads_or(changed)) break;
     }
 
-    // survivor bitmap (wave ballots over 64 consecutive offsets) and ranks
-    for (uint32_t k = 0; k < kPerThread; ++k) {
-        const uint32_t p = uint32_t(w) * 64u + uint32_t(lane) + k * kBlock;
-        const uint64_t m = __ballot(sptr[p] != kDead);
-        if (lane == 0) sbits[p >> 6] = m;
+    // survivors by node index
+    for (uint32_t k0 = uint32_t(w) * 64u; k0 < nc; k0 += kScanThreads) {
+        const uint32_t k = k0 + uint32_t(lane);
+        const uint64_t m = __ballot(k < nc && sm.nval[k] != kDead);
+        if (lane == 0) sbits[k0 >> 6] = m;
     }
     __syncthreads();
+    uint32_t ns;
     {
-        const uint32_t c = __popcll(sbits[tid]);
-        uint32_t inc = c;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t x = __shfl_up(inc, o, 64);
-            if (lane >= o) inc += x;
+        const uint32_t pc = tid < kScanWords ? (uint32_t)__popcll(sbits[tid]) : 0u;
+        const uint32_t e = block_excl_scan_u32<kScanThreads>(pc, swsum, &ns);
+        if (tid < kScanWords) spre[tid] = e;
+    }
+    // survivors go to the tile's fixed slots (no shared counter); a tile with
+    // more than kSlots of them (dense small frames) spills to a shared area
+    if (tid == 0) {
+        uint32_t spill = kNone;
+        if (ns > kSlots) {
+            spill = atomicAdd(&counters[kCntSpill], ns);
+            if (spill + ns > s_cap) { atomicOr(&counters[kCntOverflow], 1u); ns = 0; spill = kNone; }
         }
-        __shared__ uint32_t swsum[kBlock / 64];
-        if (lane == 63) swsum[w] = inc;
-        __syncthreads();
-        uint32_t off = 0, tot = 0;
-        for (int i = 0; i < kBlock / 64; ++i) {
-            off += (i < w) ? swsum[i] : 0u;
-            tot += swsum[i];
-        }
-        spre[tid] = off + inc - c;
-        if (tid == 0) {
-            uint32_t base = tot ? atomicAdd(&counters[kCntSurv], tot) : 0u;
-            if (tot && base + tot > s_cap) {
-                atomicOr(&counters[kCntOverflow], 1u);
-                tot = 0;
-            }
-            sbase = base;
-            stotal = tot;
-            tile_base[t] = base;
-            tile_count[t] = tot;
-        }
+        sbase = spill;
+        stotal = ns;
+        tile_count[t] = ns;
+        tile_spill[t] = spill;
     }
     __syncthreads();
     if (stotal == 0) return;
-    const uint32_t base = sbase;
-
-    auto rank_of = [&](uint32_t p) -> uint32_t {
-        const uint64_t m = sbits[p >> 6] & ((1ull << (p & 63u)) - 1ull);
-        return spre[p >> 6] + (uint32_t)__popcll(m);
+    fws_frame_info *out_info = sbase == kNone ? stage_info + (uint64_t)t * kSlots : spill_info + sbase;
+    uint32_t *out_leaf = sbase == kNone ? stage_leaf + (uint64_t)t * kSlots : spill_leaf + sbase;
+    auto srank = [&](uint32_t k) -> uint32_t {
+        return spre[k >> 6] + (uint32_t)__popcll(sbits[k >> 6] & ((1ull << (k & 63u)) - 1ull));
     };
-    for (uint32_t k = 0; k < kPerThread; ++k) {
-        const uint32_t p = uint32_t(tid) + k * kBlock;
-        const uint16_t v = sptr[p];
-        if (v == kDead) continue;
-        const uint64_t q = t0 + p;
-        const uint32_t idx = base + rank_of(p);
-        Hdr h;
-        const int r = parse_lds(sbuf, p, N - q, h);
-        fws_frame_info fi;
-        fi.hdr_off = q;
-        if (r > 0) {
-            fi.payload_len = h.plen;
-            fi.key = h.key;
-            fi.opcode = (uint8_t)h.opcode;
-            fi.fin = (uint8_t)h.fin;
-            fi.hdr_len = (uint8_t)r;
-            fi.flags = (q + (uint64_t)r + h.plen > N) ? (uint8_t)FWS_FRAME_TRUNCATED : (uint8_t)0;
-        } else {                                     // incomplete trailing header
-            fi.payload_len = 0;
-            fi.key = 0;
-            fi.opcode = 0;
-            fi.fin = 0;
-            fi.hdr_len = 0;
-            fi.flags = 0;
+
+    // write survivors in offset order
+#pragma unroll
+    for (int j = 0; j < kScanChunks; ++j) {
+        const uint32_t c = uint32_t(j * kScanThreads + tid);
+        uint32_t bits = cm[j];
+        uint32_t k = kfirst[j];
+        while (bits) {
+            const uint32_t b = (uint32_t)__ffs(bits) - 1u;
+            bits &= bits - 1u;
+            const uint16_t v = sm.nval[k];
+            if (v != kDead) {
+                const uint64_t q = t0 + c * 16u + b;
+                Hdr h;
+                const int r = parse_window(lo[j], hi[j], b, N - q, h);
+                fws_frame_info fi;
+                fi.hdr_off = q;
+                if (r > 0) {
+                    fi.payload_len = h.plen;
+                    fi.key = h.key;
+                    fi.opcode = (uint8_t)h.opcode;
+                    fi.fin = (uint8_t)h.fin;
+                    fi.hdr_len = (uint8_t)r;
+                    fi.flags = (q + (uint64_t)r + h.plen > N) ? (uint8_t)FWS_FRAME_TRUNCATED : (uint8_t)0;
+                } else {                                 // incomplete trailing header
+                    fi.payload_len = 0;
+                    fi.key = 0;
+                    fi.opcode = 0;
+                    fi.fin = 0;
+                    fi.hdr_len = 0;
+                    fi.flags = 0;
+                }
+                const uint32_t idx = srank(k);
+                out_info[idx] = fi;
+                out_leaf[idx] = srank(v & 0x7FFFu);            // tile-local rank of the leaf
+            }
+            ++k;
         }
-        surv_info[idx] = fi;
-        surv_leaf[idx] = base + rank_of(v & 0x7FFFu);
+    }
+}
+
+// ------------------------------------------------------------------ k_compact
+// One wave per tile: survivors from the tile's slots (or its spill range) to
+// the dense, offset-sorted arrays at tile_base[t]; leaf ranks become indices.
+__global__ __launch_bounds__(kBlock) void k_compact(const fws_frame_info *__restrict__ stage_info,
+                                                    const uint32_t *__restrict__ stage_leaf,
+                                                    const fws_frame_info *__restrict__ spill_info,
+                                                    const uint32_t *__restrict__ spill_leaf,
+                                                    const uint32_t *__restrict__ tile_spill,
+                                                    const uint32_t *__restrict__ tile_count,
+                                                    const uint32_t *__restrict__ tile_base, uint32_t n_tiles,
+                                                    fws_frame_info *__restrict__ surv_info,
+                                                    uint32_t *__restrict__ surv_leaf, uint32_t *__restrict__ counters,
+                                                    uint32_t s_cap) {
+    const uint32_t t = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (t >= n_tiles) return;
+    const uint32_t n = tile_count[t], b = tile_base[t], sp = tile_spill[t];
+    if (b + n > s_cap) {
+        if (lane == 0) atomicOr(&counters[kCntOverflow], 1u);
+        return;
+    }
+    const fws_frame_info *si = sp == kNone ? stage_info + (uint64_t)t * kSlots : spill_info + sp;
+    const uint32_t *sl = sp == kNone ? stage_leaf + (uint64_t)t * kSlots : spill_leaf + sp;
+    for (uint32_t r = lane; r < n; r += 64) {
+        surv_info[b + r] = si[r];
+        surv_leaf[b + r] = b + sl[r];
     }
 }
 
@@ -248,50 +453,42 @@ __global__ __launch_bounds__(kBlock) void k_jump(const uint32_t *__restrict__ Jp
     }
 }
 
-// ------------------------------------------------------------------ k_mark
-// One workgroup: path = {J^j(root)} expanded top-down; tile_entry[t] = the
-// first header of tile t on the true chain.
-constexpr int kMarkBlock = 1024;
-
-__global__ __launch_bounds__(kMarkBlock) void k_mark(const uint32_t *__restrict__ J, uint64_t s_cap, int K,
-                                                     const fws_frame_info *__restrict__ info,
-                                                     const uint32_t *__restrict__ leaf,
-                                                     uint32_t *__restrict__ path,
-                                                     uint32_t *__restrict__ tile_entry,
-                                                     uint32_t *__restrict__ counters,
-                                                     const uint32_t *__restrict__ root_p) {
-    __shared__ uint32_t sn;
+// ------------------------------------------------------------------ k_entry
+// One thread per tile, binary lifting over the doubling tables: the last path
+// node before the tile (headers strictly increase along the path), then its
+// successor is the tile's first true header if that lies inside the tile.
+// Thread n_tiles finds the path's last node and terminal.
+__global__ __launch_bounds__(kBlock) void k_entry(const uint32_t *__restrict__ J, uint64_t s_cap, int K,
+                                                  const fws_frame_info *__restrict__ info,
+                                                  const uint32_t *__restrict__ root_p, uint32_t n_tiles,
+                                                  uint32_t *__restrict__ tile_entry,
+                                                  uint32_t *__restrict__ counters) {
+    const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+    if (t > n_tiles) return;
     const uint32_t root = *root_p;
-    const bool ok = !counters[kCntOverflow] && root != kNone;
-    if (threadIdx.x == 0) {
-        sn = 0;
-        if (ok) { path[0] = root; sn = 1; }
-    }
-    __syncthreads();
-    if (!ok) {
-        if (threadIdx.x == 0) { counters[kCntPath] = 0; counters[kCntTerm] = kTermDead; counters[kCntLast] = kNone; }
+    if (counters[kCntOverflow] || root == kNone) {
+        if (t == n_tiles) { counters[kCntTerm] = kTermDead; counters[kCntLast] = kNone; }
         return;
     }
-    for (int k = K - 1; k >= 0; --k) {
-        const uint32_t m = sn;
-        __syncthreads();
-        const uint32_t *Jk = J + (uint64_t)k * s_cap;
-        for (uint32_t i = threadIdx.x; i < m; i += kMarkBlock) {
-            const uint32_t y = Jk[path[i]];
-            if (!is_term(y)) path[atomicAdd(&sn, 1u)] = y;
+    if (t == n_tiles) {
+        uint32_t cur = root;
+        for (int k = K - 1; k >= 0; --k) {
+            const uint32_t y = J[(uint64_t)k * s_cap + cur];
+            if (!is_term(y)) cur = y;
         }
-        __threadfence_block();
-        __syncthreads();
+        counters[kCntLast] = cur;
+        counters[kCntTerm] = J[cur];
+        return;
     }
-    const uint32_t n = sn;
-    for (uint32_t i = threadIdx.x; i < n; i += kMarkBlock) {
-        const uint32_t s = path[i];
-        const uint32_t y = J[s];                        // J_0
-        if (i == 0) tile_entry[info[s].hdr_off / kTile] = s;        // root
-        if (leaf[s] == s && !is_term(y)) tile_entry[info[y].hdr_off / kTile] = y;
-        if (is_term(y)) { counters[kCntTerm] = y; counters[kCntLast] = s; }
+    if (t == 0) { tile_entry[0] = root; return; }
+    const uint64_t T0 = (uint64_t)t * kTile;
+    uint32_t cur = root;                                  // hdr_off 0 < T0
+    for (int k = K - 1; k >= 0; --k) {
+        const uint32_t y = J[(uint64_t)k * s_cap + cur];
+        if (!is_term(y) && info[y].hdr_off < T0) cur = y;
     }
-    if (threadIdx.x == 0) counters[kCntPath] = n;
+    const uint32_t y = J[cur];
+    if (!is_term(y) && info[y].hdr_off < T0 + kTile) tile_entry[t] = y;
 }
 
 // ------------------------------------------------------------------ k_walk
@@ -322,38 +519,43 @@ __global__ __launch_bounds__(kBlock) void k_walk(const fws_frame_info *__restric
     tile_frames[t] = cnt;
 }
 
-// Single-workgroup exclusive scan of per-tile frame counts (tiles <= 2^20).
-__global__ __launch_bounds__(kMarkBlock) void k_tile_scan(const uint32_t *__restrict__ tile_frames,
-                                                          uint32_t n_tiles, uint32_t *__restrict__ fbase,
-                                                          uint32_t *__restrict__ counters) {
-    __shared__ uint32_t swsum[kMarkBlock / 64];
-    __shared__ uint32_t scarry;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    if (tid == 0) scarry = 0;
-    __syncthreads();
-    for (uint32_t b = 0; b < n_tiles; b += kMarkBlock) {
-        const uint32_t t = b + tid;
-        const uint32_t c = t < n_tiles ? tile_frames[t] : 0u;
-        uint32_t inc = c;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t x = __shfl_up(inc, o, 64);
-            if (lane >= o) inc += x;
-        }
-        if (lane == 63) swsum[w] = inc;
-        __syncthreads();
-        uint32_t off = 0, tot = 0;
-        for (int i = 0; i < kMarkBlock / 64; ++i) {
-            off += (i < w) ? swsum[i] : 0u;
-            tot += swsum[i];
-        }
-        const uint32_t carry = scarry;
-        if (t < n_tiles) fbase[t] = carry + off + inc - c;
-        __syncthreads();
-        if (tid == 0) scarry = carry + tot;
-        __syncthreads();
+// Exclusive scan of per-tile frame counts: per-1024-tile block sums, then
+// each block adds the sums of the blocks before it (few: tiles / 1024).
+__global__ __launch_bounds__(kBlock) void k_tile_sums(const uint32_t *__restrict__ tile_frames, uint32_t n_tiles,
+                                                      uint32_t *__restrict__ block_sums) {
+    __shared__ uint32_t swsum[kBlock / 64];
+    uint32_t c = 0;
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t t = blockIdx.x * 1024u + threadIdx.x * 4u + i;
+        if (t < n_tiles) c += tile_frames[t];
     }
-    if (tid == 0) counters[kCntFrames] = scarry;
+    uint32_t tot;
+    block_excl_scan_u32<kBlock>(c, swsum, &tot);
+    if (threadIdx.x == 0) block_sums[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(kBlock) void k_tile_scan(const uint32_t *__restrict__ tile_frames, uint32_t n_tiles,
+                                                      const uint32_t *__restrict__ block_sums,
+                                                      uint32_t *__restrict__ fbase, uint32_t *__restrict__ total_out) {
+    __shared__ uint32_t swsum[kBlock / 64];
+    uint32_t pre = 0, dummy;
+    for (uint32_t b = threadIdx.x; b < blockIdx.x; b += kBlock) pre += block_sums[b];
+    const uint32_t pe = block_excl_scan_u32<kBlock>(pre, swsum, &dummy);
+    __shared__ uint32_t sprefix;
+    if (threadIdx.x == kBlock - 1) sprefix = pe + pre;
+    __syncthreads();
+    const uint32_t t0 = blockIdx.x * 1024u + threadIdx.x * 4u;
+    uint32_t c[4], sum = 0;
+    for (int i = 0; i < 4; ++i) { c[i] = (t0 + i < n_tiles) ? tile_frames[t0 + i] : 0u; sum += c[i]; }
+    uint32_t tot;
+    uint32_t run = sprefix + block_excl_scan_u32<kBlock>(sum, swsum, &tot);
+    for (int i = 0; i < 4; ++i) {
+        if (t0 + i < n_tiles) {
+            fbase[t0 + i] = run;
+            run += c[i];
+            if (t0 + i == n_tiles - 1) *total_out = run;
+        }
+    }
 }
 
 // One wave per tile: write the tile's flagged frames in order.
@@ -478,7 +680,7 @@ int fws_decode_ensure(fws_gpu_ctx *ctx, uint64_t N, uint32_t cap) {
     auto rel = [](auto *&p) { if (p) (void)hipFree(p); p = nullptr; };
     rel(d.tile_count); rel(d.tile_base); rel(d.tile_entry); rel(d.tile_frames); rel(d.fbase);
     rel(d.surv_info); rel(d.surv_leaf); rel(d.jump); rel(d.on_path); rel(d.path); rel(d.counters);
-    rel(d.descs);
+    rel(d.descs); rel(d.stage_info); rel(d.stage_leaf); rel(d.spill_info); rel(d.spill_leaf); rel(d.tile_spill);
     hipError_t e = hipSuccess;
     auto al = [&](auto **p, uint64_t bytes) { if (e == hipSuccess) e = hipMalloc((void **)p, bytes ? bytes : 16); };
     al(&d.tile_count, nt * 4); al(&d.tile_base, nt * 4); al(&d.tile_entry, nt * 4);
@@ -487,6 +689,8 @@ int fws_decode_ensure(fws_gpu_ctx *ctx, uint64_t N, uint32_t cap) {
     al(&d.jump, (uint64_t)nl * ns * 4); al(&d.on_path, ns); al(&d.path, (2 * nt + 8) * 4);
     al(&d.counters, kCntCount * 4 + 16);
     al(&d.descs, (nd + 1) * sizeof(fws_frame_desc));
+    al(&d.stage_info, nt * kSlots * sizeof(fws_frame_info)); al(&d.stage_leaf, nt * kSlots * 4);
+    al(&d.spill_info, ns * sizeof(fws_frame_info)); al(&d.spill_leaf, ns * 4); al(&d.tile_spill, nt * 4);
     if (e != hipSuccess) return fws_hip_status(e);
     d.max_tiles = nt; d.max_surv = ns; d.levels = nl; d.max_descs = nd;
     return 0;
@@ -503,22 +707,31 @@ int fws_launch_decode(fws_gpu_ctx *ctx, uint8_t *wire, uint64_t N, fws_frame_inf
     if ((e = hipMemsetAsync(d.counters + kCntRoot, 0xFF, 4, s)) != hipSuccess) return fws_hip_status(e);
     if (n_tiles) {
         if ((e = hipMemsetAsync(d.tile_entry, 0xFF, (size_t)n_tiles * 4, s)) != hipSuccess) return fws_hip_status(e);
-        hipLaunchKernelGGL(k_scan, dim3(n_tiles), dim3(kBlock), 0, s, wire, N, d.surv_info, d.surv_leaf,
-                           d.tile_base, d.tile_count, d.counters, (uint32_t)d.max_surv);
+        const uint32_t tb = (n_tiles + 1023) / 1024;
+        hipLaunchKernelGGL(k_scan, dim3(n_tiles), dim3(kScanThreads), 0, s, wire, N, d.stage_info, d.stage_leaf,
+                           d.spill_info, d.spill_leaf, d.tile_spill, d.tile_count, d.counters,
+                           (uint32_t)d.max_surv);
+        hipLaunchKernelGGL(k_tile_sums, dim3(tb), dim3(kBlock), 0, s, d.tile_count, n_tiles, d.path);
+        hipLaunchKernelGGL(k_tile_scan, dim3(tb), dim3(kBlock), 0, s, d.tile_count, n_tiles, d.path, d.tile_base,
+                           d.counters + kCntSurv);
+        hipLaunchKernelGGL(k_compact, dim3((n_tiles + 3) / 4), dim3(kBlock), 0, s, d.stage_info, d.stage_leaf,
+                           d.spill_info, d.spill_leaf, d.tile_spill, d.tile_count, d.tile_base, n_tiles,
+                           d.surv_info, d.surv_leaf, d.counters, (uint32_t)d.max_surv);
         const int gl = 1024;
         hipLaunchKernelGGL(k_link, dim3(gl), dim3(kBlock), 0, s, d.surv_info, d.surv_leaf, d.tile_base,
                            d.tile_count, d.counters, N, d.jump, d.counters + kCntRoot);
         for (uint32_t k = 1; k < K; ++k)
             hipLaunchKernelGGL(k_jump, dim3(gl), dim3(kBlock), 0, s, d.jump + (uint64_t)(k - 1) * d.max_surv,
                                d.jump + (uint64_t)k * d.max_surv, d.counters);
-        hipLaunchKernelGGL(k_mark, dim3(1), dim3(kMarkBlock), 0, s, d.jump, d.max_surv, (int)K, d.surv_info,
-                           d.surv_leaf, d.path, d.tile_entry, d.counters, d.counters + kCntRoot);
+        hipLaunchKernelGGL(k_entry, dim3(n_tiles / kBlock + 1), dim3(kBlock), 0, s, d.jump, d.max_surv, (int)K,
+                           d.surv_info, d.counters + kCntRoot, n_tiles, d.tile_entry, d.counters);
         if ((e = hipMemsetAsync(d.on_path, 0, d.max_surv, s)) != hipSuccess) return fws_hip_status(e);
         hipLaunchKernelGGL(k_walk, dim3((n_tiles + kBlock - 1) / kBlock), dim3(kBlock), 0, s, d.surv_info,
                            d.surv_leaf, d.tile_base, d.tile_count, d.tile_entry, n_tiles, d.on_path,
                            d.tile_frames);
-        hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(kMarkBlock), 0, s, d.tile_frames, n_tiles, d.fbase,
-                           d.counters);
+        hipLaunchKernelGGL(k_tile_sums, dim3(tb), dim3(kBlock), 0, s, d.tile_frames, n_tiles, d.path);
+        hipLaunchKernelGGL(k_tile_scan, dim3(tb), dim3(kBlock), 0, s, d.tile_frames, n_tiles, d.path, d.fbase,
+                           d.counters + kCntFrames);
         hipLaunchKernelGGL(k_emit, dim3((n_tiles + 3) / 4), dim3(kBlock), 0, s, d.surv_info, d.tile_base,
                            d.tile_count, d.on_path, d.fbase, n_tiles, N, frames, cap, d.descs,
                            (uint32_t)d.max_descs);

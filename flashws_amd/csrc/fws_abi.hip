@@ -91,6 +91,11 @@ void fws_gpu_ctx_destroy(fws_gpu_ctx *ctx) {
     dev_free(d.path);
     dev_free(d.counters);
     dev_free(d.descs);
+    dev_free(d.stage_info);
+    dev_free(d.stage_leaf);
+    dev_free(d.spill_info);
+    dev_free(d.spill_leaf);
+    dev_free(d.tile_spill);
     delete ctx;
 }
 

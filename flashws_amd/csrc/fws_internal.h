@@ -38,6 +38,11 @@ struct fws_decode_ws {
     uint32_t *path = nullptr;         // path nodes (k_mark)
     uint32_t *counters = nullptr;     // see decode_kernels.hip Counter
     fws_frame_desc *descs = nullptr;  // payload regions of the decoded frames
+    fws_frame_info *stage_info = nullptr;  // per-tile survivor slots (k_scan)
+    uint32_t *stage_leaf = nullptr;
+    fws_frame_info *spill_info = nullptr;  // survivors of dense tiles
+    uint32_t *spill_leaf = nullptr;
+    uint32_t *tile_spill = nullptr;        // spill offset of a dense tile, or ~0
 };
 
 struct fws_gpu_ctx {

@@ -29,6 +29,7 @@ FWS_ERR_OPCODE = -9
 FWS_ERR_CAPACITY = -20
 FWS_ERR_INVALID = -21
 FWS_ERR_NO_DEVICE = -22
+FWS_ERR_INTERNAL = -23
 FWS_ERR_HIP_BASE = -1000
 
 # include/fws_gpu.h structs as numpy dtypes (device arrays are torch uint8 views)

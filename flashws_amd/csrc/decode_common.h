@@ -1,0 +1,66 @@
+// decode_common.h -- constants and node encodings shared by the stream-decode
+// kernels: k_scan (decode_kernels.hip) and k_resolve (resolve_kernels.hip).
+#pragma once
+
+#include "fws_device.h"
+#include "fws_internal.h"
+
+namespace fwsk {
+
+constexpr uint32_t kTile = 2048;             // bytes per scan tile (one wavefront)
+constexpr uint32_t kHalo = 16;               // header bytes past the tile end
+constexpr uint16_t kDead = 0xFFFF;
+constexpr uint16_t kLeaf = 0x8000;           // kLeaf | offset: chain ends at this header
+
+constexpr uint32_t kNone = 0xFFFFFFFFu;           // "no node" (memset 0xFF)
+constexpr uint32_t kTermEnd = 0xFFFFFFFEu;        // chain reaches / passes the stream end
+constexpr uint32_t kTermDead = 0xFFFFFFFDu;       // next header offset is not a survivor
+constexpr uint32_t kTermIncomplete = 0xFFFFFFFCu; // incomplete header at the stream end
+__device__ __forceinline__ bool is_term(uint32_t v) { return v >= kTermIncomplete; }
+
+// dec.counters[] (zeroed before every decode)
+enum Counter {
+    kCntSurv = 0,        // survivors (sum of the tiles' counts)
+    kCntOverflow = 1,    // bit 0: survivor capacity exceeded; bit 1: grid barrier timed out
+    kCntBarArrive = 2,   // k_resolve grid barrier: arrivals (monotonic within a launch)
+    kCntFrames = 3,      // frames emitted (device frame count, read by the unmask)
+    kCntRoot = 4,        // survivor index of the header at offset 0 (kNone if absent)
+    kCntTerm = 5,        // terminal code of the path
+    kCntLast = 6,        // last path node
+    kCntSpill = 7,       // survivors spilled by dense tiles
+    kCntBarGen = 8,      // k_resolve grid barrier: generation
+    kCntCount = 9
+};
+static_assert(kCntFrames == kDecodeFramesCounter, "fws_internal.h names the frame counter");
+
+constexpr uint32_t kSlots = 8;               // per-tile survivor slots before spilling
+
+__device__ __forceinline__ uint64_t exit_of(const fws_frame_info &fi) {
+    return fi.hdr_off + fi.hdr_len + fi.payload_len;
+}
+
+
+// Exclusive scan over a kT-thread workgroup; *total = the workgroup sum.
+template <int kT>
+__device__ __forceinline__ uint32_t block_excl_scan_u32(uint32_t c, uint32_t *swsum, uint32_t *total) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t inc = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t x = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += x;
+    }
+    if (lane == 63) swsum[w] = inc;
+    __syncthreads();
+    uint32_t off = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < kT / 64; ++i) {
+        off += (i < w) ? swsum[i] : 0u;
+        tot += swsum[i];
+    }
+    __syncthreads();
+    *total = tot;
+    return off + inc - c;
+}
+
+}  // namespace fwsk

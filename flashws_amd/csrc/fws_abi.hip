@@ -88,7 +88,6 @@ void fws_gpu_ctx_destroy(fws_gpu_ctx *ctx) {
     dev_free(d.surv_leaf);
     dev_free(d.jump);
     dev_free(d.on_path);
-    dev_free(d.path);
     dev_free(d.counters);
     dev_free(d.descs);
     dev_free(d.stage_info);
@@ -96,6 +95,8 @@ void fws_gpu_ctx_destroy(fws_gpu_ctx *ctx) {
     dev_free(d.spill_info);
     dev_free(d.spill_leaf);
     dev_free(d.tile_spill);
+    dev_free(d.scan_dummy);
+    dev_free(d.rbsums);
     delete ctx;
 }
 
@@ -168,8 +169,8 @@ int fws_gpu_decode_stream(fws_gpu_ctx *ctx, void *dev_wire, uint64_t len, fws_fr
     if ((r = fws_ctx_ensure_plan(ctx, cap, units))) return r;
     if ((r = fws_launch_decode(ctx, (uint8_t *)dev_wire, len, dev_frames, cap, dev_result, s))) return r;
     if (cap == 0 || len == 0) return 0;
+    // k_resolve left the device frame count and the unmask plan of the decoded frames
     const uint32_t *n_dev = ctx->dec.counters + kDecodeFramesCounter;
-    if ((r = fws_launch_plan((const uint8_t *)dev_wire, ctx->dec.descs, cap, n_dev, ctx->plan, s))) return r;
     if ((r = fws_launch_unmask((uint8_t *)dev_wire, ctx->dec.descs, cap, n_dev, ctx->plan,
                                len / 16 + 2ull * cap, s)))
         return r;

@@ -35,7 +35,6 @@ struct fws_decode_ws {
     uint32_t *surv_leaf = nullptr;    // leaf (last in-tile header) of each survivor's chain
     uint32_t *jump = nullptr;         // [levels][max_surv] pointer-doubling tables
     uint8_t *on_path = nullptr;       // survivor is a true frame header
-    uint32_t *path = nullptr;         // path nodes (k_mark)
     uint32_t *counters = nullptr;     // see decode_kernels.hip Counter
     fws_frame_desc *descs = nullptr;  // payload regions of the decoded frames
     fws_frame_info *stage_info = nullptr;  // per-tile survivor slots (k_scan)
@@ -43,6 +42,10 @@ struct fws_decode_ws {
     fws_frame_info *spill_info = nullptr;  // survivors of dense tiles
     uint32_t *spill_leaf = nullptr;
     uint32_t *tile_spill = nullptr;        // spill offset of a dense tile, or ~0
+    uint32_t scan_grid = 0;                // persistent k_scan workgroups
+    uint32_t *scan_dummy = nullptr;        // one 64-B line per k_scan wavefront (idle-lane stores)
+    uint32_t resolve_grid = 0;             // cooperative k_resolve workgroups (one per CU)
+    uint64_t *rbsums = nullptr;            // k_resolve per-workgroup partial sums
 };
 
 struct fws_gpu_ctx {
@@ -78,3 +81,6 @@ constexpr int kDecodeFramesCounter = 3;   // index of the device frame count in 
 int fws_decode_ensure(fws_gpu_ctx *ctx, uint64_t N, uint32_t cap);
 int fws_launch_decode(fws_gpu_ctx *ctx, uint8_t *wire, uint64_t N, fws_frame_info *frames, uint32_t cap,
                       fws_decode_result *res, hipStream_t s);
+// resolve_kernels.hip: frames, descriptors and the unmask plan from k_scan's survivors
+int fws_launch_resolve(fws_gpu_ctx *ctx, const uint8_t *wire, uint64_t N, uint32_t n_tiles, uint32_t K,
+                       fws_frame_info *frames, uint32_t cap, fws_decode_result *res, hipStream_t s);

@@ -43,6 +43,7 @@ enum {
     FWS_ERR_CAPACITY = -20,     /* an output array is too small (count still reported) */
     FWS_ERR_INVALID = -21,      /* bad argument / not initialised */
     FWS_ERR_NO_DEVICE = -22,    /* no gfx950 device visible */
+    FWS_ERR_INTERNAL = -23,     /* device-side failure (decode grid barrier timed out) */
     FWS_ERR_HIP_BASE = -1000    /* -1000 - hipError_t */
 };
 

@@ -114,7 +114,7 @@ def test_len_2p32_header_only(ctx, cuda):
 
 @pytest.mark.parametrize("seed", range(8))
 def test_random_small_frames(ctx, cuda, seed):
-    """Dense frames (0..300 B) so every 16 KiB tile holds many true headers."""
+    """Dense frames (0..300 B) so every scan tile holds many true headers."""
     rng = np.random.default_rng(100 + seed)
     out = []
     total = 0
@@ -127,9 +127,9 @@ def test_random_small_frames(ctx, cuda, seed):
     check(ctx, cuda, b"".join(out))
 
 
-@pytest.mark.parametrize("size", [1, 15, 16, 16383, 16384, 16385, 16390, 32768 + 7])
+@pytest.mark.parametrize("size", [1, 15, 16, 2030, 2047, 2048, 2049, 4103, 16383, 16384, 16385, 16390, 32768 + 7])
 def test_single_frame_tile_boundaries(ctx, cuda, size):
-    for lead in (0, 1, 7, 16370):
+    for lead in (0, 1, 7, 2030, 2041, 16370):
         wire = frame(2, b"a" * lead) + frame(1, bytes(range(256)) * (size // 256) + b"z" * (size % 256))
         check(ctx, cuda, wire)
 
@@ -164,6 +164,22 @@ def test_adversarial_all_valid_positions(ctx, cuda):
     """Every offset parses as a valid empty frame (0x80 0x80 ...): 6-byte frames."""
     wire = (bytes([0x80, 0x80]) + b"\x80" * 4) * 10000
     check(ctx, cuda, wire)
+
+
+@pytest.mark.parametrize("pattern", [b"\x82\x82\x70\x70", b"\x82\x82\x70\x70\x70", b"\x82", b"\x89\x80",
+                                     b"\x82\x82\x82\x82\x70", b"\x82\x82\x00",
+                                     b"\x81\xfe\x00"])
+def test_candidate_density(ctx, cuda, pattern):
+    """Key-0 payloads whose wire bytes make many offsets pass the two-byte test:
+    tiles with more candidate offsets than the sparse node list holds (every
+    4th / every byte) next to sparse ones, all in one stream."""
+    rng = np.random.default_rng(len(pattern))
+    parts = []
+    for i in range(12):
+        n = int(rng.integers(1000, 40000))
+        parts.append(frame(2, (pattern * (n // len(pattern) + 1))[:n], key=0))
+        parts.append(frame(2, rng.integers(0, 256, int(rng.integers(0, 5000)), dtype=np.uint8).tobytes()))
+    check(ctx, cuda, b"".join(parts))
 
 
 def test_utf8_flags_c5_shape(ctx, cuda):

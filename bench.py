@@ -221,7 +221,7 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic,
-                     "kernel": "k_unmask<false>", "kernel_us": round(kern_s * 1e6, 2),
+                     "kernel": "k_unmask_fast", "kernel_us": round(kern_s * 1e6, 2),
                      "alg_bytes_per_launch": alg_bytes},
     }
     out.update(extra)

@@ -1,0 +1,73 @@
+#!/usr/bin/env python3
+"""HBM traffic per launch of one kernel from rocprofv3 PMC passes.
+
+rocprofv3 cannot collect FETCH_SIZE (3 TCC slots) and WRITE_SIZE (2) in one
+pass on gfx950, so they come from two runs of the same command:
+
+  rocprofv3 --pmc FETCH_SIZE -f csv -d gpurun_out/pmc_fetch -- python3 bench.py ...
+  rocprofv3 --pmc WRITE_SIZE -f csv -d gpurun_out/pmc_write -- python3 bench.py ...
+
+Both counters are in KiB. Per MI355X_MICROARCH.md (HBM section), FETCH_SIZE
+reports exactly half the bytes of a 16-B-per-lane streaming read on gfx950,
+so it is doubled; WRITE_SIZE is exact for 16-B-per-lane stores.
+
+usage: python tools/pmc_summary.py --fetch DIR --write DIR --kernel k_unmask_fast \
+           --alg-bytes 537395200 --out profiles/pmc_unmask.json
+"""
+import argparse
+import csv
+import glob
+import json
+import statistics
+
+
+def per_dispatch(d, counter, kernel):
+    vals = {}
+    files = glob.glob(d + "/**/*counter_collection.csv", recursive=True)
+    if not files:
+        raise SystemExit(f"no counter_collection.csv under {d}")
+    for f in files:
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                if row.get("Counter_Name") != counter or kernel not in row.get("Kernel_Name", ""):
+                    continue
+                key = (f, row.get("Dispatch_Id"))
+                vals[key] = vals.get(key, 0.0) + float(row["Counter_Value"])
+    if not vals:
+        raise SystemExit(f"no {counter} rows for {kernel} under {d}")
+    return list(vals.values())
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--fetch", required=True)
+    ap.add_argument("--write", required=True)
+    ap.add_argument("--kernel", required=True)
+    ap.add_argument("--alg-bytes", type=int, required=True)
+    ap.add_argument("--out", required=True)
+    a = ap.parse_args()
+    f = per_dispatch(a.fetch, "FETCH_SIZE", a.kernel)
+    w = per_dispatch(a.write, "WRITE_SIZE", a.kernel)
+    fk, wk = statistics.median(f), statistics.median(w)
+    read_b = 2.0 * fk * 1024.0          # gfx950: FETCH_SIZE counts half of a wide streaming read
+    write_b = wk * 1024.0
+    out = {
+        "kernel": a.kernel,
+        "dispatches": {"fetch_pass": len(f), "write_pass": len(w)},
+        "FETCH_SIZE_KiB_median": fk,
+        "WRITE_SIZE_KiB_median": wk,
+        "read_bytes_per_launch": round(read_b),
+        "write_bytes_per_launch": round(write_b),
+        "hbm_bytes_per_launch": round(read_b + write_b),
+        "alg_bytes_per_launch": a.alg_bytes,
+        "traffic_over_alg": round((read_b + write_b) / a.alg_bytes, 4),
+        "correction": "read = 2 x FETCH_SIZE (gfx950 half-count of 16-B/lane streaming reads, "
+                      "MI355X_MICROARCH.md HBM); write = WRITE_SIZE; KiB = 1024 B",
+    }
+    with open(a.out, "w") as fh:
+        json.dump(out, fh, indent=1)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

@@ -29,7 +29,10 @@ enum Counter {
     kCntLast = 6,        // last path node
     kCntSpill = 7,       // survivors spilled by dense tiles
     kCntBarGen = 8,      // k_resolve grid barrier: generation
-    kCntCount = 9
+    kCntFallback = 9,    // super-tile resolve declined (dense super tile, capacity): k_resolve runs
+    kCntTicket = 10,     // k_merge workgroups finished (the last one resolves the path)
+    kCntTails = 11,      // super-tile exit tails appended by k_merge
+    kCntCount = 12
 };
 static_assert(kCntFrames == kDecodeFramesCounter, "fws_internal.h names the frame counter");
 

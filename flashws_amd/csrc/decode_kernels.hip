@@ -272,7 +272,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(const uint8_t *__restrict
                 if (r == 0) return (uint16_t)(kLeaf | k);      // incomplete header at the stream end
                 if (r < 0) return kDead;
                 const uint64_t nxo = t0 + p + (uint64_t)r + h.plen;
-                if (nxo >= t0 + kTile) return (uint16_t)(kLeaf | k);
+                if (nxo >= t0 + kTile || nxo >= N) return (uint16_t)(kLeaf | k);   // leaves the tile / the stream
                 const uint32_t pn = (uint32_t)(nxo - t0);
                 const uint32_t m = W.cm[pn >> 5];
                 const uint32_t bit = pn & 31u;
@@ -472,6 +472,14 @@ extern "C" int fws_internal_scan_prof(unsigned long long *out, int reset) {
 }
 #endif
 
+// tuning / test hook: 0 = super-tile resolve with k_resolve fallback, 1 = k_resolve only
+static int g_resolve_mode = 0;
+extern "C" __attribute__((visibility("default"))) int fws_internal_set_resolve_mode(int m) {
+    const int old = g_resolve_mode;
+    if (m == 0 || m == 1) g_resolve_mode = m;
+    return old;
+}
+
 static uint32_t g_scan_blocks_per_cu = 0;   // tuning override (tools/), 0 = default
 extern "C" int fws_internal_set_scan_blocks_per_cu(int v) {
     g_scan_blocks_per_cu = v > 0 ? (uint32_t)v : 0u;
@@ -519,8 +527,16 @@ int fws_decode_ensure(fws_gpu_ctx *ctx, uint64_t N, uint32_t cap) {
     if (d.rbsums == nullptr) al(&d.rbsums, (uint64_t)d.resolve_grid * 8u);
     al(&d.stage_info, nt * kSlots * sizeof(fws_frame_info)); al(&d.stage_leaf, nt * kSlots * 4);
     al(&d.spill_info, ns * sizeof(fws_frame_info)); al(&d.spill_leaf, ns * 4); al(&d.tile_spill, nt * 4);
+    // super-tile resolve: results per slot id, EXIT tails, per-ST bases
+    rel(d.nres); rel(d.tails); rel(d.gnx); rel(d.tmark); rel(d.st_entry); rel(d.st_fbase); rel(d.st_cbase);
+    const uint64_t nst = fws_merge_super_tiles(nt);
+    const uint32_t tcap = fws_merge_tail_cap(nt);
+    al(&d.nres, (nt * kSlots + ns) * sizeof(fws_node_res));
+    al(&d.tails, (uint64_t)tcap * sizeof(fws_tail_rec)); al(&d.gnx, (uint64_t)tcap * 4); al(&d.tmark, ((uint64_t)tcap / 32 + 1) * 4);
+    al(&d.st_entry, nst * 4); al(&d.st_fbase, nst * 4); al(&d.st_cbase, nst * 8);
     if (e != hipSuccess) return fws_hip_status(e);
     d.max_tiles = nt; d.max_surv = ns; d.levels = nl; d.max_descs = nd;
+    d.max_nodes = nt * kSlots + ns; d.max_st = nst; d.tail_cap = tcap;
     return 0;
 }
 
@@ -539,5 +555,12 @@ int fws_launch_decode(fws_gpu_ctx *ctx, uint8_t *wire, uint64_t N, fws_frame_inf
                            d.tile_count, d.counters, (uint32_t)d.max_surv, d.scan_dummy);
         if ((e = hipGetLastError()) != hipSuccess) return fws_hip_status(e);
     }
-    return fws_launch_resolve(ctx, wire, N, n_tiles, K, frames, cap, res, s);
+    // super-tile resolve (common case); k_resolve runs only if it set kCntFallback.
+    // Its per-chain chunk sums are 32-bit: streams of 2^35 B and more take k_resolve.
+    const bool fast = N < (1ull << 35) && g_resolve_mode != 1;
+    if (fast) {
+        int r = fws_launch_merge(ctx, wire, N, n_tiles, frames, cap, res, s);
+        if (r) return r;
+    }
+    return fws_launch_resolve(ctx, wire, N, n_tiles, K, frames, cap, res, fast ? 1 : 0, s);
 }

@@ -47,6 +47,14 @@ int fws_ctx_ensure_plan(fws_gpu_ctx *ctx, uint64_t frames, uint64_t units) {
 
 extern "C" {
 
+// Test / tuning hook (not part of the ABI): the decode counters of the last
+// decode on ctx (decode_common.h Counter), synchronously. 0 or an error.
+__attribute__((visibility("default"))) int fws_internal_decode_counters(fws_gpu_ctx *ctx, uint32_t *out, int n) {
+    if (!ctx || !out || n <= 0 || !ctx->dec.counters) return FWS_ERR_INVALID;
+    if (n > 12) n = 12;
+    return fws_hip_status(hipMemcpy(out, ctx->dec.counters, (size_t)n * 4, hipMemcpyDeviceToHost));
+}
+
 int fws_gpu_abi_version(void) { return FWS_GPU_ABI_VERSION; }
 
 int fws_gpu_device_count(int *count) {
@@ -97,6 +105,13 @@ void fws_gpu_ctx_destroy(fws_gpu_ctx *ctx) {
     dev_free(d.tile_spill);
     dev_free(d.scan_dummy);
     dev_free(d.rbsums);
+    dev_free(d.nres);
+    dev_free(d.tails);
+    dev_free(d.gnx);
+    dev_free(d.tmark);
+    dev_free(d.st_entry);
+    dev_free(d.st_fbase);
+    dev_free(d.st_cbase);
     delete ctx;
 }
 

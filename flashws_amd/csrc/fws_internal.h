@@ -20,6 +20,20 @@ struct fws_plan_ws {
     uint64_t unit_cap = 0;            // capacity of unit_first (writes are clamped)
 };
 
+// Super-tile resolve records (merge_kernels.hip).
+struct fws_node_res {                 // per survivor: its chain inside its super tile
+    uint32_t tail;                    // EXIT: tail-list index; else the tail survivor's slot id
+    uint32_t cnt_kind;                // frames up to the tail (bits 0-29) | kind << 30
+    uint64_t cs;                      // unmask chunks of those frames
+};
+struct fws_tail_rec {                 // one EXIT tail: a chain leaving its super tile
+    uint64_t exit;                    // offset of the next header
+    uint32_t id;                      // slot id of the tail survivor
+    uint32_t w;                       // slot id of the survivor at `exit`, or DEAD
+    uint32_t wst;                     // super tile of `exit`
+    uint32_t pad;
+};
+
 // Stream-decode workspace (decode_kernels.hip).
 struct fws_decode_ws {
     uint64_t max_tiles = 0;
@@ -46,6 +60,17 @@ struct fws_decode_ws {
     uint32_t *scan_dummy = nullptr;        // one 64-B line per k_scan wavefront (idle-lane stores)
     uint32_t resolve_grid = 0;             // cooperative k_resolve workgroups (one per CU)
     uint64_t *rbsums = nullptr;            // k_resolve per-workgroup partial sums
+    // super-tile resolve (merge_kernels.hip)
+    uint64_t max_nodes = 0;                // slot ids: tiles * 8 + spill capacity
+    uint64_t max_st = 0;
+    uint32_t tail_cap = 0;
+    fws_node_res *nres = nullptr;          // [max_nodes]
+    fws_tail_rec *tails = nullptr;         // [tail_cap]
+    uint32_t *gnx = nullptr;               // [tail_cap] next tail / terminal
+    uint32_t *tmark = nullptr;             // [tail_cap / 32 + 1] tails that are some tail's next
+    uint32_t *st_entry = nullptr;          // [max_st] slot id of the path's first header in the ST
+    uint32_t *st_fbase = nullptr;          // [max_st] frames before the ST
+    uint64_t *st_cbase = nullptr;          // [max_st] unmask chunks before the ST
 };
 
 struct fws_gpu_ctx {
@@ -82,5 +107,11 @@ int fws_decode_ensure(fws_gpu_ctx *ctx, uint64_t N, uint32_t cap);
 int fws_launch_decode(fws_gpu_ctx *ctx, uint8_t *wire, uint64_t N, fws_frame_info *frames, uint32_t cap,
                       fws_decode_result *res, hipStream_t s);
 // resolve_kernels.hip: frames, descriptors and the unmask plan from k_scan's survivors
+// gate != 0: only if the super-tile resolve set kCntFallback (else the launch returns at once)
 int fws_launch_resolve(fws_gpu_ctx *ctx, const uint8_t *wire, uint64_t N, uint32_t n_tiles, uint32_t K,
-                       fws_frame_info *frames, uint32_t cap, fws_decode_result *res, hipStream_t s);
+                       fws_frame_info *frames, uint32_t cap, fws_decode_result *res, int gate, hipStream_t s);
+// merge_kernels.hip: the super-tile resolve (k_merge + k_emit), the common path
+uint64_t fws_merge_super_tiles(uint64_t n_tiles);
+uint32_t fws_merge_tail_cap(uint64_t n_tiles);
+int fws_launch_merge(fws_gpu_ctx *ctx, const uint8_t *wire, uint64_t N, uint32_t n_tiles, fws_frame_info *frames,
+                     uint32_t cap, fws_decode_result *res, hipStream_t s);

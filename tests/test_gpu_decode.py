@@ -16,6 +16,29 @@ from wsframes import frame
 
 pytestmark = pytest.mark.gpu
 
+RESOLVE_MODES = {"super_tile": 0, "k_resolve": 1}
+CNT_FALLBACK = 9            # decode_common.h Counter::kCntFallback
+
+
+@pytest.fixture(params=list(RESOLVE_MODES), autouse=True)
+def resolve_mode(request):
+    """Every decode test runs on both resolve paths: the super-tile resolve
+    (merge_kernels.hip, the common path) and the cooperative k_resolve it
+    falls back to (resolve_kernels.hip), forced."""
+    from flashws_amd import _lib
+    L = _lib.lib()
+    old = L.fws_internal_set_resolve_mode(RESOLVE_MODES[request.param])
+    yield request.param
+    L.fws_internal_set_resolve_mode(old)
+
+
+def fell_back(ctx):
+    import ctypes as C
+    from flashws_amd import _lib
+    out = (C.c_uint32 * 12)()
+    assert _lib.lib().fws_internal_decode_counters(ctx.h, out, 12) == 0
+    return out[CNT_FALLBACK] != 0
+
 
 def decode(ctx, wire, cuda, cap=None):
     dev = torch.from_numpy(np.ascontiguousarray(wire)).to(cuda)
@@ -134,17 +157,21 @@ def test_single_frame_tile_boundaries(ctx, cuda, size):
         check(ctx, cuda, wire)
 
 
-def test_c3_mixed_parity(ctx, cuda):
+def test_c3_mixed_parity(ctx, cuda, resolve_mode):
     """BASELINE config 3 shape (log-uniform 64 B..64 KiB) at 64 MiB, bit-exact."""
     wire, descs, _ = gpu.config_c3(seed=9, target=64 << 20)
     r = check(ctx, cuda, wire)
     assert int(r["n_frames"]) == len(descs)
+    if resolve_mode == "super_tile":
+        assert not fell_back(ctx), "C3 must resolve on the super-tile path"
 
 
-def test_c2_full_parity(ctx, cuda):
+def test_c2_full_parity(ctx, cuda, resolve_mode):
     wire, descs, _ = gpu.config_c2()
     r = check(ctx, cuda, wire)
     assert int(r["n_frames"]) == 65536
+    if resolve_mode == "super_tile":
+        assert not fell_back(ctx), "C2 must resolve on the super-tile path"
 
 
 def test_c3_full_roundtrip(ctx, cuda):

@@ -47,10 +47,10 @@ constexpr uint32_t kWCap = 1024;                       // node list capacity of 
 
 
 // Bit i set <=> offset i of the chunk passes the two-byte header test
-// (RSV clear, opcode in {0,1,2,8,9,10}, MASK set), four offsets per dword:
-// rsv:  (b0 & 0x70) == 0      <=> bit 7 of (b0 & 0x70) + 0x7F is clear
-// op:   (b0 & 7) <= 2         <=> bit 3 of (b0 & 7) + 5 is clear
-// mask: bit 7 of b1 (= byte i+1, v_alignbyte by one)
+// (RSV clear, opcode in {0,1,2,8,9,10}, MASK set), four offsets per dword.
+// RSV clear and (b0 & 7) <= 2 <=> (b0 & 0x77) <= 2 <=> bit 7 of
+// (b0 & 0x77) + 0x7D is clear (no carry leaves the byte: 0x77 + 0x7D < 0x100);
+// MASK is bit 7 of b1 (= byte i+1, v_alignbyte by one).
 __device__ __forceinline__ uint32_t cand_bits16(const u32x4 &lo, uint32_t next_dword) {
     const uint32_t W[5] = {lo.x, lo.y, lo.z, lo.w, next_dword};
     uint32_t m = 0;
@@ -58,9 +58,7 @@ __device__ __forceinline__ uint32_t cand_bits16(const u32x4 &lo, uint32_t next_d
     for (int i = 0; i < 4; ++i) {
         const uint32_t x = W[i];
         const uint32_t b1 = __builtin_amdgcn_alignbyte(W[i + 1], x, 1u);
-        const uint32_t rsv_ok = ~((x & 0x70707070u) + 0x7F7F7F7Fu);
-        const uint32_t op_ok = (~((x & 0x07070707u) + 0x05050505u)) << 4;
-        const uint32_t f = rsv_ok & op_ok & b1 & 0x80808080u;
+        const uint32_t f = ~((x & 0x77777777u) + 0x7D7D7D7Du) & b1 & 0x80808080u;
         m |= (((f >> 7) & 1u) | ((f >> 14) & 2u) | ((f >> 21) & 4u) | ((f >> 28) & 8u)) << (4 * i);
     }
     return m;
@@ -117,6 +115,33 @@ __device__ __forceinline__ int parse_window(const u32x4 &lo, const u32x4 &hi, ui
     return n + 4;
 }
 
+
+// The chain-building part of ParseFrameHdr (w_socket.h:435-524) for an offset
+// that passed the two-byte test (so RSV, opcode and MASK are valid): header
+// length (> 0), 0 = incomplete (the same avail checks in the same order), or
+// FWS_ERR_TOO_LARGE; payload length and key. Window d = bytes p..p+15.
+__device__ __forceinline__ int lean_parse(const uint32_t d[4], uint64_t avail, uint64_t &plen, uint32_t &key) {
+    if (avail < 2) return 0;                                       // :443-445
+    const uint32_t len7 = (d[0] >> 8) & 127u;
+    if (len7 < 126u) {
+        plen = len7;
+        key = __builtin_amdgcn_alignbyte(d[1], d[0], 2u);          // bytes 2..5
+        return avail < 6 ? 0 : 6;                                  // :508-511
+    }
+    if (len7 == 126u) {                                            // :476-482
+        if (avail < 4) return 0;
+        plen = ((d[0] >> 8) & 0xFF00u) | (d[0] >> 24);
+        key = d[1];                                                // bytes 4..7
+        return avail < 8 ? 0 : 8;
+    }
+    if (avail < 10) return 0;                                      // :483-492
+    const uint32_t hi32 = __builtin_amdgcn_alignbyte(d[1], d[0], 2u);
+    const uint32_t lo32 = __builtin_amdgcn_alignbyte(d[2], d[1], 2u);
+    plen = (uint64_t(__builtin_bswap32(hi32)) << 32) | __builtin_bswap32(lo32);
+    if (plen > (1ull << 32)) return FWS_ERR_TOO_LARGE;             // :493-498
+    key = __builtin_amdgcn_alignbyte(d[3], d[2], 2u);              // bytes 10..13
+    return avail < 14 ? 0 : 14;
+}
 
 constexpr uint32_t kScanBlocksPerCu = 5;     // resident k_scan workgroups per CU (LDS-limited)
 
@@ -181,7 +206,7 @@ __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t x, uint32_t *total) 
 // set count the 6 younger operations and never drain the other set.
 // kPipe = false (streams shorter than one tile + halo): no prefetch.
 template <bool kPipe>
-__global__ __launch_bounds__(kScanThreads) void k_scan(const uint8_t *__restrict__ wire, uint64_t N,
+__global__ __launch_bounds__(kScanThreads) __attribute__((amdgpu_waves_per_eu(5, 5))) void k_scan(const uint8_t *__restrict__ wire, uint64_t N,
                                                        uint32_t n_tiles,
                                                        fws_frame_info *__restrict__ stage_info,
                                                        uint32_t *__restrict__ stage_leaf,
@@ -198,6 +223,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(const uint8_t *__restrict
     const uint32_t gw = blockIdx.x * kScanWaves + (threadIdx.x >> 6);
     const uint32_t GW = gridDim.x * kScanWaves;
     const uint32_t L32 = uint32_t(lane) * 32u;
+    const uint32_t L16 = uint32_t(lane) * 16u;
     // last tile whose bytes + halo lie inside the stream (prefetch clamp)
     const uint32_t last_inner = kPipe ? (uint32_t)((N - kHalo) / kTile) - 1u : 0u;
     // idle lanes' stores go to this wave's own 64-B line (L2-resident, no hot spot)
@@ -212,8 +238,9 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(const uint8_t *__restrict
     auto prefetch = [&](uint32_t tt, u32x4 (&pf)[2], u32x4 &halo) {
         if (!kPipe) return;
         const uint64_t o = uint64_t(tt < last_inner ? tt : last_inner) * kTile;
-        pf[0] = gload16(reinterpret_cast<uintptr_t>(wire + o + L32));
-        pf[1] = gload16(reinterpret_cast<uintptr_t>(wire + o + L32 + 16u));
+        // coalesced: each load instruction reads 1 KiB contiguous (lane L: 16 B at 16L)
+        pf[0] = gload16(reinterpret_cast<uintptr_t>(wire + o + L16));
+        pf[1] = gload16(reinterpret_cast<uintptr_t>(wire + o + 1024u + L16));
         halo = gload16(reinterpret_cast<uintptr_t>(wire + o + kTile));
     };
 
@@ -224,8 +251,8 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(const uint8_t *__restrict
         if (valid) {
             const bool inner = kPipe && t <= last_inner;
             if (inner) {
-                *reinterpret_cast<u32x4 *>(B + L32) = pf[0];
-                *reinterpret_cast<u32x4 *>(B + L32 + 16u) = pf[1];
+                *reinterpret_cast<u32x4 *>(B + L16) = pf[0];
+                *reinterpret_cast<u32x4 *>(B + 1024u + L16) = pf[1];
                 if (lane == 0) *reinterpret_cast<u32x4 *>(B + kTile) = halo;
             } else {
                 for (uint32_t i = uint32_t(lane) * 16u; i < kTile + kHalo; i += 64u * 16u) {
@@ -268,10 +295,10 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(const uint8_t *__restrict
             SCAN_COUNT(5, nc);
 
             // node value of the candidate at tile offset p: next node, kLeaf|k, or kDead
-            auto node_value = [&](uint32_t p, uint32_t k, int r, const Hdr &h) -> uint16_t {
+            auto node_value = [&](uint32_t p, uint32_t k, int r, uint64_t plen) -> uint16_t {
                 if (r == 0) return (uint16_t)(kLeaf | k);      // incomplete header at the stream end
                 if (r < 0) return kDead;
-                const uint64_t nxo = t0 + p + (uint64_t)r + h.plen;
+                const uint64_t nxo = t0 + p + (uint64_t)r + plen;
                 if (nxo >= t0 + kTile || nxo >= N) return (uint16_t)(kLeaf | k);   // leaves the tile / the stream
                 const uint32_t pn = (uint32_t)(nxo - t0);
                 const uint32_t m = W.cm[pn >> 5];
@@ -287,6 +314,9 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(const uint8_t *__restrict
             };
 
             const bool sparse = nc <= kWCap;                   // wave-uniform
+            // lean parse of nodes lane, lane + 64: payload length (low 32 bits), key, and
+            // packed = offset | b0 << 11 | (r + 2) << 19 | (payload length >> 32) << 24
+            uint32_t pl[2], ky[2], pk[2];
             uint16_t *const pos = W.nodes;
             uint16_t *const nv = sparse ? W.nodes + kWCap : W.nodes;
             if (sparse) {
@@ -297,11 +327,29 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(const uint8_t *__restrict
                     pos[k++] = (uint16_t)(L32 + b);
                 }
                 wave_sync();
-                for (uint32_t k = lane; k < nc; k += 64) {
+                // nodes lane and lane + 64: lean parse, kept in registers for the emit
+#pragma unroll
+                for (uint32_t j = 0; j < 2; ++j) {
+                    const uint32_t k = uint32_t(lane) + 64u * j;
+                    if (k < nc) {
+                        const uint32_t p = pos[k];
+                        const uint32_t a = p & ~15u;
+                        const u32x4 wl = *reinterpret_cast<const u32x4 *>(B + a);
+                        const u32x4 wh = *reinterpret_cast<const u32x4 *>(B + a + 16u);
+                        uint32_t d[4];
+                        window16(wl, wh, p & 15u, d);
+                        uint64_t plen = 0;
+                        const int r = lean_parse(d, N - (t0 + p), plen, ky[j]);
+                        pl[j] = (uint32_t)plen;
+                        pk[j] = p | ((d[0] & 0xFFu) << 11) | (uint32_t(r + 2) << 19) | (uint32_t(plen >> 32) << 24);
+                        nv[k] = node_value(p, k, r, plen);
+                    }
+                }
+                for (uint32_t k = lane + 128u; k < nc; k += 64) {
                     const uint32_t p = pos[k];
                     Hdr h;
                     const int r = parse_at(p, h);
-                    nv[k] = node_value(p, k, r, h);
+                    nv[k] = node_value(p, k, r, h.plen);
                 }
             } else {
                 uint32_t bits = cm, k = cp;
@@ -310,7 +358,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(const uint8_t *__restrict
                     bits &= bits - 1u;
                     Hdr h;
                     const int r = parse_at(L32 + b, h);
-                    nv[k] = node_value(L32 + b, k, r, h);
+                    nv[k] = node_value(L32 + b, k, r, h.plen);
                     ++k;
                 }
             }
@@ -357,28 +405,8 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(const uint8_t *__restrict
             auto srank = [&](uint32_t k) -> uint32_t {
                 return W.spre[k >> 6] + (uint32_t)__popcll(W.sbits[k >> 6] & ((1ull << (k & 63u)) - 1ull));
             };
-            // survivor k at offset p with leaf v: record to its LDS slot, or to the spill area
-            auto emit = [&](uint32_t k, uint32_t p, uint16_t v) {
-                Hdr h;
-                const int r = parse_at(p, h);
-                const uint64_t q = t0 + p;
-                fws_frame_info fi;
-                fi.hdr_off = q;
-                if (r > 0) {
-                    fi.payload_len = h.plen;
-                    fi.key = h.key;
-                    fi.opcode = (uint8_t)h.opcode;
-                    fi.fin = (uint8_t)h.fin;
-                    fi.hdr_len = (uint8_t)r;
-                    fi.flags = (q + (uint64_t)r + h.plen > N) ? (uint8_t)FWS_FRAME_TRUNCATED : (uint8_t)0;
-                } else {                                       // incomplete trailing header
-                    fi.payload_len = 0;
-                    fi.key = 0;
-                    fi.opcode = 0;
-                    fi.fin = 0;
-                    fi.hdr_len = 0;
-                    fi.flags = 0;
-                }
+            // survivor k with leaf v: record to its LDS slot, or to the spill area
+            auto put = [&](uint32_t k, uint16_t v, const fws_frame_info &fi) {
                 const uint32_t idx = srank(k), leaf = srank(v & 0x7FFFu);   // tile-local ranks
                 if (spill == kNone) {
                     W.stage[idx] = fi;
@@ -388,9 +416,47 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(const uint8_t *__restrict
                     spill_leaf[spill + idx] = leaf;
                 }
             };
+            auto record = [&](uint32_t p, int r, uint64_t plen, uint32_t key, uint32_t b0) {
+                const uint64_t q = t0 + p;
+                fws_frame_info fi;
+                fi.hdr_off = q;
+                if (r > 0) {
+                    fi.payload_len = plen;
+                    fi.key = key;
+                    fi.opcode = (uint8_t)(b0 & 15u);
+                    fi.fin = (uint8_t)(b0 >> 7);
+                    fi.hdr_len = (uint8_t)r;
+                    fi.flags = (q + (uint64_t)r + plen > N) ? (uint8_t)FWS_FRAME_TRUNCATED : (uint8_t)0;
+                } else {                                       // incomplete trailing header
+                    fi.payload_len = 0;
+                    fi.key = 0;
+                    fi.opcode = 0;
+                    fi.fin = 0;
+                    fi.hdr_len = 0;
+                    fi.flags = 0;
+                }
+                return fi;
+            };
+            auto emit = [&](uint32_t k, uint32_t p, uint16_t v) {   // re-parse from the LDS bytes
+                Hdr h;
+                const int r = parse_at(p, h);
+                put(k, v, record(p, r, h.plen, h.key, (h.fin << 7) | h.opcode));
+            };
             if (ns) {
                 if (sparse) {
-                    for (uint32_t k = lane; k < nc; k += 64) {
+#pragma unroll
+                    for (uint32_t j = 0; j < 2; ++j) {
+                        const uint32_t k = uint32_t(lane) + 64u * j;
+                        if (k < nc) {
+                            const uint16_t v = nv[k];
+                            if (v != kDead) {
+                                const uint32_t w = pk[j];
+                                put(k, v, record(w & 0x7FFu, int((w >> 19) & 31u) - 2,
+                                                 (uint64_t(w >> 24) << 32) | pl[j], ky[j], (w >> 11) & 0xFFu));
+                            }
+                        }
+                    }
+                    for (uint32_t k = lane + 128u; k < nc; k += 64) {
                         const uint16_t v = nv[k];
                         if (v != kDead) emit(k, pos[k], v);
                     }
@@ -528,11 +594,12 @@ int fws_decode_ensure(fws_gpu_ctx *ctx, uint64_t N, uint32_t cap) {
     al(&d.stage_info, nt * kSlots * sizeof(fws_frame_info)); al(&d.stage_leaf, nt * kSlots * 4);
     al(&d.spill_info, ns * sizeof(fws_frame_info)); al(&d.spill_leaf, ns * 4); al(&d.tile_spill, nt * 4);
     // super-tile resolve: results per slot id, EXIT tails, per-ST bases
-    rel(d.nres); rel(d.tails); rel(d.gnx); rel(d.tmark); rel(d.st_entry); rel(d.st_fbase); rel(d.st_cbase);
+    rel(d.nres); rel(d.tails); rel(d.gnx); rel(d.tmark); rel(d.st_nodes); rel(d.st_n); rel(d.st_entry); rel(d.st_fbase); rel(d.st_cbase);
     const uint64_t nst = fws_merge_super_tiles(nt);
     const uint32_t tcap = fws_merge_tail_cap(nt);
     al(&d.nres, (nt * kSlots + ns) * sizeof(fws_node_res));
     al(&d.tails, (uint64_t)tcap * sizeof(fws_tail_rec)); al(&d.gnx, (uint64_t)tcap * 4); al(&d.tmark, ((uint64_t)tcap / 32 + 1) * 4);
+    al(&d.st_nodes, fws_merge_st_nodes(nt) * sizeof(fws_st_node)); al(&d.st_n, nst * 4);
     al(&d.st_entry, nst * 4); al(&d.st_fbase, nst * 4); al(&d.st_cbase, nst * 8);
     if (e != hipSuccess) return fws_hip_status(e);
     d.max_tiles = nt; d.max_surv = ns; d.levels = nl; d.max_descs = nd;

@@ -34,6 +34,14 @@ struct fws_tail_rec {                 // one EXIT tail: a chain leaving its supe
     uint32_t pad;
 };
 
+struct fws_st_node {                  // one survivor in its super tile's table (k_merge -> k_emit)
+    fws_frame_info rec;
+    uint32_t ch;                      // unmask chunks of its payload
+    uint16_t nx;                      // in-ST next (local index) or an exit code
+    uint8_t wt;                       // 1: a frame, 0: an incomplete header
+    uint8_t pad;
+};
+
 // Stream-decode workspace (decode_kernels.hip).
 struct fws_decode_ws {
     uint64_t max_tiles = 0;
@@ -68,6 +76,8 @@ struct fws_decode_ws {
     fws_tail_rec *tails = nullptr;         // [tail_cap]
     uint32_t *gnx = nullptr;               // [tail_cap] next tail / terminal
     uint32_t *tmark = nullptr;             // [tail_cap / 32 + 1] tails that are some tail's next
+    fws_st_node *st_nodes = nullptr;       // [max_st * 2048] survivors per super tile
+    uint32_t *st_n = nullptr;              // [max_st] survivors per super tile
     uint32_t *st_entry = nullptr;          // [max_st] slot id of the path's first header in the ST
     uint32_t *st_fbase = nullptr;          // [max_st] frames before the ST
     uint64_t *st_cbase = nullptr;          // [max_st] unmask chunks before the ST
@@ -113,5 +123,6 @@ int fws_launch_resolve(fws_gpu_ctx *ctx, const uint8_t *wire, uint64_t N, uint32
 // merge_kernels.hip: the super-tile resolve (k_merge + k_emit), the common path
 uint64_t fws_merge_super_tiles(uint64_t n_tiles);
 uint32_t fws_merge_tail_cap(uint64_t n_tiles);
+uint64_t fws_merge_st_nodes(uint64_t n_tiles);
 int fws_launch_merge(fws_gpu_ctx *ctx, const uint8_t *wire, uint64_t N, uint32_t n_tiles, fws_frame_info *frames,
                      uint32_t cap, fws_decode_result *res, hipStream_t s);

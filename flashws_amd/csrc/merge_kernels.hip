@@ -1,6 +1,6 @@
 // merge_kernels.hip -- second half of fws_gpu_decode_stream on the common
 // path: from k_scan's per-tile survivors to the frame list, the payload
-// descriptors and the unmask plan in two launches, with no grid barrier.
+// descriptors and the unmask plan in three launches, with no grid barrier.
 //
 // OnRecvData's frame loop (net/w_socket.h:543-769) is a chain: the next
 // header starts at this header's exit (hdr_off + hdr_len + payload_len,
@@ -9,30 +9,34 @@
 // header plus a few random offsets.
 //
 //  k_merge  one workgroup per super tile (ST = 128 tiles = 256 KiB). Loads
-//           the ST's survivors into LDS in offset order, links each to the
-//           survivor at its exit inside the ST (binary search), and pointer-
-//           jumps (Wyllie) so every survivor knows the tail of its chain in
-//           the ST, the frames and unmask chunks up to that tail, and how the
-//           chain leaves the ST: EXIT (into a later ST), END (at or past the
-//           stream end), DEAD (the exit is not a header: a protocol error or a
-//           false chain) or INC (an incomplete header at the stream end).
-//           EXIT tails go to a global list.
-//  k_link   one thread per EXIT tail: the survivor its exit lands on (binary
-//           search in that tile's survivors) and next(tail) = the tail of
-//           that survivor's chain; marks every next() target in a bitmap.
+//           the ST's survivors (offset order), links each to the survivor at
+//           its exit inside the ST (binary search in LDS) and pointer-jumps
+//           (Wyllie) so every survivor knows the tail of its chain in the ST,
+//           the frames and unmask chunks up to that tail, and how the chain
+//           leaves the ST: EXIT (into a later ST), END (at or past the stream
+//           end), DEAD (the exit is not a header: a protocol error or a false
+//           chain) or INC (an incomplete header at the stream end). EXIT
+//           tails go to a global list with the survivor their exit lands on
+//           (binary search in that tile's survivors). The ST's survivors are
+//           also written as one contiguous table for k_emit.
+//  k_link   one thread per EXIT tail: next(tail) = the tail of the landing
+//           survivor's chain; marks every next() target in a bitmap.
 //  last WG  the k_link workgroup that finishes last (atomic ticket) resolves
-//           the path from the header at offset 0 over the marked tails
-//           (compacted into LDS). The path's tails are the greatest fixpoint
-//           of K = {root's tail} U next(K): offsets strictly increase along
-//           next, so a false tail has a finite chain of predecessors and
-//           drops out after a few rounds.
-//           Each landing survivor on the path is its ST's entry; a scan over
-//           the STs gives every ST's frame and chunk base. The terminal is
-//           finished with ParseFrameHdr's rules (w_socket.h:435-524): the
-//           error walk, carry-out and the fws_decode_result.
+//           the path from the header at offset 0 over the marked tails,
+//           compacted into LDS. The path's tails are the greatest fixpoint of
+//           K = {root's tail} U next(K): offsets strictly increase along next,
+//           so a false tail has a finite chain of predecessors and drops out
+//           after a few rounds. Each landing survivor on the path is its ST's
+//           entry; a scan over the STs gives every ST's frame and chunk base.
+//           The terminal is finished with ParseFrameHdr's rules
+//           (w_socket.h:435-524): error walk, carry-out, fws_decode_result.
 //  k_emit   one workgroup per ST with an entry: marks the entry's chain by
-//           pointer doubling and writes fws_frame_info, fws_frame_desc and
-//           the unmask plan (cbase, unit_first) in stream order.
+//           pointer doubling over the ST's table and writes fws_frame_info,
+//           fws_frame_desc and the unmask plan (cbase, unit_first) in order.
+//
+// Every global access on these paths is metadata (about 1 survivor per KiB of
+// stream); the kernels are latency-bound, so loads are issued in batches of
+// independent addresses before their uses.
 //
 // A super tile with more than kStCap survivors (dense small frames), a full
 // tail list, a survivor overflow in k_scan or a pruning that does not settle
@@ -47,14 +51,49 @@ constexpr uint64_t kStBytes = uint64_t(kStTiles) * kTile;
 constexpr uint32_t kStCap = 2048;                   // survivors of one ST in LDS
 constexpr int kMThreads = 512;
 constexpr int kMWaves = kMThreads / 64;
-constexpr uint32_t kTailCapMax = 1u << 18;          // LDS bitmaps of the path pruning
+constexpr uint32_t kPer = kStCap / kMThreads;       // survivors per thread: i = kPer * tid + j
+constexpr uint32_t kTailCapMax = 1u << 18;          // LDS bitmap of the path pruning
+constexpr uint32_t kCompCap = 8192;                 // tails that are some tail's next (+ the root's)
 constexpr uint32_t kMaxPruneRounds = 64;
 
 // in-ST next of a survivor: an LDS index, or how the chain leaves the ST
 constexpr uint16_t kNxInc = 0xFFFC, kNxDead = 0xFFFD, kNxEnd = 0xFFFE, kNxExit = 0xFFFF;
 constexpr uint32_t kKindExit = 0, kKindEnd = 1, kKindDead = 2, kKindInc = 3;
 constexpr uint32_t kGTerm = 0xFFFFFFF0u;            // next(tail) >= kGTerm: the path ends (kGTerm | kind)
-constexpr uint32_t kCntMask = (1u << 30) - 1u;
+constexpr uint16_t kCTerm = 0xFFFF;
+
+#ifdef FWS_SCAN_PROF
+// phase clocks (100 MHz wall clock, summed over workgroups) for tools/prof_scan.py
+__device__ unsigned long long g_merge_prof[32];
+#define MP_INIT() uint64_t mp_t = wall_clock64()
+#define MP_MARK(k)                                                                  \
+    do {                                                                            \
+        if (threadIdx.x == 0) {                                                     \
+            const uint64_t now = wall_clock64();                                    \
+            atomicAdd(&g_merge_prof[k], (unsigned long long)(now - mp_t));          \
+            mp_t = now;                                                             \
+        }                                                                           \
+    } while (0)
+#define MP_ADD(k, v) do { if (threadIdx.x == 0) atomicAdd(&g_merge_prof[k], (unsigned long long)(v)); } while (0)
+#define MP_SPAN(k0, k1)                                                             \
+    do {                                                                            \
+        if (threadIdx.x == 0) {                                                     \
+            atomicMin(&g_merge_prof[k0], (unsigned long long)mp_t0);                \
+            atomicMax(&g_merge_prof[k1], (unsigned long long)wall_clock64());       \
+        }                                                                           \
+    } while (0)
+#else
+#define MP_INIT() do { } while (0)
+#define MP_MARK(k) do { } while (0)
+#define MP_ADD(k, v) do { } while (0)
+#define MP_SPAN(k0, k1) do { } while (0)
+#endif
+
+// fws_node_res::cnt_kind = frames (bits 0-11) | ST-local index (12-22) | kind (30-31)
+__device__ __forceinline__ uint32_t res_cnt(uint32_t ck) { return ck & 0xFFFu; }
+__device__ __forceinline__ uint32_t res_lidx(uint32_t ck) { return (ck >> 12) & 0x7FFu; }
+__device__ __forceinline__ uint32_t res_kind(uint32_t ck) { return ck >> 30; }
+static_assert(kStCap <= 2048, "cnt_kind packing: 12-bit counts, 11-bit local indices");
 
 __device__ __forceinline__ uint32_t kind_of(uint16_t code) {
     return code == kNxExit ? kKindExit : code == kNxEnd ? kKindEnd : code == kNxDead ? kKindDead : kKindInc;
@@ -76,7 +115,9 @@ struct MergeParams {
     fws_tail_rec *tails;
     uint32_t *gnx;
     uint32_t *tmark;                                 // tail-target bitmap (tail_cap / 32 + 1 words)
-    uint32_t *st_entry;
+    fws_st_node *st_nodes;                           // [n_st][kStCap]
+    uint32_t *st_n;
+    uint32_t *st_entry;                              // local index of the ST's entry, or kNone
     uint32_t *st_fbase;
     uint64_t *st_cbase;
     fws_frame_info *frames;
@@ -92,19 +133,29 @@ struct MergeParams {
     __device__ __forceinline__ uint32_t sid(uint32_t t, uint32_t sp, uint32_t r) const {
         return sp == kNone ? t * kSlots + r : spill_base + sp + r;
     }
-    __device__ __forceinline__ fws_frame_info info(uint32_t id) const {
-        return id < spill_base ? stage_info[id] : spill_info[id - spill_base];
+    __device__ __forceinline__ const fws_frame_info *rec(uint32_t id) const {
+        return id < spill_base ? stage_info + id : spill_info + (id - spill_base);
     }
-    // slot id of the survivor at offset x (x < N), or kTermDead
+    // slot id of the survivor at offset x (x < N), or kTermDead. A tile's <= 8
+    // stage slots are read in one batch; a spilled (dense) tile is searched.
     __device__ uint32_t find_node(uint64_t x) const {
         const uint32_t t = (uint32_t)(x / kTile);
         const uint32_t n = tile_count[t], sp = tile_spill[t];
+        if (sp == kNone) {
+            uint64_t o[kSlots];
+#pragma unroll
+            for (uint32_t r = 0; r < kSlots; ++r) o[r] = r < n ? stage_info[t * kSlots + r].hdr_off : ~0ull;
+            uint32_t hit = kTermDead;
+#pragma unroll
+            for (uint32_t r = 0; r < kSlots; ++r) hit = o[r] == x ? t * kSlots + r : hit;
+            return hit;
+        }
         uint32_t lo = 0, hi = n;
         while (lo < hi) {
             const uint32_t mid = (lo + hi) >> 1;
-            if (info(sid(t, sp, mid)).hdr_off < x) lo = mid + 1; else hi = mid;
+            if (rec(sid(t, sp, mid))->hdr_off < x) lo = mid + 1; else hi = mid;
         }
-        return (lo < n && info(sid(t, sp, lo)).hdr_off == x) ? sid(t, sp, lo) : kTermDead;
+        return (lo < n && rec(sid(t, sp, lo))->hdr_off == x) ? sid(t, sp, lo) : kTermDead;
     }
     __device__ __forceinline__ uint64_t node_chunks(const fws_frame_info &fi) const {
         if (fi.hdr_len == 0) return 0;
@@ -140,8 +191,8 @@ __device__ __forceinline__ T block_excl(T v, T *sred, T *total) {
     return off + inc - v;
 }
 
-// One super tile's survivors in LDS, offset order.
-struct StLds {
+// ------------------------------------------------------------------ k_merge
+struct MergeLds {
     uint32_t tcnt[kStTiles];
     uint32_t tsp[kStTiles];
     uint32_t tbase[kStTiles];
@@ -150,20 +201,30 @@ struct StLds {
     uint32_t ch[kStCap];                             // unmask chunks of the payload (0: INC)
     uint16_t nx[kStCap];
     uint8_t wt[kStCap];                              // 1: a frame; 0: incomplete header
-    union {
-        uint64_t ext[kStCap];                        // exit offsets (until nx is built)
-        uint32_t sh[2][kStCap];                      // k_merge: chunk sums to P
-    };
+    uint16_t ptr[2][kStCap];                         // Wyllie pointer (tails point to themselves)
+    uint16_t sc[2][kStCap];                          // frames from i up to ptr (exclusive)
+    uint32_t sh[2][kStCap];                          // chunks from i up to ptr (exclusive)
+    uint32_t lref[kStCap];                           // EXIT tail: index in the ST's tail run
     uint32_t red32[kMWaves];
-    uint64_t red64[kMWaves];
-    uint32_t n;
+    uint32_t n_tail, tail_base;
 };
 
-// Loads ST s (survivor count returned; nothing loaded past kStCap) and builds nx.
-__device__ uint32_t st_load(const MergeParams &P, uint32_t s, StLds &L) {
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+__global__ __launch_bounds__(kMThreads) void k_merge(MergeParams P) {
+    __shared__ MergeLds L;
+    const uint32_t s = blockIdx.x, tid = threadIdx.x;
+    uint32_t *const C = P.counters;
+#ifdef FWS_SCAN_PROF
+    const uint64_t mp_t0 = wall_clock64();
+#endif
+    MP_INIT();
+    // the tail-target bitmap k_link sets
+    for (uint64_t w = (uint64_t)s * kMThreads + tid; w < P.tail_cap / 32u + 1u; w += (uint64_t)gridDim.x * kMThreads)
+        P.tmark[w] = 0u;
+    if (s >= P.n_st) return;
     const uint32_t t0 = s * kStTiles;
     const uint64_t st0 = uint64_t(s) * kStBytes, st_end = st0 + kStBytes;
+
+    // survivors per tile -> ST-local numbering
     uint32_t c = 0, sp = kNone;
     if (tid < kStTiles && t0 + tid < P.n_tiles) {
         c = P.tile_count[t0 + tid];
@@ -171,144 +232,166 @@ __device__ uint32_t st_load(const MergeParams &P, uint32_t s, StLds &L) {
     }
     uint32_t n;
     const uint32_t b = block_excl<uint32_t>(c, L.red32, &n);
-    if (n > kStCap) return n;
+    if (tid == 0) {
+        atomicAdd(&C[kCntSurv], n);
+        P.st_n[s] = n;
+    }
+    if (n > kStCap) {
+        if (tid == 0) atomicOr(&C[kCntFallback], 1u);
+        return;
+    }
     if (tid < kStTiles) {
         L.tcnt[tid] = c;
         L.tsp[tid] = sp;
         L.tbase[tid] = b;
     }
+    if (tid == 0) L.n_tail = 0;
     __syncthreads();
-    for (uint32_t tl = wv; tl < kStTiles; tl += kMWaves) {
-        const uint32_t m = L.tcnt[tl];
-        for (uint32_t r = lane; r < m; r += 64) {
-            const uint32_t i = L.tbase[tl] + r;
-            const uint32_t nid = P.sid(t0 + tl, L.tsp[tl], r);
-            const fws_frame_info fi = P.info(nid);
-            L.off[i] = (uint32_t)(fi.hdr_off - st0);
-            L.id[i] = nid;
-            L.wt[i] = fi.hdr_len ? 1 : 0;
-            L.ch[i] = (uint32_t)P.node_chunks(fi);
-            L.ext[i] = exit_of(fi);
+    MP_MARK(0);
+
+    // this thread's survivors i = kPer * tid + j: slot ids, then one batch of record loads
+    const uint32_t i0 = kPer * tid;
+    uint32_t nid[kPer];
+    fws_frame_info r[kPer];
+    if (i0 < n) {
+        uint32_t lo = 0, hi = kStTiles;              // last tile with tbase <= i0
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (L.tbase[mid] <= i0) lo = mid; else hi = mid;
+        }
+        uint32_t tl = lo;
+#pragma unroll
+        for (uint32_t j = 0; j < kPer; ++j) {
+            const uint32_t i = i0 + j;
+            while (tl + 1 < kStTiles && L.tbase[tl + 1] <= i) ++tl;
+            nid[j] = i < n ? P.sid(t0 + tl, L.tsp[tl], i - L.tbase[tl]) : 0u;
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < kPer; ++j)
+            if (i0 + j < n) r[j] = *P.rec(nid[j]);
+#pragma unroll
+        for (uint32_t j = 0; j < kPer; ++j) {
+            const uint32_t i = i0 + j;
+            if (i < n) {
+                L.off[i] = (uint32_t)(r[j].hdr_off - st0);
+                L.id[i] = nid[j];
+                L.wt[i] = r[j].hdr_len ? 1 : 0;
+                L.ch[i] = (uint32_t)P.node_chunks(r[j]);
+            }
         }
     }
     __syncthreads();
-    for (uint32_t i = tid; i < n; i += kMThreads) {
+    MP_MARK(1);
+    // in-ST next: the survivor at the exit offset, searched in the exit's tile only
+    // (the 4 searches of a thread interleaved), and the ST's node table for k_emit
+    fws_st_node *const tab = P.st_nodes + (uint64_t)s * kStCap;
+    uint32_t xr[kPer], sb[kPer], sl[kPer];
+#pragma unroll
+    for (uint32_t j = 0; j < kPer; ++j) {
+        const uint64_t x = exit_of(r[j]);
+        const bool inside = i0 + j < n && r[j].hdr_len && x < P.N && x < st_end;
+        xr[j] = inside ? (uint32_t)(x - st0) : 0u;
+        const uint32_t tl = xr[j] / kTile;
+        sb[j] = inside ? L.tbase[tl] : 0u;
+        sl[j] = inside ? L.tcnt[tl] : 0u;
+    }
+    for (;;) {
+        bool more = false;
+#pragma unroll
+        for (uint32_t j = 0; j < kPer; ++j) {
+            if (sl[j] > 1) {
+                const uint32_t half = sl[j] >> 1;
+                if (L.off[sb[j] + half - 1] < xr[j]) sb[j] += half;
+                sl[j] -= half;
+                more |= sl[j] > 1;
+            }
+        }
+        if (!more) break;
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < kPer; ++j) {
+        const uint32_t i = i0 + j;
+        if (i >= n) continue;
         uint16_t v;
-        const uint64_t x = L.ext[i];
-        if (!L.wt[i]) v = kNxInc;
+        const uint64_t x = exit_of(r[j]);
+        if (!r[j].hdr_len) v = kNxInc;
         else if (x >= P.N) v = kNxEnd;
         else if (x >= st_end) v = kNxExit;
-        else {
-            const uint32_t xr = (uint32_t)(x - st0);
-            uint32_t lo = i + 1, hi = n;
-            while (lo < hi) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (L.off[mid] < xr) lo = mid + 1; else hi = mid;
-            }
-            v = (lo < n && L.off[lo] == xr) ? (uint16_t)lo : kNxDead;
-        }
+        else v = (sl[j] == 1 && L.off[sb[j]] == xr[j]) ? (uint16_t)sb[j] : kNxDead;
         L.nx[i] = v;
-    }
-    __syncthreads();
-    return n;
-}
-
-struct MergeWork {
-    StLds st;
-    uint16_t ptr[2][kStCap];                         // Wyllie pointer (tails point to themselves)
-    uint16_t sc[2][kStCap];                          // frames from i up to ptr (exclusive)
-    uint32_t lref[kStCap];                           // EXIT tail: index in its ST's tail run
-    uint32_t n_tail, tail_base;
-};
-
-union MergeLds {
-    MergeWork m;
-};
-
-// Chain tails, counts and the EXIT tail records of one super tile.
-__device__ void merge_st(const MergeParams &P, uint32_t s, uint32_t n, MergeWork &W) {
-    StLds &L = W.st;
-    const uint32_t tid = threadIdx.x;
-    uint32_t *const C = P.counters;
-    for (uint32_t i = tid; i < n; i += kMThreads) {
-        const uint16_t v = L.nx[i];
         const bool tail = v >= kNxInc;
-        W.ptr[0][i] = tail ? (uint16_t)i : v;
-        W.sc[0][i] = tail ? 0 : L.wt[i];
-        L.sh[0][i] = tail ? 0u : L.ch[i];             // ext[] is dead after st_load
+        L.ptr[0][i] = tail ? (uint16_t)i : v;
+        L.sc[0][i] = tail ? 0 : L.wt[i];
+        L.sh[0][i] = tail ? 0u : L.ch[i];
+        if (v == kNxExit) L.lref[i] = atomicAdd(&L.n_tail, 1u);
+        {                                            // two 16-B stores of the 32-B node
+            uint32_t wd[8];
+            __builtin_memcpy(wd, &r[j], sizeof(fws_frame_info));
+            wd[6] = L.ch[i];
+            wd[7] = (uint32_t)v | ((uint32_t)L.wt[i] << 16);
+            u32x4 *dst = reinterpret_cast<u32x4 *>(tab + i);
+            dst[0] = u32x4{wd[0], wd[1], wd[2], wd[3]};
+            dst[1] = u32x4{wd[4], wd[5], wd[6], wd[7]};
+        }
     }
-    if (tid == 0) W.n_tail = 0;
     __syncthreads();
+    MP_MARK(2);
+    // reserve the ST's run of the tail list
+    if (tid == 0) {
+        const uint32_t k = L.n_tail;
+        uint32_t base = k ? atomicAdd(&C[kCntTails], k) : 0u;
+        if (k && (base > P.tail_cap || P.tail_cap - base < k)) {
+            atomicOr(&C[kCntFallback], 1u);
+            base = kNone;
+        }
+        L.tail_base = base;
+    }
+    // pointer jumping: every survivor -> its chain's tail, with frame / chunk sums
     int cur = 0;
     for (;;) {
         int changed = 0;
         for (uint32_t i = tid; i < n; i += kMThreads) {
-            const uint16_t p = W.ptr[cur][i];
-            const uint16_t q = W.ptr[cur][p];
+            const uint16_t p = L.ptr[cur][i];
+            const uint16_t q = L.ptr[cur][p];
             if (p != q) {
-                W.ptr[cur ^ 1][i] = q;
-                W.sc[cur ^ 1][i] = (uint16_t)(W.sc[cur][i] + W.sc[cur][p]);
+                L.ptr[cur ^ 1][i] = q;
+                L.sc[cur ^ 1][i] = (uint16_t)(L.sc[cur][i] + L.sc[cur][p]);
                 L.sh[cur ^ 1][i] = L.sh[cur][i] + L.sh[cur][p];
                 changed = 1;
             } else {
-                W.ptr[cur ^ 1][i] = p;
-                W.sc[cur ^ 1][i] = W.sc[cur][i];
+                L.ptr[cur ^ 1][i] = p;
+                L.sc[cur ^ 1][i] = L.sc[cur][i];
                 L.sh[cur ^ 1][i] = L.sh[cur][i];
             }
         }
         cur ^= 1;
         if (!__syncthreads_or(changed)) break;
     }
-    for (uint32_t i = tid; i < n; i += kMThreads)
-        if (L.nx[i] == kNxExit) W.lref[i] = atomicAdd(&W.n_tail, 1u);
-    __syncthreads();
-    if (tid == 0) {
-        const uint32_t k = W.n_tail;
-        uint32_t base = k ? atomicAdd(&C[kCntTails], k) : 0u;
-        if (k && (base > P.tail_cap || P.tail_cap - base < k)) {
-            atomicOr(&C[kCntFallback], 1u);
-            base = kNone;
-        }
-        W.tail_base = base;
-    }
-    __syncthreads();
-    const uint32_t tb = W.tail_base;
+    MP_MARK(3);
+    const uint32_t tb = L.tail_base;
     if (tb == kNone) return;
-    for (uint32_t i = tid; i < n; i += kMThreads) {
-        const uint32_t t = W.ptr[cur][i];
+#pragma unroll
+    for (uint32_t j = 0; j < kPer; ++j) {
+        const uint32_t i = i0 + j;
+        if (i >= n) continue;
+        const uint32_t t = L.ptr[cur][i];
         const uint32_t kind = kind_of(L.nx[t]);
-        const uint32_t cnt = W.sc[cur][i] + L.wt[t];
+        const uint32_t cnt = L.sc[cur][i] + L.wt[t];
         const uint64_t cs = (uint64_t)L.sh[cur][i] + L.ch[t];
-        const uint32_t ref = kind == kKindExit ? tb + W.lref[t] : L.id[t];
-        P.nres[L.id[i]] = fws_node_res{ref, cnt | (kind << 30), cs};
+        const uint32_t ref = kind == kKindExit ? tb + L.lref[t] : L.id[t];
+        P.nres[nid[j]] = fws_node_res{ref, cnt | (i << 12) | (kind << 30), cs};
         if (L.nx[i] == kNxExit) {
-            const uint64_t x = exit_of(P.info(L.id[i]));
-            P.tails[tb + W.lref[i]] = fws_tail_rec{x, L.id[i], kTermDead, (uint32_t)(x / kStBytes), 0u};
+            const uint64_t x = exit_of(r[j]);
+            P.tails[tb + L.lref[i]] = fws_tail_rec{x, nid[j], kTermDead, (uint32_t)(x / kStBytes), 0u};
         }
     }
-}
-
-__global__ __launch_bounds__(kMThreads) void k_merge(MergeParams P) {
-    __shared__ MergeLds L;
-    const uint32_t s = blockIdx.x, tid = threadIdx.x;
-    uint32_t *const C = P.counters;
-    // the tail-target bitmap k_link sets
-    for (uint64_t w = (uint64_t)s * kMThreads + tid; w < P.tail_cap / 32u + 1u; w += (uint64_t)gridDim.x * kMThreads)
-        P.tmark[w] = 0u;
-    if (s >= P.n_st) return;
-    const uint32_t n = st_load(P, s, L.m.st);
-    if (tid == 0) atomicAdd(&C[kCntSurv], n);
-    if (n > kStCap) {
-        if (tid == 0) atomicOr(&C[kCntFallback], 1u);
-        return;
-    }
-    merge_st(P, s, n, L.m);
+    __syncthreads();
+    MP_MARK(4);
+    MP_ADD(5, 1);
+    MP_SPAN(6, 7);
 }
 
 // ------------------------------------------------------------- k_link + path
-constexpr uint32_t kCompCap = 8192;                 // tails that are some tail's next (+ the root's)
-constexpr uint16_t kCTerm = 0xFFFF;
-
 struct PathLds {
     uint32_t words[kTailCapMax / 32];                // tail-target bitmap (+ the root's tail)
     uint32_t wpre[kTailCapMax / 32];                 // marked tails before each word
@@ -317,15 +400,37 @@ struct PathLds {
     uint32_t kb[2][kCompCap / 32];                   // kept bitmaps
     uint32_t red32[kMWaves];
     uint64_t red64[kMWaves];
-    uint32_t root, rt, crt, end_tail, mc;
+    uint32_t root, rt, crt, root_ck;
+    uint64_t root_cs;
+    uint32_t end_id, end_kind, end_set;
 };
 
+// Batched loop over c = tid + k * kMThreads < n: the loads of up to 4
+// iterations are issued before any of their uses.
+template <typename Load, typename Use>
+__device__ __forceinline__ void batched4(uint32_t n, Load load, Use use) {
+    for (uint32_t base = threadIdx.x; base < n; base += 4u * kMThreads) {
+        decltype(load(0u)) v[4];
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) {
+            const uint32_t c = base + j * kMThreads;
+            if (c < n) v[j] = load(c);
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) {
+            const uint32_t c = base + j * kMThreads;
+            if (c < n) use(c, v[j]);
+        }
+    }
+}
+
 // The path from offset 0 over the target tails: ST entries and bases,
-// terminal, result. Runs in the last k_link workgroup (after every other
-// workgroup's release; acquire done by the caller).
+// terminal, result. Runs in the last k_link workgroup, after every other
+// workgroup's release and this workgroup's acquire.
 __device__ void resolve_path(const MergeParams &P, PathLds &G) {
     uint32_t *const C = P.counters;
     const uint32_t tid = threadIdx.x;
+    MP_INIT();
     if (ld_acq(&C[kCntFallback]) || (ld_acq(&C[kCntOverflow]) & 1u)) {
         if (tid == 0) atomicOr(&C[kCntFallback], 1u);
         return;
@@ -334,20 +439,37 @@ __device__ void resolve_path(const MergeParams &P, PathLds &G) {
     const uint32_t n_st = P.n_st;
     const uint64_t N = P.N;
     if (tid == 0) {
-        uint32_t root = kNone, rt = kNone;
+        uint32_t root = kNone, rt = kNone, ck = 0;
+        uint64_t cs = 0;
         if (P.n_tiles && P.tile_count[0]) {
             const uint32_t id0 = P.sid(0, P.tile_spill[0], 0);
-            if (P.info(id0).hdr_off == 0) root = id0;
+            if (P.rec(id0)->hdr_off == 0) root = id0;
         }
+        G.end_set = 0;
         if (root != kNone) {
             const fws_node_res r = P.nres[root];
-            if ((r.cnt_kind >> 30) == kKindExit) rt = r.tail;
+            ck = r.cnt_kind;
+            cs = r.cs;
+            if (res_kind(ck) == kKindExit) rt = r.tail;
+            else {                                   // the root's chain ends in ST 0
+                G.end_id = r.tail;
+                G.end_kind = res_kind(ck);
+                G.end_set = 1;
+            }
         }
         G.root = root;
         G.rt = rt;
-        G.end_tail = kNone;
+        G.root_ck = ck;
+        G.root_cs = cs;
+    }
+    // ST bases start from zero counts
+    for (uint32_t s = tid; s < n_st; s += kMThreads) {
+        P.st_entry[s] = kNone;
+        P.st_fbase[s] = 0;
+        P.st_cbase[s] = 0;
     }
     __syncthreads();
+    MP_MARK(10);
     const uint32_t root = G.root, rt = G.rt;
 
     // compact the marked tails (every next() target, plus the root's tail), in tail order
@@ -379,15 +501,15 @@ __device__ void resolve_path(const MergeParams &P, PathLds &G) {
         }
     }
     __syncthreads();
+    MP_MARK(11);
     auto rank = [&](uint32_t x) -> uint32_t {
         return G.wpre[x >> 5] + (uint32_t)__popc(G.words[x >> 5] & ((1u << (x & 31u)) - 1u));
     };
-    for (uint32_t c = tid; c < mc; c += kMThreads) {
-        const uint32_t g = P.gnx[G.comp[c]];
-        G.cnx[c] = g >= kGTerm ? kCTerm : (uint16_t)rank(g);
-    }
+    batched4(mc, [&](uint32_t c) { return ld_acq(&P.gnx[G.comp[c]]); },
+             [&](uint32_t c, uint32_t g) { G.cnx[c] = g >= kGTerm ? kCTerm : (uint16_t)rank(g); });
     if (tid == 0) G.crt = rt == kNone ? kNone : rank(rt);
     __syncthreads();
+    MP_MARK(12);
     const uint32_t crt = G.crt;
 
     // greatest fixpoint of K = {crt} U next(K), from K = all marked tails
@@ -413,63 +535,93 @@ __device__ void resolve_path(const MergeParams &P, PathLds &G) {
         uint32_t *t = ka; ka = kb; kb = t;
         settled = !__syncthreads_or(diff);
     }
+    MP_MARK(13);
     if (!settled) {
         if (tid == 0) atomicOr(&C[kCntFallback], 1u);
         return;
     }
 
-    // entries: the root, and every kept tail's landing survivor
-    for (uint32_t s = tid; s < n_st; s += kMThreads) P.st_entry[s] = kNone;
-    __syncthreads();
-    if (tid == 0 && root != kNone) P.st_entry[0] = root;
-    for (uint32_t c = tid; c < mc; c += kMThreads) {
-        if ((ka[c >> 5] >> (c & 31u)) & 1u) {
-            const uint32_t x = G.comp[c];
-            const fws_tail_rec tr = P.tails[x];
-            if (tr.w != kTermDead) P.st_entry[tr.wst] = tr.w;
-            if (G.cnx[c] == kCTerm) G.end_tail = x;          // exactly one kept tail ends the path
+    // entries: the root, and every kept tail's landing survivor, with their chain counts
+    if (tid == 0 && root != kNone) {
+        P.st_entry[0] = res_lidx(G.root_ck);
+        P.st_fbase[0] = res_cnt(G.root_ck);
+        P.st_cbase[0] = G.root_cs;
+    }
+    for (uint32_t base = tid; base < mc; base += 4u * kMThreads) {
+        fws_tail_rec tr[4];
+        fws_node_res nr[4];
+        bool kept[4];
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) {
+            const uint32_t c = base + j * kMThreads;
+            kept[j] = c < mc && ((ka[c >> 5] >> (c & 31u)) & 1u);
+            if (kept[j]) {
+                tr[j] = P.tails[G.comp[c]];
+                tr[j].w = ld_acq(&P.tails[G.comp[c]].w);      // handed off in this launch
+            }
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j)
+            if (kept[j] && tr[j].w != kTermDead) nr[j] = P.nres[tr[j].w];
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) {
+            if (!kept[j]) continue;
+            const uint32_t c = base + j * kMThreads;
+            const bool ends = G.cnx[c] == kCTerm;    // exactly one kept tail ends the path
+            if (tr[j].w == kTermDead) {
+                if (ends) { G.end_id = tr[j].id; G.end_kind = kKindDead; G.end_set = 1; }
+                continue;
+            }
+            P.st_entry[tr[j].wst] = res_lidx(nr[j].cnt_kind);
+            P.st_fbase[tr[j].wst] = res_cnt(nr[j].cnt_kind);
+            P.st_cbase[tr[j].wst] = nr[j].cs;
+            if (ends) { G.end_id = nr[j].tail; G.end_kind = res_kind(nr[j].cnt_kind); G.end_set = 1; }
         }
     }
     __syncthreads();
+    MP_MARK(14);
 
-    // per-ST frame and chunk counts, then their exclusive prefix in ST order
-    for (uint32_t s = tid; s < n_st; s += kMThreads) {
-        const uint32_t e = P.st_entry[s];
-        uint32_t c = 0;
-        uint64_t k = 0;
-        if (e != kNone) {
-            const fws_node_res r = P.nres[e];
-            c = r.cnt_kind & kCntMask;
-            k = r.cs;
+    // exclusive prefix of the per-ST frame and chunk counts, in ST order
+    constexpr uint32_t kSper = 8;
+    uint32_t nf_path = 0;
+    uint64_t cs_path = 0;
+    for (uint32_t s0 = 0; s0 < n_st; s0 += kSper * kMThreads) {
+        const uint32_t lo = s0 + tid * kSper;
+        uint32_t fc[kSper];
+        uint64_t cc[kSper];
+        uint32_t fs = 0;
+        uint64_t cs = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < kSper; ++j) {
+            fc[j] = lo + j < n_st ? P.st_fbase[lo + j] : 0u;
+            cc[j] = lo + j < n_st ? P.st_cbase[lo + j] : 0ull;
         }
-        P.st_fbase[s] = c;
-        P.st_cbase[s] = k;
-    }
-    __syncthreads();
-    const uint32_t sper = (n_st + kMThreads - 1) / kMThreads;
-    const uint32_t lo = tid * sper < n_st ? tid * sper : n_st;
-    const uint32_t hi = lo + sper < n_st ? lo + sper : n_st;
-    uint32_t fs = 0;
-    uint64_t cs = 0;
-    for (uint32_t s = lo; s < hi; ++s) {
-        fs += P.st_fbase[s];
-        cs += P.st_cbase[s];
-    }
-    uint32_t nf_path;
-    uint64_t cs_path;
-    uint32_t fpre = block_excl<uint32_t>(fs, G.red32, &nf_path);
-    uint64_t cpre = block_excl<uint64_t>(cs, G.red64, &cs_path);
-    for (uint32_t s = lo; s < hi; ++s) {
-        const uint32_t c = P.st_fbase[s];
-        const uint64_t k = P.st_cbase[s];
-        P.st_fbase[s] = fpre;
-        P.st_cbase[s] = cpre;
-        fpre += c;
-        cpre += k;
+#pragma unroll
+        for (uint32_t j = 0; j < kSper; ++j) {
+            fs += fc[j];
+            cs += cc[j];
+        }
+        uint32_t ft;
+        uint64_t ct;
+        uint32_t fpre = nf_path + block_excl<uint32_t>(fs, G.red32, &ft);
+        uint64_t cpre = cs_path + block_excl<uint64_t>(cs, G.red64, &ct);
+#pragma unroll
+        for (uint32_t j = 0; j < kSper; ++j) {
+            if (lo + j < n_st) {
+                P.st_fbase[lo + j] = fpre;
+                P.st_cbase[lo + j] = cpre;
+            }
+            fpre += fc[j];
+            cpre += cc[j];
+        }
+        nf_path += ft;
+        cs_path += ct;
     }
 
+    MP_MARK(15);
+    MP_ADD(16, mc);
     if (tid != 0) return;
-    if (rt != kNone && G.end_tail == kNone) {        // no terminal on the path: cannot happen
+    if (root != kNone && !G.end_set) {               // no terminal on the path: cannot happen
         atomicOr(&C[kCntFallback], 1u);
         return;
     }
@@ -480,25 +632,9 @@ __device__ void resolve_path(const MergeParams &P, PathLds &G) {
     uint64_t pos = 0;
     bool walk = N > 0 && root == kNone;              // no chain from offset 0 survived
     if (root != kNone) {
-        uint32_t end_id, kind;
-        if (rt == kNone) {
-            const fws_node_res rr = P.nres[root];
-            end_id = rr.tail;
-            kind = rr.cnt_kind >> 30;
-        } else {
-            const fws_tail_rec tr = P.tails[G.end_tail];
-            if (tr.w == kTermDead) {
-                end_id = tr.id;
-                kind = kKindDead;
-            } else {
-                const fws_node_res rr = P.nres[tr.w];
-                end_id = rr.tail;
-                kind = rr.cnt_kind >> 30;
-            }
-        }
-        const fws_frame_info fi = P.info(end_id);
-        pos = kind == kKindInc ? fi.hdr_off : exit_of(fi);
-        walk = kind == kKindDead;
+        const fws_frame_info fi = *P.rec(G.end_id);
+        pos = G.end_kind == kKindInc ? fi.hdr_off : exit_of(fi);
+        walk = G.end_kind == kKindDead;
     }
     uint32_t nf = nf_path;
     uint64_t run = cs_path;
@@ -550,15 +686,27 @@ __device__ void resolve_path(const MergeParams &P, PathLds &G) {
         *P.plan_total = lim ? run : 0;
     }
     *P.res = r;
+    MP_MARK(17);
 }
 
-// One thread per EXIT tail: the survivor its exit lands on, next(tail), and
+// One thread per EXIT tail: the survivor its exit lands on, next(tail) and
 // the target bitmap. The last workgroup (atomic ticket) resolves the path.
+// Hand-off inside the launch without release / acquire fences
+// (cdna_hip_programming.md Guideline 16, MI355X_MICROARCH.md "Valid forms",
+// first row): every handed-off word is stored sc1 (relaxed agent atomic
+// store / atomicOr), each storing wave drains vmcnt before the workgroup
+// barrier, one lane adds to the ticket, and the last adder reads them only
+// with sc1 loads (ld_acq). Everything else it reads was written by earlier
+// launches. One k_link workgroup per CU (its LDS).
 __global__ __launch_bounds__(kMThreads) void k_link(MergeParams P) {
     __shared__ PathLds G;
     __shared__ uint32_t s_last;
     const uint32_t tid = threadIdx.x;
     uint32_t *const C = P.counters;
+#ifdef FWS_SCAN_PROF
+    const uint64_t mp_t0 = wall_clock64();
+#endif
+    MP_INIT();
     const uint32_t M = C[kCntTails];
     const uint32_t x = blockIdx.x * kMThreads + tid;
     if (x < M && !C[kCntFallback]) {
@@ -566,51 +714,64 @@ __global__ __launch_bounds__(kMThreads) void k_link(MergeParams P) {
         const uint32_t w = P.find_node(tr.exit);
         uint32_t g = kGTerm | kKindDead;
         if (w != kTermDead) {
-            tr.w = w;
+            __hip_atomic_store(&tr.w, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             const fws_node_res r = P.nres[w];
-            const uint32_t kind = r.cnt_kind >> 30;
-            g = kind == kKindExit ? r.tail : (kGTerm | kind);
+            g = res_kind(r.cnt_kind) == kKindExit ? r.tail : (kGTerm | res_kind(r.cnt_kind));
         }
-        P.gnx[x] = g;
+        __hip_atomic_store(&P.gnx[x], g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (g < kGTerm) atomicOr(&P.tmark[g >> 5], 1u << (g & 31u));
     }
-    __threadfence();                                 // release this workgroup's records
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains
     __syncthreads();
-    if (tid == 0) s_last = atomicAdd(&C[kCntTicket], 1u) == gridDim.x - 1u;
+    if (tid == 0)
+        s_last = __hip_atomic_fetch_add(&C[kCntTicket], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                 gridDim.x - 1u;
     __syncthreads();
+    MP_MARK(8);
+    MP_ADD(9, 1);
     if (!s_last) return;
-    __threadfence();                                 // acquire every other workgroup's
     resolve_path(P, G);
+    __syncthreads();
+    MP_SPAN(20, 21);
 }
 
+// ------------------------------------------------------------------ k_emit
 struct EmitLds {
-    StLds st;
     uint16_t ptr[2][kStCap];
     uint8_t mark[kStCap];
-    uint32_t le;
+    uint32_t red32[kMWaves];
+    uint64_t red64[kMWaves];
 };
 
 __global__ __launch_bounds__(kMThreads) void k_emit(MergeParams P) {
     __shared__ EmitLds L;
     const uint32_t s = blockIdx.x, tid = threadIdx.x;
-    uint32_t *const C = P.counters;
-    if (s >= P.n_st || C[kCntFallback]) return;
-    const uint32_t e = P.st_entry[s];
-    if (e == kNone) return;
-    const uint32_t lim = C[kCntFrames], fbase = P.st_fbase[s];
-    if (fbase >= lim) return;
-    StLds &S = L.st;
-    const uint32_t n = st_load(P, s, S);
-    if (n > kStCap) return;                          // (k_merge fell back; not reached)
-    for (uint32_t i = tid; i < n; i += kMThreads) {
-        const uint16_t v = S.nx[i];
-        L.ptr[0][i] = v >= kNxInc ? (uint16_t)i : v;
-        L.mark[i] = 0;
-        if (S.id[i] == e) L.le = i;
+    const uint32_t *const C = P.counters;
+#ifdef FWS_SCAN_PROF
+    const uint64_t mp_t0 = wall_clock64();
+#endif
+    MP_INIT();
+    if (s >= P.n_st) return;
+    const uint32_t fb = C[kCntFallback], e = P.st_entry[s], fbase = P.st_fbase[s], n = P.st_n[s];
+    const uint32_t lim = C[kCntFrames];
+    const uint64_t cbase0 = P.st_cbase[s];
+    if (fb || e == kNone || fbase >= lim || n > kStCap) return;
+    const fws_st_node *const tab = P.st_nodes + (uint64_t)s * kStCap;
+    const uint32_t i0 = kPer * tid;
+    fws_st_node nd[kPer];
+#pragma unroll
+    for (uint32_t j = 0; j < kPer; ++j)
+        if (i0 + j < n) nd[j] = tab[i0 + j];
+#pragma unroll
+    for (uint32_t j = 0; j < kPer; ++j) {
+        const uint32_t i = i0 + j;
+        if (i < n) {
+            L.ptr[0][i] = nd[j].nx >= kNxInc ? (uint16_t)i : nd[j].nx;
+            L.mark[i] = i == e;
+        }
     }
     __syncthreads();
-    if (tid == 0) L.mark[L.le] = 1;
-    __syncthreads();
+    MP_MARK(24);
     // marks double along the chain: after round k every node within 2^k steps of the entry
     int cur = 0;
     for (;;) {
@@ -626,32 +787,33 @@ __global__ __launch_bounds__(kMThreads) void k_emit(MergeParams P) {
         cur ^= 1;
         if (!__syncthreads_or(changed)) break;
     }
-    // frames of the chain in offset order: 4 consecutive nodes per thread
-    constexpr uint32_t kPer = kStCap / kMThreads;
+    MP_MARK(25);
+    // the chain's frames in offset order
+    bool fr[kPer];
     uint32_t fl = 0;
     uint64_t cl = 0;
 #pragma unroll
     for (uint32_t j = 0; j < kPer; ++j) {
-        const uint32_t i = tid * kPer + j;
-        if (i < n && L.mark[i] && S.wt[i]) {
+        const uint32_t i = i0 + j;
+        fr[j] = i < n && L.mark[i] && nd[j].wt;
+        if (fr[j]) {
             ++fl;
-            cl += S.ch[i];
+            cl += nd[j].ch;
         }
     }
     uint32_t ftot;
     uint64_t ctot;
-    uint32_t f = fbase + block_excl<uint32_t>(fl, S.red32, &ftot);
-    uint64_t cb = P.st_cbase[s] + block_excl<uint64_t>(cl, S.red64, &ctot);
+    uint32_t f = fbase + block_excl<uint32_t>(fl, L.red32, &ftot);
+    uint64_t cb = cbase0 + block_excl<uint64_t>(cl, L.red64, &ctot);
 #pragma unroll
     for (uint32_t j = 0; j < kPer; ++j) {
-        const uint32_t i = tid * kPer + j;
-        if (!(i < n && L.mark[i] && S.wt[i])) continue;
+        if (!fr[j]) continue;
+        const fws_frame_info &fi = nd[j].rec;
+        const uint64_t c = nd[j].ch;
         if (f < lim) {
-            const fws_frame_info fi = P.info(S.id[i]);
             const uint64_t po = fi.hdr_off + fi.hdr_len;
             const uint64_t pl = (po + fi.payload_len > P.N) ? P.N - po : fi.payload_len;
-            const uint64_t c = S.ch[i];
-            if (f < P.cap) P.frames[f] = fi;
+            P.frames[f] = fi;
             P.descs[f] = fws_frame_desc{po, pl, fi.key, 0u};
             P.cbase[f] = cb;
             if (c) {
@@ -666,16 +828,33 @@ __global__ __launch_bounds__(kMThreads) void k_emit(MergeParams P) {
             }
         }
         ++f;
-        cb += S.ch[i];
+        cb += c;
     }
+    __syncthreads();
+    MP_MARK(26);
+    MP_ADD(27, 1);
+    MP_SPAN(28, 29);
 }
 
 }  // namespace fwsk
+
+#ifdef FWS_SCAN_PROF
+extern "C" int fws_internal_merge_prof(unsigned long long *out, int reset) {
+    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(fwsk::g_merge_prof), sizeof(unsigned long long) * 32);
+    if (e == hipSuccess && reset) {
+        unsigned long long z[32] = {};
+        z[6] = z[20] = z[28] = ~0ull;                // span minima
+        e = hipMemcpyToSymbol(HIP_SYMBOL(fwsk::g_merge_prof), z, sizeof(z));
+    }
+    return fws_hip_status(e);
+}
+#endif
 
 // ------------------------------------------------------------------ host side
 using namespace fwsk;
 
 uint64_t fws_merge_super_tiles(uint64_t n_tiles) { return (n_tiles + kStTiles - 1) / kStTiles; }
+uint64_t fws_merge_st_nodes(uint64_t n_tiles) { return fws_merge_super_tiles(n_tiles) * kStCap; }
 
 uint32_t fws_merge_tail_cap(uint64_t n_tiles) {
     uint64_t c = fws_merge_super_tiles(n_tiles) * 64u + 4096u;
@@ -701,6 +880,8 @@ int fws_launch_merge(fws_gpu_ctx *ctx, const uint8_t *wire, uint64_t N, uint32_t
     P.tails = d.tails;
     P.gnx = d.gnx;
     P.tmark = d.tmark;
+    P.st_nodes = d.st_nodes;
+    P.st_n = d.st_n;
     P.st_entry = d.st_entry;
     P.st_fbase = d.st_fbase;
     P.st_cbase = d.st_cbase;

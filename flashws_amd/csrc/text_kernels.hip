@@ -91,10 +91,21 @@ __global__ __launch_bounds__(kBlock) void k_utf8(const uint8_t *__restrict__ bas
 }
 
 // ------------------------------------------------------------------ gather
-// dst byte space = concatenation of the payload regions (dst_off = exclusive
-// prefix of payload_len, built by k_gather_plan*). One wave per 4 KiB unit of
-// dst; a full 16-B dst chunk inside one region is two aligned 16-B source
-// loads + v_alignbyte + XOR + one 16-B store.
+// Out-of-place reassembly of a fragmented message (C4): dst byte space = the
+// payload regions concatenated (dbase = exclusive prefix of payload_len), each
+// byte XORed with its region's key at its region-relative phase. That is the
+// concatenation of the on_read() parts (w_socket.h:713-747), the user-level copy
+// of tests/new-ws-echo/test_ws_server.cpp:205-206.
+//
+// Plan: k_gather_count (block sums) -> k_gather_scan (dbase) -> k_gather_units
+// (unit_first[u] = the region holding byte u * 4 KiB, one thread per unit).
+// k_gather_fast: one wave per 4 KiB dst unit (4 steps of 64 lanes x 16 B).
+// When the unit meets at most 2 regions (regions >= 4 KiB, as C4's 4 KiB..1 MiB
+// fragments) their metadata is wave-uniform (scalar loads); a dst chunk inside
+// one region is two aligned 16-B source loads shifted by the region's source
+// misalignment, XORed and stored; all 8 loads of a lane are issued before the
+// first use. A chunk on a region seam (<= 1 per region) goes byte by byte;
+// units with more regions take the per-chunk search path.
 constexpr uint64_t kGatherUnit = 4096;
 
 __global__ __launch_bounds__(kBlock) void k_gather_count(const fws_frame_desc *__restrict__ d, uint32_t n,
@@ -113,8 +124,7 @@ __global__ __launch_bounds__(kBlock) void k_gather_count(const fws_frame_desc *_
 
 __global__ __launch_bounds__(kBlock) void k_gather_scan(const fws_frame_desc *__restrict__ d, uint32_t n,
                                                         const uint64_t *__restrict__ block_sums,
-                                                        uint64_t *__restrict__ dbase, uint32_t *__restrict__ unit_first,
-                                                        uint64_t unit_cap, uint64_t *__restrict__ total_out) {
+                                                        uint64_t *__restrict__ dbase, uint64_t *__restrict__ total_out) {
     __shared__ uint64_t wsum[kBlock / 64];
     __shared__ uint64_t sprefix;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -140,71 +150,121 @@ __global__ __launch_bounds__(kBlock) void k_gather_scan(const fws_frame_desc *__
         const uint64_t f = f0 + i;
         if (f >= n) break;
         dbase[f] = run;
-        if (c[i]) {
-            uint64_t u = (run + kGatherUnit - 1) / kGatherUnit, ue = (run + c[i] + kGatherUnit - 1) / kGatherUnit;
-            if (ue > unit_cap) ue = unit_cap;
-            for (; u < ue; ++u) unit_first[u] = (uint32_t)f;
-        }
         run += c[i];
         if (f == n - 1) { dbase[n] = run; *total_out = run; }
     }
 }
 
-__device__ __forceinline__ u32x4 load16_unaligned(const uint8_t *src) {
-    const uintptr_t a = (uintptr_t)src;
-    const uintptr_t base = a & ~uintptr_t(15);
-    const uint32_t sh = (uint32_t)(a & 15u);
-    const u32x4 v0 = *reinterpret_cast<const u32x4 *>(base);
-    if (sh == 0) return v0;
-    const u32x4 v1 = *reinterpret_cast<const u32x4 *>(base + 16);
-    const uint32_t d[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-    const uint32_t bs = 8u * (sh & 3u);
-    u32x4 r;
-    switch (sh >> 2) {
-#define FWS_AL(i, q) (uint32_t)((((uint64_t)d[(i) + (q) + 1] << 32) | d[(i) + (q)]) >> bs)
-    case 0: r = u32x4{FWS_AL(0, 0), FWS_AL(1, 0), FWS_AL(2, 0), FWS_AL(3, 0)}; break;
-    case 1: r = u32x4{FWS_AL(0, 1), FWS_AL(1, 1), FWS_AL(2, 1), FWS_AL(3, 1)}; break;
-    case 2: r = u32x4{FWS_AL(0, 2), FWS_AL(1, 2), FWS_AL(2, 2), FWS_AL(3, 2)}; break;
-    default: r = u32x4{FWS_AL(0, 3), FWS_AL(1, 3), FWS_AL(2, 3), FWS_AL(3, 3)}; break;
-#undef FWS_AL
+// unit_first[u] = last region f with dbase[f] <= u * 4 KiB (the region holding that byte)
+__global__ __launch_bounds__(kBlock) void k_gather_units(const uint64_t *__restrict__ dbase, uint32_t n,
+                                                         uint32_t *__restrict__ unit_first, uint64_t unit_cap,
+                                                         const uint64_t *__restrict__ total_ptr) {
+    const uint64_t u = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    uint64_t n_units = (*total_ptr + kGatherUnit - 1) / kGatherUnit;
+    if (n_units > unit_cap) n_units = unit_cap;
+    if (u >= n_units) return;
+    const uint64_t A = u * kGatherUnit;
+    uint32_t lo = 0, hi = n - 1;
+    while (lo < hi) {
+        const uint32_t mid = lo + ((hi - lo + 1) >> 1);
+        if (dbase[mid] <= A) lo = mid; else hi = mid - 1;
     }
-    return r;
+    unit_first[u] = lo;
 }
 
-// Requires dst 16-B aligned. Partial chunks and region seams go byte by byte.
-__global__ __launch_bounds__(kBlock) void k_gather(uint8_t *__restrict__ dst, const uint8_t *__restrict__ src,
-                                                   const fws_frame_desc *__restrict__ d, uint32_t n,
-                                                   const uint64_t *__restrict__ dbase,
-                                                   const uint32_t *__restrict__ unit_first, uint64_t unit_cap,
-                                                   const uint64_t *__restrict__ total_ptr) {
+// 16 bytes starting sh (0..15) bytes into the 32-byte window v0:v1
+__device__ __forceinline__ u32x4 shr_bytes(const u32x4 &v0, const u32x4 &v1, uint32_t sh) {
+    const bool s8 = (sh & 8u) != 0, s4 = (sh & 4u) != 0;
+    const uint32_t a0 = s8 ? v0.z : v0.x, a1 = s8 ? v0.w : v0.y, a2 = s8 ? v1.x : v0.z;
+    const uint32_t a3 = s8 ? v1.y : v0.w, a4 = s8 ? v1.z : v1.x;
+    const uint32_t c0 = s4 ? a1 : a0, c1 = s4 ? a2 : a1, c2 = s4 ? a3 : a2, c3 = s4 ? a4 : a3;
+    const uint32_t c4 = s4 ? (s8 ? v1.w : v1.y) : a4;
+    const uint32_t b = sh & 3u;
+    return u32x4{__builtin_amdgcn_alignbyte(c1, c0, b), __builtin_amdgcn_alignbyte(c2, c1, b),
+                 __builtin_amdgcn_alignbyte(c3, c2, b), __builtin_amdgcn_alignbyte(c4, c3, b)};
+}
+
+// dst bytes [a, min(a + 16, total)) one by one (region seams, the tail)
+__device__ __forceinline__ void gather_bytes(uint8_t *dst, const uint8_t *src, const fws_frame_desc *__restrict__ d,
+                                             const uint64_t *__restrict__ dbase, uint32_t f, uint64_t a,
+                                             uint64_t total) {
+    for (uint64_t b = a; b < a + 16 && b < total; ++b) {
+        while (b >= dbase[f + 1]) ++f;
+        const fws_frame_desc fd = d[f];
+        const uint64_t k = b - dbase[f];
+        const uint32_t kb = (fd.key >> (8u * ((uint32_t)(k + fd.phase) & 3u))) & 0xFFu;
+        dst[b] = (uint8_t)(src[fd.payload_off + k] ^ kb);
+    }
+}
+
+// Requires dst 16-B aligned.
+__global__ __launch_bounds__(kBlock) void k_gather_fast(uint8_t *__restrict__ dst, const uint8_t *__restrict__ src,
+                                                        const fws_frame_desc *__restrict__ d, uint32_t n,
+                                                        const uint64_t *__restrict__ dbase,
+                                                        const uint32_t *__restrict__ unit_first, uint64_t unit_cap,
+                                                        const uint64_t *__restrict__ total_ptr) {
     const uint64_t total = *total_ptr;
     uint64_t n_units = (total + kGatherUnit - 1) / kGatherUnit;
     if (n_units > unit_cap) n_units = unit_cap;
     const int lane = threadIdx.x & 63;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t nw = (uint64_t)gridDim.x * (kBlock / 64);
-    for (uint64_t u = (uint64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6); u < n_units; u += nw) {
+    for (uint64_t u = (uint64_t)blockIdx.x * (kBlock / 64) + wave; u < n_units; u += nw) {
         const uint32_t flo = unit_first[u];
         const uint32_t fhi = (u + 1 < n_units) ? unit_first[u + 1] : n - 1;
-        for (int j = 0; j < 4; ++j) {
-            const uint64_t a = u * kGatherUnit + (uint64_t)j * 1024u + (uint64_t)lane * 16u;
-            if (a >= total) break;
-            uint32_t f = find_frame(dbase, flo, fhi, a);
-            const uint64_t fb = dbase[f], fe = dbase[f + 1];
-            if (a + 16 <= fe && a + 16 <= total) {
-                const fws_frame_desc fd = d[f];
-                const uint8_t *s = src + fd.payload_off + (a - fb);
-                // key byte of dst byte a+i: (a + i - fb + phase) & 3
-                const uint32_t rk = rotr32(fd.key, 8u * ((uint32_t)(a - fb + fd.phase) & 3u));
-                *reinterpret_cast<u32x4 *>(dst + a) = load16_unaligned(s) ^ rk;
-            } else {
-                for (uint64_t b = a; b < a + 16 && b < total; ++b) {
-                    while (b >= dbase[f + 1]) ++f;
+        const uint64_t a0 = u * kGatherUnit + (uint64_t)lane * 16u;
+        if (fhi - flo >= 2u) {                         // many small regions: per-chunk search
+            for (int j = 0; j < 4; ++j) {
+                const uint64_t a = a0 + (uint64_t)j * 1024u;
+                if (a >= total) break;
+                const uint32_t f = find_frame(dbase, flo, fhi, a);
+                const uint64_t fb = dbase[f], fe = dbase[f + 1];
+                if (a + 16 <= fe) {
                     const fws_frame_desc fd = d[f];
-                    const uint64_t k = b - dbase[f];
-                    const uint32_t kb = (fd.key >> (8u * ((uint32_t)(k + fd.phase) & 3u))) & 0xFFu;
-                    dst[b] = (uint8_t)(src[fd.payload_off + k] ^ kb);
+                    const uintptr_t sa = (uintptr_t)(src + fd.payload_off + (a - fb));
+                    const uintptr_t sb = sa & ~uintptr_t(15);
+                    const uint32_t sh = (uint32_t)(sa & 15u);
+                    const u32x4 v0 = gload16(sb), v1 = gload16(sh ? sb + 16u : sb);
+                    const uint32_t rk = rotr32(fd.key, 8u * ((uint32_t)(a - fb + fd.phase) & 3u));
+                    gstore16<true>((uintptr_t)(dst + a), shr_bytes(v0, v1, sh) ^ rk);
+                } else {
+                    gather_bytes(dst, src, d, dbase, f, a, total);
                 }
             }
+            continue;
+        }
+        // at most two regions: uniform metadata
+        const uint64_t B0 = dbase[flo], B1 = dbase[flo + 1];
+        const uint64_t B2 = fhi > flo ? dbase[flo + 2] : B1;
+        const fws_frame_desc d0 = d[flo], d1 = d[fhi];
+        const uintptr_t S0 = (uintptr_t)(src + d0.payload_off) - (uintptr_t)B0;   // src of dst byte a: S + a
+        const uintptr_t S1 = (uintptr_t)(src + d1.payload_off) - (uintptr_t)B1;
+        uintptr_t sb[4];
+        uint32_t sh[4], rk[4];
+        bool full[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint64_t a = a0 + (uint64_t)j * 1024u;
+            const bool in0 = a >= B0 && a + 16 <= B1;
+            const bool in1 = fhi > flo && a >= B1 && a + 16 <= B2;
+            full[j] = (in0 || in1) && a + 16 <= total;
+            const uintptr_t sa = (in1 ? S1 : S0) + (uintptr_t)a;
+            sb[j] = full[j] ? (sa & ~uintptr_t(15)) : ((uintptr_t)(src + d0.payload_off) & ~uintptr_t(15));
+            sh[j] = (uint32_t)(sa & 15u);
+            const uint32_t ph = in1 ? (uint32_t)(a - B1) + d1.phase : (uint32_t)(a - B0) + d0.phase;
+            rk[j] = rotr32(in1 ? d1.key : d0.key, 8u * (ph & 3u));
+        }
+        u32x4 v0[4], v1[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            v0[j] = gload16<true>(sb[j]);
+            v1[j] = gload16<true>(full[j] && sh[j] ? sb[j] + 16u : sb[j]);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint64_t a = a0 + (uint64_t)j * 1024u;
+            if (full[j]) gstore16<true>((uintptr_t)(dst + a), shr_bytes(v0[j], v1[j], sh[j]) ^ rk[j]);
+            else if (a < total) gather_bytes(dst, src, d, dbase, flo, a, total);
         }
     }
 }
@@ -236,13 +296,15 @@ int fws_launch_gather(uint8_t *dst, const uint8_t *src, const fws_frame_desc *d,
     if (n == 0) return 0;
     const uint32_t nb = (n + 1023) / 1024;
     hipLaunchKernelGGL(k_gather_count, dim3(nb), dim3(kBlock), 0, s, d, n, ws.block_sums);
-    hipLaunchKernelGGL(k_gather_scan, dim3(nb), dim3(kBlock), 0, s, d, n, ws.block_sums, ws.cbase, ws.unit_first,
-                       ws.unit_cap, ws.total);
+    hipLaunchKernelGGL(k_gather_scan, dim3(nb), dim3(kBlock), 0, s, d, n, ws.block_sums, ws.cbase, ws.total);
     uint64_t units = max_bytes / kGatherUnit + 1;
+    if (units > ws.unit_cap) units = ws.unit_cap;
+    hipLaunchKernelGGL(k_gather_units, dim3((unsigned)((units + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, ws.cbase,
+                       n, ws.unit_first, ws.unit_cap, ws.total);
     uint64_t blocks = (units + 3) / 4;
-    if (blocks > 2048) blocks = 2048;
+    if (blocks > 16384) blocks = 16384;
     if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL(k_gather, dim3((unsigned)blocks), dim3(kBlock), 0, s, dst, src, d, n, ws.cbase, ws.unit_first,
-                       ws.unit_cap, ws.total);
+    hipLaunchKernelGGL(k_gather_fast, dim3((unsigned)blocks), dim3(kBlock), 0, s, dst, src, d, n, ws.cbase,
+                       ws.unit_first, ws.unit_cap, ws.total);
     return fws_hip_status(hipGetLastError());
 }

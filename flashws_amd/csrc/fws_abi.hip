@@ -113,7 +113,6 @@ void fws_gpu_ctx_destroy(fws_gpu_ctx *ctx) {
     dev_free(d.st_n);
     dev_free(d.st_entry);
     dev_free(d.st_fbase);
-    dev_free(d.st_cbase);
     delete ctx;
 }
 
@@ -186,10 +185,9 @@ int fws_gpu_decode_stream(fws_gpu_ctx *ctx, void *dev_wire, uint64_t len, fws_fr
     if ((r = fws_ctx_ensure_plan(ctx, cap, units))) return r;
     if ((r = fws_launch_decode(ctx, (uint8_t *)dev_wire, len, dev_frames, cap, dev_result, s))) return r;
     if (cap == 0 || len == 0) return 0;
-    // k_resolve left the device frame count and the unmask plan of the decoded frames
+    // the resolve left the device frame count and the stream-space unmask plan of the decoded frames
     const uint32_t *n_dev = ctx->dec.counters + kDecodeFramesCounter;
-    if ((r = fws_launch_unmask((uint8_t *)dev_wire, ctx->dec.descs, cap, n_dev, ctx->plan,
-                               len / 16 + 2ull * cap, s)))
+    if ((r = fws_launch_unmask_stream((uint8_t *)dev_wire, len, dev_frames, cap, n_dev, ctx->plan.unit_first, s)))
         return r;
     if (dev_utf8_ok) return fws_launch_utf8_frames((const uint8_t *)dev_wire, len, dev_frames, cap, n_dev,
                                                    dev_utf8_ok, s);

@@ -22,9 +22,8 @@ struct fws_plan_ws {
 
 // Super-tile resolve records (merge_kernels.hip).
 struct fws_node_res {                 // per survivor: its chain inside its super tile
-    uint32_t tail;                    // EXIT: tail-list index; else the tail survivor's slot id
-    uint32_t cnt_kind;                // frames up to the tail (bits 0-29) | kind << 30
-    uint64_t cs;                      // unmask chunks of those frames
+    uint32_t tail;                    // EXIT: tail-list index; else the tail's ST-local index
+    uint32_t cnt_kind;                // frames up to the tail | ST-local index | kind (merge_kernels.hip)
 };
 struct fws_tail_rec {                 // one EXIT tail: a chain leaving its super tile
     uint64_t exit;                    // offset of the next header
@@ -36,7 +35,7 @@ struct fws_tail_rec {                 // one EXIT tail: a chain leaving its supe
 
 struct fws_st_node {                  // one survivor in its super tile's table (k_merge -> k_emit)
     fws_frame_info rec;
-    uint32_t ch;                      // unmask chunks of its payload
+    uint32_t pad32;
     uint16_t nx;                      // in-ST next (local index) or an exit code
     uint8_t wt;                       // 1: a frame, 0: an incomplete header
     uint8_t pad;
@@ -80,7 +79,6 @@ struct fws_decode_ws {
     uint32_t *st_n = nullptr;              // [max_st] survivors per super tile
     uint32_t *st_entry = nullptr;          // [max_st] slot id of the path's first header in the ST
     uint32_t *st_fbase = nullptr;          // [max_st] frames before the ST
-    uint64_t *st_cbase = nullptr;          // [max_st] unmask chunks before the ST
 };
 
 struct fws_gpu_ctx {
@@ -102,6 +100,9 @@ int fws_launch_plan(const uint8_t *base, const fws_frame_desc *d, uint32_t n, co
                     fws_plan_ws &ws, hipStream_t s);
 int fws_launch_unmask(uint8_t *base, const fws_frame_desc *d, uint32_t n, const uint32_t *n_dev,
                       const fws_plan_ws &ws, uint64_t max_chunks, hipStream_t s);
+// Decoded stream in stream-byte space: unit_first[u] = frame spanning byte 4 KiB * u (the decode's plan).
+int fws_launch_unmask_stream(uint8_t *base, uint64_t N, const fws_frame_info *frames, uint32_t cap,
+                             const uint32_t *n_dev, const uint32_t *unit_first, hipStream_t s);
 
 // text_kernels.hip
 int fws_launch_utf8_frames(const uint8_t *base, uint64_t N, const fws_frame_info *frames, uint32_t n,

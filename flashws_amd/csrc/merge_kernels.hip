@@ -1,6 +1,6 @@
 // merge_kernels.hip -- second half of fws_gpu_decode_stream on the common
-// path: from k_scan's per-tile survivors to the frame list, the payload
-// descriptors and the unmask plan in three launches, with no grid barrier.
+// path: from k_scan's per-tile survivors to the frame list and the unmask
+// plan in three launches, with no grid barrier.
 //
 // OnRecvData's frame loop (net/w_socket.h:543-769) is a chain: the next
 // header starts at this header's exit (hdr_off + hdr_len + payload_len,
@@ -10,29 +10,31 @@
 //
 //  k_merge  one workgroup per super tile (ST = 128 tiles = 256 KiB). Loads
 //           the ST's survivors (offset order), links each to the survivor at
-//           its exit inside the ST (binary search in LDS) and pointer-jumps
-//           (Wyllie) so every survivor knows the tail of its chain in the ST,
-//           the frames and unmask chunks up to that tail, and how the chain
+//           its exit inside the ST (search in the exit's tile, in LDS) and
+//           pointer-jumps (Wyllie) so every survivor knows the tail of its
+//           chain in the ST, the frames up to that tail, and how the chain
 //           leaves the ST: EXIT (into a later ST), END (at or past the stream
 //           end), DEAD (the exit is not a header: a protocol error or a false
 //           chain) or INC (an incomplete header at the stream end). EXIT
-//           tails go to a global list with the survivor their exit lands on
-//           (binary search in that tile's survivors). The ST's survivors are
-//           also written as one contiguous table for k_emit.
-//  k_link   one thread per EXIT tail: next(tail) = the tail of the landing
-//           survivor's chain; marks every next() target in a bitmap.
+//           tails go to a global list; the ST's survivors are also written as
+//           one contiguous table for k_emit.
+//  k_link   one thread per EXIT tail: the survivor its exit lands on (the
+//           tile's slots, one batch of loads) and next(tail) = the tail of
+//           that survivor's chain; marks every next() target in a bitmap.
 //  last WG  the k_link workgroup that finishes last (atomic ticket) resolves
 //           the path from the header at offset 0 over the marked tails,
 //           compacted into LDS. The path's tails are the greatest fixpoint of
 //           K = {root's tail} U next(K): offsets strictly increase along next,
 //           so a false tail has a finite chain of predecessors and drops out
 //           after a few rounds. Each landing survivor on the path is its ST's
-//           entry; a scan over the STs gives every ST's frame and chunk base.
+//           entry; a scan over the STs gives every ST's first frame index.
 //           The terminal is finished with ParseFrameHdr's rules
 //           (w_socket.h:435-524): error walk, carry-out, fws_decode_result.
 //  k_emit   one workgroup per ST with an entry: marks the entry's chain by
-//           pointer doubling over the ST's table and writes fws_frame_info,
-//           fws_frame_desc and the unmask plan (cbase, unit_first) in order.
+//           pointer doubling over the ST's table and writes fws_frame_info in
+//           stream order and the unmask plan: unit_first[u] = the frame whose
+//           span [hdr_off, next hdr_off) holds stream byte 4 KiB * u
+//           (k_unmask_stream, unmask_kernels.hip).
 //
 // Every global access on these paths is metadata (about 1 survivor per KiB of
 // stream); the kernels are latency-bound, so loads are issued in batches of
@@ -55,6 +57,7 @@ constexpr uint32_t kPer = kStCap / kMThreads;       // survivors per thread: i =
 constexpr uint32_t kTailCapMax = 1u << 18;          // LDS bitmap of the path pruning
 constexpr uint32_t kCompCap = 8192;                 // tails that are some tail's next (+ the root's)
 constexpr uint32_t kMaxPruneRounds = 64;
+constexpr uint64_t kUnit = 4096;                    // stream bytes per unmask plan unit
 
 // in-ST next of a survivor: an LDS index, or how the chain leaves the ST
 constexpr uint16_t kNxInc = 0xFFFC, kNxDead = 0xFFFD, kNxEnd = 0xFFFE, kNxExit = 0xFFFF;
@@ -65,6 +68,7 @@ constexpr uint16_t kCTerm = 0xFFFF;
 #ifdef FWS_SCAN_PROF
 // phase clocks (100 MHz wall clock, summed over workgroups) for tools/prof_scan.py
 __device__ unsigned long long g_merge_prof[32];
+#define MP_T0() const uint64_t mp_t0 = wall_clock64()
 #define MP_INIT() uint64_t mp_t = wall_clock64()
 #define MP_MARK(k)                                                                  \
     do {                                                                            \
@@ -83,6 +87,7 @@ __device__ unsigned long long g_merge_prof[32];
         }                                                                           \
     } while (0)
 #else
+#define MP_T0() do { } while (0)
 #define MP_INIT() do { } while (0)
 #define MP_MARK(k) do { } while (0)
 #define MP_ADD(k, v) do { } while (0)
@@ -119,15 +124,11 @@ struct MergeParams {
     uint32_t *st_n;
     uint32_t *st_entry;                              // local index of the ST's entry, or kNone
     uint32_t *st_fbase;
-    uint64_t *st_cbase;
     fws_frame_info *frames;
     uint32_t cap;
-    fws_frame_desc *descs;
     fws_decode_result *res;
-    uint64_t *cbase;                                 // unmask plan (fws_plan_ws)
-    uint32_t *unit_first;
-    uint64_t *plan_total;
-    uint64_t unit_cap;
+    uint32_t *unit_first;                            // unmask plan (fws_plan_ws), stream space
+    uint64_t n_units;                                // ceil(N / kUnit), clamped to the plan's capacity
 
     // slot id of survivor r of tile t (stage slots, or the tile's spill run)
     __device__ __forceinline__ uint32_t sid(uint32_t t, uint32_t sp, uint32_t r) const {
@@ -157,11 +158,11 @@ struct MergeParams {
         }
         return (lo < n && rec(sid(t, sp, lo))->hdr_off == x) ? sid(t, sp, lo) : kTermDead;
     }
-    __device__ __forceinline__ uint64_t node_chunks(const fws_frame_info &fi) const {
-        if (fi.hdr_len == 0) return 0;
-        const uint64_t po = fi.hdr_off + fi.hdr_len;
-        const uint64_t pl = (po + fi.payload_len > N) ? N - po : fi.payload_len;
-        return chunks_of((uintptr_t)(wire + po), pl);
+    // unit_first for frame f spanning stream bytes [h, e) (e = the next frame's
+    // header; the last frame < lim spans to the end of the stream)
+    __device__ __forceinline__ void plan_units(uint32_t f, uint64_t h, uint64_t e, bool last) const {
+        const uint64_t ue = last ? n_units : ((e + kUnit - 1) / kUnit < n_units ? (e + kUnit - 1) / kUnit : n_units);
+        for (uint64_t u = (h + kUnit - 1) / kUnit; u < ue; ++u) unit_first[u] = f;
     }
 };
 
@@ -196,15 +197,14 @@ struct MergeLds {
     uint32_t tcnt[kStTiles];
     uint32_t tsp[kStTiles];
     uint32_t tbase[kStTiles];
-    uint32_t off[kStCap];                            // hdr_off - ST start
-    uint32_t id[kStCap];                             // slot id
-    uint32_t ch[kStCap];                             // unmask chunks of the payload (0: INC)
+    union {
+        uint32_t off[kStCap];                        // hdr_off - ST start (the exit search)
+        uint32_t lref[kStCap];                       // then: EXIT tail's index in the ST's tail run
+    };
     uint16_t nx[kStCap];
     uint8_t wt[kStCap];                              // 1: a frame; 0: incomplete header
     uint16_t ptr[2][kStCap];                         // Wyllie pointer (tails point to themselves)
     uint16_t sc[2][kStCap];                          // frames from i up to ptr (exclusive)
-    uint32_t sh[2][kStCap];                          // chunks from i up to ptr (exclusive)
-    uint32_t lref[kStCap];                           // EXIT tail: index in the ST's tail run
     uint32_t red32[kMWaves];
     uint32_t n_tail, tail_base;
 };
@@ -213,9 +213,7 @@ __global__ __launch_bounds__(kMThreads) void k_merge(MergeParams P) {
     __shared__ MergeLds L;
     const uint32_t s = blockIdx.x, tid = threadIdx.x;
     uint32_t *const C = P.counters;
-#ifdef FWS_SCAN_PROF
-    const uint64_t mp_t0 = wall_clock64();
-#endif
+    MP_T0();
     MP_INIT();
     // the tail-target bitmap k_link sets
     for (uint64_t w = (uint64_t)s * kMThreads + tid; w < P.tail_cap / 32u + 1u; w += (uint64_t)gridDim.x * kMThreads)
@@ -274,9 +272,7 @@ __global__ __launch_bounds__(kMThreads) void k_merge(MergeParams P) {
             const uint32_t i = i0 + j;
             if (i < n) {
                 L.off[i] = (uint32_t)(r[j].hdr_off - st0);
-                L.id[i] = nid[j];
                 L.wt[i] = r[j].hdr_len ? 1 : 0;
-                L.ch[i] = (uint32_t)P.node_chunks(r[j]);
             }
         }
     }
@@ -308,9 +304,11 @@ __global__ __launch_bounds__(kMThreads) void k_merge(MergeParams P) {
         }
         if (!more) break;
     }
+    uint16_t vv[kPer];
 #pragma unroll
     for (uint32_t j = 0; j < kPer; ++j) {
         const uint32_t i = i0 + j;
+        vv[j] = kNxDead;
         if (i >= n) continue;
         uint16_t v;
         const uint64_t x = exit_of(r[j]);
@@ -318,22 +316,25 @@ __global__ __launch_bounds__(kMThreads) void k_merge(MergeParams P) {
         else if (x >= P.N) v = kNxEnd;
         else if (x >= st_end) v = kNxExit;
         else v = (sl[j] == 1 && L.off[sb[j]] == xr[j]) ? (uint16_t)sb[j] : kNxDead;
+        vv[j] = v;
         L.nx[i] = v;
         const bool tail = v >= kNxInc;
         L.ptr[0][i] = tail ? (uint16_t)i : v;
         L.sc[0][i] = tail ? 0 : L.wt[i];
-        L.sh[0][i] = tail ? 0u : L.ch[i];
-        if (v == kNxExit) L.lref[i] = atomicAdd(&L.n_tail, 1u);
         {                                            // two 16-B stores of the 32-B node
             uint32_t wd[8];
             __builtin_memcpy(wd, &r[j], sizeof(fws_frame_info));
-            wd[6] = L.ch[i];
+            wd[6] = 0u;
             wd[7] = (uint32_t)v | ((uint32_t)L.wt[i] << 16);
             u32x4 *dst = reinterpret_cast<u32x4 *>(tab + i);
             dst[0] = u32x4{wd[0], wd[1], wd[2], wd[3]};
             dst[1] = u32x4{wd[4], wd[5], wd[6], wd[7]};
         }
     }
+    __syncthreads();                                 // off[] dead: lref[] reuses it
+#pragma unroll
+    for (uint32_t j = 0; j < kPer; ++j)
+        if (i0 + j < n && vv[j] == kNxExit) L.lref[i0 + j] = atomicAdd(&L.n_tail, 1u);
     __syncthreads();
     MP_MARK(2);
     // reserve the ST's run of the tail list
@@ -346,7 +347,7 @@ __global__ __launch_bounds__(kMThreads) void k_merge(MergeParams P) {
         }
         L.tail_base = base;
     }
-    // pointer jumping: every survivor -> its chain's tail, with frame / chunk sums
+    // pointer jumping: every survivor -> its chain's tail, with frame counts
     int cur = 0;
     for (;;) {
         int changed = 0;
@@ -356,12 +357,10 @@ __global__ __launch_bounds__(kMThreads) void k_merge(MergeParams P) {
             if (p != q) {
                 L.ptr[cur ^ 1][i] = q;
                 L.sc[cur ^ 1][i] = (uint16_t)(L.sc[cur][i] + L.sc[cur][p]);
-                L.sh[cur ^ 1][i] = L.sh[cur][i] + L.sh[cur][p];
                 changed = 1;
             } else {
                 L.ptr[cur ^ 1][i] = p;
                 L.sc[cur ^ 1][i] = L.sc[cur][i];
-                L.sh[cur ^ 1][i] = L.sh[cur][i];
             }
         }
         cur ^= 1;
@@ -377,10 +376,9 @@ __global__ __launch_bounds__(kMThreads) void k_merge(MergeParams P) {
         const uint32_t t = L.ptr[cur][i];
         const uint32_t kind = kind_of(L.nx[t]);
         const uint32_t cnt = L.sc[cur][i] + L.wt[t];
-        const uint64_t cs = (uint64_t)L.sh[cur][i] + L.ch[t];
-        const uint32_t ref = kind == kKindExit ? tb + L.lref[t] : L.id[t];
-        P.nres[nid[j]] = fws_node_res{ref, cnt | (i << 12) | (kind << 30), cs};
-        if (L.nx[i] == kNxExit) {
+        const uint32_t ref = kind == kKindExit ? tb + L.lref[t] : t;
+        P.nres[nid[j]] = fws_node_res{ref, cnt | (i << 12) | (kind << 30)};
+        if (vv[j] == kNxExit) {
             const uint64_t x = exit_of(r[j]);
             P.tails[tb + L.lref[i]] = fws_tail_rec{x, nid[j], kTermDead, (uint32_t)(x / kStBytes), 0u};
         }
@@ -399,10 +397,8 @@ struct PathLds {
     uint16_t cnx[kCompCap];                          // compact next, or kCTerm
     uint32_t kb[2][kCompCap / 32];                   // kept bitmaps
     uint32_t red32[kMWaves];
-    uint64_t red64[kMWaves];
-    uint32_t root, rt, crt, root_ck;
-    uint64_t root_cs;
-    uint32_t end_id, end_kind, end_set;
+    uint32_t root, rt, crt, root_ck, end_kind, end_set;
+    const fws_frame_info *end_rec;                   // the path's last header
 };
 
 // Batched loop over c = tid + k * kMThreads < n: the loads of up to 4
@@ -424,9 +420,8 @@ __device__ __forceinline__ void batched4(uint32_t n, Load load, Use use) {
     }
 }
 
-// The path from offset 0 over the target tails: ST entries and bases,
-// terminal, result. Runs in the last k_link workgroup, after every other
-// workgroup's release and this workgroup's acquire.
+// The path from offset 0 over the target tails: ST entries and frame bases,
+// terminal, result. Runs in the last k_link workgroup.
 __device__ void resolve_path(const MergeParams &P, PathLds &G) {
     uint32_t *const C = P.counters;
     const uint32_t tid = threadIdx.x;
@@ -440,7 +435,6 @@ __device__ void resolve_path(const MergeParams &P, PathLds &G) {
     const uint64_t N = P.N;
     if (tid == 0) {
         uint32_t root = kNone, rt = kNone, ck = 0;
-        uint64_t cs = 0;
         if (P.n_tiles && P.tile_count[0]) {
             const uint32_t id0 = P.sid(0, P.tile_spill[0], 0);
             if (P.rec(id0)->hdr_off == 0) root = id0;
@@ -449,10 +443,9 @@ __device__ void resolve_path(const MergeParams &P, PathLds &G) {
         if (root != kNone) {
             const fws_node_res r = P.nres[root];
             ck = r.cnt_kind;
-            cs = r.cs;
             if (res_kind(ck) == kKindExit) rt = r.tail;
             else {                                   // the root's chain ends in ST 0
-                G.end_id = r.tail;
+                G.end_rec = &P.st_nodes[r.tail].rec;
                 G.end_kind = res_kind(ck);
                 G.end_set = 1;
             }
@@ -460,13 +453,11 @@ __device__ void resolve_path(const MergeParams &P, PathLds &G) {
         G.root = root;
         G.rt = rt;
         G.root_ck = ck;
-        G.root_cs = cs;
     }
     // ST bases start from zero counts
     for (uint32_t s = tid; s < n_st; s += kMThreads) {
         P.st_entry[s] = kNone;
         P.st_fbase[s] = 0;
-        P.st_cbase[s] = 0;
     }
     __syncthreads();
     MP_MARK(10);
@@ -545,7 +536,6 @@ __device__ void resolve_path(const MergeParams &P, PathLds &G) {
     if (tid == 0 && root != kNone) {
         P.st_entry[0] = res_lidx(G.root_ck);
         P.st_fbase[0] = res_cnt(G.root_ck);
-        P.st_cbase[0] = G.root_cs;
     }
     for (uint32_t base = tid; base < mc; base += 4u * kMThreads) {
         fws_tail_rec tr[4];
@@ -569,55 +559,41 @@ __device__ void resolve_path(const MergeParams &P, PathLds &G) {
             const uint32_t c = base + j * kMThreads;
             const bool ends = G.cnx[c] == kCTerm;    // exactly one kept tail ends the path
             if (tr[j].w == kTermDead) {
-                if (ends) { G.end_id = tr[j].id; G.end_kind = kKindDead; G.end_set = 1; }
+                if (ends) { G.end_rec = P.rec(tr[j].id); G.end_kind = kKindDead; G.end_set = 1; }
                 continue;
             }
             P.st_entry[tr[j].wst] = res_lidx(nr[j].cnt_kind);
             P.st_fbase[tr[j].wst] = res_cnt(nr[j].cnt_kind);
-            P.st_cbase[tr[j].wst] = nr[j].cs;
-            if (ends) { G.end_id = nr[j].tail; G.end_kind = res_kind(nr[j].cnt_kind); G.end_set = 1; }
+            if (ends) {
+                G.end_rec = &P.st_nodes[(uint64_t)tr[j].wst * kStCap + nr[j].tail].rec;
+                G.end_kind = res_kind(nr[j].cnt_kind);
+                G.end_set = 1;
+            }
         }
     }
     __syncthreads();
     MP_MARK(14);
 
-    // exclusive prefix of the per-ST frame and chunk counts, in ST order
+    // exclusive prefix of the per-ST frame counts, in ST order
     constexpr uint32_t kSper = 8;
     uint32_t nf_path = 0;
-    uint64_t cs_path = 0;
     for (uint32_t s0 = 0; s0 < n_st; s0 += kSper * kMThreads) {
         const uint32_t lo = s0 + tid * kSper;
         uint32_t fc[kSper];
-        uint64_t cc[kSper];
         uint32_t fs = 0;
-        uint64_t cs = 0;
 #pragma unroll
-        for (uint32_t j = 0; j < kSper; ++j) {
-            fc[j] = lo + j < n_st ? P.st_fbase[lo + j] : 0u;
-            cc[j] = lo + j < n_st ? P.st_cbase[lo + j] : 0ull;
-        }
+        for (uint32_t j = 0; j < kSper; ++j) fc[j] = lo + j < n_st ? P.st_fbase[lo + j] : 0u;
 #pragma unroll
-        for (uint32_t j = 0; j < kSper; ++j) {
-            fs += fc[j];
-            cs += cc[j];
-        }
+        for (uint32_t j = 0; j < kSper; ++j) fs += fc[j];
         uint32_t ft;
-        uint64_t ct;
         uint32_t fpre = nf_path + block_excl<uint32_t>(fs, G.red32, &ft);
-        uint64_t cpre = cs_path + block_excl<uint64_t>(cs, G.red64, &ct);
 #pragma unroll
         for (uint32_t j = 0; j < kSper; ++j) {
-            if (lo + j < n_st) {
-                P.st_fbase[lo + j] = fpre;
-                P.st_cbase[lo + j] = cpre;
-            }
+            if (lo + j < n_st) P.st_fbase[lo + j] = fpre;
             fpre += fc[j];
-            cpre += cc[j];
         }
         nf_path += ft;
-        cs_path += ct;
     }
-
     MP_MARK(15);
     MP_ADD(16, mc);
     if (tid != 0) return;
@@ -632,12 +608,11 @@ __device__ void resolve_path(const MergeParams &P, PathLds &G) {
     uint64_t pos = 0;
     bool walk = N > 0 && root == kNone;              // no chain from offset 0 survived
     if (root != kNone) {
-        const fws_frame_info fi = *P.rec(G.end_id);
+        const fws_frame_info fi = *G.end_rec;
         pos = G.end_kind == kKindInc ? fi.hdr_off : exit_of(fi);
         walk = G.end_kind == kKindDead;
     }
     uint32_t nf = nf_path;
-    uint64_t run = cs_path;
     const uint32_t cap = P.cap;
     if (walk) {
         for (;;) {
@@ -648,23 +623,12 @@ __device__ void resolve_path(const MergeParams &P, PathLds &G) {
             if (rc < 0) { r.status = rc; r.err_off = q; break; }
             if (rc == 0) break;                      // incomplete trailing header
             const uint64_t po = q + rc;
-            const uint64_t pl = (po + h.plen > N) ? N - po : h.plen;
             if (nf < cap) {
                 fws_frame_info fi;
                 fi.hdr_off = q; fi.payload_len = h.plen; fi.key = h.key; fi.opcode = (uint8_t)h.opcode;
                 fi.fin = (uint8_t)h.fin; fi.hdr_len = (uint8_t)rc;
                 fi.flags = (po + h.plen > N) ? (uint8_t)FWS_FRAME_TRUNCATED : (uint8_t)0;
                 P.frames[nf] = fi;
-                P.descs[nf] = fws_frame_desc{po, pl, h.key, 0u};
-                const uint64_t c = chunks_of((uintptr_t)(P.wire + po), pl);
-                P.cbase[nf] = run;
-                if (c) {
-                    uint64_t u = (run + kUnitChunks - 1) / kUnitChunks;
-                    uint64_t ue = (run + c + kUnitChunks - 1) / kUnitChunks;
-                    if (ue > P.unit_cap) ue = P.unit_cap;
-                    for (; u < ue; ++u) P.unit_first[u] = nf;
-                }
-                run += c;
             }
             ++nf;
             pos = po + h.plen;
@@ -681,9 +645,13 @@ __device__ void resolve_path(const MergeParams &P, PathLds &G) {
     r.n_frames = nf;
     const uint32_t lim = nf < cap ? nf : cap;
     C[kCntFrames] = lim;
-    if (lim == 0 || lim > nf_path) {                 // else k_emit's writer of frame lim - 1 closes the plan
-        P.cbase[lim] = lim ? run : 0;
-        *P.plan_total = lim ? run : 0;
+    if (lim > nf_path) {
+        // walk frames (within one tile; k_emit spans the path frames): each
+        // walk frame's span, the last one's to the end of the stream
+        for (uint32_t f = nf_path; f < lim; ++f) {
+            const uint64_t h = P.frames[f].hdr_off;
+            P.plan_units(f, h, f + 1 < lim ? P.frames[f + 1].hdr_off : 0, f + 1 == lim);
+        }
     }
     *P.res = r;
     MP_MARK(17);
@@ -703,9 +671,7 @@ __global__ __launch_bounds__(kMThreads) void k_link(MergeParams P) {
     __shared__ uint32_t s_last;
     const uint32_t tid = threadIdx.x;
     uint32_t *const C = P.counters;
-#ifdef FWS_SCAN_PROF
-    const uint64_t mp_t0 = wall_clock64();
-#endif
+    MP_T0();
     MP_INIT();
     const uint32_t M = C[kCntTails];
     const uint32_t x = blockIdx.x * kMThreads + tid;
@@ -740,21 +706,17 @@ struct EmitLds {
     uint16_t ptr[2][kStCap];
     uint8_t mark[kStCap];
     uint32_t red32[kMWaves];
-    uint64_t red64[kMWaves];
 };
 
 __global__ __launch_bounds__(kMThreads) void k_emit(MergeParams P) {
     __shared__ EmitLds L;
     const uint32_t s = blockIdx.x, tid = threadIdx.x;
     const uint32_t *const C = P.counters;
-#ifdef FWS_SCAN_PROF
-    const uint64_t mp_t0 = wall_clock64();
-#endif
+    MP_T0();
     MP_INIT();
     if (s >= P.n_st) return;
     const uint32_t fb = C[kCntFallback], e = P.st_entry[s], fbase = P.st_fbase[s], n = P.st_n[s];
     const uint32_t lim = C[kCntFrames];
-    const uint64_t cbase0 = P.st_cbase[s];
     if (fb || e == kNone || fbase >= lim || n > kStCap) return;
     const fws_st_node *const tab = P.st_nodes + (uint64_t)s * kStCap;
     const uint32_t i0 = kPer * tid;
@@ -788,47 +750,26 @@ __global__ __launch_bounds__(kMThreads) void k_emit(MergeParams P) {
         if (!__syncthreads_or(changed)) break;
     }
     MP_MARK(25);
-    // the chain's frames in offset order
+    // the chain's frames in offset order, and their stream-space plan units
     bool fr[kPer];
     uint32_t fl = 0;
-    uint64_t cl = 0;
 #pragma unroll
     for (uint32_t j = 0; j < kPer; ++j) {
         const uint32_t i = i0 + j;
         fr[j] = i < n && L.mark[i] && nd[j].wt;
-        if (fr[j]) {
-            ++fl;
-            cl += nd[j].ch;
-        }
+        fl += fr[j];
     }
     uint32_t ftot;
-    uint64_t ctot;
     uint32_t f = fbase + block_excl<uint32_t>(fl, L.red32, &ftot);
-    uint64_t cb = cbase0 + block_excl<uint64_t>(cl, L.red64, &ctot);
 #pragma unroll
     for (uint32_t j = 0; j < kPer; ++j) {
         if (!fr[j]) continue;
-        const fws_frame_info &fi = nd[j].rec;
-        const uint64_t c = nd[j].ch;
         if (f < lim) {
-            const uint64_t po = fi.hdr_off + fi.hdr_len;
-            const uint64_t pl = (po + fi.payload_len > P.N) ? P.N - po : fi.payload_len;
+            const fws_frame_info &fi = nd[j].rec;
             P.frames[f] = fi;
-            P.descs[f] = fws_frame_desc{po, pl, fi.key, 0u};
-            P.cbase[f] = cb;
-            if (c) {
-                uint64_t u = (cb + kUnitChunks - 1) / kUnitChunks;
-                uint64_t ue = (cb + c + kUnitChunks - 1) / kUnitChunks;
-                if (ue > P.unit_cap) ue = P.unit_cap;
-                for (; u < ue; ++u) P.unit_first[u] = f;
-            }
-            if (f == lim - 1) {
-                P.cbase[lim] = cb + c;
-                *P.plan_total = cb + c;
-            }
+            P.plan_units(f, fi.hdr_off, exit_of(fi), f == lim - 1);
         }
         ++f;
-        cb += c;
     }
     __syncthreads();
     MP_MARK(26);
@@ -884,15 +825,12 @@ int fws_launch_merge(fws_gpu_ctx *ctx, const uint8_t *wire, uint64_t N, uint32_t
     P.st_n = d.st_n;
     P.st_entry = d.st_entry;
     P.st_fbase = d.st_fbase;
-    P.st_cbase = d.st_cbase;
     P.frames = frames;
     P.cap = cap;
-    P.descs = d.descs;
     P.res = res;
-    P.cbase = ctx->plan.cbase;
     P.unit_first = ctx->plan.unit_first;
-    P.plan_total = ctx->plan.total;
-    P.unit_cap = ctx->plan.unit_cap;
+    const uint64_t units = (N + kUnit - 1) / kUnit;
+    P.n_units = units < ctx->plan.unit_cap ? units : ctx->plan.unit_cap;
     const dim3 grid(P.n_st ? P.n_st : 1u), blk(kMThreads);
     hipLaunchKernelGGL(k_merge, grid, blk, 0, s, P);
     hipLaunchKernelGGL(k_link, dim3((P.tail_cap + kMThreads - 1) / kMThreads), blk, 0, s, P);

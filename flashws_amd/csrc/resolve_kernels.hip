@@ -23,8 +23,8 @@
 //   9  finish         terminal -> fws_decode_result; a protocol error is
 //                     located by re-walking from the last good header with
 //                     ParseFrameHdr's rules (w_socket.h:435-524)
-//  10  plan           chunk prefix + unit map of the emitted descriptors for
-//                     k_unmask (the same plan k_plan_count / k_plan_scan make)
+//  10  plan           stream-space unit map of the emitted frames for
+//                     k_unmask_stream (unmask_kernels.hip)
 #include "decode_common.h"
 
 namespace fwsk {
@@ -178,7 +178,6 @@ __device__ __forceinline__ T grid_excl_scan(uint64_t n, Val val, Out out, uint64
 }
 
 __global__ __launch_bounds__(kRThreads) void k_resolve(ResolveParams P) {
-    __shared__ uint64_t sred64[kRThreads / 64];
     __shared__ uint32_t sred32[kRThreads / 64];
     GridBarrier bar{P.counters + kCntBarArrive, P.counters + kCntBarGen, P.counters + kCntOverflow};
     uint32_t *const C = P.counters;
@@ -399,24 +398,15 @@ __global__ __launch_bounds__(kRThreads) void k_resolve(ResolveParams P) {
     }
     bar.sync();
 
-    // 10  unmask plan of the emitted descriptors (k_plan_scan's outputs)
+    // 10  unmask plan in stream space (k_unmask_stream): frame f spans stream
+    //     bytes [hdr_off_f, hdr_off_{f+1}); the last frame spans to the end
     const uint32_t n = C[kCntFrames];
-    const uint8_t *const base = P.wire;
-    const uint64_t total = grid_excl_scan<uint64_t>(
-        n, [&](uint64_t f) { return chunks_of((uintptr_t)(base + P.descs[f].payload_off), P.descs[f].payload_len); },
-        [&](uint64_t f, uint64_t pre, uint64_t c) {
-            P.cbase[f] = pre;
-            if (c) {
-                uint64_t u = (pre + kUnitChunks - 1) / kUnitChunks;
-                uint64_t ue = (pre + c + kUnitChunks - 1) / kUnitChunks;
-                if (ue > P.unit_cap) ue = P.unit_cap;
-                for (; u < ue; ++u) P.unit_first[u] = (uint32_t)f;
-            }
-        },
-        P.bsums, sred64, bar);
-    if (gid == 0) {
-        P.cbase[n] = total;
-        *P.plan_total = total;
+    const uint64_t n_units = (P.N + 4095) / 4096 < P.unit_cap ? (P.N + 4095) / 4096 : P.unit_cap;
+    for (uint64_t f = gid; f < n; f += G) {
+        const uint64_t h = P.frames[f].hdr_off;
+        const uint64_t e = f + 1 < n ? P.frames[f + 1].hdr_off : n_units * 4096;
+        const uint64_t ue = (e + 4095) / 4096 < n_units ? (e + 4095) / 4096 : n_units;
+        for (uint64_t u = (h + 4095) / 4096; u < ue; ++u) P.unit_first[u] = (uint32_t)f;
     }
 }
 

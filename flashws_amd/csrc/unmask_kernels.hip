@@ -323,6 +323,113 @@ __global__ __launch_bounds__(kBlock) void k_unmask_fast(uint8_t *base, const fws
     }
 }
 
+// ----------------------------------------------------------- stream space
+// Unmask of a decoded wire stream (fws_gpu_decode_stream) in stream-byte
+// space: unit u = stream bytes [4 KiB u, 4 KiB (u + 1)), unit_first[u] = the
+// frame whose span [hdr_off, next hdr_off) holds the unit's first byte (the
+// decode writes it). Every 16-B chunk of the stream belongs to exactly one
+// lane, so a chunk is one 16-B load, an XOR with a per-byte key mask (zero on
+// header bytes and outside the decoded payloads) and one 16-B store -- no
+// partial stores. When the unit meets at most 2 frames (frames >= 4 KiB) the
+// metadata is wave-uniform; otherwise each chunk finds its frames.
+
+// Bytes of the dword at w that lie in [lo, hi), as a byte-select mask.
+__device__ __forceinline__ uint32_t byte_sel(uint64_t w, uint64_t lo, uint64_t hi) {
+    if (w + 4u <= lo || w >= hi) return 0u;
+    const uint32_t s = lo > w ? (uint32_t)(lo - w) : 0u;          // 0..3
+    const uint32_t e = hi < w + 4u ? (uint32_t)(w + 4u - hi) : 0u; // 0..3
+    return (0xFFFFFFFFu << (8u * s)) & (0xFFFFFFFFu >> (8u * e));
+}
+
+// Key mask of the chunk at stream offset c (16-aligned) for one payload region
+// [po, pe) with key k (phase 0 at po: w_socket.h:504,758).
+__device__ __forceinline__ u32x4 region_mask(uint64_t c, uint64_t po, uint64_t pe, uint32_t k) {
+    const uint32_t rk = rotr32(k, 8u * ((uint32_t)(c - po) & 3u));
+    return u32x4{rk & byte_sel(c, po, pe), rk & byte_sel(c + 4u, po, pe), rk & byte_sel(c + 8u, po, pe),
+                 rk & byte_sel(c + 12u, po, pe)};
+}
+
+struct StreamFrame {
+    uint64_t po, pe;                                 // payload [po, pe), clipped to the stream
+    uint32_t key;
+};
+
+__device__ __forceinline__ StreamFrame stream_frame(const fws_frame_info &fi, uint64_t N) {
+    const uint64_t po = fi.hdr_off + fi.hdr_len;
+    const uint64_t pe = po + fi.payload_len < N ? po + fi.payload_len : N;
+    return StreamFrame{po, pe, fi.key};
+}
+
+template <bool kNT>
+__global__ __launch_bounds__(kBlock) void k_unmask_stream(uint8_t *base, uint64_t N,
+                                                          const fws_frame_info *__restrict__ fr, uint32_t cap,
+                                                          const uint32_t *__restrict__ n_dev,
+                                                          const uint32_t *__restrict__ unit_first, uint64_t n_units) {
+    uint32_t n = *n_dev;
+    if (n > cap) n = cap;
+    if (n == 0) return;
+    const int lane = threadIdx.x & (kWave - 1);
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const uint64_t nwaves = uint64_t(gridDim.x) * (kBlock / kWave);
+    const uintptr_t b0 = (uintptr_t)base;
+    for (uint64_t u = uint64_t(blockIdx.x) * (kBlock / kWave) + wave; u < n_units; u += nwaves) {
+        const uint32_t flo = unit_first[u];
+        const uint32_t fhi = (u + 1 < n_units) ? unit_first[u + 1] : n - 1;
+        const uint64_t c0 = u * 4096u + uint64_t(lane) * 16u;
+        if (fhi - flo >= 2u) {                       // small frames: per-chunk search
+#pragma unroll 1
+            for (int j = 0; j < kUnmaskU; ++j) {
+                const uint64_t c = c0 + uint64_t(j) * 1024u;
+                if (c >= N) break;
+                uint32_t lo = flo, hi = fhi;         // last frame with hdr_off <= c
+                while (lo < hi) {
+                    const uint32_t mid = lo + ((hi - lo + 1u) >> 1);
+                    if (fr[mid].hdr_off <= c) lo = mid; else hi = mid - 1u;
+                }
+                u32x4 m{0u, 0u, 0u, 0u};
+                for (uint32_t f = lo; f < n; ++f) {
+                    const fws_frame_info fi = fr[f];
+                    if (fi.hdr_off >= c + 16u) break;
+                    const StreamFrame sf = stream_frame(fi, N);
+                    m |= region_mask(c, sf.po, sf.pe, sf.key);
+                }
+                if (m.x | m.y | m.z | m.w) {
+                    const uintptr_t a = b0 + c;
+                    gstore16<kNT>(a, gload16<kNT>(a) ^ m);
+                }
+            }
+            continue;
+        }
+        const StreamFrame A = stream_frame(fr[flo], N), B = stream_frame(fr[fhi], N);
+        const bool two = fhi != flo;
+        uintptr_t ca[kUnmaskU];
+        u32x4 mk[kUnmaskU];
+        bool live[kUnmaskU];
+#pragma unroll
+        for (int j = 0; j < kUnmaskU; ++j) {
+            const uint64_t c = c0 + uint64_t(j) * 1024u;
+            ca[j] = b0 + c;
+            const bool inA = c >= A.po && c + 16u <= A.pe, inB = two && c >= B.po && c + 16u <= B.pe;
+            if (inA || inB) {
+                const uint32_t rk = inA ? rotr32(A.key, 8u * ((uint32_t)(c - A.po) & 3u))
+                                        : rotr32(B.key, 8u * ((uint32_t)(c - B.po) & 3u));
+                mk[j] = u32x4{rk, rk, rk, rk};
+            } else {
+                mk[j] = region_mask(c, A.po, A.pe, A.key);
+                if (two) mk[j] |= region_mask(c, B.po, B.pe, B.key);
+            }
+            live[j] = c < N && (mk[j].x | mk[j].y | mk[j].z | mk[j].w);
+        }
+        const uintptr_t safe = b0 + (A.po & ~uint64_t(15));
+        u32x4 v[kUnmaskU];
+#pragma unroll
+        for (int j = 0; j < kUnmaskU; ++j) v[j] = gload16<kNT>(live[j] ? ca[j] : safe);
+#pragma unroll
+        for (int j = 0; j < kUnmaskU; ++j)
+            if (live[j]) gstore16<kNT>(ca[j], v[j] ^ mk[j]);
+    }
+}
+
 }  // namespace fwsk
 
 // ---------------------------------------------------------------- launchers
@@ -368,6 +475,15 @@ int fws_launch_plan(const uint8_t *base, const fws_frame_desc *d, uint32_t n, co
     hipLaunchKernelGGL(k_plan_count, dim3(nb), dim3(kBlock), 0, s, base, d, n, n_dev, ws.block_sums);
     hipLaunchKernelGGL(k_plan_scan, dim3(nb), dim3(kBlock), 0, s, base, d, n, n_dev, ws.block_sums, ws.cbase,
                        ws.unit_first, ws.total, ws.unit_cap);
+    return fws_hip_status(hipGetLastError());
+}
+
+int fws_launch_unmask_stream(uint8_t *base, uint64_t N, const fws_frame_info *frames, uint32_t cap,
+                             const uint32_t *n_dev, const uint32_t *unit_first, hipStream_t s) {
+    const uint64_t units = (N + 4095) / 4096;
+    if (units == 0 || cap == 0) return 0;
+    hipLaunchKernelGGL(k_unmask_stream<true>, dim3(grid_for_units(units)), dim3(kBlock), 0, s, (uint8_t *)base, N,
+                       frames, cap, n_dev, unit_first, units);
     return fws_hip_status(hipGetLastError());
 }
 

@@ -34,6 +34,7 @@ enum Counter {
     kCntTails = 11,      // super-tile exit tails appended by k_merge
     kCntCount = 12
 };
+constexpr uint32_t kCntStride = 16;          // words per counter set (fws_decode_ws::cnt_base)
 static_assert(kCntFrames == kDecodeFramesCounter, "fws_internal.h names the frame counter");
 
 constexpr uint32_t kSlots = 8;               // per-tile survivor slots before spilling

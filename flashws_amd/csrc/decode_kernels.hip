@@ -565,7 +565,7 @@ int fws_decode_ensure(fws_gpu_ctx *ctx, uint64_t N, uint32_t cap) {
     const uint64_t nd = cap > d.max_descs ? cap : d.max_descs;
     auto rel = [](auto *&p) { if (p) (void)hipFree(p); p = nullptr; };
     rel(d.tile_count); rel(d.tile_base); rel(d.tile_entry); rel(d.tile_frames); rel(d.fbase);
-    rel(d.surv_info); rel(d.surv_leaf); rel(d.jump); rel(d.on_path); rel(d.counters);
+    rel(d.surv_info); rel(d.surv_leaf); rel(d.jump); rel(d.on_path); rel(d.cnt_base);
     rel(d.descs); rel(d.stage_info); rel(d.stage_leaf); rel(d.spill_info); rel(d.spill_leaf); rel(d.tile_spill);
     hipError_t e = hipSuccess;
     auto al = [&](auto **p, uint64_t bytes) { if (e == hipSuccess) e = hipMalloc((void **)p, bytes ? bytes : 16); };
@@ -573,7 +573,9 @@ int fws_decode_ensure(fws_gpu_ctx *ctx, uint64_t N, uint32_t cap) {
     al(&d.tile_frames, nt * 4); al(&d.fbase, nt * 4);
     al(&d.surv_info, ns * sizeof(fws_frame_info)); al(&d.surv_leaf, ns * 4);
     al(&d.jump, (uint64_t)nl * ns * 4); al(&d.on_path, ns);
-    al(&d.counters, kCntCount * 4 + 16);
+    al(&d.cnt_base, 2 * kCntStride * 4);
+    d.counters = d.cnt_base;
+    d.cnt_dirty = true;
     al(&d.descs, (nd + 1) * sizeof(fws_frame_desc));
     if (d.scan_grid == 0) {
         int cus = 0;
@@ -613,7 +615,15 @@ int fws_launch_decode(fws_gpu_ctx *ctx, uint8_t *wire, uint64_t N, fws_frame_inf
     const uint32_t n_tiles = (uint32_t)((N + kTile - 1) / kTile);
     const uint32_t K = ceil_log2(2ull * n_tiles + 2) + 1;
     hipError_t e;
-    if ((e = hipMemsetAsync(d.counters, 0, kCntCount * 4, s)) != hipSuccess) return fws_hip_status(e);
+    // counters: this call's set was zeroed by the previous call's k_resolve launch
+    d.parity ^= 1u;
+    d.counters = d.cnt_base + d.parity * kCntStride;
+    uint32_t *const next = d.cnt_base + (d.parity ^ 1u) * kCntStride;
+    if (d.cnt_dirty) {
+        if ((e = hipMemsetAsync(d.counters, 0, kCntStride * 4, s)) != hipSuccess) return fws_hip_status(e);
+        d.cnt_dirty = false;
+    }
+    d.cnt_dirty = true;                  // until every launch of this call is queued
     if (n_tiles) {
         const uint32_t need = (n_tiles + kScanWaves - 1) / kScanWaves;
         const uint32_t sg = need < d.scan_grid ? need : d.scan_grid;
@@ -623,11 +633,13 @@ int fws_launch_decode(fws_gpu_ctx *ctx, uint8_t *wire, uint64_t N, fws_frame_inf
         if ((e = hipGetLastError()) != hipSuccess) return fws_hip_status(e);
     }
     // super-tile resolve (common case); k_resolve runs only if it set kCntFallback.
-    // Its per-chain chunk sums are 32-bit: streams of 2^35 B and more take k_resolve.
-    const bool fast = N < (1ull << 35) && g_resolve_mode != 1;
+    // Slot ids are 32-bit (8 per tile): streams of 2^39 B and more take k_resolve.
+    const bool fast = N < (1ull << 39) && g_resolve_mode != 1;
     if (fast) {
         int r = fws_launch_merge(ctx, wire, N, n_tiles, frames, cap, res, s);
         if (r) return r;
     }
-    return fws_launch_resolve(ctx, wire, N, n_tiles, K, frames, cap, res, fast ? 1 : 0, s);
+    const int r = fws_launch_resolve(ctx, wire, N, n_tiles, K, frames, cap, res, fast ? 1 : 0, next, s);
+    if (r == 0) d.cnt_dirty = false;
+    return r;
 }

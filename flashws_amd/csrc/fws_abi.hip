@@ -96,7 +96,7 @@ void fws_gpu_ctx_destroy(fws_gpu_ctx *ctx) {
     dev_free(d.surv_leaf);
     dev_free(d.jump);
     dev_free(d.on_path);
-    dev_free(d.counters);
+    dev_free(d.cnt_base);
     dev_free(d.descs);
     dev_free(d.stage_info);
     dev_free(d.stage_leaf);

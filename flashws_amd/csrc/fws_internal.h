@@ -33,13 +33,9 @@ struct fws_tail_rec {                 // one EXIT tail: a chain leaving its supe
     uint32_t pad;
 };
 
-struct fws_st_node {                  // one survivor in its super tile's table (k_merge -> k_emit)
-    fws_frame_info rec;
-    uint32_t pad32;
-    uint16_t nx;                      // in-ST next (local index) or an exit code
-    uint8_t wt;                       // 1: a frame, 0: an incomplete header
-    uint8_t pad;
-};
+// one survivor in its super tile's table (k_merge -> k_emit):
+// slot id (bits 0-31) | in-ST next or exit code (32-47) | frame bit (48)
+typedef uint64_t fws_st_node;
 
 // Stream-decode workspace (decode_kernels.hip).
 struct fws_decode_ws {
@@ -56,7 +52,10 @@ struct fws_decode_ws {
     uint32_t *surv_leaf = nullptr;    // leaf (last in-tile header) of each survivor's chain
     uint32_t *jump = nullptr;         // [levels][max_surv] pointer-doubling tables
     uint8_t *on_path = nullptr;       // survivor is a true frame header
-    uint32_t *counters = nullptr;     // see decode_kernels.hip Counter
+    uint32_t *counters = nullptr;     // this call's set (decode_common.h Counter)
+    uint32_t *cnt_base = nullptr;     // two sets of kCntStride words: a call uses one, its k_resolve
+    uint32_t parity = 0;              //   launch zeroes the other for the next call (no memset launch)
+    bool cnt_dirty = true;            // zero this call's set first (new allocation, failed call)
     fws_frame_desc *descs = nullptr;  // payload regions of the decoded frames
     fws_frame_info *stage_info = nullptr;  // per-tile survivor slots (k_scan)
     uint32_t *stage_leaf = nullptr;
@@ -75,7 +74,7 @@ struct fws_decode_ws {
     fws_tail_rec *tails = nullptr;         // [tail_cap]
     uint32_t *gnx = nullptr;               // [tail_cap] next tail / terminal
     uint32_t *tmark = nullptr;             // [tail_cap / 32 + 1] tails that are some tail's next
-    fws_st_node *st_nodes = nullptr;       // [max_st * 2048] survivors per super tile
+    fws_st_node *st_nodes = nullptr;       // [max_st * 2048] survivors per super tile (8 B each)
     uint32_t *st_n = nullptr;              // [max_st] survivors per super tile
     uint32_t *st_entry = nullptr;          // [max_st] slot id of the path's first header in the ST
     uint32_t *st_fbase = nullptr;          // [max_st] frames before the ST
@@ -120,7 +119,8 @@ int fws_launch_decode(fws_gpu_ctx *ctx, uint8_t *wire, uint64_t N, fws_frame_inf
 // resolve_kernels.hip: frames, descriptors and the unmask plan from k_scan's survivors
 // gate != 0: only if the super-tile resolve set kCntFallback (else the launch returns at once)
 int fws_launch_resolve(fws_gpu_ctx *ctx, const uint8_t *wire, uint64_t N, uint32_t n_tiles, uint32_t K,
-                       fws_frame_info *frames, uint32_t cap, fws_decode_result *res, int gate, hipStream_t s);
+                       fws_frame_info *frames, uint32_t cap, fws_decode_result *res, int gate,
+                       uint32_t *zero_next, hipStream_t s);
 // merge_kernels.hip: the super-tile resolve (k_merge + k_emit), the common path
 uint64_t fws_merge_super_tiles(uint64_t n_tiles);
 uint32_t fws_merge_tail_cap(uint64_t n_tiles);

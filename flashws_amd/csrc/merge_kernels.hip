@@ -321,15 +321,7 @@ __global__ __launch_bounds__(kMThreads) void k_merge(MergeParams P) {
         const bool tail = v >= kNxInc;
         L.ptr[0][i] = tail ? (uint16_t)i : v;
         L.sc[0][i] = tail ? 0 : L.wt[i];
-        {                                            // two 16-B stores of the 32-B node
-            uint32_t wd[8];
-            __builtin_memcpy(wd, &r[j], sizeof(fws_frame_info));
-            wd[6] = 0u;
-            wd[7] = (uint32_t)v | ((uint32_t)L.wt[i] << 16);
-            u32x4 *dst = reinterpret_cast<u32x4 *>(tab + i);
-            dst[0] = u32x4{wd[0], wd[1], wd[2], wd[3]};
-            dst[1] = u32x4{wd[4], wd[5], wd[6], wd[7]};
-        }
+        tab[i] = (uint64_t)nid[j] | ((uint64_t)v << 32) | ((uint64_t)L.wt[i] << 48);
     }
     __syncthreads();                                 // off[] dead: lref[] reuses it
 #pragma unroll
@@ -445,7 +437,7 @@ __device__ void resolve_path(const MergeParams &P, PathLds &G) {
             ck = r.cnt_kind;
             if (res_kind(ck) == kKindExit) rt = r.tail;
             else {                                   // the root's chain ends in ST 0
-                G.end_rec = &P.st_nodes[r.tail].rec;
+                G.end_rec = P.rec((uint32_t)P.st_nodes[r.tail]);
                 G.end_kind = res_kind(ck);
                 G.end_set = 1;
             }
@@ -565,7 +557,7 @@ __device__ void resolve_path(const MergeParams &P, PathLds &G) {
             P.st_entry[tr[j].wst] = res_lidx(nr[j].cnt_kind);
             P.st_fbase[tr[j].wst] = res_cnt(nr[j].cnt_kind);
             if (ends) {
-                G.end_rec = &P.st_nodes[(uint64_t)tr[j].wst * kStCap + nr[j].tail].rec;
+                G.end_rec = P.rec((uint32_t)P.st_nodes[(uint64_t)tr[j].wst * kStCap + nr[j].tail]);
                 G.end_kind = res_kind(nr[j].cnt_kind);
                 G.end_set = 1;
             }
@@ -722,13 +714,13 @@ __global__ __launch_bounds__(kMThreads) void k_emit(MergeParams P) {
     const uint32_t i0 = kPer * tid;
     fws_st_node nd[kPer];
 #pragma unroll
-    for (uint32_t j = 0; j < kPer; ++j)
-        if (i0 + j < n) nd[j] = tab[i0 + j];
+    for (uint32_t j = 0; j < kPer; ++j) nd[j] = i0 + j < n ? tab[i0 + j] : 0ull;
 #pragma unroll
     for (uint32_t j = 0; j < kPer; ++j) {
         const uint32_t i = i0 + j;
         if (i < n) {
-            L.ptr[0][i] = nd[j].nx >= kNxInc ? (uint16_t)i : nd[j].nx;
+            const uint16_t v = (uint16_t)(nd[j] >> 32);
+            L.ptr[0][i] = v >= kNxInc ? (uint16_t)i : v;
             L.mark[i] = i == e;
         }
     }
@@ -750,24 +742,28 @@ __global__ __launch_bounds__(kMThreads) void k_emit(MergeParams P) {
         if (!__syncthreads_or(changed)) break;
     }
     MP_MARK(25);
-    // the chain's frames in offset order, and their stream-space plan units
+    // the chain's frames in offset order (records loaded in one batch), and
+    // their stream-space plan units
     bool fr[kPer];
     uint32_t fl = 0;
 #pragma unroll
     for (uint32_t j = 0; j < kPer; ++j) {
         const uint32_t i = i0 + j;
-        fr[j] = i < n && L.mark[i] && nd[j].wt;
+        fr[j] = i < n && L.mark[i] && ((nd[j] >> 48) & 1u);
         fl += fr[j];
     }
+    fws_frame_info rc[kPer];
+#pragma unroll
+    for (uint32_t j = 0; j < kPer; ++j)
+        if (fr[j]) rc[j] = *P.rec((uint32_t)nd[j]);
     uint32_t ftot;
     uint32_t f = fbase + block_excl<uint32_t>(fl, L.red32, &ftot);
 #pragma unroll
     for (uint32_t j = 0; j < kPer; ++j) {
         if (!fr[j]) continue;
         if (f < lim) {
-            const fws_frame_info &fi = nd[j].rec;
-            P.frames[f] = fi;
-            P.plan_units(f, fi.hdr_off, exit_of(fi), f == lim - 1);
+            P.frames[f] = rc[j];
+            P.plan_units(f, rc[j].hdr_off, exit_of(rc[j]), f == lim - 1);
         }
         ++f;
     }

@@ -64,6 +64,7 @@ struct ResolveParams {
     uint64_t *plan_total;
     uint64_t unit_cap;
     uint32_t gate;                                // 1: run only if the super-tile resolve fell back
+    uint32_t *zero_next;                          // the next call's counter set (zeroed here)
 };
 
 // Grid barrier of a cooperative launch. Arrivals only grow within a launch
@@ -185,6 +186,7 @@ __global__ __launch_bounds__(kRThreads) void k_resolve(ResolveParams P) {
     const uint64_t gid = (uint64_t)blockIdx.x * kRThreads + tid, G = (uint64_t)gridDim.x * kRThreads;
     const uint64_t gwave = gid >> 6, nwaves = G >> 6;
     const uint32_t n_tiles = P.n_tiles;
+    if (blockIdx.x == 0 && threadIdx.x < kCntStride) P.zero_next[threadIdx.x] = 0u;
     if (P.gate && C[kCntFallback] == 0) return;   // merge_kernels.hip resolved this stream
 
     // 1  tile prefix (+ per-tile / global defaults)
@@ -416,10 +418,12 @@ __global__ __launch_bounds__(kRThreads) void k_resolve(ResolveParams P) {
 using namespace fwsk;
 
 int fws_launch_resolve(fws_gpu_ctx *ctx, const uint8_t *wire, uint64_t N, uint32_t n_tiles, uint32_t K,
-                       fws_frame_info *frames, uint32_t cap, fws_decode_result *res, int gate, hipStream_t s) {
+                       fws_frame_info *frames, uint32_t cap, fws_decode_result *res, int gate, uint32_t *zero_next,
+                       hipStream_t s) {
     fws_decode_ws &d = ctx->dec;
     ResolveParams P;
     P.gate = gate ? 1u : 0u;
+    P.zero_next = zero_next;
     P.wire = wire;
     P.N = N;
     P.n_tiles = n_tiles;

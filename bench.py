@@ -268,7 +268,8 @@ def stream_decode_extra(ctx, wire_c2, dev, args):
         assert int(r["status"]) == 0 and int(r["n_frames"]) == n_frames, (name, r)
         payload = int(gpu.read_frames(frames, n_frames)["payload_len"].sum())
         rec = {"GiB_per_s": round(payload / t / GIB, 1), "ms_per_step": round(t * 1e3, 4), "frames": n_frames,
-               "wire_bytes": len(wire), "alg_GB_per_s": round((len(wire) + payload) / t / 1e9, 1)}
+               "wire_bytes": len(wire), "alg_GB_per_s": round((len(wire) + payload) / t / 1e9, 1),
+               "resolve": "k_resolve (fallback)" if gpu.decode_fell_back(c) else "super-tile"}
         if utf8:
             rec["utf8_invalid_frames"] = int((ok[:n_frames] == 0).sum().item())
         del bufs

@@ -109,6 +109,7 @@ void fws_gpu_ctx_destroy(fws_gpu_ctx *ctx) {
     dev_free(d.tails);
     dev_free(d.gnx);
     dev_free(d.tmark);
+    dev_free(d.comp);
     dev_free(d.st_nodes);
     dev_free(d.st_n);
     dev_free(d.st_entry);

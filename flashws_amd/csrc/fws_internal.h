@@ -74,6 +74,7 @@ struct fws_decode_ws {
     fws_tail_rec *tails = nullptr;         // [tail_cap]
     uint32_t *gnx = nullptr;               // [tail_cap] next tail / terminal
     uint32_t *tmark = nullptr;             // [tail_cap / 32 + 1] tails that are some tail's next
+    uint32_t *comp = nullptr;              // [fws_merge_comp_cap()] marked tails, compacted
     fws_st_node *st_nodes = nullptr;       // [max_st * 2048] survivors per super tile (8 B each)
     uint32_t *st_n = nullptr;              // [max_st] survivors per super tile
     uint32_t *st_entry = nullptr;          // [max_st] slot id of the path's first header in the ST
@@ -125,5 +126,6 @@ int fws_launch_resolve(fws_gpu_ctx *ctx, const uint8_t *wire, uint64_t N, uint32
 uint64_t fws_merge_super_tiles(uint64_t n_tiles);
 uint32_t fws_merge_tail_cap(uint64_t n_tiles);
 uint64_t fws_merge_st_nodes(uint64_t n_tiles);
+uint32_t fws_merge_comp_cap();
 int fws_launch_merge(fws_gpu_ctx *ctx, const uint8_t *wire, uint64_t N, uint32_t n_tiles, fws_frame_info *frames,
                      uint32_t cap, fws_decode_result *res, hipStream_t s);

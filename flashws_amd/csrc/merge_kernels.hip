@@ -55,7 +55,7 @@ constexpr int kMThreads = 512;
 constexpr int kMWaves = kMThreads / 64;
 constexpr uint32_t kPer = kStCap / kMThreads;       // survivors per thread: i = kPer * tid + j
 constexpr uint32_t kTailCapMax = 1u << 18;          // LDS bitmap of the path pruning
-constexpr uint32_t kCompCap = 8192;                 // tails that are some tail's next (+ the root's)
+constexpr uint32_t kCompCap = 32768;                // tails that are some tail's next (+ the root's)
 constexpr uint32_t kMaxPruneRounds = 64;
 constexpr uint64_t kUnit = 4096;                    // stream bytes per unmask plan unit
 
@@ -120,6 +120,7 @@ struct MergeParams {
     fws_tail_rec *tails;
     uint32_t *gnx;
     uint32_t *tmark;                                 // tail-target bitmap (tail_cap / 32 + 1 words)
+    uint32_t *comp;                                  // [kCompCap] compact index -> tail index
     fws_st_node *st_nodes;                           // [n_st][kStCap]
     uint32_t *st_n;
     uint32_t *st_entry;                              // local index of the ST's entry, or kNone
@@ -385,8 +386,7 @@ __global__ __launch_bounds__(kMThreads) void k_merge(MergeParams P) {
 struct PathLds {
     uint32_t words[kTailCapMax / 32];                // tail-target bitmap (+ the root's tail)
     uint32_t wpre[kTailCapMax / 32];                 // marked tails before each word
-    uint32_t comp[kCompCap];                         // compact index -> tail index
-    uint16_t cnx[kCompCap];                          // compact next, or kCTerm
+    uint16_t cnx[kCompCap];                          // compact next, or kCTerm (comp: P.comp)
     uint32_t kb[2][kCompCap / 32];                   // kept bitmaps
     uint32_t red32[kMWaves];
     uint32_t root, rt, crt, root_ck, end_kind, end_set;
@@ -480,7 +480,7 @@ __device__ void resolve_path(const MergeParams &P, PathLds &G) {
         while (v) {
             const uint32_t b = (uint32_t)__ffs(v) - 1u;
             v &= v - 1u;
-            G.comp[pre++] = w * 32u + b;
+            P.comp[pre++] = w * 32u + b;
         }
     }
     __syncthreads();
@@ -488,7 +488,7 @@ __device__ void resolve_path(const MergeParams &P, PathLds &G) {
     auto rank = [&](uint32_t x) -> uint32_t {
         return G.wpre[x >> 5] + (uint32_t)__popc(G.words[x >> 5] & ((1u << (x & 31u)) - 1u));
     };
-    batched4(mc, [&](uint32_t c) { return ld_acq(&P.gnx[G.comp[c]]); },
+    batched4(mc, [&](uint32_t c) { return ld_acq(&P.gnx[P.comp[c]]); },
              [&](uint32_t c, uint32_t g) { G.cnx[c] = g >= kGTerm ? kCTerm : (uint16_t)rank(g); });
     if (tid == 0) G.crt = rt == kNone ? kNone : rank(rt);
     __syncthreads();
@@ -538,8 +538,9 @@ __device__ void resolve_path(const MergeParams &P, PathLds &G) {
             const uint32_t c = base + j * kMThreads;
             kept[j] = c < mc && ((ka[c >> 5] >> (c & 31u)) & 1u);
             if (kept[j]) {
-                tr[j] = P.tails[G.comp[c]];
-                tr[j].w = ld_acq(&P.tails[G.comp[c]].w);      // handed off in this launch
+                const uint32_t x = P.comp[c];
+                tr[j] = P.tails[x];
+                tr[j].w = ld_acq(&P.tails[x].w);              // handed off in this launch
             }
         }
 #pragma unroll
@@ -793,6 +794,8 @@ using namespace fwsk;
 uint64_t fws_merge_super_tiles(uint64_t n_tiles) { return (n_tiles + kStTiles - 1) / kStTiles; }
 uint64_t fws_merge_st_nodes(uint64_t n_tiles) { return fws_merge_super_tiles(n_tiles) * kStCap; }
 
+uint32_t fws_merge_comp_cap() { return kCompCap; }
+
 uint32_t fws_merge_tail_cap(uint64_t n_tiles) {
     uint64_t c = fws_merge_super_tiles(n_tiles) * 64u + 4096u;
     return (uint32_t)(c < kTailCapMax ? c : kTailCapMax);
@@ -817,6 +820,7 @@ int fws_launch_merge(fws_gpu_ctx *ctx, const uint8_t *wire, uint64_t N, uint32_t
     P.tails = d.tails;
     P.gnx = d.gnx;
     P.tmark = d.tmark;
+    P.comp = d.comp;
     P.st_nodes = d.st_nodes;
     P.st_n = d.st_n;
     P.st_entry = d.st_entry;

@@ -8,56 +8,56 @@
 // F5..FF, the second byte after E0/ED/F0/F4 lies in its narrowed range, and
 // no lead runs past the end. That test needs only the 3 preceding bytes, so a
 // 16-B window is checked independently given its 3-byte left context: one
-// wave per frame, 1 KiB per wave step, a wave-wide AND per frame.
+// wave per frame, 1 KiB per wave step, bytewise in 32-bit SWAR, a wave-wide
+// OR of the error flags per frame.
 #include "fws_device.h"
 #include "fws_internal.h"
 
 namespace fwsk {
 
-__device__ __forceinline__ uint32_t utf8_need(uint32_t c) {
-    return (c >= 0xC2u && c <= 0xDFu) ? 1u : (c >= 0xE0u && c <= 0xEFu) ? 2u : (c >= 0xF0u && c <= 0xF4u) ? 3u : 0u;
+// Byte-select mask of the dword at address w: bytes inside [lo, hi).
+__device__ __forceinline__ uint32_t sel_bytes(uintptr_t w, uintptr_t lo, uintptr_t hi) {
+    if (w + 4u <= lo || w >= hi) return 0u;
+    const uint32_t s = lo > w ? (uint32_t)(lo - w) : 0u;
+    const uint32_t e = hi < w + 4u ? (uint32_t)(w + 4u - hi) : 0u;
+    return (0xFFFFFFFFu << (8u * s)) & (0xFFFFFFFFu >> (8u * e));
 }
 
-// Validate bytes [w, w+16) intersected with [lo, hi); ctx = the up-to-3
-// bytes before w that lie in the region (need() of bytes outside is 0).
-__device__ __forceinline__ bool utf8_window(const uint8_t *__restrict__ p, uintptr_t w, uintptr_t lo, uintptr_t hi) {
-    uint32_t n1 = 0, n2 = 0, n3 = 0;       // need of bytes j-1, j-2, j-3
-    uint32_t prev = 0;                     // byte j-1
-    for (int b = -3; b < 0; ++b) {
-        const uintptr_t a = w + b;
-        uint32_t c = 0, nd = 0;
-        if (a >= lo && a < hi) { c = p[a - lo]; nd = utf8_need(c); }
-        n3 = n2; n2 = n1; n1 = nd; prev = c;
-    }
-    bool ok = true;
-#pragma unroll
-    for (int b = 0; b < 16; ++b) {
-        const uintptr_t a = w + b;
-        if (a < lo || a >= hi) {           // outside: shift an empty byte through
-            n3 = n2; n2 = n1; n1 = 0; prev = 0;
-            continue;
-        }
-        const uint32_t c = p[a - lo];
-        const uint32_t req = (n1 >= 1u) + (n2 >= 2u) + (n3 >= 3u);
-        const bool cont = (c & 0xC0u) == 0x80u;
-        ok &= req <= 1u;
-        ok &= cont == (req == 1u);
-        ok &= !(c == 0xC0u || c == 0xC1u || c >= 0xF5u);
-        if (n1 >= 1u) {                    // c is the second byte of prev's sequence
-            ok &= !(prev == 0xE0u && c < 0xA0u);
-            ok &= !(prev == 0xEDu && c > 0x9Fu);
-            ok &= !(prev == 0xF0u && c < 0x90u);
-            ok &= !(prev == 0xF4u && c > 0x8Fu);
-        }
-        const uint32_t nd = utf8_need(c);
-        ok &= (uint64_t)nd < (uint64_t)(hi - a);   // the sequence must end inside the region
-        n3 = n2; n2 = n1; n1 = nd; prev = c;
-    }
-    return ok;
+// bit 7 of each byte of t set <=> that byte is zero
+__device__ __forceinline__ uint32_t zero_bytes(uint32_t t) {
+    return ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t) & 0x80808080u;
 }
 
-// One wave per region. kFrames: regions come from fws_frame_info (payload
-// after the header; result 0 unless TEXT, FIN and complete).
+// UTF-8 error flags (bit 7 of each byte) of the 4 bytes of x, p = the dword
+// before x. Bytes outside the region are zero, so a sequence cut by the region
+// end fails the continuation rule at the first zero byte after it.
+//   continuation (10xxxxxx) <=> prev1 >= C0 or prev2 >= E0 or prev3 >= F0
+//   never C0, C1, F5..FF
+//   after E0: >= A0, after ED: <= 9F, after F0: >= 90, after F4: <= 8F
+__device__ __forceinline__ uint32_t utf8_err(uint32_t x, uint32_t p) {
+    const uint32_t H = 0x80808080u;
+    const uint32_t p1 = __builtin_amdgcn_alignbyte(x, p, 3u);   // the byte before each byte of x
+    const uint32_t p2 = __builtin_amdgcn_alignbyte(x, p, 2u);
+    const uint32_t p3 = __builtin_amdgcn_alignbyte(x, p, 1u);
+    const uint32_t cont = x & ~(x << 1);
+    const uint32_t req = (p1 & (p1 << 1)) | (p2 & (p2 << 1) & (p2 << 2)) | (p3 & (p3 << 1) & (p3 << 2) & (p3 << 3));
+    uint32_t err = cont ^ req;
+    err |= zero_bytes((x & 0xFEFEFEFEu) ^ 0xC0C0C0C0u);
+    err |= ((x & 0x7F7F7F7Fu) + 0x0B0B0B0Bu) & x;
+    const uint32_t b5 = x << 2, b54 = (x << 2) | (x << 3);      // bit 5 / bits 5|4 of each byte at bit 7
+    err |= zero_bytes(p1 ^ 0xE0E0E0E0u) & ~b5;
+    err |= zero_bytes(p1 ^ 0xEDEDEDEDu) & b5;
+    err |= zero_bytes(p1 ^ 0xF0F0F0F0u) & ~b54;
+    err |= zero_bytes(p1 ^ 0xF4F4F4F4u) & b54;
+    return err & H;
+}
+
+// One wave per region, 1 KiB per step (lane L: the 16-B chunk at 16 L); the
+// 3-byte left context of a chunk is the previous lane's last dword (lane 0:
+// lane 63's of the previous step; none before the region). Chunks run to
+// hi + 3 so an unfinished sequence at the end meets zero bytes.
+// kFrames: regions come from fws_frame_info (payload after the header; result
+// 0 unless TEXT, FIN and complete).
 template <bool kFrames>
 __global__ __launch_bounds__(kBlock) void k_utf8(const uint8_t *__restrict__ base, uint64_t N,
                                                  const fws_frame_desc *__restrict__ descs,
@@ -78,14 +78,26 @@ __global__ __launch_bounds__(kBlock) void k_utf8(const uint8_t *__restrict__ bas
             off = descs[f].payload_off;
             len = descs[f].payload_len;
         }
-        bool ok = eligible;
+        uint32_t bad = 0;
         if (eligible) {
-            const uint8_t *p = base + off;
-            const uintptr_t lo = (uintptr_t)p, hi = lo + len;
-            for (uintptr_t w = (lo & ~uintptr_t(15)) + uintptr_t(lane) * 16u; w < hi; w += 1024u)
-                ok &= utf8_window(p, w, lo, hi);
-            ok = __all(ok);
+            const uintptr_t lo = (uintptr_t)(base + off), hi = lo + len;
+            uint32_t carry = 0;                      // lane 63's last dword of the previous step
+            for (uintptr_t w0 = lo & ~uintptr_t(15); w0 < hi + 3u; w0 += 1024u) {
+                const uintptr_t w = w0 + uintptr_t(lane) * 16u;
+                u32x4 v{0u, 0u, 0u, 0u};
+                if (w < hi) v = gload16(w);
+                v.x &= sel_bytes(w, lo, hi);
+                v.y &= sel_bytes(w + 4u, lo, hi);
+                v.z &= sel_bytes(w + 8u, lo, hi);
+                v.w &= sel_bytes(w + 12u, lo, hi);
+                uint32_t prev = __shfl_up(v.w, 1, 64);
+                if (lane == 0) prev = carry;
+                carry = __shfl(v.w, 63, 64);
+                if (w < hi + 3u && ((v.x | v.y | v.z | v.w | prev) & 0x80808080u))
+                    bad |= utf8_err(v.x, prev) | utf8_err(v.y, v.x) | utf8_err(v.z, v.y) | utf8_err(v.w, v.z);
+            }
         }
+        const bool ok = eligible && !__any(bad != 0);
         if (lane == 0) ok_out[f] = ok ? 1 : 0;
     }
 }

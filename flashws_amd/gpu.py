@@ -193,3 +193,11 @@ class RxSession:
             self.close()
         except Exception:
             pass
+
+
+def decode_fell_back(ctx):
+    """True if the last decode on ctx took the cooperative k_resolve fallback
+    instead of the super-tile resolve (diagnostic; synchronises)."""
+    out = (C.c_uint32 * 12)()
+    check("fws_internal_decode_counters", lib().fws_internal_decode_counters(ctx.h, out, 12))
+    return out[9] != 0          # decode_common.h Counter::kCntFallback

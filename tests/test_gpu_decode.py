@@ -234,15 +234,27 @@ def test_validate_utf8_edge_cases(ctx, cuda):
         if len(b) and rng.random() < 0.5:
             b[int(rng.integers(0, len(b)))] = int(rng.integers(0x80, 0x100))
         cases.append(bytes(b))
+    # long strings: sequences across lanes and 1 KiB wave steps, errors anywhere
+    for _ in range(60):
+        s = "".join(chr(int(c)) for c in rng.integers(0x20, 0x10FFFF, int(rng.integers(100, 1500)))
+                    if not 0xD800 <= int(c) <= 0xDFFF)
+        b = bytearray(s.encode())
+        k = int(rng.integers(0, 4))
+        if k == 1:
+            b[int(rng.integers(0, len(b)))] = int(rng.integers(0x80, 0x100))
+        elif k == 2:
+            b = b[:-1]                                  # maybe cut a sequence at the end
+        cases.append(bytes(b))
     blob, regions, pos = bytearray(), [], 0
     for c in cases:
         pad = int(rng.integers(0, 20))
-        blob += b"\0" * pad
+        # bytes around a region are arbitrary (leads, continuations): outside bytes never count
+        blob += rng.integers(0x80, 0x100, pad, dtype=np.uint8).tobytes()
         pos += pad
         regions.append((pos, len(c), 0, 0))
         blob += c
         pos += len(c)
-    dev = torch.frombuffer(bytearray(blob) + b"\0" * 32, dtype=torch.uint8).to(cuda)
+    dev = torch.frombuffer(bytearray(blob) + b"\xf0" * 32, dtype=torch.uint8).to(cuda)
     descs = np.array(regions, dtype=gpu.FRAME_DESC)
     ok = torch.zeros(len(descs), dtype=torch.uint8, device=cuda)
     gpu.validate_utf8(ctx, dev, gpu.descs_to_device(descs, cuda), len(descs), ok)

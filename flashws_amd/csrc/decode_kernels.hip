@@ -611,7 +611,7 @@ int fws_decode_ensure(fws_gpu_ctx *ctx, uint64_t N, uint32_t cap) {
 }
 
 int fws_launch_decode(fws_gpu_ctx *ctx, uint8_t *wire, uint64_t N, fws_frame_info *frames, uint32_t cap,
-                      fws_decode_result *res, hipStream_t s) {
+                      fws_decode_result *res, uint8_t *utf8_ok, hipStream_t s) {
     fws_decode_ws &d = ctx->dec;
     const uint32_t n_tiles = (uint32_t)((N + kTile - 1) / kTile);
     const uint32_t K = ceil_log2(2ull * n_tiles + 2) + 1;
@@ -637,10 +637,10 @@ int fws_launch_decode(fws_gpu_ctx *ctx, uint8_t *wire, uint64_t N, fws_frame_inf
     // Slot ids are 32-bit (8 per tile): streams of 2^39 B and more take k_resolve.
     const bool fast = N < (1ull << 39) && g_resolve_mode != 1;
     if (fast) {
-        int r = fws_launch_merge(ctx, wire, N, n_tiles, frames, cap, res, s);
+        int r = fws_launch_merge(ctx, wire, N, n_tiles, frames, cap, res, utf8_ok, s);
         if (r) return r;
     }
-    const int r = fws_launch_resolve(ctx, wire, N, n_tiles, K, frames, cap, res, fast ? 1 : 0, next, s);
+    const int r = fws_launch_resolve(ctx, wire, N, n_tiles, K, frames, cap, res, fast ? 1 : 0, next, utf8_ok, s);
     if (r == 0) d.cnt_dirty = false;
     return r;
 }

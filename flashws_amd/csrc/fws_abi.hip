@@ -184,15 +184,15 @@ int fws_gpu_decode_stream(fws_gpu_ctx *ctx, void *dev_wire, uint64_t len, fws_fr
     if ((r = fws_decode_ensure(ctx, len, cap))) return r;
     const uint64_t units = (len / 16 + 2ull * cap) / 256 + 2;
     if ((r = fws_ctx_ensure_plan(ctx, cap, units))) return r;
-    if ((r = fws_launch_decode(ctx, (uint8_t *)dev_wire, len, dev_frames, cap, dev_result, s))) return r;
-    if (cap == 0 || len == 0) return 0;
-    // the resolve left the device frame count and the stream-space unmask plan of the decoded frames
-    const uint32_t *n_dev = ctx->dec.counters + kDecodeFramesCounter;
-    if ((r = fws_launch_unmask_stream((uint8_t *)dev_wire, len, dev_frames, cap, n_dev, ctx->plan.unit_first, s)))
+    if ((r = fws_launch_decode(ctx, (uint8_t *)dev_wire, len, dev_frames, cap, dev_result, dev_utf8_ok, s)))
         return r;
-    if (dev_utf8_ok) return fws_launch_utf8_frames((const uint8_t *)dev_wire, len, dev_frames, cap, n_dev,
-                                                   dev_utf8_ok, s);
-    return 0;
+    if (cap == 0 || len == 0) return 0;
+    // the resolve left the device frame count, the stream-space unmask plan of the
+    // decoded frames and (with dev_utf8_ok) each frame's TEXT/FIN/complete preset;
+    // the unmask checks UTF-8 while the payload is in registers
+    const uint32_t *n_dev = ctx->dec.counters + kDecodeFramesCounter;
+    return fws_launch_unmask_stream((uint8_t *)dev_wire, len, dev_frames, cap, n_dev, ctx->plan.unit_first,
+                                    dev_utf8_ok, s);
 }
 
 }  // extern "C"

@@ -101,12 +101,12 @@ int fws_launch_plan(const uint8_t *base, const fws_frame_desc *d, uint32_t n, co
 int fws_launch_unmask(uint8_t *base, const fws_frame_desc *d, uint32_t n, const uint32_t *n_dev,
                       const fws_plan_ws &ws, uint64_t max_chunks, hipStream_t s);
 // Decoded stream in stream-byte space: unit_first[u] = frame spanning byte 4 KiB * u (the decode's plan).
+// utf8_ok (optional): per-frame flags, preset by the resolve to TEXT && FIN && complete; cleared here on
+// a UTF-8 error found while the payload is in registers (+ k_utf8_seam for unit seams).
 int fws_launch_unmask_stream(uint8_t *base, uint64_t N, const fws_frame_info *frames, uint32_t cap,
-                             const uint32_t *n_dev, const uint32_t *unit_first, hipStream_t s);
+                             const uint32_t *n_dev, const uint32_t *unit_first, uint8_t *utf8_ok, hipStream_t s);
 
 // text_kernels.hip
-int fws_launch_utf8_frames(const uint8_t *base, uint64_t N, const fws_frame_info *frames, uint32_t n,
-                           const uint32_t *n_dev, uint8_t *ok, hipStream_t s);
 int fws_launch_utf8_descs(const uint8_t *base, const fws_frame_desc *descs, uint32_t n, uint8_t *ok,
                           hipStream_t s);
 int fws_launch_gather(uint8_t *dst, const uint8_t *src, const fws_frame_desc *d, uint32_t n, fws_plan_ws &ws,
@@ -115,17 +115,18 @@ int fws_launch_gather(uint8_t *dst, const uint8_t *src, const fws_frame_desc *d,
 // decode_kernels.hip
 constexpr int kDecodeFramesCounter = 3;   // index of the device frame count in dec.counters
 int fws_decode_ensure(fws_gpu_ctx *ctx, uint64_t N, uint32_t cap);
+// utf8_ok (optional): per-frame UTF-8 flags, preset here, finished by fws_launch_unmask_stream
 int fws_launch_decode(fws_gpu_ctx *ctx, uint8_t *wire, uint64_t N, fws_frame_info *frames, uint32_t cap,
-                      fws_decode_result *res, hipStream_t s);
+                      fws_decode_result *res, uint8_t *utf8_ok, hipStream_t s);
 // resolve_kernels.hip: frames, descriptors and the unmask plan from k_scan's survivors
 // gate != 0: only if the super-tile resolve set kCntFallback (else the launch returns at once)
 int fws_launch_resolve(fws_gpu_ctx *ctx, const uint8_t *wire, uint64_t N, uint32_t n_tiles, uint32_t K,
                        fws_frame_info *frames, uint32_t cap, fws_decode_result *res, int gate,
-                       uint32_t *zero_next, hipStream_t s);
+                       uint32_t *zero_next, uint8_t *utf8_ok, hipStream_t s);
 // merge_kernels.hip: the super-tile resolve (k_merge + k_emit), the common path
 uint64_t fws_merge_super_tiles(uint64_t n_tiles);
 uint32_t fws_merge_tail_cap(uint64_t n_tiles);
 uint64_t fws_merge_st_nodes(uint64_t n_tiles);
 uint32_t fws_merge_comp_cap();
 int fws_launch_merge(fws_gpu_ctx *ctx, const uint8_t *wire, uint64_t N, uint32_t n_tiles, fws_frame_info *frames,
-                     uint32_t cap, fws_decode_result *res, hipStream_t s);
+                     uint32_t cap, fws_decode_result *res, uint8_t *utf8_ok, hipStream_t s);

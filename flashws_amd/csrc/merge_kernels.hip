@@ -128,6 +128,7 @@ struct MergeParams {
     fws_frame_info *frames;
     uint32_t cap;
     fws_decode_result *res;
+    uint8_t *utf8_ok;                                // optional: preset per frame (TEXT, FIN, complete)
     uint32_t *unit_first;                            // unmask plan (fws_plan_ws), stream space
     uint64_t n_units;                                // ceil(N / kUnit), clamped to the plan's capacity
 
@@ -161,6 +162,13 @@ struct MergeParams {
     }
     // unit_first for frame f spanning stream bytes [h, e) (e = the next frame's
     // header; the last frame < lim spans to the end of the stream)
+    // a frame as written to the output: the record, and its UTF-8 flag preset
+    __device__ __forceinline__ void put_frame(uint32_t f, const fws_frame_info &fi) const {
+        frames[f] = fi;
+        if (utf8_ok)
+            utf8_ok[f] = fi.opcode == 1u && fi.fin && !(fi.flags & FWS_FRAME_TRUNCATED) &&
+                         fi.hdr_off + fi.hdr_len + fi.payload_len <= N;
+    }
     __device__ __forceinline__ void plan_units(uint32_t f, uint64_t h, uint64_t e, bool last) const {
         const uint64_t ue = last ? n_units : ((e + kUnit - 1) / kUnit < n_units ? (e + kUnit - 1) / kUnit : n_units);
         for (uint64_t u = (h + kUnit - 1) / kUnit; u < ue; ++u) unit_first[u] = f;
@@ -621,7 +629,7 @@ __device__ void resolve_path(const MergeParams &P, PathLds &G) {
                 fi.hdr_off = q; fi.payload_len = h.plen; fi.key = h.key; fi.opcode = (uint8_t)h.opcode;
                 fi.fin = (uint8_t)h.fin; fi.hdr_len = (uint8_t)rc;
                 fi.flags = (po + h.plen > N) ? (uint8_t)FWS_FRAME_TRUNCATED : (uint8_t)0;
-                P.frames[nf] = fi;
+                P.put_frame(nf, fi);
             }
             ++nf;
             pos = po + h.plen;
@@ -763,7 +771,7 @@ __global__ __launch_bounds__(kMThreads) void k_emit(MergeParams P) {
     for (uint32_t j = 0; j < kPer; ++j) {
         if (!fr[j]) continue;
         if (f < lim) {
-            P.frames[f] = rc[j];
+            P.put_frame(f, rc[j]);
             P.plan_units(f, rc[j].hdr_off, exit_of(rc[j]), f == lim - 1);
         }
         ++f;
@@ -802,7 +810,7 @@ uint32_t fws_merge_tail_cap(uint64_t n_tiles) {
 }
 
 int fws_launch_merge(fws_gpu_ctx *ctx, const uint8_t *wire, uint64_t N, uint32_t n_tiles, fws_frame_info *frames,
-                     uint32_t cap, fws_decode_result *res, hipStream_t s) {
+                     uint32_t cap, fws_decode_result *res, uint8_t *utf8_ok, hipStream_t s) {
     fws_decode_ws &d = ctx->dec;
     MergeParams P;
     P.wire = wire;
@@ -828,6 +836,7 @@ int fws_launch_merge(fws_gpu_ctx *ctx, const uint8_t *wire, uint64_t N, uint32_t
     P.frames = frames;
     P.cap = cap;
     P.res = res;
+    P.utf8_ok = utf8_ok;
     P.unit_first = ctx->plan.unit_first;
     const uint64_t units = (N + kUnit - 1) / kUnit;
     P.n_units = units < ctx->plan.unit_cap ? units : ctx->plan.unit_cap;

@@ -65,7 +65,15 @@ struct ResolveParams {
     uint64_t unit_cap;
     uint32_t gate;                                // 1: run only if the super-tile resolve fell back
     uint32_t *zero_next;                          // the next call's counter set (zeroed here)
+    uint8_t *utf8_ok;                             // optional: preset per frame (TEXT, FIN, complete)
 };
+
+__device__ __forceinline__ void put_frame(const ResolveParams &P, uint32_t f, const fws_frame_info &fi) {
+    P.frames[f] = fi;
+    if (P.utf8_ok)
+        P.utf8_ok[f] = fi.opcode == 1u && fi.fin && !(fi.flags & FWS_FRAME_TRUNCATED) &&
+                       fi.hdr_off + fi.hdr_len + fi.payload_len <= P.N;
+}
 
 // Grid barrier of a cooperative launch. Arrivals only grow within a launch
 // (reset by the counters memset before k_scan), so generation g is complete
@@ -324,7 +332,7 @@ __global__ __launch_bounds__(kRThreads) void k_resolve(ResolveParams P) {
                 if (f) {
                     const uint32_t o = out + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
                     const fws_frame_info fi = P.surv_info[i];
-                    if (o < P.cap) P.frames[o] = fi;
+                    if (o < P.cap) put_frame(P, o, fi);
                     if (o < P.desc_cap) {
                         const uint64_t po = fi.hdr_off + fi.hdr_len;
                         const uint64_t pl = (po + fi.payload_len > P.N) ? (P.N - po) : fi.payload_len;
@@ -376,7 +384,7 @@ __global__ __launch_bounds__(kRThreads) void k_resolve(ResolveParams P) {
                     fi.hdr_off = q; fi.payload_len = h.plen; fi.key = h.key; fi.opcode = (uint8_t)h.opcode;
                     fi.fin = (uint8_t)h.fin; fi.hdr_len = (uint8_t)rc;
                     fi.flags = (q + rc + h.plen > N) ? (uint8_t)FWS_FRAME_TRUNCATED : (uint8_t)0;
-                    if (nf < P.cap) P.frames[nf] = fi;
+                    if (nf < P.cap) put_frame(P, nf, fi);
                     if (nf < P.desc_cap) {
                         const uint64_t po = q + rc;
                         P.descs[nf] = fws_frame_desc{po, (po + h.plen > N) ? N - po : h.plen, h.key, 0u};
@@ -419,9 +427,10 @@ using namespace fwsk;
 
 int fws_launch_resolve(fws_gpu_ctx *ctx, const uint8_t *wire, uint64_t N, uint32_t n_tiles, uint32_t K,
                        fws_frame_info *frames, uint32_t cap, fws_decode_result *res, int gate, uint32_t *zero_next,
-                       hipStream_t s) {
+                       uint8_t *utf8_ok, hipStream_t s) {
     fws_decode_ws &d = ctx->dec;
     ResolveParams P;
+    P.utf8_ok = utf8_ok;
     P.gate = gate ? 1u : 0u;
     P.zero_next = zero_next;
     P.wire = wire;

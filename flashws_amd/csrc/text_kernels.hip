@@ -15,43 +15,6 @@
 
 namespace fwsk {
 
-// Byte-select mask of the dword at address w: bytes inside [lo, hi).
-__device__ __forceinline__ uint32_t sel_bytes(uintptr_t w, uintptr_t lo, uintptr_t hi) {
-    if (w + 4u <= lo || w >= hi) return 0u;
-    const uint32_t s = lo > w ? (uint32_t)(lo - w) : 0u;
-    const uint32_t e = hi < w + 4u ? (uint32_t)(w + 4u - hi) : 0u;
-    return (0xFFFFFFFFu << (8u * s)) & (0xFFFFFFFFu >> (8u * e));
-}
-
-// bit 7 of each byte of t set <=> that byte is zero
-__device__ __forceinline__ uint32_t zero_bytes(uint32_t t) {
-    return ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t) & 0x80808080u;
-}
-
-// UTF-8 error flags (bit 7 of each byte) of the 4 bytes of x, p = the dword
-// before x. Bytes outside the region are zero, so a sequence cut by the region
-// end fails the continuation rule at the first zero byte after it.
-//   continuation (10xxxxxx) <=> prev1 >= C0 or prev2 >= E0 or prev3 >= F0
-//   never C0, C1, F5..FF
-//   after E0: >= A0, after ED: <= 9F, after F0: >= 90, after F4: <= 8F
-__device__ __forceinline__ uint32_t utf8_err(uint32_t x, uint32_t p) {
-    const uint32_t H = 0x80808080u;
-    const uint32_t p1 = __builtin_amdgcn_alignbyte(x, p, 3u);   // the byte before each byte of x
-    const uint32_t p2 = __builtin_amdgcn_alignbyte(x, p, 2u);
-    const uint32_t p3 = __builtin_amdgcn_alignbyte(x, p, 1u);
-    const uint32_t cont = x & ~(x << 1);
-    const uint32_t req = (p1 & (p1 << 1)) | (p2 & (p2 << 1) & (p2 << 2)) | (p3 & (p3 << 1) & (p3 << 2) & (p3 << 3));
-    uint32_t err = cont ^ req;
-    err |= zero_bytes((x & 0xFEFEFEFEu) ^ 0xC0C0C0C0u);
-    err |= ((x & 0x7F7F7F7Fu) + 0x0B0B0B0Bu) & x;
-    const uint32_t b5 = x << 2, b54 = (x << 2) | (x << 3);      // bit 5 / bits 5|4 of each byte at bit 7
-    err |= zero_bytes(p1 ^ 0xE0E0E0E0u) & ~b5;
-    err |= zero_bytes(p1 ^ 0xEDEDEDEDu) & b5;
-    err |= zero_bytes(p1 ^ 0xF0F0F0F0u) & ~b54;
-    err |= zero_bytes(p1 ^ 0xF4F4F4F4u) & b54;
-    return err & H;
-}
-
 // One wave per region, 1 KiB per step (lane L: the 16-B chunk at 16 L); the
 // 3-byte left context of a chunk is the previous lane's last dword (lane 0:
 // lane 63's of the previous step; none before the region). Chunks run to
@@ -284,15 +247,6 @@ __global__ __launch_bounds__(kBlock) void k_gather_fast(uint8_t *__restrict__ ds
 }  // namespace fwsk
 
 using namespace fwsk;
-
-int fws_launch_utf8_frames(const uint8_t *base, uint64_t N, const fws_frame_info *frames, uint32_t n,
-                           const uint32_t *n_dev, uint8_t *ok, hipStream_t s) {
-    if (n == 0) return 0;
-    uint32_t blocks = (n + 3) / 4;
-    if (blocks > 4096) blocks = 4096;
-    hipLaunchKernelGGL(k_utf8<true>, dim3(blocks), dim3(kBlock), 0, s, base, N, nullptr, frames, n, n_dev, ok);
-    return fws_hip_status(hipGetLastError());
-}
 
 int fws_launch_utf8_descs(const uint8_t *base, const fws_frame_desc *descs, uint32_t n, uint8_t *ok,
                           hipStream_t s) {

@@ -352,19 +352,42 @@ __device__ __forceinline__ u32x4 region_mask(uint64_t c, uint64_t po, uint64_t p
 struct StreamFrame {
     uint64_t po, pe;                                 // payload [po, pe), clipped to the stream
     uint32_t key;
+    bool text;                                       // UTF-8 checked: TEXT, FIN, complete
 };
 
 __device__ __forceinline__ StreamFrame stream_frame(const fws_frame_info &fi, uint64_t N) {
     const uint64_t po = fi.hdr_off + fi.hdr_len;
     const uint64_t pe = po + fi.payload_len < N ? po + fi.payload_len : N;
-    return StreamFrame{po, pe, fi.key};
+    const bool text = fi.opcode == 1u && fi.fin && !(fi.flags & FWS_FRAME_TRUNCATED) && po + fi.payload_len <= N;
+    return StreamFrame{po, pe, fi.key, text};
 }
 
-template <bool kNT>
+// UTF-8 errors of region R in the unmasked chunk u at stream offset c, given
+// the unmasked dword before the chunk; bytes outside R count as zero. The
+// first `skip` bytes are not judged (their context is in another unit).
+__device__ __forceinline__ bool utf8_chunk_bad(const u32x4 &u, uint32_t prev, uint64_t c, uint64_t lo, uint64_t hi,
+                                               uint32_t skip) {
+    u32x4 x = u;
+    uint32_t p = prev;
+    if (!(c >= lo && c + 16u <= hi)) {               // not wholly inside R: zero the outside bytes
+        x.x &= sel_bytes(c, lo, hi);
+        x.y &= sel_bytes(c + 4u, lo, hi);
+        x.z &= sel_bytes(c + 8u, lo, hi);
+        x.w &= sel_bytes(c + 12u, lo, hi);
+    }
+    if (!(c >= lo + 4u && c <= hi)) p &= sel_bytes(c - 4u, lo, hi);
+    if (!((x.x | x.y | x.z | x.w | p) & 0x80808080u)) return false;   // ASCII, no open sequence
+    uint32_t e0 = utf8_err(x.x, p);
+    if (skip) e0 &= 0x80000000u;                     // bytes 0..2 are judged by k_utf8_seam
+    return (e0 | utf8_err(x.y, x.x) | utf8_err(x.z, x.y) | utf8_err(x.w, x.z)) != 0u;
+}
+
+template <bool kNT, bool kUtf8>
 __global__ __launch_bounds__(kBlock) void k_unmask_stream(uint8_t *base, uint64_t N,
                                                           const fws_frame_info *__restrict__ fr, uint32_t cap,
                                                           const uint32_t *__restrict__ n_dev,
-                                                          const uint32_t *__restrict__ unit_first, uint64_t n_units) {
+                                                          const uint32_t *__restrict__ unit_first, uint64_t n_units,
+                                                          uint8_t *__restrict__ ok) {
     uint32_t n = *n_dev;
     if (n > cap) n = cap;
     if (n == 0) return;
@@ -377,10 +400,10 @@ __global__ __launch_bounds__(kBlock) void k_unmask_stream(uint8_t *base, uint64_
         const uint32_t fhi = (u + 1 < n_units) ? unit_first[u + 1] : n - 1;
         const uint64_t c0 = u * 4096u + uint64_t(lane) * 16u;
         if (fhi - flo >= 2u) {                       // small frames: per-chunk search
+            uint32_t carry = 0;                      // lane 63's last unmasked dword of step j - 1
 #pragma unroll 1
             for (int j = 0; j < kUnmaskU; ++j) {
                 const uint64_t c = c0 + uint64_t(j) * 1024u;
-                if (c >= N) break;
                 uint32_t lo = flo, hi = fhi;         // last frame with hdr_off <= c
                 while (lo < hi) {
                     const uint32_t mid = lo + ((hi - lo + 1u) >> 1);
@@ -393,9 +416,24 @@ __global__ __launch_bounds__(kBlock) void k_unmask_stream(uint8_t *base, uint64_
                     const StreamFrame sf = stream_frame(fi, N);
                     m |= region_mask(c, sf.po, sf.pe, sf.key);
                 }
-                if (m.x | m.y | m.z | m.w) {
-                    const uintptr_t a = b0 + c;
-                    gstore16<kNT>(a, gload16<kNT>(a) ^ m);
+                u32x4 v{0u, 0u, 0u, 0u};
+                const bool touched = c < N && (m.x | m.y | m.z | m.w);
+                if (kUtf8 ? c < N : touched) v = gload16<kNT>(b0 + c);
+                if (touched) gstore16<kNT>(b0 + c, v ^ m);
+                if constexpr (kUtf8) {
+                    const u32x4 x = v ^ m;
+                    uint32_t prev = __shfl_up(x.w, 1, 64);
+                    if (lane == 0) prev = carry;
+                    carry = __shfl(x.w, 63, 64);
+                    // frames whose payload or 3-byte tail meets the chunk (lo - 1: the tail of the one before)
+                    for (uint32_t f = lo > flo ? lo - 1u : lo; f < n; ++f) {
+                        const fws_frame_info fi = fr[f];
+                        if (fi.hdr_off >= c + 16u) break;
+                        const StreamFrame sf = stream_frame(fi, N);
+                        if (sf.text && c + 16u > sf.po && c < sf.pe + 3u &&
+                            utf8_chunk_bad(x, prev, c, sf.po, sf.pe, j == 0 && lane == 0))
+                            ok[f] = 0;
+                    }
                 }
             }
             continue;
@@ -427,6 +465,52 @@ __global__ __launch_bounds__(kBlock) void k_unmask_stream(uint8_t *base, uint64_
 #pragma unroll
         for (int j = 0; j < kUnmaskU; ++j)
             if (live[j]) gstore16<kNT>(ca[j], v[j] ^ mk[j]);
+        if constexpr (kUtf8) {
+            if (A.text || (two && B.text)) {
+                bool badA = false, badB = false;
+                uint32_t carry = 0;
+#pragma unroll
+                for (int j = 0; j < kUnmaskU; ++j) {
+                    const uint64_t c = c0 + uint64_t(j) * 1024u;
+                    const u32x4 x = v[j] ^ mk[j];    // bytes outside A, B are zeroed below
+                    uint32_t prev = __shfl_up(x.w, 1, 64);
+                    if (lane == 0) prev = carry;
+                    carry = __shfl(x.w, 63, 64);
+                    const uint32_t skip = j == 0 && lane == 0;
+                    if (A.text && c + 16u > A.po && c < A.pe + 3u)
+                        badA |= utf8_chunk_bad(x, prev, c, A.po, A.pe, skip);
+                    if (two && B.text && c + 16u > B.po && c < B.pe + 3u)
+                        badB |= utf8_chunk_bad(x, prev, c, B.po, B.pe, skip);
+                }
+                if (__any(badA) && lane == 0) ok[flo] = 0;
+                if (__any(badB) && lane == 0) ok[fhi] = 0;
+            }
+        }
+    }
+}
+
+// The first 3 bytes of every stream unit u in [1, n_units], whose left context
+// lies in unit u - 1 (k_unmask_stream skipped them), for the frame holding
+// byte 4 KiB * u and the one before it (the 3-byte tail past its payload).
+// Reads the already unmasked stream.
+__global__ __launch_bounds__(kBlock) void k_utf8_seam(const uint8_t *base, uint64_t N,
+                                                      const fws_frame_info *__restrict__ fr, uint32_t cap,
+                                                      const uint32_t *__restrict__ n_dev,
+                                                      const uint32_t *__restrict__ unit_first, uint64_t n_units,
+                                                      uint8_t *__restrict__ ok) {
+    uint32_t n = *n_dev;
+    if (n > cap) n = cap;
+    const uint64_t u = uint64_t(blockIdx.x) * kBlock + threadIdx.x + 1u;
+    if (n == 0 || u > n_units) return;
+    const uint64_t P = u * 4096u;
+    const uint32_t f = u < n_units ? unit_first[u] : n - 1;
+    const uint32_t cur = P < N ? *(const uint32_t *)(base + P) : 0u;      // bytes past N: zeroed below
+    const uint32_t prev = *(const uint32_t *)(base + P - 4u);
+    for (uint32_t g = f > 0 ? f - 1u : 0u; g <= f; ++g) {
+        const StreamFrame sf = stream_frame(fr[g], N);
+        if (!sf.text || P + 3u <= sf.po || P >= sf.pe + 3u) continue;
+        const uint32_t x = cur & sel_bytes(P, sf.po, sf.pe), p = prev & sel_bytes(P - 4u, sf.po, sf.pe);
+        if (utf8_err(x, p) & 0x00808080u) ok[g] = 0;
     }
 }
 
@@ -479,11 +563,18 @@ int fws_launch_plan(const uint8_t *base, const fws_frame_desc *d, uint32_t n, co
 }
 
 int fws_launch_unmask_stream(uint8_t *base, uint64_t N, const fws_frame_info *frames, uint32_t cap,
-                             const uint32_t *n_dev, const uint32_t *unit_first, hipStream_t s) {
+                             const uint32_t *n_dev, const uint32_t *unit_first, uint8_t *utf8_ok, hipStream_t s) {
     const uint64_t units = (N + 4095) / 4096;
     if (units == 0 || cap == 0) return 0;
-    hipLaunchKernelGGL(k_unmask_stream<true>, dim3(grid_for_units(units)), dim3(kBlock), 0, s, (uint8_t *)base, N,
-                       frames, cap, n_dev, unit_first, units);
+    if (utf8_ok == nullptr) {
+        hipLaunchKernelGGL((k_unmask_stream<true, false>), dim3(grid_for_units(units)), dim3(kBlock), 0, s,
+                           (uint8_t *)base, N, frames, cap, n_dev, unit_first, units, nullptr);
+    } else {
+        hipLaunchKernelGGL((k_unmask_stream<true, true>), dim3(grid_for_units(units)), dim3(kBlock), 0, s,
+                           (uint8_t *)base, N, frames, cap, n_dev, unit_first, units, utf8_ok);
+        hipLaunchKernelGGL(k_utf8_seam, dim3((unsigned)((units + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
+                           (const uint8_t *)base, N, frames, cap, n_dev, unit_first, units, utf8_ok);
+    }
     return fws_hip_status(hipGetLastError());
 }
 

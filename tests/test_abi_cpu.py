@@ -34,6 +34,12 @@ def test_library_exports_every_declared_symbol():
     assert not missing, missing
 
 
+def test_library_resolves_every_symbol_at_load():
+    """dlopen with RTLD_NOW: an internal symbol left undefined (a stale object
+    after a signature change) fails here, on the CPU, not on the GPU box."""
+    C.CDLL(_lib.LIB_PATH, mode=os.RTLD_NOW | os.RTLD_LOCAL)
+
+
 def test_python_signatures_cover_the_header():
     assert set(declared_functions()) == {n for n, _, _ in _lib.SIGNATURES}
 

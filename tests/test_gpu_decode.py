@@ -222,6 +222,93 @@ def test_utf8_flags_c5_shape(ctx, cuda):
     assert np.array_equal(got.astype(bool), np.array(exp))
 
 
+def _utf8_payload(rng, n_chars, corrupt):
+    s = "".join(chr(int(c)) for c in rng.integers(0x20, 0x10FFFF, n_chars) if not 0xD800 <= int(c) <= 0xDFFF)
+    b = bytearray(s.encode())
+    if corrupt == 1 and len(b):
+        b[int(rng.integers(0, len(b)))] = int(rng.integers(0x80, 0x100))
+    elif corrupt == 2 and len(b):
+        b = b[:-1]                                   # a sequence cut at the frame end (or not)
+    return bytes(b)
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_utf8_flags_mixed_stream(ctx, cuda, seed):
+    """Fused decode + UTF-8 flags on TEXT frames of every size (tiny frames take
+    the per-chunk unmask path, big ones the uniform path), misaligned against
+    the 4 KiB stream units and 16-B chunks, next to BIN / non-FIN / control
+    frames; flags must equal Python's strict decoder on eligible frames."""
+    rng = np.random.default_rng(40 + seed)
+    parts, kinds = [], []
+    total = 0
+    while total < 600_000:
+        r = rng.random()
+        if r < 0.08:
+            op, fin, body = 2, 1, _utf8_payload(rng, int(rng.integers(0, 2000)), 0)
+        elif r < 0.12:
+            op, fin, body = 1, 0, _utf8_payload(rng, int(rng.integers(0, 500)), 0)
+        elif r < 0.15:
+            op, fin, body = 9, 1, _utf8_payload(rng, int(rng.integers(0, 30)), 0)
+        else:
+            size = int(rng.choice([rng.integers(0, 40), rng.integers(40, 2000), rng.integers(2000, 9000)]))
+            op, fin, body = 1, 1, _utf8_payload(rng, size, int(rng.integers(0, 3)))
+        parts.append(frame(op, body, fin=fin, key=int(rng.integers(0, 2**32))))
+        kinds.append((op, fin, body))
+        total += len(parts[-1])
+    wire = np.frombuffer(b"".join(parts), dtype=np.uint8)
+    dev = torch.from_numpy(wire.copy()).to(cuda)
+    flags = torch.full((len(parts) + 4,), 7, dtype=torch.uint8, device=cuda)
+    rc, fr, res, _ = gpu.decode_stream(ctx, dev, cap=len(parts) + 4, utf8_ok=flags)
+    assert rc == 0
+    r = gpu.read_result(res)
+    assert int(r["status"]) == 0 and int(r["n_frames"]) == len(parts)
+    got = flags.cpu().numpy()[:len(parts)]
+    for i, (op, fin, body) in enumerate(kinds):
+        exp = False
+        if op == 1 and fin:
+            try:
+                body.decode("utf-8")
+                exp = True
+            except UnicodeDecodeError:
+                pass
+        assert bool(got[i]) == exp, (i, op, fin, body[-8:])
+
+
+def test_utf8_flags_unit_seams(ctx, cuda):
+    """TEXT frames placed so that multi-byte sequences, cut sequences and frame
+    ends straddle 4 KiB stream-unit boundaries (the seam kernel's bytes)."""
+    rng = np.random.default_rng(77)
+    parts, bodies = [], []
+    pos = 0
+    for k in range(60):
+        # the payload end lands at unit boundary + d, d in -3..3
+        d = int(rng.integers(-3, 4))
+        target = (pos // 4096 + 2) * 4096 + d
+        seq = rng.choice([b"\xe2\x82\xac", b"\xf0\x9d\x84\x9e", b"\xc3\xa9", b"a"])
+        n = target - pos - 8
+        body = bytearray((seq * (n // len(seq) + 2))[:n])
+        if k % 3 == 1:
+            body[-1] = 0xE2                              # cut at the end
+        elif k % 3 == 2:
+            body[-int(rng.integers(1, 4))] = 0x80        # stray continuation near the end
+        parts.append(frame(1, bytes(body), key=int(rng.integers(0, 2**32)), len_form=126))
+        bodies.append(bytes(body))
+        pos += len(parts[-1])
+    wire = np.frombuffer(b"".join(parts), dtype=np.uint8)
+    dev = torch.from_numpy(wire.copy()).to(cuda)
+    flags = torch.zeros(len(parts), dtype=torch.uint8, device=cuda)
+    rc, _, res, _ = gpu.decode_stream(ctx, dev, cap=len(parts), utf8_ok=flags)
+    assert rc == 0 and int(gpu.read_result(res)["n_frames"]) == len(parts)
+    got = flags.cpu().numpy()
+    for i, b in enumerate(bodies):
+        try:
+            b.decode("utf-8")
+            exp = True
+        except UnicodeDecodeError:
+            exp = False
+        assert bool(got[i]) == exp, (i, b[-6:])
+
+
 def test_validate_utf8_edge_cases(ctx, cuda):
     cases = [b"", b"a", b"\xc2\x80", b"\xc2", b"\xe0\xa0\x80", b"\xe0\x9f\x80", b"\xed\x9f\xbf", b"\xed\xa0\x80",
              b"\xf0\x90\x80\x80", b"\xf0\x8f\xbf\xbf", b"\xf4\x8f\xbf\xbf", b"\xf4\x90\x80\x80", b"\xf5\x80\x80\x80",

@@ -314,6 +314,27 @@ def stream_decode_extra(ctx, wire_c2, dev, args):
     out["C2_end_to_end_pcie"] = {"GiB_per_s": round(int(descs["payload_len"].sum()) / t / GIB, 1),
                                  "ms_per_step": round(t * 1e3, 3),
                                  "path": "pinned H2D + fws_gpu_unmask_batch + D2H, one stream"}
+    # end to end, pipelined: C2 wire batches from pinned host memory through fws_rx_pipe
+    # (H2D -> parse + unmask -> D2H of bytes, frames, result; depth 3 streams)
+    del dbuf
+    pipe = gpu.RxPipe(dev.index or 0, max_batch_bytes=len(wire_c2), max_frames=n + 64, depth=3)
+    hosts = [torch.from_numpy(wire_c2.copy()).pin_memory() for _ in range(4)]
+    for i in range(3):
+        pipe.wait(pipe.submit(hosts[i]), copy_frames=False)
+    k = 12
+    t0 = time.perf_counter()
+    tickets = [pipe.submit(hosts[i % 4]) for i in range(k)]   # submit waits when a slot is busy
+    for tk in tickets[-3:]:
+        pipe.wait(tk, copy_frames=False)
+    t = (time.perf_counter() - t0) / k
+    _, res, _ = pipe.wait(tickets[-1], copy_frames=False)
+    assert int(res["status"]) == 0 and int(res["n_frames"]) == n
+    out["C2_stream_end_to_end_pipelined"] = {
+        "GiB_per_s": round(int(descs["payload_len"].sum()) / t / GIB, 1), "ms_per_batch": round(t * 1e3, 3),
+        "path": "fws_rx_pipe: pinned H2D -> fws_gpu_decode_stream -> D2H (bytes + frames + result), 3 streams; "
+                "bound by PCIe: H2D and D2H do not overlap on this box (profiles/r01/pcie_probe.json)",
+        "batches": k}
+    pipe.close()
     return {"extra": out}
 
 

@@ -83,6 +83,12 @@ SIGNATURES = [
     ("fws_rx_session_feed", _I, [_P, _P, _U64, _U64, _P, _U64, _PU64, _P, _U64, _PU64]),
     ("fws_rx_session_state", _I, [_P, _P]),
     ("fws_gen_batch", _I, [C.POINTER(GenParams), _P, _U64, _PU64, _P, _U64, _PU64, _P]),
+    ("fws_gpu_host_register", _I, [_P, _U64]),
+    ("fws_gpu_host_unregister", _I, [_P]),
+    ("fws_rx_pipe_create", _I, [_I, _U64, _U32, _U32, _I, C.POINTER(C.c_void_p)]),
+    ("fws_rx_pipe_destroy", None, [_P]),
+    ("fws_rx_pipe_submit", _I, [_P, _P, _U64, _PU64]),
+    ("fws_rx_pipe_wait", _I, [_P, _U64, C.POINTER(C.c_void_p), _PU64, _P, C.POINTER(C.c_void_p)]),
 ]
 
 _lib = None

@@ -201,3 +201,50 @@ def decode_fell_back(ctx):
     out = (C.c_uint32 * 12)()
     check("fws_internal_decode_counters", lib().fws_internal_decode_counters(ctx.h, out, 12))
     return out[9] != 0          # decode_common.h Counter::kCntFallback
+
+
+class RxPipe:
+    """fws_rx_pipe: batched, pipelined decode of host batches (H2D -> parse +
+    unmask -> D2H on `depth` streams). Batches are pinned CPU uint8 tensors;
+    each is unmasked in place once its wait() returns."""
+
+    def __init__(self, device=0, max_batch_bytes=1 << 28, max_frames=1 << 17, depth=3, utf8=False):
+        h = C.c_void_p()
+        check("fws_rx_pipe_create", lib().fws_rx_pipe_create(device, max_batch_bytes, max_frames, depth,
+                                                             1 if utf8 else 0, C.byref(h)))
+        self.h = h
+        self.max_frames = max_frames
+        self.utf8 = utf8
+
+    def submit(self, batch, n=None):
+        t = C.c_uint64()
+        n = batch.numel() if n is None else n
+        check("fws_rx_pipe_submit", lib().fws_rx_pipe_submit(self.h, C.c_void_p(batch.data_ptr()), n, C.byref(t)))
+        return t.value
+
+    def wait(self, ticket, copy_frames=True):
+        """(frames structured array, result record, utf8 flags or None)."""
+        fp, up = C.c_void_p(), C.c_void_p()
+        nf = C.c_uint64()
+        res = np.zeros(1, dtype=DECODE_RESULT)
+        check("fws_rx_pipe_wait", lib().fws_rx_pipe_wait(self.h, ticket, C.byref(fp), C.byref(nf),
+                                                         C.c_void_p(res.ctypes.data), C.byref(up)))
+        frames = None
+        if copy_frames and nf.value:
+            raw = (C.c_uint8 * (nf.value * FRAME_INFO.itemsize)).from_address(fp.value)
+            frames = np.frombuffer(bytes(raw), dtype=FRAME_INFO)
+        ok = None
+        if self.utf8 and nf.value:
+            ok = np.frombuffer(bytes((C.c_uint8 * nf.value).from_address(up.value)), dtype=np.uint8)
+        return frames, res[0], ok
+
+    def close(self):
+        if self.h:
+            lib().fws_rx_pipe_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

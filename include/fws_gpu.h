@@ -186,6 +186,33 @@ int fws_rx_session_feed(fws_rx_session *s, uint8_t *buf, uint64_t size, uint64_t
                         uint8_t *ctl_out, uint64_t ctl_cap, uint64_t *ctl_used);
 int fws_rx_session_state(const fws_rx_session *s, fws_rx_state *out);
 
+/* ---- batched, pipelined receive over host memory ---------------------------
+ * the reads of one event-loop step (FLoop::OneStep,
+ * floop.h:661-703; TCPSocket::Read, tcp_socket.h:387-402) aggregated into one
+ * host batch per submit. Each of `depth` slots runs H2D -> decode (header parse
+ * + unmask, optional per-frame UTF-8 flags) -> D2H of the unmasked bytes (back
+ * into the batch), the frame list and the result on its own stream, so
+ * successive batches overlap on the full-duplex link. The batch must stay
+ * valid (and should be pinned) until its wait returns; a batch starts at a
+ * frame header (the per-connection carry is the session's job). */
+typedef struct fws_rx_pipe fws_rx_pipe;
+
+/* Pin / unpin caller memory (e.g. MemPool blocks, flash_alloc.h:44-73) for async copies. */
+int fws_gpu_host_register(void *host_ptr, uint64_t bytes);
+int fws_gpu_host_unregister(void *host_ptr);
+
+int fws_rx_pipe_create(int device, uint64_t max_batch_bytes, uint32_t max_frames, uint32_t depth, int utf8,
+                       fws_rx_pipe **out);
+void fws_rx_pipe_destroy(fws_rx_pipe *p);
+/* Enqueue a batch; *ticket identifies it. Waits first if its slot is still busy. */
+int fws_rx_pipe_submit(fws_rx_pipe *p, uint8_t *batch, uint64_t len, uint64_t *ticket);
+/* Block until batch `ticket` is done: the batch holds the unmasked bytes, *frames
+ * points at min(n_frames, max_frames) decoded frames (pinned, valid until the
+ * slot is reused `depth` submits later), *result is the decode result, and
+ * *utf8_ok the per-frame flags (pipes created with utf8 != 0). */
+int fws_rx_pipe_wait(fws_rx_pipe *p, uint64_t ticket, const fws_frame_info **frames, uint64_t *n_frames,
+                     fws_decode_result *result, const uint8_t **utf8_ok);
+
 /* ---- synthetic workloads (BASELINE configs, not test oracles) ------------ */
 typedef struct fws_gen_params {
     uint64_t seed;

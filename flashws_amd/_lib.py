@@ -43,7 +43,9 @@ DECODE_RESULT = np.dtype([("status", "<i4"), ("n_frames", "<u4"), ("consumed", "
 RX_EVENT = np.dtype([("kind", "<u4"), ("opcode", "<u4"), ("is_ctl", "u1"), ("frame_end", "u1"),
                      ("msg_end", "u1"), ("fin", "u1"), ("code", "<u4"), ("size", "<u8"),
                      ("data_off", "<u8"), ("ctl_off", "<u8"), ("capacity", "<u8")])
-assert FRAME_DESC.itemsize == 24 and FRAME_INFO.itemsize == 24
+TX_DESC = np.dtype([("src_off", "<u8"), ("len", "<u8"), ("key", "<u4"), ("opcode", "u1"), ("fin", "u1"),
+                    ("masked", "u1"), ("pad", "u1")])
+assert FRAME_DESC.itemsize == 24 and FRAME_INFO.itemsize == 24 and TX_DESC.itemsize == 24
 assert DECODE_RESULT.itemsize == 40 and RX_EVENT.itemsize == 48
 
 
@@ -83,6 +85,8 @@ SIGNATURES = [
     ("fws_rx_session_feed", _I, [_P, _P, _U64, _U64, _P, _U64, _PU64, _P, _U64, _PU64]),
     ("fws_rx_session_state", _I, [_P, _P]),
     ("fws_gen_batch", _I, [C.POINTER(GenParams), _P, _U64, _PU64, _P, _U64, _PU64, _P]),
+    ("fws_tx_next", None, [_U32, _I, C.POINTER(C.c_uint8), C.POINTER(C.c_uint8), C.POINTER(C.c_uint8)]),
+    ("fws_gpu_encode_frames", _I, [_P, _P, _U64, _P, _P, _U32, _P, _P]),
     ("fws_gpu_host_register", _I, [_P, _U64]),
     ("fws_gpu_host_unregister", _I, [_P]),
     ("fws_rx_pipe_create", _I, [_I, _U64, _U32, _U32, _I, C.POINTER(C.c_void_p)]),

@@ -1,0 +1,257 @@
+// tx_kernels.hip -- batch frame builder for the send path:
+// the bytes WSocket::SendFrame (net/w_socket.h:832-944) writes for each frame,
+// for a whole batch in one pass over the output.
+//
+// A frame is header + payload: b0 = FIN << 7 | opcode (:914), b1 = MASK << 7 |
+// len7 with the 16- or 64-bit big-endian length after it (:867-881), then for
+// a client frame the 4 key bytes (native LE u32, :862-866) and the payload
+// XORed with them from phase 0 (WSMaskBytesFast, :861). The opcode / FIN
+// sequencing of a connection (last_msg_not_fin_, :903-913) is host logic
+// (fws_tx_next); the device builds bytes.
+//
+// Plan: k_tx_count (block sums of frame sizes) -> k_tx_scan (obase = exclusive
+// prefix, total) -> k_tx_units (unit_first[u] = the frame spanning output byte
+// 4 KiB * u). k_tx_encode: one wave per 4 KiB output unit; each lane owns 16-B
+// output chunks, so every chunk is one full 16-B store (the last chunk of the
+// output stops at the total). A chunk inside one payload is two aligned source
+// loads shifted by the payload's source misalignment, XORed with the key at the
+// frame-relative phase -- the k_gather_fast data path; header bytes and chunks
+// on a frame seam are built bytewise. HBM bytes = payload read + frames written.
+#include "fws_device.h"
+#include "fws_internal.h"
+
+namespace fwsk {
+
+constexpr uint64_t kTxUnit = 4096;
+
+__device__ __forceinline__ uint32_t tx_hdr_len(const fws_tx_desc &d) {   // w_socket.h:49-65
+    const uint32_t ext = d.len < 126u ? 0u : (d.len <= 65535u ? 2u : 8u);
+    return 2u + (d.masked ? 4u : 0u) + ext;
+}
+
+// Byte i (< tx_hdr_len) of the frame header.
+__device__ __forceinline__ uint32_t tx_hdr_byte(const fws_tx_desc &d, uint32_t i) {
+    const uint32_t m = d.masked ? 0x80u : 0u;
+    const uint32_t ext = d.len < 126u ? 0u : (d.len <= 65535u ? 2u : 8u);
+    if (i == 0) return ((uint32_t)(d.fin != 0) << 7) | (d.opcode & 15u);
+    if (i == 1) return m | (ext == 0 ? (uint32_t)d.len : (ext == 2 ? 126u : 127u));
+    if (i < 2u + ext) return (uint32_t)(d.len >> (8u * (ext - 1u - (i - 2u)))) & 0xFFu;   // big endian
+    return (d.key >> (8u * (i - 2u - ext))) & 0xFFu;                                     // key bytes, LE
+}
+
+__global__ __launch_bounds__(kBlock) void k_tx_count(const fws_tx_desc *__restrict__ d, uint32_t n,
+                                                     uint64_t *__restrict__ block_sums) {
+    __shared__ uint64_t ws[kBlock / 64];
+    uint64_t s = 0;
+    for (uint32_t i = 0; i < 4; ++i) {
+        const uint64_t f = (uint64_t)blockIdx.x * 1024u + threadIdx.x * 4u + i;
+        if (f < n) s += tx_hdr_len(d[f]) + d[f].len;
+    }
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o, 64);
+    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) block_sums[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
+}
+
+// obase[f] = output offset of frame f; obase[n] = *total = all bytes;
+// *out_len = total, or ~0 when it exceeds out_cap (then nothing is written).
+__global__ __launch_bounds__(kBlock) void k_tx_scan(const fws_tx_desc *__restrict__ d, uint32_t n,
+                                                    const uint64_t *__restrict__ block_sums,
+                                                    uint64_t *__restrict__ obase, uint64_t *__restrict__ total_out,
+                                                    uint64_t *__restrict__ out_len, uint64_t out_cap) {
+    __shared__ uint64_t wsum[kBlock / 64];
+    __shared__ uint64_t sprefix;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint64_t p = 0;
+    for (uint32_t b = threadIdx.x; b < blockIdx.x; b += kBlock) p += block_sums[b];
+    for (int o = 32; o > 0; o >>= 1) p += __shfl_down(p, o, 64);
+    if (lane == 0) wsum[w] = p;
+    __syncthreads();
+    if (threadIdx.x == 0) sprefix = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    __syncthreads();
+    const uint64_t f0 = (uint64_t)blockIdx.x * 1024u + threadIdx.x * 4u;
+    uint64_t c[4], s = 0;
+    for (int i = 0; i < 4; ++i) {
+        c[i] = (f0 + i < n) ? tx_hdr_len(d[f0 + i]) + d[f0 + i].len : 0;
+        s += c[i];
+    }
+    uint64_t inc = s;
+    for (int o = 1; o < 64; o <<= 1) { const uint64_t x = __shfl_up(inc, o, 64); if (lane >= o) inc += x; }
+    __syncthreads();
+    if (lane == 63) wsum[w] = inc;
+    __syncthreads();
+    uint64_t off = sprefix;
+    for (int i = 0; i < w; ++i) off += wsum[i];
+    uint64_t run = off + inc - s;
+    for (int i = 0; i < 4; ++i) {
+        const uint64_t f = f0 + i;
+        if (f >= n) break;
+        obase[f] = run;
+        run += c[i];
+        if (f == n - 1) {
+            obase[n] = run;
+            const bool fits = run <= out_cap;
+            *total_out = fits ? run : 0;               // nothing is encoded when it does not fit
+            *out_len = fits ? run : ~0ull;
+        }
+    }
+}
+
+// unit_first[u] = last frame f with obase[f] <= u * 4 KiB
+__global__ __launch_bounds__(kBlock) void k_tx_units(const uint64_t *__restrict__ obase, uint32_t n,
+                                                     uint32_t *__restrict__ unit_first, uint64_t unit_cap,
+                                                     const uint64_t *__restrict__ total_ptr) {
+    const uint64_t u = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    uint64_t n_units = (*total_ptr + kTxUnit - 1) / kTxUnit;
+    if (n_units > unit_cap) n_units = unit_cap;
+    if (u >= n_units) return;
+    const uint64_t A = u * kTxUnit;
+    uint32_t lo = 0, hi = n - 1;
+    while (lo < hi) {
+        const uint32_t mid = lo + ((hi - lo + 1) >> 1);
+        if (obase[mid] <= A) lo = mid; else hi = mid - 1;
+    }
+    unit_first[u] = lo;
+}
+
+// 16 bytes starting sh (0..15) bytes into the 32-byte window v0:v1
+__device__ __forceinline__ u32x4 tx_shr_bytes(const u32x4 &v0, const u32x4 &v1, uint32_t sh) {
+    const bool s8 = (sh & 8u) != 0, s4 = (sh & 4u) != 0;
+    const uint32_t a0 = s8 ? v0.z : v0.x, a1 = s8 ? v0.w : v0.y, a2 = s8 ? v1.x : v0.z;
+    const uint32_t a3 = s8 ? v1.y : v0.w, a4 = s8 ? v1.z : v1.x;
+    const uint32_t c0 = s4 ? a1 : a0, c1 = s4 ? a2 : a1, c2 = s4 ? a3 : a2, c3 = s4 ? a4 : a3;
+    const uint32_t c4 = s4 ? (s8 ? v1.w : v1.y) : a4;
+    const uint32_t b = sh & 3u;
+    return u32x4{__builtin_amdgcn_alignbyte(c1, c0, b), __builtin_amdgcn_alignbyte(c2, c1, b),
+                 __builtin_amdgcn_alignbyte(c3, c2, b), __builtin_amdgcn_alignbyte(c4, c3, b)};
+}
+
+// Output bytes [a, min(a + 16, total)) built one by one from frame f on.
+__device__ void tx_bytes(uint8_t *out, const uint8_t *src, const fws_tx_desc *__restrict__ d,
+                         const uint64_t *__restrict__ obase, uint32_t f, uint64_t a, uint64_t total) {
+    for (uint64_t b = a; b < a + 16 && b < total; ++b) {
+        while (b >= obase[f + 1]) ++f;
+        const fws_tx_desc fd = d[f];
+        const uint32_t h = tx_hdr_len(fd);
+        const uint64_t k = b - obase[f];
+        uint32_t v;
+        if (k < h) {
+            v = tx_hdr_byte(fd, (uint32_t)k);
+        } else {
+            const uint64_t j = k - h;
+            v = src[fd.src_off + j] ^ (fd.masked ? (fd.key >> (8u * (uint32_t)(j & 3u))) & 0xFFu : 0u);
+        }
+        out[b] = (uint8_t)v;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_tx_encode(uint8_t *__restrict__ out, const uint8_t *__restrict__ src,
+                                                      const fws_tx_desc *__restrict__ d, uint32_t n,
+                                                      const uint64_t *__restrict__ obase,
+                                                      const uint32_t *__restrict__ unit_first, uint64_t unit_cap,
+                                                      const uint64_t *__restrict__ total_ptr) {
+    const uint64_t total = *total_ptr;
+    uint64_t n_units = (total + kTxUnit - 1) / kTxUnit;
+    if (n_units > unit_cap) n_units = unit_cap;
+    const int lane = threadIdx.x & 63;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t nw = (uint64_t)gridDim.x * (kBlock / 64);
+    for (uint64_t u = (uint64_t)blockIdx.x * (kBlock / 64) + wave; u < n_units; u += nw) {
+        const uint32_t flo = unit_first[u];
+        const uint32_t fhi = (u + 1 < n_units) ? unit_first[u + 1] : n - 1;
+        const uint64_t a0 = u * kTxUnit + (uint64_t)lane * 16u;
+        if (fhi - flo >= 2u) {                         // small frames: bytewise with a search
+            for (int j = 0; j < 4; ++j) {
+                const uint64_t a = a0 + (uint64_t)j * 1024u;
+                if (a >= total) break;
+                const uint32_t f = find_frame(obase, flo, fhi, a);
+                tx_bytes(out, src, d, obase, f, a, total);
+            }
+            continue;
+        }
+        // at most two frames: uniform metadata; payload k of frame X covers [PX, EX)
+        const fws_tx_desc dA = d[flo], dB = d[fhi];
+        const uint64_t PA = obase[flo] + tx_hdr_len(dA), EA = PA + dA.len;
+        const uint64_t PB = obase[fhi] + tx_hdr_len(dB), EB = PB + dB.len;
+        const bool two = fhi != flo;
+        const uintptr_t SA = (uintptr_t)(src + dA.src_off) - (uintptr_t)PA;   // src of output byte a: S + a
+        const uintptr_t SB = (uintptr_t)(src + dB.src_off) - (uintptr_t)PB;
+        uintptr_t sb[4];
+        uint32_t sh[4], rk[4];
+        bool full[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint64_t a = a0 + (uint64_t)j * 1024u;
+            const bool inA = a >= PA && a + 16 <= EA;
+            const bool inB = two && a >= PB && a + 16 <= EB;
+            full[j] = inA || inB;
+            const uintptr_t sa = (inB ? SB : SA) + (uintptr_t)a;
+            sb[j] = sa & ~uintptr_t(15);
+            sh[j] = (uint32_t)(sa & 15u);
+            const fws_tx_desc &dx = inB ? dB : dA;
+            const uint32_t ph = (uint32_t)(a - (inB ? PB : PA));
+            rk[j] = dx.masked ? rotr32(dx.key, 8u * (ph & 3u)) : 0u;
+        }
+        u32x4 v0[4], v1[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {              // only blocks holding payload bytes are read
+            v0[j] = v1[j] = u32x4{0u, 0u, 0u, 0u};
+            if (full[j]) {
+                v0[j] = gload16<true>(sb[j]);
+                v1[j] = gload16<true>(sh[j] ? sb[j] + 16u : sb[j]);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint64_t a = a0 + (uint64_t)j * 1024u;
+            if (full[j]) gstore16<true>((uintptr_t)(out + a), tx_shr_bytes(v0[j], v1[j], sh[j]) ^ rk[j]);
+            else if (a < total) tx_bytes(out, src, d, obase, flo, a, total);
+        }
+    }
+}
+
+}  // namespace fwsk
+
+using namespace fwsk;
+
+extern "C" {
+
+void fws_tx_next(uint32_t frame_type, int last_frame_if_possible, uint8_t *last_msg_not_fin, uint8_t *opcode,
+                 uint8_t *fin) {
+    // w_socket.h:845-848, 903-913: a data frame continuing an unfinished message
+    // is a continuation (opcode 0); control frames neither use nor change the state.
+    const bool is_last = last_frame_if_possible != 0;
+    const bool is_control = (frame_type & 8u) != 0;
+    uint8_t op = 0;
+    if (!*last_msg_not_fin || is_control) op = (uint8_t)frame_type;
+    if (!is_control) *last_msg_not_fin = is_last ? 0 : 1;
+    *opcode = op;
+    *fin = is_last ? 1 : 0;
+}
+
+int fws_gpu_encode_frames(fws_gpu_ctx *ctx, void *dev_out, uint64_t out_cap, const void *dev_src,
+                          const fws_tx_desc *dev_descs, uint32_t n, uint64_t *dev_out_len, void *stream) {
+    if (!ctx || !dev_out_len || (n && (!dev_out || !dev_src || !dev_descs))) return FWS_ERR_INVALID;
+    if (((uintptr_t)dev_out & 15u) != 0) return FWS_ERR_INVALID;
+    hipStream_t s = (hipStream_t)stream;
+    int r = fws_hip_status(hipSetDevice(ctx->device));
+    if (r) return r;
+    if (n == 0) return fws_hip_status(hipMemsetAsync(dev_out_len, 0, sizeof(uint64_t), s));
+    const uint64_t units = out_cap / kTxUnit + 2;
+    if ((r = fws_ctx_ensure_plan(ctx, n, units))) return r;
+    fws_plan_ws &ws = ctx->plan;
+    const uint32_t nb = (n + 1023) / 1024;
+    hipLaunchKernelGGL(k_tx_count, dim3(nb), dim3(kBlock), 0, s, dev_descs, n, ws.block_sums);
+    hipLaunchKernelGGL(k_tx_scan, dim3(nb), dim3(kBlock), 0, s, dev_descs, n, ws.block_sums, ws.cbase, ws.total,
+                       dev_out_len, out_cap);
+    uint64_t u = units < ws.unit_cap ? units : ws.unit_cap;
+    hipLaunchKernelGGL(k_tx_units, dim3((unsigned)((u + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, ws.cbase, n,
+                       ws.unit_first, ws.unit_cap, ws.total);
+    uint64_t blocks = (u + 3) / 4;
+    if (blocks > 16384) blocks = 16384;
+    hipLaunchKernelGGL(k_tx_encode, dim3((unsigned)blocks), dim3(kBlock), 0, s, (uint8_t *)dev_out,
+                       (const uint8_t *)dev_src, dev_descs, n, ws.cbase, ws.unit_first, ws.unit_cap, ws.total);
+    return fws_hip_status(hipGetLastError());
+}
+
+}  // extern "C"

@@ -9,7 +9,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._lib import FRAME_DESC, FRAME_INFO, DECODE_RESULT, RX_EVENT, GenParams, check, lib
+from ._lib import FRAME_DESC, FRAME_INFO, DECODE_RESULT, RX_EVENT, TX_DESC, GenParams, check, lib
 
 
 def _stream_handle(stream=None):
@@ -248,3 +248,27 @@ class RxPipe:
             self.close()
         except Exception:
             pass
+
+
+def encode_frames(ctx, out, src, dev_descs, n, out_len=None, stream=None):
+    """fws_gpu_encode_frames: out (device uint8, 16-B aligned) = the frames of
+    dev_descs (device TX_DESC bytes) back to back. Returns the device u64 total
+    tensor (~0 if out is too small); nothing synchronised."""
+    if out_len is None:
+        out_len = torch.empty(1, dtype=torch.int64, device=out.device)
+    check("fws_gpu_encode_frames", lib().fws_gpu_encode_frames(ctx.h, _ptr(out), out.numel(), _ptr(src),
+                                                               _ptr(dev_descs), n, _ptr(out_len),
+                                                               _stream_handle(stream)))
+    return out_len
+
+
+class TxState:
+    """One connection's send sequencing (fws_tx_next, SendFrame's opcode / FIN rule)."""
+
+    def __init__(self):
+        self.last_msg_not_fin = C.c_uint8(0)
+
+    def next(self, frame_type, last):
+        op, fin = C.c_uint8(), C.c_uint8()
+        lib().fws_tx_next(frame_type, int(last), C.byref(self.last_msg_not_fin), C.byref(op), C.byref(fin))
+        return op.value, fin.value

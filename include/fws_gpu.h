@@ -186,6 +186,35 @@ int fws_rx_session_feed(fws_rx_session *s, uint8_t *buf, uint64_t size, uint64_t
                         uint8_t *ctl_out, uint64_t ctl_cap, uint64_t *ctl_used);
 int fws_rx_session_state(const fws_rx_session *s, fws_rx_state *out);
 
+/* ---- send path: batch frame builder -------------------
+ * The bytes WSocket::SendFrame (w_socket.h:832-944) writes for one frame:
+ * b0 = FIN << 7 | opcode, b1 = MASK << 7 | len7, the BE 16 / 64-bit length,
+ * for a client frame the key (native LE u32 of the wire bytes) and the payload
+ * XORed with it from phase 0 (w_socket.h:858-866). The reference draws the key
+ * from SemiSecureRand32 (w_socket.h:860); here the caller supplies it. */
+typedef struct fws_tx_desc {
+    uint64_t src_off;       /* payload bytes at dev_src + src_off */
+    uint64_t len;           /* payload length */
+    uint32_t key;           /* mask key (masked frames) */
+    uint8_t opcode;         /* wire opcode: 0 continuation, 1 TEXT, 2 BIN, 8 CLOSE, 9 PING, 10 PONG */
+    uint8_t fin;
+    uint8_t masked;         /* 1: client frame (MASK bit + key + masked payload); 0: server frame */
+    uint8_t pad;
+} fws_tx_desc;              /* 24 bytes */
+
+/* Opcode and FIN of a connection's next frame by SendFrame's rule
+ * (w_socket.h:845-848, 903-913): a data frame that continues an unfinished
+ * message is a continuation; control frames neither use nor change the state.
+ * frame_type: WSTxFrameType (1 TEXT, 2 BIN, 8 CLOSE, 9 PING, 10 PONG). Host code. */
+void fws_tx_next(uint32_t frame_type, int last_frame_if_possible, uint8_t *last_msg_not_fin, uint8_t *opcode,
+                 uint8_t *fin);
+
+/* dev_out (16-B aligned) = the frames of dev_descs[0..n) back to back;
+ * *dev_out_len (device u64) = their total size, or ~0 if it exceeds out_cap
+ * (then nothing is written). One launch sequence for any mix of sizes. */
+int fws_gpu_encode_frames(fws_gpu_ctx *ctx, void *dev_out, uint64_t out_cap, const void *dev_src,
+                          const fws_tx_desc *dev_descs, uint32_t n, uint64_t *dev_out_len, void *stream);
+
 /* ---- batched, pipelined receive over host memory ---------------------------
  * the reads of one event-loop step (FLoop::OneStep,
  * floop.h:661-703; TCPSocket::Read, tcp_socket.h:387-402) aggregated into one

@@ -128,6 +128,22 @@ size_t orc_reassemble(const uint8_t *unmasked, const orc_frame *frames, size_t n
  * reference; cross-checked against Python's strict decoder in tests. */
 int orc_utf8_valid(const uint8_t *s, size_t n);
 
+/* ---- client / server TX ----------------------------------
+ * w_socket.h:49-65 GetTxWSFrameHdrSize: 2 + (client ? 4 : 0) + (0 | 2 | 8). */
+size_t orc_tx_hdr_size(size_t payload, int is_server);
+/* w_socket.h:832-944 SendFrame, the bytes it writes: b0 = FIN << 7 | opcode,
+ * where a data frame continuing an unfinished message carries opcode 0
+ * (last_msg_not_fin_, :903-913; control frames neither use nor change it);
+ * b1 = MASK << 7 | len7, then the BE 16 / 64-bit length, then (client) the key
+ * as its native LE bytes (:862-866) and the payload masked with it
+ * (WSMaskBytesFast, :861). The reference draws the key from SemiSecureRand32
+ * (:860); here it is an argument. Writes hdr + n bytes to out, returns that. */
+typedef struct orc_tx_state {
+    int last_msg_not_fin;
+} orc_tx_state;
+size_t orc_tx_frame(orc_tx_state *st, int is_server, const uint8_t *payload, size_t n, uint32_t frame_type,
+                    int last_frame_if_possible, uint32_t key, uint8_t *out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -255,4 +255,78 @@ double ref_time_mask_parts(uint8_t *buf, const uint64_t *offs, const uint64_t *l
     return std::chrono::duration<double>(t1 - t0).count();
 }
 
+// ---- client TX: WSClientSocket::WriteFrame -> WSocket::SendFrame (w_socket.h:832-944)
+// The under-socket is one end of a socketpair; the frame bytes SendFrame writes
+// (header built backwards into the IOBuffer's headroom, payload masked with a
+// SemiSecureRand32 key, w_socket.h:858-866) are read back from the other end.
+struct TxProbe : fws::WSClientSocket<false> {
+    using Base = fws::WSClientSocket<false>;
+    using Base::InitWSPart;
+};
+struct TxSrvProbe : fws::WSServerSocket<false> {
+    using Base = fws::WSServerSocket<false>;
+    using Base::InitWSPart;
+};
+
+struct TxSession {
+    bool server = false;
+    TxProbe cli;
+    TxSrvProbe srv;
+    int peer_fd = -1;
+};
+
+void *ref_tx_new(int is_server) {
+    auto *s = new TxSession();
+    s->server = is_server != 0;
+    int sv[2];
+    if (::socketpair(AF_UNIX, SOCK_STREAM, 0, sv) != 0) { delete s; return nullptr; }
+    int big = 8 << 20;
+    ::setsockopt(sv[0], SOL_SOCKET, SO_SNDBUF, &big, sizeof(big));
+    ::setsockopt(sv[1], SOL_SOCKET, SO_RCVBUF, &big, sizeof(big));
+    s->peer_fd = sv[1];
+    if (s->server) {
+        s->srv.under_socket().Init(sv[0], true, fws::NORMAL_SOCKET_STATUS, nullptr, false, false, false);
+        s->srv.InitWSPart();
+    } else {
+        s->cli.under_socket().Init(sv[0], true, fws::NORMAL_SOCKET_STATUS, nullptr, false, false, false);
+        s->cli.InitWSPart();
+    }
+    return s;
+}
+
+void ref_tx_free(void *h) {
+    auto *s = static_cast<TxSession *>(h);
+    if (!s) return;
+    if (s->server) s->srv.under_socket().Close(); else s->cli.under_socket().Close();
+    ::close(s->peer_fd);                        // the probes are leaked, as ref_session_free does
+}
+
+// One WriteFrame(payload, frame_type, last_frame_if_possible) -> SendFrame
+// (w_socket.h:832-944); the frame bytes go to out (*out_len). Returns its value.
+long ref_tx_write(void *h, const uint8_t *payload, size_t n, uint32_t frame_type, int last_frame_if_possible,
+                  uint8_t *out, size_t out_cap, size_t *out_len) {
+    auto *s = static_cast<TxSession *>(h);
+    const size_t head = fws::constants::MAX_WS_FRAME_HEADER_SIZE;
+    fws::IOBuffer io = fws::RequestBuf(head + n + 16);
+    io.start_pos = head;
+    io.size = (ssize_t)n;
+    if (n) std::memcpy(io.data + head, payload, n);
+    const size_t expect = (s->server ? fws::GetTxWSFrameHdrSize<true>(n) : fws::GetTxWSFrameHdrSize<false>(n)) + n;
+    long ret = s->server
+        ? (long)s->srv.WriteFrame(std::move(io), fws::WSTxFrameType(frame_type), last_frame_if_possible != 0)
+        : (long)s->cli.WriteFrame(std::move(io), fws::WSTxFrameType(frame_type), last_frame_if_possible != 0);
+    size_t got = 0;
+    while (ret >= 0 && got < expect && got < out_cap) {
+        ssize_t r = ::read(s->peer_fd, out + got, std::min(out_cap - got, expect - got));
+        if (r <= 0) break;
+        got += (size_t)r;
+    }
+    *out_len = got;
+    return ret;
+}
+
+size_t ref_tx_hdr_size(size_t payload, int is_server) {
+    return is_server ? fws::GetTxWSFrameHdrSize<true>(payload) : fws::GetTxWSFrameHdrSize<false>(payload);
+}
+
 }  // extern "C"

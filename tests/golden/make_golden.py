@@ -7,7 +7,11 @@ own headers by oracle/ref_driver.cpp) drives WSServerSocket<false>::OnRecvData
 (net/w_socket.h:543-769) and fws::WSMaskBytesFast (crypto/ws_mask.h:175).
 The fixtures are data only (inputs + the reference's outputs / digests).
 
-    make -C oracle ref && python tests/golden/make_golden.py
+    make -C oracle ref && python tests/golden/make_golden.py [tx]
+
+tx_cases.json.gz holds the send side: sequences of WriteFrame calls on a
+WSClientSocket<false> / WSServerSocket<false> (-> SendFrame, w_socket.h:832-944)
+with the frame bytes each call wrote (full hex for small frames, sha256 above).
 
 Cases the reference cannot run (it dereferences a null control buffer: empty
 PING/CLOSE, a control header that ends a read before its payload, a PONG whose
@@ -251,8 +255,61 @@ def config_digests():
         json.dump(out, f, indent=1, sort_keys=True)
 
 
+def tx_payload(seed, n):
+    """Payload of a TX golden record: PCG64(seed) bytes (stable across numpy)."""
+    return np.random.default_rng(seed).integers(0, 256, n, dtype=np.uint8).tobytes()
+
+
+TX_HEX_MAX = 512
+
+
+def tx_sequence(rng):
+    """(len, frame_type, last) calls: every length form edge, a fragmented
+    message with a control frame inside it, then random calls, then CLOSE."""
+    calls = [(n, 2, 1) for n in (0, 1, 2, 3, 4, 5, 7, 125, 126, 127, 128, 65535, 65536, 65537, (1 << 20) + 3)]
+    calls += [(10, 1, 0), (300, 2, 0), (0, 9, 1), (70000, 1, 0), (5, 10, 1), (1, 2, 1), (0, 1, 1)]
+    for _ in range(160):
+        kind = rng.random()
+        if kind < 0.25:
+            calls.append((int(rng.integers(0, 126)), int(rng.choice([9, 10])), 1))
+        else:
+            n = int(rng.choice([rng.integers(0, 126), rng.integers(126, 65536), rng.integers(65536, 200000)],
+                               p=[0.5, 0.4, 0.1]))
+            calls.append((n, int(rng.choice([1, 2])), int(rng.random() < 0.6)))
+    calls.append((2, 8, 1))
+    return calls
+
+
+def tx_cases():
+    out = []
+    for is_server in (0, 1):
+        rng = np.random.default_rng(77 + is_server)
+        h, write = orc.ref_tx_session(is_server)
+        frames = []
+        for i, (n, ft, last) in enumerate(tx_sequence(rng)):
+            seed = 1000 * (1 + is_server) + i
+            b = write(tx_payload(seed, n), ft, last)
+            rec = {"seed": seed, "len": n, "frame_type": ft, "last": last, "size": len(b)}
+            hl = len(b) - n
+            rec["key"] = 0 if is_server else int.from_bytes(b[hl - 4:hl], "little")
+            if len(b) <= TX_HEX_MAX:
+                rec["hex"] = b.hex()
+            else:
+                rec["head_hex"] = b[:64].hex()
+                rec["sha256"] = hashlib.sha256(b).hexdigest()
+            frames.append(rec)
+        orc.ref().ref_tx_free(h)
+        out.append({"server": is_server, "frames": frames})
+    with gzip.open(os.path.join(HERE, "tx_cases.json.gz"), "wt") as f:
+        json.dump(out, f, sort_keys=True)
+    print("tx sessions:", [len(x["frames"]) for x in out], flush=True)
+
+
 def main():
     assert orc.ref_available(), "build oracle/_ref first: make -C oracle ref"
+    if sys.argv[1:] == ["tx"]:
+        tx_cases()
+        return
     cases = {}
     for name, reads in kat_cases() + random_stream_cases():
         cases[name] = {"reads": [r.hex() for r in reads], "expected": run_ref(reads)}
@@ -262,6 +319,7 @@ def main():
     mask_sweep()
     print("mask sweep done", flush=True)
     config_digests()
+    tx_cases()
 
 
 if __name__ == "__main__":

@@ -69,6 +69,11 @@ def orc():
         lib.orc_reassemble.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]
         lib.orc_reassemble.restype = C.c_size_t
         lib.orc_utf8_valid.argtypes = [C.c_void_p, C.c_size_t]
+        lib.orc_tx_hdr_size.argtypes = [C.c_size_t, C.c_int]
+        lib.orc_tx_hdr_size.restype = C.c_size_t
+        lib.orc_tx_frame.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t, C.c_uint32, C.c_int,
+                                     C.c_uint32, C.c_void_p]
+        lib.orc_tx_frame.restype = C.c_size_t
         lib.orc_utf8_valid.restype = C.c_int
         _orc = lib
     return _orc
@@ -233,3 +238,45 @@ def orc_to_reference_view(ev, ctl):
         else:
             out.append(rec)
     return out
+
+
+class OrcTx:
+    """The oracle's SendFrame byte builder for one connection (orc_tx_frame)."""
+
+    def __init__(self, is_server=False):
+        self.state = C.c_int(0)
+        self.is_server = int(is_server)
+
+    def frame(self, payload, frame_type, last, key):
+        n = len(payload)
+        out = (C.c_uint8 * (n + 14))()
+        src = (C.c_uint8 * max(n, 1)).from_buffer_copy(bytes(payload) or b"\0")
+        k = orc().orc_tx_frame(C.byref(self.state), self.is_server, src, n, frame_type, int(last), key & 0xFFFFFFFF,
+                               out)
+        return bytes(out[:k])
+
+
+def ref_tx_session(is_server=False):
+    """A real reference WSClientSocket (or WSServerSocket) over a socketpair
+    (oracle/_ref); write(payload, frame_type, last) returns the frame bytes."""
+    L = ref()
+    if not getattr(L, "_tx_bound", False):
+        L.ref_tx_new.restype = C.c_void_p
+        L.ref_tx_new.argtypes = [C.c_int]
+        L.ref_tx_free.argtypes = [C.c_void_p]
+        L.ref_tx_write.restype = C.c_long
+        L.ref_tx_write.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_uint32, C.c_int, C.c_void_p,
+                                   C.c_size_t, C.POINTER(C.c_size_t)]
+        L._tx_bound = True
+    h = L.ref_tx_new(int(is_server))
+
+    def write(payload, frame_type, last):
+        n = len(payload)
+        out = (C.c_uint8 * (n + 14))()
+        src = (C.c_uint8 * max(n, 1)).from_buffer_copy(bytes(payload) or b"\0")
+        got = C.c_size_t()
+        r = L.ref_tx_write(h, src, n, frame_type, int(last), out, n + 14, C.byref(got))
+        assert r == n, r
+        return bytes(out[:got.value])
+
+    return h, write

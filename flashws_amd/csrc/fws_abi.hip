@@ -24,7 +24,11 @@ void free_plan(fws_plan_ws &w) {
     dev_free(w.block_sums);
     dev_free(w.cbase);
     dev_free(w.unit_first);
+    dev_free(w.unit_rec);
     dev_free(w.total);
+    dev_free(w.status);
+    dev_free(w.ticket);
+    dev_free(w.mode);
 }
 
 }  // namespace
@@ -38,7 +42,16 @@ int fws_ctx_ensure_plan(fws_gpu_ctx *ctx, uint64_t frames, uint64_t units) {
     if ((r = dev_alloc(&ctx->plan.block_sums, frames / 1024 + 2))) return r;
     if ((r = dev_alloc(&ctx->plan.cbase, frames + 2))) return r;
     if ((r = dev_alloc(&ctx->plan.unit_first, units + 2))) return r;
+    if ((r = dev_alloc(&ctx->plan.unit_rec, 4 * (units + 2)))) return r;
     if ((r = dev_alloc(&ctx->plan.total, 2))) return r;
+    if ((r = dev_alloc(&ctx->plan.status, frames / 256 + 2))) return r;
+    if ((r = dev_alloc(&ctx->plan.ticket, 2))) return r;
+    if ((r = dev_alloc(&ctx->plan.mode, sizeof(fws_plan_mode) / 8))) return r;
+    if ((r = fws_hip_status(hipMemset(ctx->plan.status, 0, (frames / 256 + 2) * 8)))) return r;
+    if ((r = fws_hip_status(hipMemset(ctx->plan.ticket, 0, 8)))) return r;
+    if ((r = fws_hip_status(hipMemset(ctx->plan.mode, 0, sizeof(fws_plan_mode))))) return r;
+    ctx->plan.status_cap = frames / 256 + 2;
+    ctx->plan.epoch = 0;
     ctx->cap_frames = frames;
     ctx->cap_units = units;
     ctx->plan.unit_cap = units + 1;
@@ -53,6 +66,13 @@ __attribute__((visibility("default"))) int fws_internal_decode_counters(fws_gpu_
     if (!ctx || !out || n <= 0 || !ctx->dec.counters) return FWS_ERR_INVALID;
     if (n > 12) n = 12;
     return fws_hip_status(hipMemcpy(out, ctx->dec.counters, (size_t)n * 4, hipMemcpyDeviceToHost));
+}
+
+// Test hook (not part of the ABI): the last descriptor plan's fws_plan_mode
+// words (byte_space, s0, first_po, last_pe, n_units), synchronously.
+__attribute__((visibility("default"))) int fws_internal_plan_mode(fws_gpu_ctx *ctx, uint64_t *out5) {
+    if (!ctx || !out5 || !ctx->plan.mode) return FWS_ERR_INVALID;
+    return fws_hip_status(hipMemcpy(out5, ctx->plan.mode, 5 * 8, hipMemcpyDeviceToHost));
 }
 
 int fws_gpu_abi_version(void) { return FWS_GPU_ABI_VERSION; }

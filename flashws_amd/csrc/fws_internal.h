@@ -12,12 +12,32 @@ static inline int fws_hip_status(hipError_t e) {
 }
 
 // Device workspace for the chunk plan of one descriptor batch.
+// Descriptor batches are planned two ways in one launch (k_plan): chunk space
+// (cbase / unit_first: any descriptor order) and byte space (unit_first_s:
+// sorted, non-overlapping payloads, one owner per 16-B chunk, no partial
+// stores inside the batch). mode[] tells k_unmask_desc which one holds.
 struct fws_plan_ws {
-    uint64_t *block_sums = nullptr;   // ceil(n / 1024)
+    uint64_t *block_sums = nullptr;   // ceil(n / 1024): gather plan (text_kernels.hip)
     uint64_t *cbase = nullptr;        // n + 1
     uint32_t *unit_first = nullptr;   // units (total chunks / 256) + 1
+    uint32_t *unit_rec = nullptr;     // byte-space units + 1, 4 words each (fws_unit_rec, k_plan)
     uint64_t *total = nullptr;        // 1
-    uint64_t unit_cap = 0;            // capacity of unit_first (writes are clamped)
+    uint64_t *status = nullptr;       // ceil(n / 1024): k_plan look-back words (epoch-tagged)
+    uint32_t *ticket = nullptr;       // k_plan's ordered block ticket (reset by its last block)
+    uint64_t *mode = nullptr;         // kPlanModeWords: fws_plan_mode
+    uint64_t status_cap = 0;
+    uint32_t epoch = 0;               // tag of the last k_plan's status words (1..0xFFFF)
+    uint64_t unit_cap = 0;            // capacity of unit_first / unit_first_s (writes are clamped)
+};
+
+// k_plan's result for the run (device words, base-relative offsets).
+struct fws_plan_mode {
+    uint64_t byte_space;              // 1: unit_first_s holds (sorted, non-overlapping, dense)
+    uint64_t s0;                      // base offset of byte-space unit 0 (first payload, 16-B floor)
+    uint64_t first_po;                // first payload byte of the batch
+    uint64_t last_pe;                 // end of the last payload of the batch
+    uint64_t n_units;                 // byte-space units
+    uint64_t pad[3];
 };
 
 // Super-tile resolve records (merge_kernels.hip).

@@ -16,7 +16,7 @@
 namespace fwsk {
 
 // ---------------------------------------------------------------- plan
-constexpr int kPlanItems = 4;                        // frames per thread
+constexpr int kPlanItems = 1;                        // frames per thread (k_plan)
 constexpr int kPlanTile = kBlock * kPlanItems;       // frames per block
 
 __device__ __forceinline__ uint64_t wave_incl_scan(uint64_t v, int lane) {
@@ -51,73 +51,252 @@ __device__ __forceinline__ uint64_t desc_chunks(const uint8_t *base, const fws_f
     return chunks_of((uintptr_t)(base + d.payload_off), d.payload_len);
 }
 
-__global__ __launch_bounds__(kBlock) void k_plan_count(const uint8_t *base,
-                                                       const fws_frame_desc *__restrict__ d,
-                                                       uint32_t n, const uint32_t *__restrict__ n_dev,
-                                                       uint64_t *__restrict__ block_sums) {
-    if (n_dev && *n_dev < n) n = *n_dev;
-    const uint64_t f0 = uint64_t(blockIdx.x) * kPlanTile + uint64_t(threadIdx.x) * kPlanItems;
-    uint64_t s = 0;
-#pragma unroll
-    for (int i = 0; i < kPlanItems; ++i)
-        if (f0 + i < n) s += desc_chunks(base, d[f0 + i]);
-    uint64_t tot;
-    block_excl_scan(s, &tot);
-    if (threadIdx.x == 0) block_sums[blockIdx.x] = tot;
+// k_plan: the whole descriptor plan in one launch (single-pass scan with a
+// decoupled look-back over ticket-ordered blocks, so it never waits on a block
+// that has not started). Per frame: the chunk prefix cbase and the chunk-space
+// unit map (any descriptor order); the byte-space unit map (frame f owns the
+// 4 KiB unit starts in [po_f, po_{f+1})); and whether the payloads are sorted
+// and non-overlapping, carried through the look-back with the chunk sums. The
+// block holding the last frame writes fws_plan_mode.
+//
+// Look-back word: chunks (bits 0-44) | sorted (45) | state (46-47: 1 block
+// aggregate, 2 inclusive prefix) | epoch (48-63, the call's tag: words of
+// earlier calls are ignored, so nothing is cleared between calls).
+constexpr uint64_t kLbValue = (1ull << 45) - 1;
+constexpr uint64_t kLbSorted = 1ull << 45;
+constexpr uint64_t kLbAgg = 1ull << 46, kLbPrefix = 2ull << 46;
+
+struct PlanArgs {
+    uint64_t *cbase;
+    uint32_t *unit_first;
+    u32x4 *unit_rec;
+    uint64_t *total;
+    uint64_t *status;
+    uint32_t *ticket;
+    fws_plan_mode *mode;
+    uint64_t unit_cap;
+    uint32_t epoch;
+    uint32_t dbg;                                    // timing experiments only: 1 no ticket, 2 no look-back, 4 no maps
+};
+
+// Byte-space unit record (16 B, written by k_plan, one scalar load in the
+// run). Fast kind: the unit meets at most two frames A = the owner of its
+// first byte and B = the next one, and no outer edge of the batch: x, y =
+// their keys rotated for 4-aligned dwords, z = A's payload clipped to the
+// unit as [a0, a1) (13 bits each), w = B's [b0, b1). Slow kind (z bit 30):
+// x = the owner frame; the run walks the frames from there.
+constexpr uint32_t kRecSlow = 1u << 30;
+
+__device__ __forceinline__ uint32_t rec_clip(uint64_t x, uint64_t U0) {
+    return x <= U0 ? 0u : (x >= U0 + 4096u ? 4096u : (uint32_t)(x - U0));
 }
 
-// cbase[f] = chunks of frames [0, f); cbase[n] = total; unit_first[u] = frame
-// holding chunk u * kUnitChunks; *total_out = total chunks.
-__global__ __launch_bounds__(kBlock) void k_plan_scan(const uint8_t *base,
-                                                      const fws_frame_desc *__restrict__ d, uint32_t n,
-                                                      const uint32_t *__restrict__ n_dev,
-                                                      const uint64_t *__restrict__ block_sums,
-                                                      uint64_t *__restrict__ cbase,
-                                                      uint32_t *__restrict__ unit_first,
-                                                      uint64_t *__restrict__ total_out,
-                                                      uint64_t unit_cap) {
-    if (n_dev && *n_dev < n) n = *n_dev;
-    __shared__ uint64_t s_prefix;
-    // prefix of earlier blocks (n_blocks is small: n / 1024)
-    uint64_t p = 0;
-    for (uint32_t b = threadIdx.x; b < blockIdx.x; b += kBlock) p += block_sums[b];
-    uint64_t dummy;
-    uint64_t pe = block_excl_scan(p, &dummy);
-    if (threadIdx.x == kBlock - 1) s_prefix = pe + p;
-    __syncthreads();
-    const uint64_t prefix = s_prefix;
+// U0, E0, E1, po*, pe* base-relative; rk* = aligned_key of the frame.
+__device__ __forceinline__ u32x4 unit_record(uint64_t U0, uint64_t E0, uint64_t E1, uint32_t f, uint64_t poA,
+                                             uint64_t peA, uint32_t rkA, bool hasB, uint64_t poB, uint64_t peB,
+                                             uint32_t rkB, bool hasC, uint64_t poC) {
+    if (U0 < E0 || U0 + 4096u > E1 || (hasC && poC < U0 + 4096u)) return u32x4{f, 0u, kRecSlow, 0u};
+    const uint32_t a0 = rec_clip(poA, U0), a1 = rec_clip(peA, U0);
+    const uint32_t b0 = hasB ? rec_clip(poB, U0) : 0u, b1 = hasB ? rec_clip(peB, U0) : 0u;
+    return u32x4{rkA, hasB ? rkB : 0u, a0 | (a1 << 13), b0 | (b1 << 13)};
+}
 
-    const uint64_t f0 = uint64_t(blockIdx.x) * kPlanTile + uint64_t(threadIdx.x) * kPlanItems;
-    uint64_t c[kPlanItems];
-    uint64_t s = 0;
+__device__ __forceinline__ uint64_t lb_load(const uint64_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void lb_store(uint64_t *p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Last lane whose (non-decreasing) excl is <= x; excl of lane 0 is 0. Fixed
+// trip count, so every lane takes part in every shuffle.
+__device__ __forceinline__ int last_lane_le(uint32_t excl, uint32_t x) {
+    int lo = 0;
 #pragma unroll
-    for (int i = 0; i < kPlanItems; ++i) {
-        c[i] = (f0 + i < n) ? desc_chunks(base, d[f0 + i]) : 0;
-        s += c[i];
+    for (int step = kWave / 2; step > 0; step >>= 1)
+        if ((uint32_t)__shfl(excl, lo + step, kWave) <= x) lo += step;
+    return lo;
+}
+
+__global__ __launch_bounds__(kBlock) void k_plan(const uint8_t *base, const fws_frame_desc *__restrict__ d,
+                                                 uint32_t n, const uint32_t *__restrict__ n_dev, PlanArgs a) {
+    __shared__ uint32_t s_blk;
+    __shared__ uint64_t s_prefix, s_sorted;
+    __shared__ uint64_t s_wsum[kBlock / kWave];
+    __shared__ uint32_t s_wbad[kBlock / kWave];
+    if (n_dev && *n_dev < n) n = *n_dev;
+    const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+    // Look-back order: blockIdx for grids that are co-resident on the chip
+    // (<= 1024 blocks of 256 threads and 8 KB LDS: 4 per CU suffice); larger
+    // grids take an ordered ticket so a block only waits on started blocks.
+    const bool ticketed = gridDim.x > 1024u && !(a.dbg & 1);
+    uint32_t blk = blockIdx.x;
+    if (ticketed) {
+        if (threadIdx.x == 0) s_blk = atomicAdd(a.ticket, 1u);
+        __syncthreads();
+        blk = s_blk;
+        if (blk == gridDim.x - 1 && threadIdx.x == 0) *a.ticket = 0u;   // every ticket is taken
     }
-    uint64_t tot;
-    uint64_t run = prefix + block_excl_scan(s, &tot);
+    if (n == 0) {
+        if (blk == 0 && threadIdx.x == 0) {
+            a.cbase[0] = 0;
+            *a.total = 0;
+            *a.mode = fws_plan_mode{0, 0, 0, 0, 0, {0, 0, 0}};
+        }
+        return;
+    }
+    const uint64_t tag = (uint64_t)a.epoch << 48;
+    const uintptr_t b0 = (uintptr_t)base;
+    // one round of loads: this thread's frame, the next one and the payload
+    // start of the one after (unit records), the batch's first and last frame
+    static_assert(kPlanItems == 1, "k_plan: one frame per thread");
+    const uint64_t f = uint64_t(blk) * kPlanTile + threadIdx.x;
+    const bool has = f < n, hasB = f + 1 < n, hasC = f + 2 < n;
+    fws_frame_desc fa{0, 0, 0, 0}, fb{0, 0, 0, 0};
+    if (has) fa = d[f];
+    if (hasB) fb = d[f + 1];
+    const uint64_t poC = hasC ? d[f + 2].payload_off : 0;
+    const uint64_t po0 = d[0].payload_off;            // byte-space units start at S = (b0 + po_0) & ~15
+    const uint64_t last_pe = d[n - 1].payload_off + d[n - 1].payload_len;
+    const uint64_t poA = fa.payload_off, peA = fa.payload_off + fa.payload_len;
+    const uint64_t poB = fb.payload_off, peB = fb.payload_off + fb.payload_len;
+    const uint64_t s = has ? chunks_of(b0 + poA, fa.payload_len) : 0;
+    const bool srt = !hasB || (peA >= poA && peA <= poB);
+    // block scan of the chunk counts and AND of the sorted bits, one barrier
+    const uint64_t inc = wave_incl_scan(s, lane);
+    const uint64_t bad = __ballot(!srt);
+    if (lane == kWave - 1) {
+        s_wsum[w] = inc;
+        s_wbad[w] = bad != 0;
+    }
+    __syncthreads();
+    uint64_t run0 = inc - s, agg = 0;
+    bool blk_sorted = true;
 #pragma unroll
-    for (int i = 0; i < kPlanItems; ++i) {
-        const uint64_t f = f0 + i;
-        if (f < n) {
-            cbase[f] = run;
-            if (c[i]) {
-                uint64_t u = (run + kUnitChunks - 1) / kUnitChunks;
-                uint64_t ue = (run + c[i] + kUnitChunks - 1) / kUnitChunks;
-                if (ue > unit_cap) ue = unit_cap;   // contract violation guard, never OOB
-                for (; u < ue; ++u) unit_first[u] = (uint32_t)f;
+    for (int i = 0; i < kBlock / kWave; ++i) {
+        run0 += i < w ? s_wsum[i] : 0;
+        agg += s_wsum[i];
+        blk_sorted = blk_sorted && !s_wbad[i];
+    }
+    // Look-back by the whole block: each round reads the 256 nearest earlier
+    // blocks' words at once (every block publishes its aggregate before it
+    // looks back, so one round covers a 256-block grid) and stops at the
+    // nearest inclusive prefix.
+    __shared__ uint32_t s_pstop[kBlock / kWave];
+    __shared__ uint64_t s_lsum[kBlock / kWave];
+    __shared__ uint32_t s_lbad[kBlock / kWave];
+    if (threadIdx.x == 0)
+        lb_store(a.status + blk, tag | (blk == 0 ? kLbPrefix : kLbAgg) | (blk_sorted ? kLbSorted : 0) | agg);
+    uint64_t excl = 0;
+    bool all_sorted = blk_sorted;
+    if (!(a.dbg & 2)) {
+        for (int64_t j = (int64_t)blk - 1; j >= 0; j -= kBlock) {
+            const int64_t idx = j - (int64_t)threadIdx.x;
+            uint64_t st = tag | kLbPrefix | kLbSorted;   // before block 0: an empty prefix
+            if (idx >= 0) {
+                do {
+                    st = lb_load(a.status + idx);
+                } while ((st >> 48) != a.epoch || (st & (3ull << 46)) == 0);
             }
-            run += c[i];
-            if (f == n - 1) {   // the thread holding the last frame has the grand total
-                cbase[n] = run;
-                *total_out = run;
+            const uint64_t pm = __ballot((st & (3ull << 46)) == kLbPrefix);
+            if (lane == 0) s_pstop[w] = pm ? (uint32_t)(w * kWave + __builtin_ctzll(pm)) : (uint32_t)kBlock;
+            __syncthreads();
+            uint32_t stop = kBlock;
+#pragma unroll
+            for (int i = 0; i < kBlock / kWave; ++i) stop = s_pstop[i] < stop ? s_pstop[i] : stop;
+            const bool use = threadIdx.x <= stop && idx >= 0;
+            uint64_t v = use ? (st & kLbValue) : 0;
+            for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+            const uint64_t vb = __ballot(use && !(st & kLbSorted));
+            if (lane == 0) {
+                s_lsum[w] = v;
+                s_lbad[w] = vb != 0;
             }
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < kBlock / kWave; ++i) {
+                excl += s_lsum[i];
+                all_sorted = all_sorted && !s_lbad[i];
+            }
+            __syncthreads();                             // s_pstop / s_lsum reused next round
+            if (stop < (uint32_t)kBlock) break;
         }
     }
-    if (n == 0 && blockIdx.x == 0 && threadIdx.x == 0) {
-        cbase[0] = 0;
-        *total_out = 0;
+    if (threadIdx.x == 0) {
+        if (blk != 0)
+            lb_store(a.status + blk, tag | kLbPrefix | (all_sorted ? kLbSorted : 0) | ((excl + agg) & kLbValue));
+        s_prefix = excl;
+        s_sorted = all_sorted;
+    }
+    __syncthreads();
+    const uint64_t prefix = s_prefix;
+    const uint64_t S = po0 - ((b0 + po0) & 15u);
+    const uint64_t cap = a.unit_cap;
+    const uint64_t nus = last_pe > S ? (last_pe - S + 4095u) / 4096u : 0;
+    uint64_t run = prefix + run0;
+    // this frame's unit-map runs: chunk space [cu, cue), byte space [bu, bue)
+    uint64_t cu = 0, cue = 0, bu = 0, bue = 0;
+    if (has) {
+        a.cbase[f] = run;
+        if (s) {                                      // chunk space: units starting in this frame
+            cu = (run + kUnitChunks - 1) / kUnitChunks;
+            cue = (run + s + kUnitChunks - 1) / kUnitChunks;
+        }
+        run += s;
+        // byte space: the unit starts in [po_f, po_{f+1})
+        bu = f == 0 ? 0 : (poA >= S ? (poA - S + 4095u) / 4096u : cap);
+        bue = !hasB ? nus : (poB >= S ? (poB - S + 4095u) / 4096u : 0);
+        if (f == n - 1) {                             // the thread holding the last frame
+            a.cbase[n] = run;
+            *a.total = run;
+            const bool dense = s_sorted && nus + 1 <= cap && (last_pe - S) <= 2u * (run * 16u) + 65536u;
+            fws_plan_mode m{dense ? 1ull : 0ull, S, po0, last_pe, nus, {0, 0, 0}};
+            *a.mode = m;
+        }
+    }
+    if (cue > cap) cue = cap;                         // contract violation guard, never OOB
+    if (bue > cap) bue = cap;
+    if (cue < cu || (a.dbg & 4)) cue = cu;
+    if (bue < bu || (a.dbg & 4)) bue = bu;
+    // Write both runs wave-cooperatively: the wave's runs are flattened by a
+    // wave prefix so every lane writes one entry per step, whatever mix of
+    // frame sizes (one 4 KiB frame: one entry; a 64 KiB frame: 16).
+    {
+        const uint32_t len = (uint32_t)(cue - cu);
+        const uint32_t incl = (uint32_t)wave_incl_scan(len, lane), excl = incl - len;
+        const uint32_t T = __builtin_amdgcn_readlane(incl, kWave - 1);
+        if (__all(len <= 1u)) {
+            if (len) a.unit_first[cu] = (uint32_t)f;
+        } else for (uint32_t xb = 0; xb < T; xb += kWave) {   // uniform trip count: every lane
+            const uint32_t x = xb + lane;              // stays active for the shuffles (a shuffle
+            const int lo = last_lane_le(excl, x);       // from an inactive lane reads 0)
+            const uint64_t u0 = __shfl(cu, lo, kWave) + (x - (uint32_t)__shfl(excl, lo, kWave));
+            const uint32_t fl = (uint32_t)__shfl(f, lo, kWave);
+            if (x < T) a.unit_first[u0] = fl;
+        }
+    }
+    {
+        const uint32_t rkA = aligned_key(fa.key, fa.phase, b0 + poA);
+        const uint32_t rkB = aligned_key(fb.key, fb.phase, b0 + poB);
+        const uint32_t len = (uint32_t)(bue - bu);
+        const uint32_t incl = (uint32_t)wave_incl_scan(len, lane), excl = incl - len;
+        const uint32_t T = __builtin_amdgcn_readlane(incl, kWave - 1);
+        if (__all(len <= 1u)) {                       // runs of at most one unit: each lane its own
+            if (len)
+                a.unit_rec[bu] = unit_record(S + 4096u * bu, po0, last_pe, (uint32_t)f, poA, peA, rkA, hasB, poB,
+                                             peB, rkB, hasC, poC);
+        } else for (uint32_t xb = 0; xb < T; xb += kWave) {   // uniform trip count (see above)
+            const uint32_t x = xb + lane;
+            const int lo = last_lane_le(excl, x);
+            const uint64_t u0 = __shfl(bu, lo, kWave) + (x - (uint32_t)__shfl(excl, lo, kWave));
+            const u32x4 r = unit_record(S + 4096u * u0, po0, last_pe, (uint32_t)__shfl(f, lo, kWave),
+                                        __shfl(poA, lo, kWave), __shfl(peA, lo, kWave),
+                                        (uint32_t)__shfl(rkA, lo, kWave), __shfl((int)hasB, lo, kWave) != 0,
+                                        __shfl(poB, lo, kWave), __shfl(peB, lo, kWave),
+                                        (uint32_t)__shfl(rkB, lo, kWave), __shfl((int)hasC, lo, kWave) != 0,
+                                        __shfl(poC, lo, kWave));
+            if (x < T) a.unit_rec[u0] = r;
+        }
     }
 }
 
@@ -323,6 +502,70 @@ __global__ __launch_bounds__(kBlock) void k_unmask_fast(uint8_t *base, const fws
     }
 }
 
+// One plan unit per wave, no grid-stride loop: the grid covers every unit of
+// the host-side bound, so the hardware dispatcher balances the waves and no
+// wave runs a second unit at the tail. The scalar metadata is two dependent
+// rounds: {total, unit_first[u], unit_first[u + 1]}, then {d[flo], d[flo + 1],
+// cbase[flo], cbase[flo + 1]}; then all 4 payload loads of a lane issue.
+template <bool kNT>
+__global__ __launch_bounds__(kBlock) void k_unmask_one(uint8_t *base, const fws_frame_desc *__restrict__ d,
+                                                       uint32_t n, const uint32_t *__restrict__ n_dev,
+                                                       const uint64_t *__restrict__ cbase,
+                                                       const uint32_t *__restrict__ unit_first,
+                                                       const uint64_t *__restrict__ total_ptr, uint64_t unit_cap) {
+    constexpr int J = kUnmaskU;
+    const uint64_t u = uint64_t(blockIdx.x) * (kBlock / kWave) + __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    if (u >= unit_cap) return;
+    if (n_dev && *n_dev < n) n = *n_dev;
+    const uint64_t total = *total_ptr;
+    const uint32_t uf0 = unit_first[u];
+    const uint32_t uf1 = (u + 1 < unit_cap) ? unit_first[u + 1] : 0u;
+    uint64_t n_units = (total + kUnitChunks - 1) / kUnitChunks;
+    if (n_units > unit_cap) n_units = unit_cap;
+    if (n == 0 || u >= n_units) return;
+    const uint32_t flo = uf0, fhi = (u + 1 < n_units) ? uf1 : n - 1;
+    const int lane = threadIdx.x & (kWave - 1);
+    const uint64_t g0 = u * kUnitChunks + lane;
+    if (fhi - flo >= 2u) {                              // many small frames: generic path
+#pragma unroll 1
+        for (int j = 0; j < J; ++j) {
+            const uint64_t g = g0 + uint64_t(j) * kWave;
+            if (g < total) unmask_one_chunk(base, d, cbase, flo, fhi, g);
+        }
+        return;
+    }
+    const uint32_t f1 = fhi;                            // flo or flo + 1
+    const fws_frame_desc d0 = d[flo], d1 = d[f1];
+    const uint64_t c0 = cbase[flo], CB1 = cbase[flo + 1];
+    const uintptr_t a0 = (uintptr_t)(base + d0.payload_off), a1 = (uintptr_t)(base + d1.payload_off);
+    const uint64_t A0 = (uint64_t)(a0 & ~uintptr_t(15)) - (c0 << 4);
+    const uint64_t A1 = (uint64_t)(a1 & ~uintptr_t(15)) - (CB1 << 4);
+    const uint64_t L0 = a0, H0 = a0 + d0.payload_len, L1 = a1, H1 = a1 + d1.payload_len;
+    const uint32_t R0 = aligned_key(d0.key, d0.phase, a0), R1 = aligned_key(d1.key, d1.phase, a1);
+    const uint64_t S1 = (f1 > flo) ? CB1 : ~0ull;
+    uintptr_t ca[J];
+    bool live[J], s1[J];
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        const uint64_t g = g0 + uint64_t(j) * kWave;
+        s1[j] = g >= S1;
+        ca[j] = (uintptr_t)((s1[j] ? A1 : A0) + (g << 4));
+        live[j] = g < total;
+    }
+    const uintptr_t safe = (uintptr_t)L0 & ~uintptr_t(15);
+    u32x4 v[J];
+#pragma unroll
+    for (int j = 0; j < J; ++j) v[j] = gload16<kNT>(live[j] ? ca[j] : safe);
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        if (!live[j]) continue;
+        const uintptr_t lo = s1[j] ? L1 : L0, hi = s1[j] ? H1 : H0;
+        const uint32_t rk = s1[j] ? R1 : R0;
+        if (ca[j] >= lo && ca[j] + 16u <= hi) gstore16<kNT>(ca[j], v[j] ^ rk);
+        else store_partial(ca[j], v[j], rk, lo, hi);
+    }
+}
+
 // ----------------------------------------------------------- stream space
 // Unmask of a decoded wire stream (fws_gpu_decode_stream) in stream-byte
 // space: unit u = stream bytes [4 KiB u, 4 KiB (u + 1)), unit_first[u] = the
@@ -514,6 +757,244 @@ __global__ __launch_bounds__(kBlock) void k_utf8_seam(const uint8_t *base, uint6
     }
 }
 
+
+// ------------------------------------------------- descriptor batch, byte space
+// k_unmask_desc: the run of a k_plan. When the payloads are sorted and do not
+// overlap (fws_plan_mode.byte_space) the batch is unmasked in byte space like a
+// decoded stream: unit u = bytes [S + 4 KiB u, S + 4 KiB (u + 1)), every 16-B
+// chunk belongs to one lane, and a chunk is one load, an XOR with a per-byte
+// key mask (zero outside the payloads) and one full 16-B store. Non-payload
+// bytes that share a chunk with payload bytes between the batch's first and
+// last payload byte are stored back unchanged; only the batch's two outer edge
+// chunks use byte-exact stores. No partial-line writes reach HBM inside the
+// batch. Otherwise the chunk-space path (k_unmask_fast's unit body).
+
+// Store the bytes of x that lie in [lo, hi) (dword stores where whole).
+__device__ __forceinline__ void store_bytes(uintptr_t ca, const u32x4 &x, uintptr_t lo, uintptr_t hi) {
+    const uint32_t w4[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uintptr_t w = ca + 4u * i;
+        if (w >= lo && w + 4u <= hi) {
+            *(__attribute__((address_space(1))) uint32_t *)w = w4[i];
+        } else if (w + 4u > lo && w < hi) {
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+                if (w + b >= lo && w + b < hi)
+                    *(__attribute__((address_space(1))) uint8_t *)(w + b) = (uint8_t)(w4[i] >> (8 * b));
+        }
+    }
+}
+
+struct DescRegion {
+    uint64_t po, pe;                                 // absolute payload [po, pe)
+    uint32_t rk;                                     // key for 4-aligned dwords (phase applied)
+};
+
+__device__ __forceinline__ DescRegion desc_region(const fws_frame_desc &fd, uintptr_t b0) {
+    const uint64_t po = b0 + fd.payload_off;
+    return DescRegion{po, po + fd.payload_len, aligned_key(fd.key, fd.phase, po)};
+}
+
+__device__ __forceinline__ u32x4 desc_mask(uint64_t c, const DescRegion &r) {
+    return u32x4{r.rk & byte_sel(c, r.po, r.pe), r.rk & byte_sel(c + 4u, r.po, r.pe),
+                 r.rk & byte_sel(c + 8u, r.po, r.pe), r.rk & byte_sel(c + 12u, r.po, r.pe)};
+}
+
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int k) {
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, k), hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), k);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// Bytes of the dword at unit offset o that lie in [lo, hi) (all < 2^13).
+__device__ __forceinline__ uint32_t byte_sel32(uint32_t o, uint32_t lo, uint32_t hi) {
+    if (o + 4u <= lo || o >= hi) return 0u;
+    const uint32_t s = lo > o ? lo - o : 0u, e = hi < o + 4u ? o + 4u - hi : 0u;
+    return (0xFFFFFFFFu << (8u * s)) & (0xFFFFFFFFu >> (8u * e));
+}
+
+// Slow-kind unit (3+ frames, or an outer edge of the batch): the wave loads
+// the frames from the owner on, 64 at a time (lane i: frame flo + i), clips
+// each payload to the unit ([0, 4096] offsets, 32-bit) and every lane ORs the
+// key masks of the frames starting before the unit's end into its 4 chunks
+// (frame k broadcast by readlane); then the 4 loads, XOR and stores. Chunks
+// reaching outside [E0, E1) are stored byte-exact.
+template <bool kNT>
+__device__ __forceinline__ void byte_space_unit_slow(uint8_t *base, const fws_frame_desc *__restrict__ d,
+                                                     uint32_t n, uint32_t flo, uint64_t E0, uint64_t E1, uint64_t U0,
+                                                     int lane) {
+    const uintptr_t b0 = (uintptr_t)base;
+    const uint64_t c0 = U0 + uint64_t(lane) * 16u;
+    const uint64_t safe = (E1 - 1u) & ~uint64_t(15);   // chunks in [S, E1) hold a byte of the span
+    u32x4 m[kUnmaskU];
+#pragma unroll
+    for (int j = 0; j < kUnmaskU; ++j) m[j] = u32x4{0u, 0u, 0u, 0u};
+    uint32_t o0 = (uint32_t)lane * 16u;
+    asm volatile("" : "+v"(o0));                     // opaque: keeps the 16 dword offsets out of registers
+    for (uint32_t fb = flo; fb < n; fb += kWave) {
+        const uint32_t f = fb + (uint32_t)lane;
+        uint32_t lo = 0, hi = 0, rk = 0;
+        bool starts = false;
+        if (f < n) {
+            const fws_frame_desc fd = d[f];
+            const uint64_t po = b0 + fd.payload_off;
+            starts = po < U0 + 4096u;
+            lo = rec_clip(po, U0);
+            hi = rec_clip(po + fd.payload_len, U0);
+            rk = aligned_key(fd.key, fd.phase, po);
+        }
+        const int cnt = __popcll(__ballot(starts));  // sorted: a prefix of the lanes
+#pragma unroll
+        for (int j = 0; j < kUnmaskU; ++j) {         // chunk by chunk: few live registers
+            const uint32_t o = o0 + (uint32_t)j * 1024u;
+            u32x4 mj = m[j];
+#pragma unroll 1
+            for (int k = 0; k < cnt; ++k) {
+                const uint32_t l = __builtin_amdgcn_readlane(lo, k), h = __builtin_amdgcn_readlane(hi, k);
+                if (o + 16u <= l || o >= h) continue;
+                const uint32_t r = __builtin_amdgcn_readlane(rk, k);
+                mj |= u32x4{r & byte_sel32(o, l, h), r & byte_sel32(o + 4u, l, h), r & byte_sel32(o + 8u, l, h),
+                            r & byte_sel32(o + 12u, l, h)};
+            }
+            m[j] = mj;
+        }
+        if (cnt < kWave) break;
+    }
+    u32x4 v[kUnmaskU];
+#pragma unroll
+    for (int j = 0; j < kUnmaskU; ++j) {
+        const uint64_t c = c0 + uint64_t(j) * 1024u;
+        v[j] = gload16<kNT>(c < E1 ? c : safe);
+    }
+#pragma unroll
+    for (int j = 0; j < kUnmaskU; ++j) {
+        const uint64_t c = c0 + uint64_t(j) * 1024u;
+        if (c >= E1 || !(m[j].x | m[j].y | m[j].z | m[j].w)) continue;
+        const u32x4 x = v[j] ^ m[j];
+        if (c >= E0 && c + 16u <= E1) gstore16<kNT>(c, x);
+        else store_bytes(c, x, E0, E1);
+    }
+}
+
+// One byte-space unit from its k_plan record (fast kind: <= 2 frames, no
+// outer edge, so every chunk of the unit lies inside the batch's span).
+template <bool kNT>
+__device__ __forceinline__ void byte_space_unit(uint8_t *base, const fws_frame_desc *__restrict__ d, uint32_t n,
+                                                const u32x4 &rec, const fws_plan_mode &pm, uint64_t u, int lane) {
+    const uintptr_t b0 = (uintptr_t)base;
+    const uint64_t U0 = b0 + pm.s0 + u * 4096u;
+    if (rec.z & kRecSlow) {
+        if (pm.last_pe > pm.first_po)
+            byte_space_unit_slow<kNT>(base, d, n, rec.x, b0 + pm.first_po, b0 + pm.last_pe, U0, lane);
+        return;
+    }
+    const uint32_t a0 = rec.z & 0x1FFFu, a1 = (rec.z >> 13) & 0x1FFFu;
+    const uint32_t e0 = rec.w & 0x1FFFu, e1 = (rec.w >> 13) & 0x1FFFu;
+    uint32_t o0 = (uint32_t)lane * 16u;
+    asm volatile("" : "+v"(o0));                     // opaque per unit: no hoisted per-dword offsets
+    u32x4 mk[kUnmaskU];
+#pragma unroll
+    for (int j = 0; j < kUnmaskU; ++j) {
+        const uint32_t o = o0 + (uint32_t)j * 1024u;
+        const bool inA = o >= a0 && o + 16u <= a1, inB = o >= e0 && o + 16u <= e1;
+        if (inA || inB) {
+            const uint32_t rk = inA ? rec.x : rec.y;
+            mk[j] = u32x4{rk, rk, rk, rk};
+        } else {
+            mk[j] = u32x4{(rec.x & byte_sel32(o, a0, a1)) | (rec.y & byte_sel32(o, e0, e1)),
+                          (rec.x & byte_sel32(o + 4u, a0, a1)) | (rec.y & byte_sel32(o + 4u, e0, e1)),
+                          (rec.x & byte_sel32(o + 8u, a0, a1)) | (rec.y & byte_sel32(o + 8u, e0, e1)),
+                          (rec.x & byte_sel32(o + 12u, a0, a1)) | (rec.y & byte_sel32(o + 12u, e0, e1))};
+        }
+    }
+    const uint64_t c0 = U0 + uint64_t(lane) * 16u;
+    u32x4 v[kUnmaskU];
+#pragma unroll
+    for (int j = 0; j < kUnmaskU; ++j) v[j] = gload16<kNT>(c0 + uint64_t(j) * 1024u);
+#pragma unroll
+    for (int j = 0; j < kUnmaskU; ++j)
+        if (mk[j].x | mk[j].y | mk[j].z | mk[j].w) gstore16<kNT>(c0 + uint64_t(j) * 1024u, v[j] ^ mk[j]);
+}
+
+// One chunk-space plan unit (any descriptor order): k_unmask_fast's body.
+template <bool kNT>
+__device__ __forceinline__ void chunk_space_unit(uint8_t *base, const fws_frame_desc *__restrict__ d, uint32_t n,
+                                                 const uint64_t *__restrict__ cbase,
+                                                 const uint32_t *__restrict__ unit_first, uint64_t total,
+                                                 uint64_t n_units, uint64_t u, int lane) {
+    constexpr int J = kUnmaskU;
+    const uint32_t flo = unit_first[u];
+    const uint32_t fhi = (u + 1 < n_units) ? unit_first[u + 1] : n - 1;
+    const uint64_t g0 = u * kUnitChunks + lane;
+    if (fhi - flo >= 2u) {
+#pragma unroll 1
+        for (int j = 0; j < J; ++j) {
+            const uint64_t g = g0 + uint64_t(j) * kWave;
+            if (g < total) unmask_one_chunk(base, d, cbase, flo, fhi, g);
+        }
+        return;
+    }
+    const fws_frame_desc d0 = d[flo], d1 = d[fhi];
+    const uint64_t CB1 = cbase[flo + 1];
+    const uintptr_t a0 = (uintptr_t)(base + d0.payload_off), a1 = (uintptr_t)(base + d1.payload_off);
+    const uint64_t A0 = (uint64_t)(a0 & ~uintptr_t(15)) - (cbase[flo] << 4);
+    const uint64_t A1 = (uint64_t)(a1 & ~uintptr_t(15)) - (CB1 << 4);
+    const uint32_t R0 = aligned_key(d0.key, d0.phase, a0), R1 = aligned_key(d1.key, d1.phase, a1);
+    const uint64_t S1 = (fhi > flo) ? CB1 : ~0ull;
+    uintptr_t ca[J];
+    bool live[J], s1[J];
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        const uint64_t g = g0 + uint64_t(j) * kWave;
+        s1[j] = g >= S1;
+        ca[j] = (uintptr_t)((s1[j] ? A1 : A0) + (g << 4));
+        live[j] = g < total;
+    }
+    const uintptr_t safe = a0 & ~uintptr_t(15);
+    u32x4 v[J];
+#pragma unroll
+    for (int j = 0; j < J; ++j) v[j] = gload16<kNT>(live[j] ? ca[j] : safe);
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        if (!live[j]) continue;
+        const uintptr_t lo = s1[j] ? a1 : a0, hi = s1[j] ? a1 + d1.payload_len : a0 + d0.payload_len;
+        const uint32_t rk = s1[j] ? R1 : R0;
+        if (ca[j] >= lo && ca[j] + 16u <= hi) gstore16<kNT>(ca[j], v[j] ^ rk);
+        else store_partial(ca[j], v[j], rk, lo, hi);
+    }
+}
+
+template <bool kNT>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) void k_unmask_desc(uint8_t *base, const fws_frame_desc *__restrict__ d,
+                                                        uint32_t n, const uint64_t *__restrict__ cbase,
+                                                        const uint32_t *__restrict__ unit_first,
+                                                        const u32x4 *__restrict__ unit_rec,
+                                                        const uint64_t *__restrict__ total_ptr,
+                                                        const fws_plan_mode *__restrict__ mode, uint64_t unit_cap) {
+    if (n == 0) return;
+    const int lane = threadIdx.x & (kWave - 1);
+    const uint64_t nwaves = uint64_t(gridDim.x) * (kBlock / kWave);
+    const uint64_t u0 = uint64_t(blockIdx.x) * (kBlock / kWave) + __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    // first round of scalar loads: the plan words and this wave's first unit
+    // record together (index clamped in-bounds; used only if the unit exists)
+    const u32x4 rec0 = unit_rec[u0 < unit_cap ? u0 : unit_cap - 1];
+    const fws_plan_mode pm = *mode;
+    const uint64_t total = *total_ptr;
+    if (pm.byte_space) {
+        u32x4 rec = rec0;
+        for (uint64_t u = u0; u < pm.n_units; u += nwaves) {
+            const u32x4 next = (u + nwaves < pm.n_units) ? unit_rec[u + nwaves] : rec;   // prefetch
+            byte_space_unit<kNT>(base, d, n, rec, pm, u, lane);
+            rec = next;
+        }
+        return;
+    }
+    uint64_t n_units = (total + kUnitChunks - 1) / kUnitChunks;
+    if (n_units > unit_cap) n_units = unit_cap;
+    for (uint64_t u = u0; u < n_units; u += nwaves)
+        chunk_space_unit<kNT>(base, d, n, cbase, unit_first, total, n_units, u, lane);
+}
+
 }  // namespace fwsk
 
 // ---------------------------------------------------------------- launchers
@@ -521,7 +1002,13 @@ using namespace fwsk;
 
 // Kernel variant used by fws_launch_unmask (tuning hook, not part of the ABI):
 // 0 = k_unmask (per-lane search), 1 = k_unmask_fast, 5 = k_unmask_fast nontemporal.
-static int g_unmask_variant = 5;
+static int g_unmask_variant = 7;
+static int g_plan_dbg = 0;
+extern "C" __attribute__((visibility("default"))) int fws_internal_set_plan_dbg(int v) {
+    const int old = g_plan_dbg;
+    g_plan_dbg = v;
+    return old;
+}
 extern "C" __attribute__((visibility("default"))) int fws_internal_set_unmask_variant(int v) {
     const int old = g_unmask_variant;
     if (v >= 0 && v <= 7) g_unmask_variant = v;
@@ -556,9 +1043,16 @@ int fws_launch_mask_single(void *dev_ptr, uint64_t n, uint32_t key, uint32_t pha
 int fws_launch_plan(const uint8_t *base, const fws_frame_desc *d, uint32_t n, const uint32_t *n_dev,
                     fws_plan_ws &ws, hipStream_t s) {
     const uint32_t nb = (n + kPlanTile - 1) / kPlanTile;
-    hipLaunchKernelGGL(k_plan_count, dim3(nb), dim3(kBlock), 0, s, base, d, n, n_dev, ws.block_sums);
-    hipLaunchKernelGGL(k_plan_scan, dim3(nb), dim3(kBlock), 0, s, base, d, n, n_dev, ws.block_sums, ws.cbase,
-                       ws.unit_first, ws.total, ws.unit_cap);
+    if (nb == 0) return 0;
+    if (nb > ws.status_cap) return FWS_ERR_CAPACITY;
+    if (++ws.epoch > 0xFFFFu) {                      // tags wrapped: clear the words of old calls
+        int r = fws_hip_status(hipMemsetAsync(ws.status, 0, ws.status_cap * 8, s));
+        if (r) return r;
+        ws.epoch = 1;
+    }
+    PlanArgs a{ws.cbase, ws.unit_first, (u32x4 *)ws.unit_rec, ws.total, ws.status, ws.ticket,
+               (fws_plan_mode *)ws.mode, ws.unit_cap, ws.epoch, (uint32_t)g_plan_dbg};
+    hipLaunchKernelGGL(k_plan, dim3(nb), dim3(kBlock), 0, s, base, d, n, n_dev, a);
     return fws_hip_status(hipGetLastError());
 }
 
@@ -587,6 +1081,12 @@ int fws_launch_unmask(uint8_t *base, const fws_frame_desc *d, uint32_t n, const 
     if (v == 0 || v == 4)
         hipLaunchKernelGGL(k_unmask<false>, grid, blk, 0, s, base, d, n, n_dev, ws.cbase, ws.unit_first, ws.total,
                            ws.unit_cap, none);
+    else if (v == 7)
+        hipLaunchKernelGGL(k_unmask_desc<true>, grid, blk, 0, s, base, d, n, ws.cbase, ws.unit_first,
+                           (const u32x4 *)ws.unit_rec, ws.total, (const fws_plan_mode *)ws.mode, ws.unit_cap);
+    else if (v == 6)
+        hipLaunchKernelGGL(k_unmask_one<true>, dim3((unsigned)((units + (kBlock / kWave) - 1) / (kBlock / kWave))),
+                           blk, 0, s, base, d, n, n_dev, ws.cbase, ws.unit_first, ws.total, ws.unit_cap);
     else if (v < 4)
         hipLaunchKernelGGL(k_unmask_fast<false>, grid, blk, 0, s, base, d, n, n_dev, ws.cbase, ws.unit_first,
                            ws.total, ws.unit_cap);

@@ -195,6 +195,15 @@ class RxSession:
             pass
 
 
+def plan_mode(ctx):
+    """The last descriptor plan's mode (diagnostic; synchronises): dict with
+    byte_space (payloads sorted and disjoint: byte-space unmask), s0, first_po,
+    last_pe, n_units."""
+    out = (C.c_uint64 * 5)()
+    check("fws_internal_plan_mode", lib().fws_internal_plan_mode(ctx.h, out))
+    return dict(zip(("byte_space", "s0", "first_po", "last_pe", "n_units"), list(out)))
+
+
 def decode_fell_back(ctx):
     """True if the last decode on ctx took the cooperative k_resolve fallback
     instead of the super-tile resolve (diagnostic; synchronises)."""

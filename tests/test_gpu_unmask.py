@@ -129,3 +129,99 @@ def test_unmask_batch_involution(ctx, cuda):
     gpu.unmask_batch(ctx, dev, dd, len(descs))
     torch.cuda.synchronize()
     assert torch.equal(dev.cpu(), torch.from_numpy(wire))
+
+
+# ---- k_plan modes: byte space (sorted, disjoint payloads) vs chunk space ----
+
+def _rand_regions(rng, n, max_len, max_gap, start=5):
+    regions, pos = [], start
+    for _ in range(n):
+        ln = int(rng.integers(0, max_len + 1))
+        regions.append((pos, ln, int(rng.integers(0, 2**32)), int(rng.integers(0, 4))))
+        pos += ln + int(rng.integers(0, max_gap + 1))
+    return regions, pos
+
+
+@pytest.mark.parametrize("permute", [False, True])
+def test_plan_mode_sorted_vs_permuted(ctx, cuda, permute):
+    """The same regions sorted take the byte-space run, permuted the chunk-space
+    run; both bit-exact (alignment sweep layout, gaps up to 70 B)."""
+    rng = np.random.default_rng(21)
+    regions, pos = [], 0
+    for ln in range(0, 400):
+        for sh in (0, 3, 9, 15, 40):
+            pos = (pos + 63) // 64 * 64 + sh
+            regions.append((pos, ln, int(rng.integers(0, 2**32)), int(rng.integers(0, 4))))
+            pos += ln + int(rng.integers(0, 9))
+    host = aligned_host(pos + 64)
+    host[:] = rng.integers(0, 256, len(host), dtype=np.uint8)
+    descs = np.array(regions, dtype=gpu.FRAME_DESC)
+    if permute:
+        descs = descs[rng.permutation(len(descs))]
+    got = run_batch(ctx, host, descs, cuda)
+    assert gpu.plan_mode(ctx)["byte_space"] == (0 if permute else 1)
+    assert np.array_equal(got, oracle_unmask_regions(host, descs))
+
+
+@pytest.mark.parametrize("n,max_len,max_gap", [(1, 5, 0), (3, 20, 3), (1023, 64, 2), (1024, 64, 2),
+                                                (1025, 64, 2), (70000, 30, 3), (300000, 12, 1)])
+def test_plan_lookback_many_blocks(ctx, cuda, n, max_len, max_gap):
+    """Frame counts around the 1024-frame plan block and far past it (the
+    look-back runs over up to 293 blocks), tiny frames with 0-3-byte gaps."""
+    rng = np.random.default_rng(n)
+    regions, pos = _rand_regions(rng, n, max_len, max_gap)
+    host = aligned_host(pos + 32)
+    host[:] = rng.integers(0, 256, len(host), dtype=np.uint8)
+    descs = np.array(regions, dtype=gpu.FRAME_DESC)
+    got = run_batch(ctx, host, descs, cuda)
+    assert gpu.plan_mode(ctx)["byte_space"] == 1
+    assert np.array_equal(got, oracle_unmask_regions(host, descs))
+
+
+def test_plan_large_frames_block_fill(ctx, cuda):
+    """Frames spanning many 4 KiB units (unit maps filled by the whole block):
+    16 MiB + 1 MiB + odd sizes, sorted then permuted."""
+    rng = np.random.default_rng(31)
+    lens = [16 << 20, 3, 1 << 20, 4097, 12345, 0, 65536 * 3 + 7, 9]
+    regions, pos = [], 7
+    for ln in lens:
+        regions.append((pos, ln, int(rng.integers(0, 2**32)), int(rng.integers(0, 4))))
+        pos += ln + 14
+    host = aligned_host(pos + 32)
+    host[:] = rng.integers(0, 256, len(host), dtype=np.uint8)
+    for perm in (False, True):
+        descs = np.array(regions, dtype=gpu.FRAME_DESC)
+        if perm:
+            descs = descs[rng.permutation(len(descs))]
+        got = run_batch(ctx, host, descs, cuda)
+        assert gpu.plan_mode(ctx)["byte_space"] == (0 if perm else 1)
+        assert np.array_equal(got, oracle_unmask_regions(host, descs)), perm
+
+
+def test_plan_sparse_batch_takes_chunk_space(ctx, cuda):
+    """Sorted but sparse payloads (64 B every 1 MiB) stay in chunk space."""
+    rng = np.random.default_rng(41)
+    regions = [(i * (1 << 20) + 3, 64, int(rng.integers(0, 2**32)), 0) for i in range(64)]
+    host = aligned_host(64 << 20)
+    host[:] = rng.integers(0, 256, len(host), dtype=np.uint8)
+    descs = np.array(regions, dtype=gpu.FRAME_DESC)
+    got = run_batch(ctx, host, descs, cuda)
+    assert gpu.plan_mode(ctx)["byte_space"] == 0
+    assert np.array_equal(got, oracle_unmask_regions(host, descs))
+
+
+def test_plan_reused_across_buffers(ctx, cuda):
+    """unmask_plan on one buffer, unmask_run on another of the same alignment
+    (the plan is base-relative), C3-shaped mixed frames."""
+    wire, descs, _ = gpu.config_c3(seed=9, target=8 << 20)
+    a = torch.from_numpy(wire).to(cuda)
+    b = torch.from_numpy(wire).to(cuda)
+    dd = gpu.descs_to_device(descs, cuda)
+    gpu.unmask_plan(ctx, a, dd, len(descs))
+    gpu.unmask_run(ctx, b, dd, len(descs))
+    torch.cuda.synchronize()
+    assert gpu.plan_mode(ctx)["byte_space"] == 1
+    exp = wire.copy()
+    orc.orc_decode_stream(exp)
+    assert np.array_equal(b.cpu().numpy(), exp)
+    assert torch.equal(a.cpu(), torch.from_numpy(wire))

@@ -105,8 +105,14 @@ int fws_gpu_ctx_reserve(fws_gpu_ctx *ctx, uint64_t max_frames, uint64_t max_stre
 int fws_gpu_mask(void *dev_ptr, uint64_t n, uint32_t key, void *stream);
 
 /* Descriptor-mode batch unmask: every region of dev_descs[0..n) (device
- * memory) inside dev_base is unmasked in place. Load-balanced over 16-byte
- * chunks, so one launch covers any mix of frame sizes. */
+ * memory) inside dev_base is unmasked in place. Load-balanced over 4 KiB
+ * units, so one launch covers any mix of frame sizes. Regions must not
+ * overlap; any order is accepted. When they are sorted by offset (a batch cut
+ * from a wire stream) the run works in byte space: non-payload bytes that
+ * share a 16-byte aligned chunk with payload bytes, between the batch's first
+ * and last payload byte, are written back with their own value (no other
+ * writer may change them during the call); bytes outside that span are never
+ * written. */
 int fws_gpu_unmask_batch(fws_gpu_ctx *ctx, void *dev_base, const fws_frame_desc *dev_descs,
                          uint32_t n, void *stream);
 

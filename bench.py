@@ -253,7 +253,7 @@ def stream_decode_extra(ctx, wire_c2, dev, args):
     steps = max(4, min(args.steps, 50)) // 2 * 2         # even: in-place XOR restores the input
     out = {}
 
-    def decode_cfg(name, wire, n_frames, utf8=False, nbuf=4):
+    def decode_cfg(name, wire, n_frames, utf8=False, nbuf=4, pipelined=True):
         c = gpu.Ctx(dev.index or 0, max_frames=n_frames + 64, max_stream_bytes=len(wire))
         bufs = [torch.from_numpy(wire).to(dev) for _ in range(nbuf)]
         cap = n_frames + 64
@@ -272,6 +272,29 @@ def stream_decode_extra(ctx, wire_c2, dev, args):
                "resolve": "k_resolve (fallback)" if gpu.decode_fell_back(c) else "super-tile"}
         if utf8:
             rec["utf8_invalid_frames"] = int((ok[:n_frames] == 0).sum().item())
+        if pipelined and nbuf >= 4:
+            # two batches in flight (two connections' reads): a context, a frame list and a
+            # stream each, so one batch's latency-bound resolve overlaps the other's streaming
+            c2 = gpu.Ctx(dev.index or 0, max_frames=n_frames + 64, max_stream_bytes=len(wire))
+            ctxs = [c, c2]
+            fr2 = [frames, torch.empty_like(frames)]
+            rs2 = [res, torch.empty_like(res)]
+            sts = [torch.cuda.Stream(), torch.cuda.Stream()]
+            def pstep(i):
+                rc, _, _, _ = gpu.decode_stream(ctxs[i % 2], bufs[i % nbuf], cap, frames=fr2[i % 2],
+                                                result=rs2[i % 2], stream=sts[i % 2])
+                assert rc == 0, rc
+            for i in range(4):
+                pstep(i)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for i in range(steps):
+                pstep(i)
+            torch.cuda.synchronize()
+            tp = (time.perf_counter() - t0) / steps
+            rec["two_in_flight"] = {"GiB_per_s": round(payload / tp / GIB, 1), "ms_per_batch": round(tp * 1e3, 4),
+                                    "path": "2 contexts x 2 streams, batches alternate"}
+            c2.close()
         del bufs
         c.close()
         return rec
@@ -292,6 +315,32 @@ def stream_decode_extra(ctx, wire_c2, dev, args):
                                        "fragments": len(d4), "alg_GB_per_s": round((len(w4) + total) / t / 1e9, 1)}
     c.close()
     del src, dsts, w4
+    # TX: the C2 shape sent by a client -- 65 536 x 4 KiB payloads (back to
+    # back in HBM) framed and masked into one wire buffer by fws_gpu_encode_frames
+    n = args.frames
+    pl = args.payload
+    rng = np.random.default_rng(7)
+    txd = np.zeros(n, dtype=gpu.TX_DESC)
+    txd["src_off"] = np.arange(n, dtype=np.uint64) * pl
+    txd["len"] = pl
+    txd["key"] = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    txd["opcode"] = 2
+    txd["fin"] = 1
+    txd["masked"] = 1
+    tsrc = torch.from_numpy(rng.integers(0, 256, n * pl, dtype=np.uint8)).to(dev)
+    tdd = torch.from_numpy(txd.view(np.uint8).copy()).to(dev)
+    hdr = 2 + 4 + (0 if pl < 126 else 2 if pl < 65536 else 8)
+    tx_total = n * (pl + hdr)
+    c = gpu.Ctx(dev.index or 0, max_frames=n, max_stream_bytes=tx_total)
+    touts = [torch.empty(tx_total, dtype=torch.uint8, device=dev) for _ in range(4)]
+    olen = torch.empty(1, dtype=torch.int64, device=dev)
+    t = _time(lambda i: gpu.encode_frames(c, touts[i % 4], tsrc, tdd, n, out_len=olen), steps, stream)
+    assert int(olen.item()) == tx_total
+    out["C2_tx_encode"] = {"GiB_per_s": round(n * pl / t / GIB, 1), "ms_per_step": round(t * 1e3, 4),
+                           "frames": n, "alg_GB_per_s": round((n * pl + tx_total) / t / 1e9, 1),
+                           "path": "fws_gpu_encode_frames: client frames (header + key + masked payload)"}
+    c.close()
+    del touts, tsrc
     # C5 per-GPU share: 262 144 x 16 KiB TEXT frames (4 GiB), decode + fused-launch UTF-8 flags
     if args.c5:
         w5, d5, ok5 = gpu.config_c5()

@@ -126,7 +126,8 @@ __device__ __forceinline__ u32x4 tx_shr_bytes(const u32x4 &v0, const u32x4 &v1, 
                  __builtin_amdgcn_alignbyte(c3, c2, b), __builtin_amdgcn_alignbyte(c4, c3, b)};
 }
 
-// Output bytes [a, min(a + 16, total)) built one by one from frame f on.
+// Output bytes [a, min(a + 16, total)) built one by one from frame f on
+// (units meeting 3+ frames).
 __device__ void tx_bytes(uint8_t *out, const uint8_t *src, const fws_tx_desc *__restrict__ d,
                          const uint64_t *__restrict__ obase, uint32_t f, uint64_t a, uint64_t total) {
     for (uint64_t b = a; b < a + 16 && b < total; ++b) {
@@ -143,6 +144,95 @@ __device__ void tx_bytes(uint8_t *out, const uint8_t *src, const fws_tx_desc *__
         }
         out[b] = (uint8_t)v;
     }
+}
+
+// A 16-B output chunk at a that meets a frame seam, in a unit of at most two
+// frames A (output [OA, EA)) and B (from OB = EA): header bytes come from the
+// descriptors in registers, payload bytes from each frame's shifted, keyed
+// 16-B source window (two aligned block loads each, issued with the unit's
+// other loads), selected byte by byte.
+struct TxSeam {
+    uint64_t PA, EA, PB, EB;
+};
+
+// Source blocks of a seam chunk at a for frame X (payload [PX, EX) in the
+// output, source bytes [s0, s0 + len)): the two aligned 16-B blocks of the
+// window at SX + a; a block that holds no byte of the source range is replaced
+// by `safe16` (its bytes are never selected), so every load is in bounds.
+__device__ __forceinline__ void tx_seam_blocks(uint64_t a, uintptr_t SX, uintptr_t s0, uint64_t len, uintptr_t safe16,
+                                               uintptr_t &b0, uintptr_t &b1, uint32_t &sh) {
+    const uintptr_t sa = SX + (uintptr_t)a;
+    sh = (uint32_t)(sa & 15u);
+    b0 = sa & ~uintptr_t(15);
+    b1 = b0 + 16u;
+    if (len == 0 || b0 + 16u <= s0 || b0 >= s0 + len) b0 = safe16;
+    if (len == 0 || b1 + 16u <= s0 || b1 >= s0 + len) b1 = safe16;
+}
+
+// The frame header as 16 bytes (<= 14 used, rest zero), little-endian dwords:
+// b0, b1, the big-endian 16/64-bit length, then the key bytes (masked frames).
+__device__ __forceinline__ u32x4 tx_hdr_vec(const fws_tx_desc &d) {
+    const uint32_t b0 = ((uint32_t)(d.fin != 0) << 7) | (d.opcode & 15u);
+    const uint32_t m = d.masked ? 0x80u : 0u;
+    const uint32_t k = d.masked ? d.key : 0u;
+    const uint64_t L = d.len;
+    if (L < 126u) return u32x4{b0 | ((m | (uint32_t)L) << 8) | ((k & 0xFFFFu) << 16), k >> 16, 0u, 0u};
+    if (L <= 65535u)
+        return u32x4{b0 | ((m | 126u) << 8) | ((uint32_t)((L >> 8) & 0xFFu) << 16) | ((uint32_t)(L & 0xFFu) << 24), k,
+                     0u, 0u};
+    const uint32_t hi = __builtin_bswap32((uint32_t)(L >> 32)), lo = __builtin_bswap32((uint32_t)L);
+    // bytes 2..9 = L big endian = bswap(hi32) bswap(lo32)
+    return u32x4{b0 | ((m | 127u) << 8) | (hi << 16), (hi >> 16) | (lo << 16), (lo >> 16) | ((k & 0xFFFFu) << 16),
+                 k >> 16};
+}
+
+// 16 bytes of v as seen from byte offset off (-16 < off < 16): byte i of the
+// result is v's byte i + off, zero outside v.
+__device__ __forceinline__ u32x4 tx_bytes_at(const u32x4 &v, int off) {
+    const u32x4 z{0u, 0u, 0u, 0u};
+    return off >= 0 ? tx_shr_bytes(v, z, (uint32_t)off) : tx_shr_bytes(z, v, (uint32_t)(16 + off));
+}
+
+// x clipped to [a, a + 16), as an offset from a.
+__device__ __forceinline__ uint32_t tx_rel(uint64_t x, uint64_t a) {
+    return x <= a ? 0u : (x >= a + 16u ? 16u : (uint32_t)(x - a));
+}
+
+// Byte-select mask of the chunk's bytes [lo, hi) (offsets 0..16) for dword i.
+__device__ __forceinline__ uint32_t tx_sel(uint32_t lo, uint32_t hi, int i) {
+    const uint32_t o = 4u * (uint32_t)i;
+    if (hi <= o || lo >= o + 4u) return 0u;
+    const uint32_t s = lo > o ? lo - o : 0u, e = hi < o + 4u ? o + 4u - hi : 0u;
+    return (0xFFFFFFFFu << (8u * s)) & (0xFFFFFFFFu >> (8u * e));
+}
+
+// The seam chunk at a: A's header, A's payload (pA: keyed source window), B's
+// header, B's payload (pB), each selected on its byte range; 32-bit offsets.
+__device__ __forceinline__ u32x4 tx_seam_combine(uint64_t a, const fws_tx_desc &dA, uint64_t OA, const fws_tx_desc &dB,
+                                                 uint64_t OB, bool two, const TxSeam &z, uint64_t total,
+                                                 const u32x4 &pA, const u32x4 &pB) {
+    const uint32_t t = tx_rel(total, a);
+    const uint32_t oa = tx_rel(OA, a), pa = tx_rel(z.PA, a), ea = tx_rel(z.EA, a);
+    const uint32_t pb = two ? tx_rel(z.PB, a) : ea, eb = two ? tx_rel(z.EB, a) : ea;
+    const int hoA = (int)((int64_t)a - (int64_t)OA), hoB = (int)((int64_t)a - (int64_t)OB);
+    const u32x4 HA = (hoA > -16 && hoA < 16) ? tx_bytes_at(tx_hdr_vec(dA), hoA) : u32x4{0u, 0u, 0u, 0u};
+    const u32x4 HB = (two && hoB > -16 && hoB < 16) ? tx_bytes_at(tx_hdr_vec(dB), hoB) : u32x4{0u, 0u, 0u, 0u};
+    const uint32_t ha[4] = {HA.x, HA.y, HA.z, HA.w}, hb[4] = {HB.x, HB.y, HB.z, HB.w};
+    const uint32_t wa[4] = {pA.x, pA.y, pA.z, pA.w}, wb[4] = {pB.x, pB.y, pB.z, pB.w};
+    uint32_t w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t live = tx_sel(0u, t, i);
+        w[i] = live & ((ha[i] & tx_sel(oa, pa, i)) | (wa[i] & tx_sel(pa, ea, i)) | (hb[i] & tx_sel(ea, pb, i)) |
+                       (wb[i] & tx_sel(pb, eb, i)));
+    }
+    return u32x4{w[0], w[1], w[2], w[3]};
+}
+
+// The output bytes [a, min(a + 16, total)) of x (the output's last chunk).
+__device__ __forceinline__ void tx_store_tail(uint8_t *out, uint64_t a, uint64_t total, const u32x4 &x) {
+    const uint32_t xw[4] = {x.x, x.y, x.z, x.w};
+    for (uint64_t b = a; b < total && b < a + 16u; ++b) out[b] = (uint8_t)(xw[(b - a) >> 2] >> (8u * ((b - a) & 3u)));
 }
 
 __global__ __launch_bounds__(kBlock) void k_tx_encode(uint8_t *__restrict__ out, const uint8_t *__restrict__ src,
@@ -171,41 +261,87 @@ __global__ __launch_bounds__(kBlock) void k_tx_encode(uint8_t *__restrict__ out,
         }
         // at most two frames: uniform metadata; payload k of frame X covers [PX, EX)
         const fws_tx_desc dA = d[flo], dB = d[fhi];
-        const uint64_t PA = obase[flo] + tx_hdr_len(dA), EA = PA + dA.len;
-        const uint64_t PB = obase[fhi] + tx_hdr_len(dB), EB = PB + dB.len;
+        const uint64_t OA = obase[flo], OB = obase[fhi];
+        TxSeam z;
+        z.PA = OA + tx_hdr_len(dA);
+        z.EA = z.PA + dA.len;
+        z.PB = OB + tx_hdr_len(dB);
+        z.EB = z.PB + dB.len;
         const bool two = fhi != flo;
-        const uintptr_t SA = (uintptr_t)(src + dA.src_off) - (uintptr_t)PA;   // src of output byte a: S + a
-        const uintptr_t SB = (uintptr_t)(src + dB.src_off) - (uintptr_t)PB;
+        const bool any_pay = dA.len != 0 || (two && dB.len != 0);          // wave-uniform
+        const uint8_t *const safe = src + (dA.len != 0 ? dA.src_off : dB.src_off);
+        const uintptr_t safe16 = (uintptr_t)safe & ~uintptr_t(15);
+        const uintptr_t SA = (uintptr_t)(src + dA.src_off) - (uintptr_t)z.PA;   // src of output byte a: S + a
+        const uintptr_t SB = (uintptr_t)(src + dB.src_off) - (uintptr_t)z.PB;
         uintptr_t sb[4];
         uint32_t sh[4], rk[4];
-        bool full[4];
+        uint32_t full = 0, seam = 0;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const uint64_t a = a0 + (uint64_t)j * 1024u;
-            const bool inA = a >= PA && a + 16 <= EA;
-            const bool inB = two && a >= PB && a + 16 <= EB;
-            full[j] = inA || inB;
+            const bool inA = a >= z.PA && a + 16 <= z.EA;
+            const bool inB = two && a >= z.PB && a + 16 <= z.EB;
+            if (inA || inB) full |= 1u << j;
+            else if (a < total) seam |= 1u << j;
             const uintptr_t sa = (inB ? SB : SA) + (uintptr_t)a;
-            sb[j] = sa & ~uintptr_t(15);
+            sb[j] = (inA || inB) ? (sa & ~uintptr_t(15)) : safe16;
             sh[j] = (uint32_t)(sa & 15u);
             const fws_tx_desc &dx = inB ? dB : dA;
-            const uint32_t ph = (uint32_t)(a - (inB ? PB : PA));
+            const uint32_t ph = (uint32_t)(a - (inB ? z.PB : z.PA));
             rk[j] = dx.masked ? rotr32(dx.key, 8u * (ph & 3u)) : 0u;
         }
-        u32x4 v0[4], v1[4];
+        // one batch of loads: the full chunks' two aligned source blocks and the
+        // A and B source blocks of this lane's first seam chunk
+        u32x4 v0[4], v1[4], sa0, sa1, sb0, sb1;
+        const int js = seam ? __builtin_ctz(seam) : 0;
+        const uint64_t as = a0 + (uint64_t)js * 1024u;
+        const uintptr_t sA0 = (uintptr_t)(src + dA.src_off), sB0 = (uintptr_t)(src + dB.src_off);
+        uintptr_t qa0, qa1, qb0, qb1;
+        uint32_t sha, shb;
+        tx_seam_blocks(as, SA, sA0, dA.len, safe16, qa0, qa1, sha);
+        tx_seam_blocks(as, SB, sB0, two ? dB.len : 0, safe16, qb0, qb1, shb);
+        if (any_pay) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {              // only blocks holding payload bytes are read
-            v0[j] = v1[j] = u32x4{0u, 0u, 0u, 0u};
-            if (full[j]) {
-                v0[j] = gload16<true>(sb[j]);
-                v1[j] = gload16<true>(sh[j] ? sb[j] + 16u : sb[j]);
+            for (int j = 0; j < 4; ++j) {
+                // default-policy loads: the second block of lane L is the first of lane
+                // L + 1, so it must stay in cache (a nontemporal pair reads it twice)
+                v0[j] = gload16<false>(sb[j]);
+                v1[j] = gload16<false>(sh[j] && ((full >> j) & 1u) ? sb[j] + 16u : sb[j]);
             }
+            sa0 = gload16<false>(qa0);
+            sa1 = gload16<false>(qa1);
+            sb0 = gload16<false>(qb0);
+            sb1 = gload16<false>(qb1);
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v0[j] = v1[j] = u32x4{0u, 0u, 0u, 0u};
+            sa0 = sa1 = sb0 = sb1 = u32x4{0u, 0u, 0u, 0u};
         }
 #pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if ((full >> j) & 1u)
+                gstore16<true>((uintptr_t)(out + a0 + (uint64_t)j * 1024u), tx_shr_bytes(v0[j], v1[j], sh[j]) ^ rk[j]);
+        auto seam_chunk = [&](uint64_t a, const u32x4 &A0, const u32x4 &A1, uint32_t shA, const u32x4 &B0,
+                              const u32x4 &B1, uint32_t shB) {
+            const uint32_t rka = dA.masked ? rotr32(dA.key, 8u * ((uint32_t)(a - z.PA) & 3u)) : 0u;
+            const uint32_t rkb = dB.masked ? rotr32(dB.key, 8u * ((uint32_t)(a - z.PB) & 3u)) : 0u;
+            const u32x4 x = tx_seam_combine(a, dA, OA, dB, OB, two, z, total, tx_shr_bytes(A0, A1, shA) ^ rka,
+                                            tx_shr_bytes(B0, B1, shB) ^ rkb);
+            if (a + 16u <= total) gstore16<true>((uintptr_t)(out + a), x);
+            else tx_store_tail(out, a, total, x);
+        };
+        if (seam) {
+            seam_chunk(as, sa0, sa1, sha, sb0, sb1, shb);
+            seam &= seam - 1u;
+        }
+        if (!__any(seam)) continue;                    // a lane with a second seam chunk (rare)
+#pragma unroll 1
         for (int j = 0; j < 4; ++j) {
+            if (!((seam >> j) & 1u)) continue;
             const uint64_t a = a0 + (uint64_t)j * 1024u;
-            if (full[j]) gstore16<true>((uintptr_t)(out + a), tx_shr_bytes(v0[j], v1[j], sh[j]) ^ rk[j]);
-            else if (a < total) tx_bytes(out, src, d, obase, flo, a, total);
+            tx_seam_blocks(a, SA, sA0, dA.len, safe16, qa0, qa1, sha);
+            tx_seam_blocks(a, SB, sB0, two ? dB.len : 0, safe16, qb0, qb1, shb);
+            seam_chunk(a, gload16<true>(qa0), gload16<true>(qa1), sha, gload16<true>(qb0), gload16<true>(qb1), shb);
         }
     }
 }

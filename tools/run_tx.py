@@ -1,0 +1,34 @@
+#!/usr/bin/env python3
+"""C2-shaped TX encode (65 536 x 4 KiB client frames) run repeatedly, for
+rocprofv3 kernel traces of the fws_gpu_encode_frames launch sequence."""
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from flashws_amd import gpu  # noqa: E402
+
+
+def main(steps=20, n=65536, pl=4096):
+    dev = torch.device("cuda:0")
+    rng = np.random.default_rng(7)
+    txd = np.zeros(n, dtype=gpu.TX_DESC)
+    txd["src_off"] = np.arange(n, dtype=np.uint64) * pl
+    txd["len"] = pl
+    txd["key"] = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    txd["opcode"], txd["fin"], txd["masked"] = 2, 1, 1
+    src = torch.from_numpy(rng.integers(0, 256, n * pl, dtype=np.uint8)).to(dev)
+    dd = torch.from_numpy(txd.view(np.uint8).copy()).to(dev)
+    total = n * (pl + 8)
+    ctx = gpu.Ctx(0, max_frames=n, max_stream_bytes=total)
+    outs = [torch.empty(total, dtype=torch.uint8, device=dev) for _ in range(4)]
+    for i in range(steps):
+        gpu.encode_frames(ctx, outs[i % 4], src, dd, n)
+    torch.cuda.synchronize()
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()

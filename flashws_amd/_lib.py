@@ -87,6 +87,10 @@ SIGNATURES = [
     ("fws_gen_batch", _I, [C.POINTER(GenParams), _P, _U64, _PU64, _P, _U64, _PU64, _P]),
     ("fws_tx_next", None, [_U32, _I, C.POINTER(C.c_uint8), C.POINTER(C.c_uint8), C.POINTER(C.c_uint8)]),
     ("fws_gpu_encode_frames", _I, [_P, _P, _U64, _P, _P, _U32, _P, _P]),
+    ("fws_tx_session_create", _I, [_P, _I, C.POINTER(C.c_void_p)]),
+    ("fws_tx_session_destroy", None, [_P]),
+    ("fws_tx_session_send", _I, [_P, _P, _P, _P, _P, _P, _U32, _P, _U64, _PU64]),
+    ("fws_tx_session_state", _I, [_P, C.POINTER(C.c_uint8)]),
     ("fws_gpu_host_register", _I, [_P, _U64]),
     ("fws_gpu_host_unregister", _I, [_P]),
     ("fws_rx_pipe_create", _I, [_I, _U64, _U32, _U32, _I, C.POINTER(C.c_void_p)]),

@@ -195,6 +195,49 @@ class RxSession:
             pass
 
 
+class TxSession:
+    """fws_tx_session: SendFrame (w_socket.h:832-944) for host payloads of one
+    connection; the frame bytes are built on the GPU."""
+
+    def __init__(self, ctx, is_server=False):
+        h = C.c_void_p()
+        check("fws_tx_session_create", lib().fws_tx_session_create(ctx.h, 1 if is_server else 0, C.byref(h)))
+        self.h = h
+
+    def send(self, frames, out_cap=None):
+        """frames: [(payload bytes, frame_type, last, key)]. Returns (rc, wire
+        bytes, needed length); rc != 0 leaves the session state unchanged."""
+        n = len(frames)
+        bufs = [np.frombuffer(bytes(p), dtype=np.uint8).copy() for p, _, _, _ in frames]
+        ptrs = np.array([b.ctypes.data if len(b) else 0 for b in bufs], dtype=np.uint64)
+        lens = np.array([len(b) for b in bufs], dtype=np.uint64)
+        types = np.array([f[1] for f in frames], dtype=np.uint32)
+        last = np.array([1 if f[2] else 0 for f in frames], dtype=np.uint8)
+        keys = np.array([f[3] & 0xFFFFFFFF for f in frames], dtype=np.uint32)
+        cap = int(lens.sum()) + 14 * n if out_cap is None else out_cap
+        out = np.zeros(max(cap, 1), dtype=np.uint8)
+        ol = C.c_uint64(0)
+        rc = lib().fws_tx_session_send(self.h, ptrs.ctypes.data, lens.ctypes.data, types.ctypes.data,
+                                       last.ctypes.data, keys.ctypes.data, n, out.ctypes.data, cap, C.byref(ol))
+        return rc, out[:ol.value].tobytes() if rc == 0 else b"", ol.value
+
+    def last_msg_not_fin(self):
+        v = C.c_uint8(0)
+        check("fws_tx_session_state", lib().fws_tx_session_state(self.h, C.byref(v)))
+        return v.value
+
+    def close(self):
+        if self.h:
+            lib().fws_tx_session_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def plan_mode(ctx):
     """The last descriptor plan's mode (diagnostic; synchronises): dict with
     byte_space (payloads sorted and disjoint: byte-space unmask), s0, first_po,

@@ -111,4 +111,55 @@ private:
     std::vector<uint8_t> ctl_;
 };
 
+// SendFrame over the GPU for one connection (w_socket.h:832-944): frames are
+// queued with the reference's WriteFrame arguments and sent as one batch;
+// the wire bytes of the whole batch come back in `wire`. A client encoder
+// masks with the keys it is given (the reference draws SemiSecureRand32,
+// w_socket.h:860). Opcode / FIN sequencing carries across batches.
+class GpuTxEncoder {
+public:
+    GpuTxEncoder(GpuContext &ctx, bool is_server) {
+        if (fws_tx_session_create(ctx.get(), is_server ? 1 : 0, &s_) != 0)
+            throw std::runtime_error("fws_tx_session_create failed");
+    }
+    ~GpuTxEncoder() { fws_tx_session_destroy(s_); }
+    GpuTxEncoder(const GpuTxEncoder &) = delete;
+    GpuTxEncoder &operator=(const GpuTxEncoder &) = delete;
+
+    // WriteFrame(buf, frame_type, last_frame_if_possible) for a payload that
+    // stays valid until Flush().
+    void Queue(const uint8_t *payload, uint64_t len, uint32_t frame_type, bool last, uint32_t key = 0) {
+        ptrs_.push_back(payload);
+        lens_.push_back(len);
+        types_.push_back(frame_type);
+        last_.push_back(last ? 1 : 0);
+        keys_.push_back(key);
+    }
+
+    // Frames queued since the last Flush, as wire bytes; 0 or an FWS_ERR_* code.
+    int Flush(std::vector<uint8_t> &wire) {
+        uint64_t need = 0;
+        for (uint64_t l : lens_) need += l + 14;
+        wire.resize(need);
+        uint64_t len = 0;
+        const int r = fws_tx_session_send(s_, ptrs_.data(), lens_.data(), types_.data(), last_.data(), keys_.data(),
+                                          (uint32_t)ptrs_.size(), wire.data(), need, &len);
+        wire.resize(r == 0 ? len : 0);
+        ptrs_.clear();
+        lens_.clear();
+        types_.clear();
+        last_.clear();
+        keys_.clear();
+        return r;
+    }
+
+private:
+    fws_tx_session *s_ = nullptr;
+    std::vector<const uint8_t *> ptrs_;
+    std::vector<uint64_t> lens_;
+    std::vector<uint32_t> types_;
+    std::vector<uint8_t> last_;
+    std::vector<uint32_t> keys_;
+};
+
 }  // namespace fws_amd

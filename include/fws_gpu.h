@@ -221,6 +221,25 @@ void fws_tx_next(uint32_t frame_type, int last_frame_if_possible, uint8_t *last_
 int fws_gpu_encode_frames(fws_gpu_ctx *ctx, void *dev_out, uint64_t out_cap, const void *dev_src,
                           const fws_tx_desc *dev_descs, uint32_t n, uint64_t *dev_out_len, void *stream);
 
+/* Host-memory send for one connection: WSocket::SendFrame (w_socket.h:832-944)
+ * for its next n frames, in order. Frame i = payloads[i][0..lens[i]) of
+ * WSTxFrameType frame_types[i] with last_frame_if_possible = last[i]; a client
+ * session (is_server = 0) masks with keys[i] (the reference draws
+ * SemiSecureRand32, w_socket.h:860; here the caller supplies it). The frames'
+ * wire bytes, back to back, go to out; *out_len = their size. If out_cap is
+ * too small: FWS_ERR_CAPACITY, *out_len = the size needed, nothing sent and
+ * the sequencing state unchanged. Opcode / FIN sequencing (last_msg_not_fin_,
+ * w_socket.h:903-913) is carried across calls. Synchronous; empty control
+ * payloads are sent as empty frames (the reference dereferences a null
+ * buffer there). */
+typedef struct fws_tx_session fws_tx_session;
+int fws_tx_session_create(fws_gpu_ctx *ctx, int is_server, fws_tx_session **out);
+void fws_tx_session_destroy(fws_tx_session *s);
+int fws_tx_session_send(fws_tx_session *s, const uint8_t *const *payloads, const uint64_t *lens,
+                        const uint32_t *frame_types, const uint8_t *last, const uint32_t *keys, uint32_t n,
+                        uint8_t *out, uint64_t out_cap, uint64_t *out_len);
+int fws_tx_session_state(const fws_tx_session *s, uint8_t *last_msg_not_fin);
+
 /* ---- batched, pipelined receive over host memory ---------------------------
  * the reads of one event-loop step (FLoop::OneStep,
  * floop.h:661-703; TCPSocket::Read, tcp_socket.h:387-402) aggregated into one

@@ -33,6 +33,13 @@ int main() {
     EchoSink sink;
     int r = rx.OnRecvData(io, sink);
     std::printf("ret=%d bytes=%zu msgs=%zu\n", r, sink.bytes, sink.msgs);
+    // echo the payload back as a client-masked BIN frame: WriteFrame's
+    // arguments with flashws's own WSTxFrameType (net/w_socket.h:25-31)
+    fws_amd::GpuTxEncoder tx(ctx, /*is_server=*/false);
+    tx.Queue(io.data + 32 + 6, 5, fws::WS_BIN_FRAME, true, 0x3d21fa37u);
+    std::vector<uint8_t> wire;
+    r |= tx.Flush(wire);
+    std::printf("tx bytes=%zu\n", wire.size());
     int dev_count = 0;
     fws_gpu_device_count(&dev_count);
     return r;

@@ -153,3 +153,67 @@ def test_encode_then_decode_round_trip(ctx, cuda):
         assert fi[i]["opcode"] == metas[i][0] and fi[i]["fin"] == metas[i][1] and fi[i]["key"] == metas[i][2]
         o = int(fi[i]["hdr_off"]) + int(fi[i]["hdr_len"])
         assert host[o:o + len(payloads[i])].tobytes() == payloads[i], i
+
+
+# ---- fws_tx_session: SendFrame for host payloads of one connection ----------
+
+@pytest.mark.parametrize("sess", SESSIONS, ids=lambda s: "server" if s["server"] else "client")
+@pytest.mark.parametrize("batch", [1, 7, 1000])
+def test_tx_session_reference(ctx, cuda, sess, batch):
+    """The reference's own WriteFrame sequence (tests/golden/tx_cases.json.gz)
+    sent through one session in calls of `batch` frames: every frame's bytes
+    equal the reference's; sequencing carried across calls."""
+    tx = gpu.TxSession(ctx, is_server=bool(sess["server"]))
+    frames = [(tx_payload(r["seed"], r["len"]), r["frame_type"], r["last"], r["key"]) for r in sess["frames"]]
+    recs = sess["frames"]
+    for i0 in range(0, len(frames), batch):
+        rc, out, n = tx.send(frames[i0:i0 + batch])
+        assert rc == 0 and len(out) == n
+        pos = 0
+        for i in range(i0, min(i0 + batch, len(frames))):
+            assert frame_matches(recs[i], out[pos:pos + recs[i]["size"]]), (i, recs[i]["len"])
+            pos += recs[i]["size"]
+        assert pos == len(out)
+    tx.close()
+
+
+def test_tx_session_capacity_keeps_state(ctx, cuda):
+    """Too small an output: FWS_ERR_CAPACITY with the size needed, nothing sent,
+    the open message stays open; the retry emits the same bytes."""
+    tx = gpu.TxSession(ctx, is_server=False)
+    rc, out, n = tx.send([(b"abc", 1, False, 0x11223344)])
+    assert rc == 0 and out[0] == 0x01 and tx.last_msg_not_fin() == 1
+    frames = [(b"x" * 200, 1, True, 0x01020304)]
+    rc, _, need = tx.send(frames, out_cap=10)
+    assert rc == -20 and need == 2 + 2 + 4 + 200 and tx.last_msg_not_fin() == 1
+    rc, out, n = tx.send(frames)
+    assert rc == 0 and n == need and out[0] == 0x80                 # FIN continuation of the open message
+    exp = orc.OrcTx(False)
+    exp.frame(b"abc", 1, 0, 0x11223344)
+    assert out == exp.frame(b"x" * 200, 1, 1, 0x01020304)
+    assert tx.last_msg_not_fin() == 0
+    tx.close()
+
+
+def test_tx_session_then_rx_session(ctx, cuda):
+    """Client frames sent by fws_tx_session decode through the server-side
+    fws_rx_session to the same payloads and message boundaries."""
+    rng = np.random.default_rng(12)
+    tx = gpu.TxSession(ctx, is_server=False)
+    rx = gpu.RxSession(ctx, is_server=True)
+    frames, wire = [], b""
+    for i in range(300):
+        ln = int(rng.choice([0, 5, 125, 126, 3000, 70000]))
+        frames.append((rng.integers(0, 256, ln, dtype=np.uint8).tobytes(), int(rng.choice([1, 2])),
+                       bool(rng.random() < 0.7), int(rng.integers(0, 1 << 32))))
+    for i0 in range(0, 300, 64):
+        rc, out, _ = tx.send(frames[i0:i0 + 64])
+        assert rc == 0
+        wire += out
+    ret, buf, ev, ctl = rx.feed(wire)
+    assert ret == 0
+    got = b"".join(bytes(buf[int(e["data_off"]):int(e["data_off"]) + int(e["size"])]) for e in ev if e["kind"] == 0 and not e["is_ctl"])
+    assert got == b"".join(f[0] for f in frames)
+    assert sum(int(e["msg_end"]) for e in ev if e["kind"] == 0) == sum(1 for f in frames if f[2])
+    tx.close()
+    rx.close()

@@ -265,8 +265,9 @@ __global__ __launch_bounds__(kBlock) void k_plan(const uint8_t *base, const fws_
         const uint32_t len = (uint32_t)(cue - cu);
         const uint32_t incl = (uint32_t)wave_incl_scan(len, lane), excl = incl - len;
         const uint32_t T = __builtin_amdgcn_readlane(incl, kWave - 1);
-        if (__all(len <= 1u)) {
+        if (__all(len <= 2u)) {                       // runs of at most two units: each lane its own
             if (len) a.unit_first[cu] = (uint32_t)f;
+            if (len > 1u) a.unit_first[cu + 1] = (uint32_t)f;
         } else for (uint32_t xb = 0; xb < T; xb += kWave) {   // uniform trip count: every lane
             const uint32_t x = xb + lane;              // stays active for the shuffles (a shuffle
             const int lo = last_lane_le(excl, x);       // from an inactive lane reads 0)
@@ -281,10 +282,10 @@ __global__ __launch_bounds__(kBlock) void k_plan(const uint8_t *base, const fws_
         const uint32_t len = (uint32_t)(bue - bu);
         const uint32_t incl = (uint32_t)wave_incl_scan(len, lane), excl = incl - len;
         const uint32_t T = __builtin_amdgcn_readlane(incl, kWave - 1);
-        if (__all(len <= 1u)) {                       // runs of at most one unit: each lane its own
-            if (len)
-                a.unit_rec[bu] = unit_record(S + 4096u * bu, po0, last_pe, (uint32_t)f, poA, peA, rkA, hasB, poB,
-                                             peB, rkB, hasC, poC);
+        if (__all(len <= 2u)) {                       // runs of at most two units: each lane its own
+            for (uint32_t k = 0; k < len; ++k)
+                a.unit_rec[bu + k] = unit_record(S + 4096u * (bu + k), po0, last_pe, (uint32_t)f, poA, peA, rkA, hasB,
+                                                 poB, peB, rkB, hasC, poC);
         } else for (uint32_t xb = 0; xb < T; xb += kWave) {   // uniform trip count (see above)
             const uint32_t x = xb + lane;
             const int lo = last_lane_le(excl, x);

@@ -126,6 +126,12 @@ int fws_launch_unmask(uint8_t *base, const fws_frame_desc *d, uint32_t n, const 
 int fws_launch_unmask_stream(uint8_t *base, uint64_t N, const fws_frame_info *frames, uint32_t cap,
                              const uint32_t *n_dev, const uint32_t *unit_first, uint8_t *utf8_ok, hipStream_t s);
 
+// outplan_kernels.hip: one-launch output-space plans (base = ws.cbase, unit map, total)
+int fws_plan_next_epoch(fws_plan_ws &ws, hipStream_t s);
+int fws_launch_gather_plan(const fws_frame_desc *d, uint32_t n, fws_plan_ws &ws, hipStream_t s);
+int fws_launch_tx_plan(const fws_tx_desc *d, uint32_t n, fws_plan_ws &ws, uint64_t out_cap, uint64_t *out_len,
+                       hipStream_t s);
+
 // text_kernels.hip
 int fws_launch_utf8_descs(const uint8_t *base, const fws_frame_desc *descs, uint32_t n, uint8_t *ok,
                           hipStream_t s);

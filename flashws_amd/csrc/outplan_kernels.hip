@@ -1,0 +1,102 @@
+// outplan_kernels.hip -- one-launch plan of an output-space batch: the
+// out-of-place reassembly (fws_gpu_unmask_gather, C4: region f's payload goes
+// to dst + dbase[f]) and the TX frame builder (fws_gpu_encode_frames: frame f
+// goes to out + obase[f]). One thread per descriptor; the block scan of the
+// output sizes and a decoupled look-back (plan_common.h) give base[f]; frame f
+// owns the 4 KiB output units whose first byte lies in [base[f], base[f + 1]),
+// written wave-cooperatively. Replaces a count / scan / unit-search sequence
+// of three launches.
+#include "fws_device.h"
+#include "fws_internal.h"
+#include "plan_common.h"
+
+namespace fwsk {
+
+struct OutPlanArgs {
+    uint64_t *base;         // n + 1
+    uint32_t *unit_first;   // output units
+    uint64_t unit_cap;
+    uint64_t *total;        // bytes to write (0 when they do not fit out_cap)
+    uint64_t *out_len;      // TX: total, or ~0 when it exceeds out_cap; may be null
+    uint64_t out_cap;
+    uint64_t *status;
+    uint32_t *ticket;
+    uint32_t epoch;
+};
+
+__device__ __forceinline__ uint64_t out_size(const fws_frame_desc &d) { return d.payload_len; }
+__device__ __forceinline__ uint64_t out_size(const fws_tx_desc &d) {   // w_socket.h:49-65
+    return 2u + (d.masked ? 4u : 0u) + (d.len < 126u ? 0u : (d.len <= 65535u ? 2u : 8u)) + d.len;
+}
+
+template <typename Desc>
+__global__ __launch_bounds__(kBlock) void k_out_plan(const Desc *__restrict__ d, uint32_t n, OutPlanArgs a) {
+    __shared__ uint64_t s_wsum[kBlock / kWave];
+    const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+    const uint32_t blk = plan_block_order(a.ticket);
+    const uint64_t f = uint64_t(blk) * kBlock + threadIdx.x;
+    const bool has = f < n;
+    const uint64_t sz = has ? out_size(d[f]) : 0;
+    const uint64_t inc = wave_incl_scan64(sz, lane);
+    if (lane == kWave - 1) s_wsum[w] = inc;
+    __syncthreads();
+    uint64_t run = inc - sz, agg = 0;
+#pragma unroll
+    for (int i = 0; i < kBlock / kWave; ++i) {
+        run += i < w ? s_wsum[i] : 0;
+        agg += s_wsum[i];
+    }
+    bool unused;
+    run += block_lookback(a.status, blk, agg, true, a.epoch, &unused);
+    uint64_t u0 = 0, ue = 0;
+    if (has) {
+        a.base[f] = run;
+        u0 = (run + 4095u) / 4096u;
+        ue = (run + sz + 4095u) / 4096u;
+        if (f == n - 1) {
+            const uint64_t tot = run + sz;
+            const bool fits = tot <= a.out_cap;
+            a.base[n] = tot;
+            *a.total = fits ? tot : 0;                // nothing is written when it does not fit
+            if (a.out_len) *a.out_len = fits ? tot : ~0ull;
+        }
+    }
+    if (ue > a.unit_cap) ue = a.unit_cap;             // contract violation guard, never OOB
+    if (ue < u0) ue = u0;
+    wave_fill_runs(a.unit_first, u0, (uint32_t)(ue - u0), (uint32_t)f, lane);
+}
+
+}  // namespace fwsk
+
+using namespace fwsk;
+
+int fws_plan_next_epoch(fws_plan_ws &ws, hipStream_t s) {
+    if (++ws.epoch > 0xFFFFu) {                       // tags wrapped: clear the words of old calls
+        int r = fws_hip_status(hipMemsetAsync(ws.status, 0, ws.status_cap * 8, s));
+        if (r) return r;
+        ws.epoch = 1;
+    }
+    return 0;
+}
+
+template <typename Desc>
+static int launch_out_plan(const Desc *d, uint32_t n, fws_plan_ws &ws, uint64_t out_cap, uint64_t *out_len,
+                           hipStream_t s) {
+    const uint32_t nb = (n + kBlock - 1) / kBlock;
+    if (nb == 0) return 0;
+    if (nb > ws.status_cap) return FWS_ERR_CAPACITY;
+    int r = fws_plan_next_epoch(ws, s);
+    if (r) return r;
+    OutPlanArgs a{ws.cbase, ws.unit_first, ws.unit_cap, ws.total, out_len, out_cap, ws.status, ws.ticket, ws.epoch};
+    hipLaunchKernelGGL(k_out_plan<Desc>, dim3(nb), dim3(kBlock), 0, s, d, n, a);
+    return fws_hip_status(hipGetLastError());
+}
+
+int fws_launch_gather_plan(const fws_frame_desc *d, uint32_t n, fws_plan_ws &ws, hipStream_t s) {
+    return launch_out_plan(d, n, ws, ~0ull, nullptr, s);
+}
+
+int fws_launch_tx_plan(const fws_tx_desc *d, uint32_t n, fws_plan_ws &ws, uint64_t out_cap, uint64_t *out_len,
+                       hipStream_t s) {
+    return launch_out_plan(d, n, ws, out_cap, out_len, s);
+}

@@ -72,8 +72,8 @@ __global__ __launch_bounds__(kBlock) void k_utf8(const uint8_t *__restrict__ bas
 // concatenation of the on_read() parts (w_socket.h:713-747), the user-level copy
 // of tests/new-ws-echo/test_ws_server.cpp:205-206.
 //
-// Plan: k_gather_count (block sums) -> k_gather_scan (dbase) -> k_gather_units
-// (unit_first[u] = the region holding byte u * 4 KiB, one thread per unit).
+// Plan: k_out_plan (outplan_kernels.hip: dbase, the unit map unit_first[u] = the
+// region holding byte u * 4 KiB, and the total, in one launch).
 // k_gather_fast: one wave per 4 KiB dst unit (4 steps of 64 lanes x 16 B).
 // When the unit meets at most 2 regions (regions >= 4 KiB, as C4's 4 KiB..1 MiB
 // fragments) their metadata is wave-uniform (scalar loads); a dst chunk inside
@@ -82,70 +82,6 @@ __global__ __launch_bounds__(kBlock) void k_utf8(const uint8_t *__restrict__ bas
 // first use. A chunk on a region seam (<= 1 per region) goes byte by byte;
 // units with more regions take the per-chunk search path.
 constexpr uint64_t kGatherUnit = 4096;
-
-__global__ __launch_bounds__(kBlock) void k_gather_count(const fws_frame_desc *__restrict__ d, uint32_t n,
-                                                         uint64_t *__restrict__ block_sums) {
-    __shared__ uint64_t ws[kBlock / 64];
-    uint64_t s = 0;
-    for (uint32_t i = 0; i < 4; ++i) {
-        const uint64_t f = (uint64_t)blockIdx.x * 1024u + threadIdx.x * 4u + i;
-        if (f < n) s += d[f].payload_len;
-    }
-    for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o, 64);
-    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = s;
-    __syncthreads();
-    if (threadIdx.x == 0) block_sums[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
-}
-
-__global__ __launch_bounds__(kBlock) void k_gather_scan(const fws_frame_desc *__restrict__ d, uint32_t n,
-                                                        const uint64_t *__restrict__ block_sums,
-                                                        uint64_t *__restrict__ dbase, uint64_t *__restrict__ total_out) {
-    __shared__ uint64_t wsum[kBlock / 64];
-    __shared__ uint64_t sprefix;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    uint64_t p = 0;
-    for (uint32_t b = threadIdx.x; b < blockIdx.x; b += kBlock) p += block_sums[b];
-    for (int o = 32; o > 0; o >>= 1) p += __shfl_down(p, o, 64);
-    if (lane == 0) wsum[w] = p;
-    __syncthreads();
-    if (threadIdx.x == 0) sprefix = wsum[0] + wsum[1] + wsum[2] + wsum[3];
-    __syncthreads();
-    const uint64_t f0 = (uint64_t)blockIdx.x * 1024u + threadIdx.x * 4u;
-    uint64_t c[4], s = 0;
-    for (int i = 0; i < 4; ++i) { c[i] = (f0 + i < n) ? d[f0 + i].payload_len : 0; s += c[i]; }
-    uint64_t inc = s;
-    for (int o = 1; o < 64; o <<= 1) { const uint64_t x = __shfl_up(inc, o, 64); if (lane >= o) inc += x; }
-    __syncthreads();
-    if (lane == 63) wsum[w] = inc;
-    __syncthreads();
-    uint64_t off = sprefix;
-    for (int i = 0; i < w; ++i) off += wsum[i];
-    uint64_t run = off + inc - s;
-    for (int i = 0; i < 4; ++i) {
-        const uint64_t f = f0 + i;
-        if (f >= n) break;
-        dbase[f] = run;
-        run += c[i];
-        if (f == n - 1) { dbase[n] = run; *total_out = run; }
-    }
-}
-
-// unit_first[u] = last region f with dbase[f] <= u * 4 KiB (the region holding that byte)
-__global__ __launch_bounds__(kBlock) void k_gather_units(const uint64_t *__restrict__ dbase, uint32_t n,
-                                                         uint32_t *__restrict__ unit_first, uint64_t unit_cap,
-                                                         const uint64_t *__restrict__ total_ptr) {
-    const uint64_t u = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    uint64_t n_units = (*total_ptr + kGatherUnit - 1) / kGatherUnit;
-    if (n_units > unit_cap) n_units = unit_cap;
-    if (u >= n_units) return;
-    const uint64_t A = u * kGatherUnit;
-    uint32_t lo = 0, hi = n - 1;
-    while (lo < hi) {
-        const uint32_t mid = lo + ((hi - lo + 1) >> 1);
-        if (dbase[mid] <= A) lo = mid; else hi = mid - 1;
-    }
-    unit_first[u] = lo;
-}
 
 // 16 bytes starting sh (0..15) bytes into the 32-byte window v0:v1
 __device__ __forceinline__ u32x4 shr_bytes(const u32x4 &v0, const u32x4 &v1, uint32_t sh) {
@@ -260,13 +196,10 @@ int fws_launch_utf8_descs(const uint8_t *base, const fws_frame_desc *descs, uint
 int fws_launch_gather(uint8_t *dst, const uint8_t *src, const fws_frame_desc *d, uint32_t n, fws_plan_ws &ws,
                       uint64_t max_bytes, hipStream_t s) {
     if (n == 0) return 0;
-    const uint32_t nb = (n + 1023) / 1024;
-    hipLaunchKernelGGL(k_gather_count, dim3(nb), dim3(kBlock), 0, s, d, n, ws.block_sums);
-    hipLaunchKernelGGL(k_gather_scan, dim3(nb), dim3(kBlock), 0, s, d, n, ws.block_sums, ws.cbase, ws.total);
+    int r = fws_launch_gather_plan(d, n, ws, s);
+    if (r) return r;
     uint64_t units = max_bytes / kGatherUnit + 1;
     if (units > ws.unit_cap) units = ws.unit_cap;
-    hipLaunchKernelGGL(k_gather_units, dim3((unsigned)((units + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, ws.cbase,
-                       n, ws.unit_first, ws.unit_cap, ws.total);
     uint64_t blocks = (units + 3) / 4;
     if (blocks > 16384) blocks = 16384;
     if (blocks < 1) blocks = 1;

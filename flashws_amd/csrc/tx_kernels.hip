@@ -9,9 +9,9 @@
 // sequencing of a connection (last_msg_not_fin_, :903-913) is host logic
 // (fws_tx_next); the device builds bytes.
 //
-// Plan: k_tx_count (block sums of frame sizes) -> k_tx_scan (obase = exclusive
-// prefix, total) -> k_tx_units (unit_first[u] = the frame spanning output byte
-// 4 KiB * u). k_tx_encode: one wave per 4 KiB output unit; each lane owns 16-B
+// Plan: k_out_plan (outplan_kernels.hip, one launch): obase = exclusive prefix
+// of the frame sizes, total, unit_first[u] = the frame spanning output byte
+// 4 KiB * u. k_tx_encode: one wave per 4 KiB output unit; each lane owns 16-B
 // output chunks, so every chunk is one full 16-B store (the last chunk of the
 // output stops at the total). A chunk inside one payload is two aligned source
 // loads shifted by the payload's source misalignment, XORed with the key at the
@@ -37,81 +37,6 @@ __device__ __forceinline__ uint32_t tx_hdr_byte(const fws_tx_desc &d, uint32_t i
     if (i == 1) return m | (ext == 0 ? (uint32_t)d.len : (ext == 2 ? 126u : 127u));
     if (i < 2u + ext) return (uint32_t)(d.len >> (8u * (ext - 1u - (i - 2u)))) & 0xFFu;   // big endian
     return (d.key >> (8u * (i - 2u - ext))) & 0xFFu;                                     // key bytes, LE
-}
-
-__global__ __launch_bounds__(kBlock) void k_tx_count(const fws_tx_desc *__restrict__ d, uint32_t n,
-                                                     uint64_t *__restrict__ block_sums) {
-    __shared__ uint64_t ws[kBlock / 64];
-    uint64_t s = 0;
-    for (uint32_t i = 0; i < 4; ++i) {
-        const uint64_t f = (uint64_t)blockIdx.x * 1024u + threadIdx.x * 4u + i;
-        if (f < n) s += tx_hdr_len(d[f]) + d[f].len;
-    }
-    for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o, 64);
-    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = s;
-    __syncthreads();
-    if (threadIdx.x == 0) block_sums[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
-}
-
-// obase[f] = output offset of frame f; obase[n] = *total = all bytes;
-// *out_len = total, or ~0 when it exceeds out_cap (then nothing is written).
-__global__ __launch_bounds__(kBlock) void k_tx_scan(const fws_tx_desc *__restrict__ d, uint32_t n,
-                                                    const uint64_t *__restrict__ block_sums,
-                                                    uint64_t *__restrict__ obase, uint64_t *__restrict__ total_out,
-                                                    uint64_t *__restrict__ out_len, uint64_t out_cap) {
-    __shared__ uint64_t wsum[kBlock / 64];
-    __shared__ uint64_t sprefix;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    uint64_t p = 0;
-    for (uint32_t b = threadIdx.x; b < blockIdx.x; b += kBlock) p += block_sums[b];
-    for (int o = 32; o > 0; o >>= 1) p += __shfl_down(p, o, 64);
-    if (lane == 0) wsum[w] = p;
-    __syncthreads();
-    if (threadIdx.x == 0) sprefix = wsum[0] + wsum[1] + wsum[2] + wsum[3];
-    __syncthreads();
-    const uint64_t f0 = (uint64_t)blockIdx.x * 1024u + threadIdx.x * 4u;
-    uint64_t c[4], s = 0;
-    for (int i = 0; i < 4; ++i) {
-        c[i] = (f0 + i < n) ? tx_hdr_len(d[f0 + i]) + d[f0 + i].len : 0;
-        s += c[i];
-    }
-    uint64_t inc = s;
-    for (int o = 1; o < 64; o <<= 1) { const uint64_t x = __shfl_up(inc, o, 64); if (lane >= o) inc += x; }
-    __syncthreads();
-    if (lane == 63) wsum[w] = inc;
-    __syncthreads();
-    uint64_t off = sprefix;
-    for (int i = 0; i < w; ++i) off += wsum[i];
-    uint64_t run = off + inc - s;
-    for (int i = 0; i < 4; ++i) {
-        const uint64_t f = f0 + i;
-        if (f >= n) break;
-        obase[f] = run;
-        run += c[i];
-        if (f == n - 1) {
-            obase[n] = run;
-            const bool fits = run <= out_cap;
-            *total_out = fits ? run : 0;               // nothing is encoded when it does not fit
-            *out_len = fits ? run : ~0ull;
-        }
-    }
-}
-
-// unit_first[u] = last frame f with obase[f] <= u * 4 KiB
-__global__ __launch_bounds__(kBlock) void k_tx_units(const uint64_t *__restrict__ obase, uint32_t n,
-                                                     uint32_t *__restrict__ unit_first, uint64_t unit_cap,
-                                                     const uint64_t *__restrict__ total_ptr) {
-    const uint64_t u = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    uint64_t n_units = (*total_ptr + kTxUnit - 1) / kTxUnit;
-    if (n_units > unit_cap) n_units = unit_cap;
-    if (u >= n_units) return;
-    const uint64_t A = u * kTxUnit;
-    uint32_t lo = 0, hi = n - 1;
-    while (lo < hi) {
-        const uint32_t mid = lo + ((hi - lo + 1) >> 1);
-        if (obase[mid] <= A) lo = mid; else hi = mid - 1;
-    }
-    unit_first[u] = lo;
 }
 
 // 16 bytes starting sh (0..15) bytes into the 32-byte window v0:v1
@@ -376,13 +301,8 @@ int fws_gpu_encode_frames(fws_gpu_ctx *ctx, void *dev_out, uint64_t out_cap, con
     const uint64_t units = out_cap / kTxUnit + 2;
     if ((r = fws_ctx_ensure_plan(ctx, n, units))) return r;
     fws_plan_ws &ws = ctx->plan;
-    const uint32_t nb = (n + 1023) / 1024;
-    hipLaunchKernelGGL(k_tx_count, dim3(nb), dim3(kBlock), 0, s, dev_descs, n, ws.block_sums);
-    hipLaunchKernelGGL(k_tx_scan, dim3(nb), dim3(kBlock), 0, s, dev_descs, n, ws.block_sums, ws.cbase, ws.total,
-                       dev_out_len, out_cap);
+    if ((r = fws_launch_tx_plan(dev_descs, n, ws, out_cap, dev_out_len, s))) return r;
     uint64_t u = units < ws.unit_cap ? units : ws.unit_cap;
-    hipLaunchKernelGGL(k_tx_units, dim3((unsigned)((u + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, ws.cbase, n,
-                       ws.unit_first, ws.unit_cap, ws.total);
     uint64_t blocks = (u + 3) / 4;
     if (blocks > 16384) blocks = 16384;
     hipLaunchKernelGGL(k_tx_encode, dim3((unsigned)blocks), dim3(kBlock), 0, s, (uint8_t *)dev_out,

@@ -12,6 +12,7 @@
 // covered chunks). No LDS, no MFMA.
 #include "fws_device.h"
 #include "fws_internal.h"
+#include "plan_common.h"
 
 namespace fwsk {
 
@@ -59,13 +60,6 @@ __device__ __forceinline__ uint64_t desc_chunks(const uint8_t *base, const fws_f
 // and non-overlapping, carried through the look-back with the chunk sums. The
 // block holding the last frame writes fws_plan_mode.
 //
-// Look-back word: chunks (bits 0-44) | sorted (45) | state (46-47: 1 block
-// aggregate, 2 inclusive prefix) | epoch (48-63, the call's tag: words of
-// earlier calls are ignored, so nothing is cleared between calls).
-constexpr uint64_t kLbValue = (1ull << 45) - 1;
-constexpr uint64_t kLbSorted = 1ull << 45;
-constexpr uint64_t kLbAgg = 1ull << 46, kLbPrefix = 2ull << 46;
-
 struct PlanArgs {
     uint64_t *cbase;
     uint32_t *unit_first;
@@ -76,7 +70,6 @@ struct PlanArgs {
     fws_plan_mode *mode;
     uint64_t unit_cap;
     uint32_t epoch;
-    uint32_t dbg;                                    // timing experiments only: 1 no ticket, 2 no look-back, 4 no maps
 };
 
 // Byte-space unit record (16 B, written by k_plan, one scalar load in the
@@ -101,42 +94,14 @@ __device__ __forceinline__ u32x4 unit_record(uint64_t U0, uint64_t E0, uint64_t 
     return u32x4{rkA, hasB ? rkB : 0u, a0 | (a1 << 13), b0 | (b1 << 13)};
 }
 
-__device__ __forceinline__ uint64_t lb_load(const uint64_t *p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void lb_store(uint64_t *p, uint64_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Last lane whose (non-decreasing) excl is <= x; excl of lane 0 is 0. Fixed
-// trip count, so every lane takes part in every shuffle.
-__device__ __forceinline__ int last_lane_le(uint32_t excl, uint32_t x) {
-    int lo = 0;
-#pragma unroll
-    for (int step = kWave / 2; step > 0; step >>= 1)
-        if ((uint32_t)__shfl(excl, lo + step, kWave) <= x) lo += step;
-    return lo;
-}
 
 __global__ __launch_bounds__(kBlock) void k_plan(const uint8_t *base, const fws_frame_desc *__restrict__ d,
                                                  uint32_t n, const uint32_t *__restrict__ n_dev, PlanArgs a) {
-    __shared__ uint32_t s_blk;
-    __shared__ uint64_t s_prefix, s_sorted;
     __shared__ uint64_t s_wsum[kBlock / kWave];
     __shared__ uint32_t s_wbad[kBlock / kWave];
     if (n_dev && *n_dev < n) n = *n_dev;
     const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
-    // Look-back order: blockIdx for grids that are co-resident on the chip
-    // (<= 1024 blocks of 256 threads and 8 KB LDS: 4 per CU suffice); larger
-    // grids take an ordered ticket so a block only waits on started blocks.
-    const bool ticketed = gridDim.x > 1024u && !(a.dbg & 1);
-    uint32_t blk = blockIdx.x;
-    if (ticketed) {
-        if (threadIdx.x == 0) s_blk = atomicAdd(a.ticket, 1u);
-        __syncthreads();
-        blk = s_blk;
-        if (blk == gridDim.x - 1 && threadIdx.x == 0) *a.ticket = 0u;   // every ticket is taken
-    }
+    const uint32_t blk = plan_block_order(a.ticket);
     if (n == 0) {
         if (blk == 0 && threadIdx.x == 0) {
             a.cbase[0] = 0;
@@ -145,7 +110,6 @@ __global__ __launch_bounds__(kBlock) void k_plan(const uint8_t *base, const fws_
         }
         return;
     }
-    const uint64_t tag = (uint64_t)a.epoch << 48;
     const uintptr_t b0 = (uintptr_t)base;
     // one round of loads: this thread's frame, the next one and the payload
     // start of the one after (unit records), the batch's first and last frame
@@ -163,7 +127,7 @@ __global__ __launch_bounds__(kBlock) void k_plan(const uint8_t *base, const fws_
     const uint64_t s = has ? chunks_of(b0 + poA, fa.payload_len) : 0;
     const bool srt = !hasB || (peA >= poA && peA <= poB);
     // block scan of the chunk counts and AND of the sorted bits, one barrier
-    const uint64_t inc = wave_incl_scan(s, lane);
+    const uint64_t inc = wave_incl_scan64(s, lane);
     const uint64_t bad = __ballot(!srt);
     if (lane == kWave - 1) {
         s_wsum[w] = inc;
@@ -178,58 +142,8 @@ __global__ __launch_bounds__(kBlock) void k_plan(const uint8_t *base, const fws_
         agg += s_wsum[i];
         blk_sorted = blk_sorted && !s_wbad[i];
     }
-    // Look-back by the whole block: each round reads the 256 nearest earlier
-    // blocks' words at once (every block publishes its aggregate before it
-    // looks back, so one round covers a 256-block grid) and stops at the
-    // nearest inclusive prefix.
-    __shared__ uint32_t s_pstop[kBlock / kWave];
-    __shared__ uint64_t s_lsum[kBlock / kWave];
-    __shared__ uint32_t s_lbad[kBlock / kWave];
-    if (threadIdx.x == 0)
-        lb_store(a.status + blk, tag | (blk == 0 ? kLbPrefix : kLbAgg) | (blk_sorted ? kLbSorted : 0) | agg);
-    uint64_t excl = 0;
-    bool all_sorted = blk_sorted;
-    if (!(a.dbg & 2)) {
-        for (int64_t j = (int64_t)blk - 1; j >= 0; j -= kBlock) {
-            const int64_t idx = j - (int64_t)threadIdx.x;
-            uint64_t st = tag | kLbPrefix | kLbSorted;   // before block 0: an empty prefix
-            if (idx >= 0) {
-                do {
-                    st = lb_load(a.status + idx);
-                } while ((st >> 48) != a.epoch || (st & (3ull << 46)) == 0);
-            }
-            const uint64_t pm = __ballot((st & (3ull << 46)) == kLbPrefix);
-            if (lane == 0) s_pstop[w] = pm ? (uint32_t)(w * kWave + __builtin_ctzll(pm)) : (uint32_t)kBlock;
-            __syncthreads();
-            uint32_t stop = kBlock;
-#pragma unroll
-            for (int i = 0; i < kBlock / kWave; ++i) stop = s_pstop[i] < stop ? s_pstop[i] : stop;
-            const bool use = threadIdx.x <= stop && idx >= 0;
-            uint64_t v = use ? (st & kLbValue) : 0;
-            for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
-            const uint64_t vb = __ballot(use && !(st & kLbSorted));
-            if (lane == 0) {
-                s_lsum[w] = v;
-                s_lbad[w] = vb != 0;
-            }
-            __syncthreads();
-#pragma unroll
-            for (int i = 0; i < kBlock / kWave; ++i) {
-                excl += s_lsum[i];
-                all_sorted = all_sorted && !s_lbad[i];
-            }
-            __syncthreads();                             // s_pstop / s_lsum reused next round
-            if (stop < (uint32_t)kBlock) break;
-        }
-    }
-    if (threadIdx.x == 0) {
-        if (blk != 0)
-            lb_store(a.status + blk, tag | kLbPrefix | (all_sorted ? kLbSorted : 0) | ((excl + agg) & kLbValue));
-        s_prefix = excl;
-        s_sorted = all_sorted;
-    }
-    __syncthreads();
-    const uint64_t prefix = s_prefix;
+    bool all_sorted;
+    const uint64_t prefix = block_lookback(a.status, blk, agg, blk_sorted, a.epoch, &all_sorted);
     const uint64_t S = po0 - ((b0 + po0) & 15u);
     const uint64_t cap = a.unit_cap;
     const uint64_t nus = last_pe > S ? (last_pe - S + 4095u) / 4096u : 0;
@@ -249,56 +163,39 @@ __global__ __launch_bounds__(kBlock) void k_plan(const uint8_t *base, const fws_
         if (f == n - 1) {                             // the thread holding the last frame
             a.cbase[n] = run;
             *a.total = run;
-            const bool dense = s_sorted && nus + 1 <= cap && (last_pe - S) <= 2u * (run * 16u) + 65536u;
+            const bool dense = all_sorted && nus + 1 <= cap && (last_pe - S) <= 2u * (run * 16u) + 65536u;
             fws_plan_mode m{dense ? 1ull : 0ull, S, po0, last_pe, nus, {0, 0, 0}};
             *a.mode = m;
         }
     }
     if (cue > cap) cue = cap;                         // contract violation guard, never OOB
     if (bue > cap) bue = cap;
-    if (cue < cu || (a.dbg & 4)) cue = cu;
-    if (bue < bu || (a.dbg & 4)) bue = bu;
-    // Write both runs wave-cooperatively: the wave's runs are flattened by a
-    // wave prefix so every lane writes one entry per step, whatever mix of
-    // frame sizes (one 4 KiB frame: one entry; a 64 KiB frame: 16).
-    {
-        const uint32_t len = (uint32_t)(cue - cu);
-        const uint32_t incl = (uint32_t)wave_incl_scan(len, lane), excl = incl - len;
-        const uint32_t T = __builtin_amdgcn_readlane(incl, kWave - 1);
-        if (__all(len <= 2u)) {                       // runs of at most two units: each lane its own
-            if (len) a.unit_first[cu] = (uint32_t)f;
-            if (len > 1u) a.unit_first[cu + 1] = (uint32_t)f;
-        } else for (uint32_t xb = 0; xb < T; xb += kWave) {   // uniform trip count: every lane
-            const uint32_t x = xb + lane;              // stays active for the shuffles (a shuffle
-            const int lo = last_lane_le(excl, x);       // from an inactive lane reads 0)
-            const uint64_t u0 = __shfl(cu, lo, kWave) + (x - (uint32_t)__shfl(excl, lo, kWave));
-            const uint32_t fl = (uint32_t)__shfl(f, lo, kWave);
-            if (x < T) a.unit_first[u0] = fl;
-        }
-    }
-    {
-        const uint32_t rkA = aligned_key(fa.key, fa.phase, b0 + poA);
-        const uint32_t rkB = aligned_key(fb.key, fb.phase, b0 + poB);
-        const uint32_t len = (uint32_t)(bue - bu);
-        const uint32_t incl = (uint32_t)wave_incl_scan(len, lane), excl = incl - len;
-        const uint32_t T = __builtin_amdgcn_readlane(incl, kWave - 1);
-        if (__all(len <= 2u)) {                       // runs of at most two units: each lane its own
-            for (uint32_t k = 0; k < len; ++k)
-                a.unit_rec[bu + k] = unit_record(S + 4096u * (bu + k), po0, last_pe, (uint32_t)f, poA, peA, rkA, hasB,
-                                                 poB, peB, rkB, hasC, poC);
-        } else for (uint32_t xb = 0; xb < T; xb += kWave) {   // uniform trip count (see above)
-            const uint32_t x = xb + lane;
-            const int lo = last_lane_le(excl, x);
-            const uint64_t u0 = __shfl(bu, lo, kWave) + (x - (uint32_t)__shfl(excl, lo, kWave));
-            const u32x4 r = unit_record(S + 4096u * u0, po0, last_pe, (uint32_t)__shfl(f, lo, kWave),
-                                        __shfl(poA, lo, kWave), __shfl(peA, lo, kWave),
-                                        (uint32_t)__shfl(rkA, lo, kWave), __shfl((int)hasB, lo, kWave) != 0,
-                                        __shfl(poB, lo, kWave), __shfl(peB, lo, kWave),
-                                        (uint32_t)__shfl(rkB, lo, kWave), __shfl((int)hasC, lo, kWave) != 0,
-                                        __shfl(poC, lo, kWave));
-            if (x < T) a.unit_rec[u0] = r;
-        }
-    }
+    if (cue < cu) cue = cu;
+    if (bue < bu) bue = bu;
+    wave_fill_runs(a.unit_first, cu, (uint32_t)(cue - cu), (uint32_t)f, lane);
+    // byte-space records, wave-cooperatively like wave_fill_runs
+    struct RecCtx {
+        uint64_t poA, peA, poB, peB, poC;
+        uint32_t f, rkA, rkB;
+        bool hasB, hasC;
+    };
+    const RecCtx mine{poA, peA, poB, peB, poC, (uint32_t)f, aligned_key(fa.key, fa.phase, b0 + poA),
+                      aligned_key(fb.key, fb.phase, b0 + poB), hasB, hasC};
+    wave_for_runs(
+        bu, (uint32_t)(bue - bu),
+        [&](int L) -> RecCtx {
+            if (L < 0) return mine;
+            return RecCtx{readlane64(mine.poA, L), readlane64(mine.peA, L), readlane64(mine.poB, L),
+                          readlane64(mine.peB, L), readlane64(mine.poC, L),
+                          (uint32_t)__builtin_amdgcn_readlane(mine.f, L), (uint32_t)__builtin_amdgcn_readlane(mine.rkA, L),
+                          (uint32_t)__builtin_amdgcn_readlane(mine.rkB, L),
+                          __builtin_amdgcn_readlane((int)mine.hasB, L) != 0,
+                          __builtin_amdgcn_readlane((int)mine.hasC, L) != 0};
+        },
+        [&](const RecCtx &c, uint64_t u) {
+            a.unit_rec[u] = unit_record(S + 4096u * u, po0, last_pe, c.f, c.poA, c.peA, c.rkA, c.hasB, c.poB, c.peB,
+                                        c.rkB, c.hasC, c.poC);
+        });
 }
 
 // ---------------------------------------------------------------- unmask
@@ -802,10 +699,6 @@ __device__ __forceinline__ u32x4 desc_mask(uint64_t c, const DescRegion &r) {
                  r.rk & byte_sel(c + 8u, r.po, r.pe), r.rk & byte_sel(c + 12u, r.po, r.pe)};
 }
 
-__device__ __forceinline__ uint64_t readlane64(uint64_t v, int k) {
-    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, k), hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), k);
-    return ((uint64_t)hi << 32) | lo;
-}
 
 // Bytes of the dword at unit offset o that lie in [lo, hi) (all < 2^13).
 __device__ __forceinline__ uint32_t byte_sel32(uint32_t o, uint32_t lo, uint32_t hi) {
@@ -1004,12 +897,7 @@ using namespace fwsk;
 // Kernel variant used by fws_launch_unmask (tuning hook, not part of the ABI):
 // 0 = k_unmask (per-lane search), 1 = k_unmask_fast, 5 = k_unmask_fast nontemporal.
 static int g_unmask_variant = 7;
-static int g_plan_dbg = 0;
-extern "C" __attribute__((visibility("default"))) int fws_internal_set_plan_dbg(int v) {
-    const int old = g_plan_dbg;
-    g_plan_dbg = v;
-    return old;
-}
+
 extern "C" __attribute__((visibility("default"))) int fws_internal_set_unmask_variant(int v) {
     const int old = g_unmask_variant;
     if (v >= 0 && v <= 7) g_unmask_variant = v;
@@ -1046,13 +934,10 @@ int fws_launch_plan(const uint8_t *base, const fws_frame_desc *d, uint32_t n, co
     const uint32_t nb = (n + kPlanTile - 1) / kPlanTile;
     if (nb == 0) return 0;
     if (nb > ws.status_cap) return FWS_ERR_CAPACITY;
-    if (++ws.epoch > 0xFFFFu) {                      // tags wrapped: clear the words of old calls
-        int r = fws_hip_status(hipMemsetAsync(ws.status, 0, ws.status_cap * 8, s));
-        if (r) return r;
-        ws.epoch = 1;
-    }
+    int r = fws_plan_next_epoch(ws, s);
+    if (r) return r;
     PlanArgs a{ws.cbase, ws.unit_first, (u32x4 *)ws.unit_rec, ws.total, ws.status, ws.ticket,
-               (fws_plan_mode *)ws.mode, ws.unit_cap, ws.epoch, (uint32_t)g_plan_dbg};
+               (fws_plan_mode *)ws.mode, ws.unit_cap, ws.epoch};
     hipLaunchKernelGGL(k_plan, dim3(nb), dim3(kBlock), 0, s, base, d, n, n_dev, a);
     return fws_hip_status(hipGetLastError());
 }

@@ -463,7 +463,12 @@ int fws_launch_resolve(fws_gpu_ctx *ctx, const uint8_t *wire, uint64_t N, uint32
     P.unit_first = ctx->plan.unit_first;
     P.plan_total = ctx->plan.total;
     P.unit_cap = ctx->plan.unit_cap;
-    void *args[] = {&P};
-    return fws_hip_status(hipLaunchCooperativeKernel(reinterpret_cast<const void *>(&k_resolve),
-                                                     dim3(d.resolve_grid), dim3(kRThreads), args, 0, s));
+    // A plain launch: one workgroup per CU is co-resident on an otherwise idle
+    // device, and GridBarrier times out (FWS_ERR_INTERNAL in the result, never
+    // a hang) if workgroups of other streams' kernels keep some of them out.
+    // hipLaunchCooperativeKernel would guarantee residency but goes through the
+    // runtime's cooperative queue: ~12 us of cross-queue waits before and after
+    // the launch, paid by every decode although the common path returns at once.
+    hipLaunchKernelGGL(k_resolve, dim3(d.resolve_grid), dim3(kRThreads), 0, s, P);
+    return fws_hip_status(hipGetLastError());
 }

@@ -29,13 +29,20 @@ __device__ __forceinline__ uint64_t out_size(const fws_tx_desc &d) {   // w_sock
     return 2u + (d.masked ? 4u : 0u) + (d.len < 126u ? 0u : (d.len <= 65535u ? 2u : 8u)) + d.len;
 }
 
-template <typename Desc>
+// One frame per thread for the first kF threads (kF = 64 for batches of few
+// frames -- C4: 1427 fragments of up to 1 MiB, 46 units each on average --
+// so they still spread over many workgroups; 256 for large batches, where the
+// look-back over fewer workgroups is the shorter chain). Then the four waves
+// write the kF frames' unit-map runs, kF / 4 runs each, 64 entries per store.
+template <typename Desc, int kF>
 __global__ __launch_bounds__(kBlock) void k_out_plan(const Desc *__restrict__ d, uint32_t n, OutPlanArgs a) {
+    __shared__ uint64_t s_u0[kF];
+    __shared__ uint32_t s_len[kF];
     __shared__ uint64_t s_wsum[kBlock / kWave];
     const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
     const uint32_t blk = plan_block_order(a.ticket);
-    const uint64_t f = uint64_t(blk) * kBlock + threadIdx.x;
-    const bool has = f < n;
+    const uint64_t f = uint64_t(blk) * kF + threadIdx.x;
+    const bool mine = threadIdx.x < (uint32_t)kF, has = mine && f < n;
     const uint64_t sz = has ? out_size(d[f]) : 0;
     const uint64_t inc = wave_incl_scan64(sz, lane);
     if (lane == kWave - 1) s_wsum[w] = inc;
@@ -48,22 +55,37 @@ __global__ __launch_bounds__(kBlock) void k_out_plan(const Desc *__restrict__ d,
     }
     bool unused;
     run += block_lookback(a.status, blk, agg, true, a.epoch, &unused);
-    uint64_t u0 = 0, ue = 0;
-    if (has) {
-        a.base[f] = run;
-        u0 = (run + 4095u) / 4096u;
-        ue = (run + sz + 4095u) / 4096u;
-        if (f == n - 1) {
-            const uint64_t tot = run + sz;
-            const bool fits = tot <= a.out_cap;
-            a.base[n] = tot;
-            *a.total = fits ? tot : 0;                // nothing is written when it does not fit
-            if (a.out_len) *a.out_len = fits ? tot : ~0ull;
+    if (mine) {
+        uint64_t u0 = 0, ue = 0;
+        if (has) {
+            a.base[f] = run;
+            u0 = (run + 4095u) / 4096u;
+            ue = (run + sz + 4095u) / 4096u;
+            if (f == n - 1) {
+                const uint64_t tot = run + sz;
+                const bool fits = tot <= a.out_cap;
+                a.base[n] = tot;
+                *a.total = fits ? tot : 0;            // nothing is written when it does not fit
+                if (a.out_len) *a.out_len = fits ? tot : ~0ull;
+            }
         }
+        if (ue > a.unit_cap) ue = a.unit_cap;         // contract violation guard, never OOB
+        s_u0[threadIdx.x] = u0;
+        s_len[threadIdx.x] = ue > u0 ? (uint32_t)(ue - u0) : 0u;
     }
-    if (ue > a.unit_cap) ue = a.unit_cap;             // contract violation guard, never OOB
-    if (ue < u0) ue = u0;
-    wave_fill_runs(a.unit_first, u0, (uint32_t)(ue - u0), (uint32_t)f, lane);
+    // short runs (frames of a few KiB): each thread writes its own
+    const uint32_t my_len = mine ? s_len[threadIdx.x] : 0u;
+    if (__syncthreads_and(my_len <= 4u)) {
+        for (uint32_t k = 0; k < my_len; ++k) a.unit_first[s_u0[threadIdx.x] + k] = (uint32_t)f;
+        return;
+    }
+    constexpr uint32_t kPerWave = kF / (kBlock / kWave);
+    for (uint32_t L = (uint32_t)w * kPerWave; L < (uint32_t)(w + 1) * kPerWave; ++L) {
+        const uint32_t len = s_len[L];
+        const uint64_t u0 = s_u0[L];
+        const uint32_t fl = blk * kF + L;
+        for (uint32_t k = (uint32_t)lane; k < len; k += kWave) a.unit_first[u0 + k] = fl;
+    }
 }
 
 }  // namespace fwsk
@@ -82,13 +104,17 @@ int fws_plan_next_epoch(fws_plan_ws &ws, hipStream_t s) {
 template <typename Desc>
 static int launch_out_plan(const Desc *d, uint32_t n, fws_plan_ws &ws, uint64_t out_cap, uint64_t *out_len,
                            hipStream_t s) {
-    const uint32_t nb = (n + kBlock - 1) / kBlock;
-    if (nb == 0) return 0;
+    if (n == 0) return 0;
+    const bool small = n <= 16384u;                   // few frames: 64 per workgroup
+    const uint32_t nb = small ? (n + 63u) / 64u : (n + kBlock - 1) / kBlock;
     if (nb > ws.status_cap) return FWS_ERR_CAPACITY;
     int r = fws_plan_next_epoch(ws, s);
     if (r) return r;
     OutPlanArgs a{ws.cbase, ws.unit_first, ws.unit_cap, ws.total, out_len, out_cap, ws.status, ws.ticket, ws.epoch};
-    hipLaunchKernelGGL(k_out_plan<Desc>, dim3(nb), dim3(kBlock), 0, s, d, n, a);
+    if (small)
+        hipLaunchKernelGGL((k_out_plan<Desc, 64>), dim3(nb), dim3(kBlock), 0, s, d, n, a);
+    else
+        hipLaunchKernelGGL((k_out_plan<Desc, kBlock>), dim3(nb), dim3(kBlock), 0, s, d, n, a);
     return fws_hip_status(hipGetLastError());
 }
 

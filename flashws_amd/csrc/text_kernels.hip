@@ -114,15 +114,23 @@ __global__ __launch_bounds__(kBlock) void k_gather_fast(uint8_t *__restrict__ ds
                                                         const uint64_t *__restrict__ dbase,
                                                         const uint32_t *__restrict__ unit_first, uint64_t unit_cap,
                                                         const uint64_t *__restrict__ total_ptr) {
-    const uint64_t total = *total_ptr;
-    uint64_t n_units = (total + kGatherUnit - 1) / kGatherUnit;
-    if (n_units > unit_cap) n_units = unit_cap;
     const int lane = threadIdx.x & 63;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t nw = (uint64_t)gridDim.x * (kBlock / 64);
-    for (uint64_t u = (uint64_t)blockIdx.x * (kBlock / 64) + wave; u < n_units; u += nw) {
-        const uint32_t flo = unit_first[u];
-        const uint32_t fhi = (u + 1 < n_units) ? unit_first[u + 1] : n - 1;
+    const uint64_t ufirst = (uint64_t)blockIdx.x * (kBlock / 64) + wave;
+    // one scalar round: the total and this wave's first unit map entries (clamped in bounds)
+    const uint64_t uc = ufirst + 1 < unit_cap ? ufirst : (unit_cap >= 2 ? unit_cap - 2 : 0);
+    uint32_t uf0 = unit_first[uc], uf1 = unit_first[uc + 1];
+    const uint64_t total = *total_ptr;
+    uint64_t n_units = (total + kGatherUnit - 1) / kGatherUnit;
+    if (n_units > unit_cap) n_units = unit_cap;
+    for (uint64_t u = ufirst; u < n_units; u += nw) {
+        if (u != ufirst) {
+            uf0 = unit_first[u];
+            uf1 = u + 1 < unit_cap ? unit_first[u + 1] : 0u;
+        }
+        const uint32_t flo = uf0;
+        const uint32_t fhi = (u + 1 < n_units) ? uf1 : n - 1;
         const uint64_t a0 = u * kGatherUnit + (uint64_t)lane * 16u;
         if (fhi - flo >= 2u) {                         // many small regions: per-chunk search
             for (int j = 0; j < 4; ++j) {
@@ -167,9 +175,9 @@ __global__ __launch_bounds__(kBlock) void k_gather_fast(uint8_t *__restrict__ ds
         }
         u32x4 v0[4], v1[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            v0[j] = gload16<true>(sb[j]);
-            v1[j] = gload16<true>(full[j] && sh[j] ? sb[j] + 16u : sb[j]);
+        for (int j = 0; j < 4; ++j) {                 // default policy: lane L's second block is
+            v0[j] = gload16(sb[j]);                     // lane L + 1's first (nontemporal pairs
+            v1[j] = gload16(full[j] && sh[j] ? sb[j] + 16u : sb[j]);   // fetched it twice)
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {

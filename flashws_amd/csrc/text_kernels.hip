@@ -176,8 +176,10 @@ __global__ __launch_bounds__(kBlock) void k_gather_fast(uint8_t *__restrict__ ds
         u32x4 v0[4], v1[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {                 // default policy: lane L's second block is
-            v0[j] = gload16(sb[j]);                     // lane L + 1's first (nontemporal pairs
-            v1[j] = gload16(full[j] && sh[j] ? sb[j] + 16u : sb[j]);   // fetched it twice)
+            uintptr_t s1 = full[j] && sh[j] ? sb[j] + 16u : sb[j];   // lane L + 1's first (nontemporal
+            asm volatile("" : "+v"(s1));                // pairs fetched it twice); opaque: no
+            v0[j] = gload16(sb[j]);                     // "same address" copy of v0 (a copy
+            v1[j] = gload16(s1);                        // would wait for the load)
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {

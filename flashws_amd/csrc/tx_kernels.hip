@@ -165,15 +165,23 @@ __global__ __launch_bounds__(kBlock) void k_tx_encode(uint8_t *__restrict__ out,
                                                       const uint64_t *__restrict__ obase,
                                                       const uint32_t *__restrict__ unit_first, uint64_t unit_cap,
                                                       const uint64_t *__restrict__ total_ptr) {
-    const uint64_t total = *total_ptr;
-    uint64_t n_units = (total + kTxUnit - 1) / kTxUnit;
-    if (n_units > unit_cap) n_units = unit_cap;
     const int lane = threadIdx.x & 63;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t nw = (uint64_t)gridDim.x * (kBlock / 64);
-    for (uint64_t u = (uint64_t)blockIdx.x * (kBlock / 64) + wave; u < n_units; u += nw) {
-        const uint32_t flo = unit_first[u];
-        const uint32_t fhi = (u + 1 < n_units) ? unit_first[u + 1] : n - 1;
+    const uint64_t ufirst = (uint64_t)blockIdx.x * (kBlock / 64) + wave;
+    // one scalar round: the total and this wave's first unit map entries (clamped in bounds)
+    const uint64_t uc = ufirst + 1 < unit_cap ? ufirst : (unit_cap >= 2 ? unit_cap - 2 : 0);
+    uint32_t uf0 = unit_first[uc], uf1 = unit_first[uc + 1];
+    const uint64_t total = *total_ptr;
+    uint64_t n_units = (total + kTxUnit - 1) / kTxUnit;
+    if (n_units > unit_cap) n_units = unit_cap;
+    for (uint64_t u = ufirst; u < n_units; u += nw) {
+        if (u != ufirst) {
+            uf0 = unit_first[u];
+            uf1 = u + 1 < unit_cap ? unit_first[u + 1] : 0u;
+        }
+        const uint32_t flo = uf0;
+        const uint32_t fhi = (u + 1 < n_units) ? uf1 : n - 1;
         const uint64_t a0 = u * kTxUnit + (uint64_t)lane * 16u;
         if (fhi - flo >= 2u) {                         // small frames: bytewise with a search
             for (int j = 0; j < 4; ++j) {
@@ -230,13 +238,16 @@ __global__ __launch_bounds__(kBlock) void k_tx_encode(uint8_t *__restrict__ out,
             for (int j = 0; j < 4; ++j) {
                 // default-policy loads: the second block of lane L is the first of lane
                 // L + 1, so it must stay in cache (a nontemporal pair reads it twice)
-                v0[j] = gload16<false>(sb[j]);
-                v1[j] = gload16<false>(sh[j] && ((full >> j) & 1u) ? sb[j] + 16u : sb[j]);
+                uintptr_t s1 = sh[j] && ((full >> j) & 1u) ? sb[j] + 16u : sb[j];
+                asm volatile("" : "+v"(s1));            // opaque: no "same address as v0" copy
+                v0[j] = gload16<false>(sb[j]);          // (a copy would wait for the load)
+                v1[j] = gload16<false>(s1);
             }
             sa0 = gload16<false>(qa0);
             sa1 = gload16<false>(qa1);
             sb0 = gload16<false>(qb0);
             sb1 = gload16<false>(qb1);
+            __builtin_amdgcn_sched_barrier(0);          // keep every load ahead of the first use
         } else {
 #pragma unroll
             for (int j = 0; j < 4; ++j) v0[j] = v1[j] = u32x4{0u, 0u, 0u, 0u};

@@ -274,8 +274,7 @@ __global__ __launch_bounds__(kMThreads) void k_merge(MergeParams P) {
             nid[j] = i < n ? P.sid(t0 + tl, L.tsp[tl], i - L.tbase[tl]) : 0u;
         }
 #pragma unroll
-        for (uint32_t j = 0; j < kPer; ++j)
-            if (i0 + j < n) r[j] = *P.rec(nid[j]);
+        for (uint32_t j = 0; j < kPer; ++j) r[j] = *P.rec(nid[j]);   // unconditional: slot 0 past n
 #pragma unroll
         for (uint32_t j = 0; j < kPer; ++j) {
             const uint32_t i = i0 + j;
@@ -408,9 +407,9 @@ __device__ __forceinline__ void batched4(uint32_t n, Load load, Use use) {
     for (uint32_t base = threadIdx.x; base < n; base += 4u * kMThreads) {
         decltype(load(0u)) v[4];
 #pragma unroll
-        for (uint32_t j = 0; j < 4; ++j) {
-            const uint32_t c = base + j * kMThreads;
-            if (c < n) v[j] = load(c);
+        for (uint32_t j = 0; j < 4; ++j) {             // unconditional (index 0 past n: n > 0 here), so
+            const uint32_t c = base + j * kMThreads;   // no load waits for its data before the next issues
+            v[j] = load(c < n ? c : 0u);
         }
 #pragma unroll
         for (uint32_t j = 0; j < 4; ++j) {
@@ -545,15 +544,12 @@ __device__ void resolve_path(const MergeParams &P, PathLds &G) {
         for (uint32_t j = 0; j < 4; ++j) {
             const uint32_t c = base + j * kMThreads;
             kept[j] = c < mc && ((ka[c >> 5] >> (c & 31u)) & 1u);
-            if (kept[j]) {
-                const uint32_t x = P.comp[c];
-                tr[j] = P.tails[x];
-                tr[j].w = ld_acq(&P.tails[x].w);              // handed off in this launch
-            }
+            const uint32_t x = P.comp[kept[j] ? c : base];    // unconditional loads (base < mc)
+            tr[j] = P.tails[x];
+            tr[j].w = ld_acq(&P.tails[x].w);                  // handed off in this launch
         }
 #pragma unroll
-        for (uint32_t j = 0; j < 4; ++j)
-            if (kept[j] && tr[j].w != kTermDead) nr[j] = P.nres[tr[j].w];
+        for (uint32_t j = 0; j < 4; ++j) nr[j] = P.nres[kept[j] && tr[j].w != kTermDead ? tr[j].w : 0u];
 #pragma unroll
         for (uint32_t j = 0; j < 4; ++j) {
             if (!kept[j]) continue;
@@ -761,10 +757,9 @@ __global__ __launch_bounds__(kMThreads) void k_emit(MergeParams P) {
         fr[j] = i < n && L.mark[i] && ((nd[j] >> 48) & 1u);
         fl += fr[j];
     }
-    fws_frame_info rc[kPer];
-#pragma unroll
-    for (uint32_t j = 0; j < kPer; ++j)
-        if (fr[j]) rc[j] = *P.rec((uint32_t)nd[j]);
+    fws_frame_info rc[kPer];                         // unconditional (slot 0 for the unused ones):
+#pragma unroll                                        // conditional loads each waited for their data
+    for (uint32_t j = 0; j < kPer; ++j) rc[j] = *P.rec(fr[j] ? (uint32_t)nd[j] : 0u);
     uint32_t ftot;
     uint32_t f = fbase + block_excl<uint32_t>(fl, L.red32, &ftot);
 #pragma unroll

@@ -392,3 +392,38 @@ def test_gather_small_regions(ctx, cuda):
         exp[w:w + n] = seg
         w += n
     assert np.array_equal(dst[:total].cpu().numpy(), exp)
+
+
+@pytest.mark.parametrize("shape", ["many_mixed", "one_huge_among_small", "permuted_sources"])
+def test_gather_plan_shapes(ctx, cuda, shape):
+    """k_out_plan layouts: > 16 384 regions (256 per workgroup), a long run of
+    unit-map entries among short ones (64 per workgroup), sources in any order."""
+    rng = np.random.default_rng({"many_mixed": 21, "one_huge_among_small": 22, "permuted_sources": 23}[shape])
+    if shape == "many_mixed":
+        lens = [int(x) for x in rng.choice([0, 7, 100, 4096, 9000, 70000], 20000)]
+    elif shape == "one_huge_among_small":
+        lens = [int(x) for x in rng.integers(0, 3000, 500)]
+        lens[217] = 8 << 20
+    else:
+        lens = [int(x) for x in rng.integers(1, 20000, 3000)]
+    offs, pos = [], 3
+    for n in lens:
+        offs.append(pos)
+        pos += n + int(rng.integers(0, 9))
+    host = rng.integers(0, 256, pos + 64, dtype=np.uint8)
+    regions = [(o, n, int(rng.integers(0, 2**32)), int(rng.integers(0, 4))) for o, n in zip(offs, lens)]
+    if shape == "permuted_sources":
+        regions = [regions[i] for i in rng.permutation(len(regions))]
+    descs = np.array(regions, dtype=gpu.FRAME_DESC)
+    total = int(descs["payload_len"].sum())
+    dst = torch.zeros(total + 16, dtype=torch.uint8, device=cuda)
+    gpu.unmask_gather(ctx, dst, torch.from_numpy(host).to(cuda), gpu.descs_to_device(descs, cuda), len(descs))
+    exp, w = np.zeros(total, dtype=np.uint8), 0
+    for o, n, k, ph in regions:
+        seg = host[o:o + n].copy()
+        orc.orc_mask("ws_mask_fast", seg, orc.orc().orc_rotr32(k, 8 * ph))
+        exp[w:w + n] = seg
+        w += n
+    got = dst[:total].cpu().numpy()
+    assert np.array_equal(got, exp), int(np.flatnonzero(got != exp)[0])
+    assert int(dst[total:].sum()) == 0

@@ -23,6 +23,10 @@ def main():
     setv = L.fws_internal_set_unmask_variant
     setv.argtypes = [C.c_int]
     setv.restype = C.c_int
+    setg = L.fws_internal_set_grid_cap
+    setg.argtypes = [C.c_int]
+    setg.restype = C.c_int
+    caps = [int(c) for c in os.environ.get("FWS_GRID_CAPS", "16384").split(",")]
     res = {}
     for cfg in ("C2", "C3"):
         wire, descs, _ = gpu.config_c2() if cfg == "C2" else gpu.config_c3()
@@ -43,9 +47,10 @@ def main():
         times = {}
         steps = 40
         for rnd in range(6):
-            for v in VARIANTS:
+            for v, cap in [(v, c) for v in VARIANTS for c in caps]:
                 for mode in ("run", "step"):
                     setv(v)
+                    setg(cap)
                     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                     torch.cuda.synchronize()
                     e0.record()
@@ -56,7 +61,7 @@ def main():
                             gpu.unmask_batch(ctx, bufs[i % 4], dd, n)
                     e1.record()
                     torch.cuda.synchronize()
-                    times.setdefault(f"v{v}_{mode}", []).append(e0.elapsed_time(e1) / steps * 1e3)
+                    times.setdefault(f"v{v}_g{cap}_{mode}", []).append(e0.elapsed_time(e1) / steps * 1e3)
         out = {}
         for k, ts in times.items():
             us = float(np.median(ts))

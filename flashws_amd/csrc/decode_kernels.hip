@@ -538,13 +538,15 @@ extern "C" int fws_internal_scan_prof(unsigned long long *out, int reset) {
 }
 #endif
 
-// tuning / test hook: 0 = super-tile resolve with k_resolve fallback, 1 = k_resolve only
+// tuning / test hook: 0 = super-tile resolve with k_resolve fallback, 1 = k_resolve only,
+// 2 = the RX session's small-read kernel first (fws_gpu_decode_stream, tests only)
 static int g_resolve_mode = 0;
 extern "C" __attribute__((visibility("default"))) int fws_internal_set_resolve_mode(int m) {
     const int old = g_resolve_mode;
-    if (m == 0 || m == 1) g_resolve_mode = m;
+    if (m >= 0 && m <= 2) g_resolve_mode = m;
     return old;
 }
+int fws_resolve_mode() { return g_resolve_mode; }
 
 static uint32_t g_scan_blocks_per_cu = 0;   // tuning override (tools/), 0 = default
 extern "C" int fws_internal_set_scan_blocks_per_cu(int v) {
@@ -635,7 +637,7 @@ int fws_launch_decode(fws_gpu_ctx *ctx, uint8_t *wire, uint64_t N, fws_frame_inf
     }
     // super-tile resolve (common case); k_resolve runs only if it set kCntFallback.
     // Slot ids are 32-bit (8 per tile): streams of 2^39 B and more take k_resolve.
-    const bool fast = N < (1ull << 39) && g_resolve_mode != 1;
+    const bool fast = N < (1ull << 39) && g_resolve_mode != 1;   // mode 2 decodes as mode 0 here
     if (fast) {
         int r = fws_launch_merge(ctx, wire, N, n_tiles, frames, cap, res, utf8_ok, s);
         if (r) return r;

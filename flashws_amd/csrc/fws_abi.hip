@@ -201,6 +201,15 @@ int fws_gpu_decode_stream(fws_gpu_ctx *ctx, void *dev_wire, uint64_t len, fws_fr
     hipStream_t s = (hipStream_t)stream;
     int r;
     if ((r = fws_hip_status(hipSetDevice(ctx->device)))) return r;
+    if (fws_resolve_mode() == 2 && len <= kSmallMax && !dev_utf8_ok) {
+        // test hook: the RX session's one-launch small-read decode, with its
+        // fallback taken synchronously as rx_session.cpp does
+        if ((r = fws_launch_decode_small((uint8_t *)dev_wire, len, dev_frames, cap, dev_result, s))) return r;
+        int32_t st = 0;
+        if ((r = fws_hip_status(hipMemcpyAsync(&st, dev_result, 4, hipMemcpyDeviceToHost, s)))) return r;
+        if ((r = fws_hip_status(hipStreamSynchronize(s)))) return r;
+        if (st != FWS_SMALL_DECLINED) return 0;
+    }
     if ((r = fws_decode_ensure(ctx, len, cap))) return r;
     const uint64_t units = (len / 16 + 2ull * cap) / 256 + 2;
     if ((r = fws_ctx_ensure_plan(ctx, cap, units))) return r;

@@ -11,6 +11,16 @@ static inline int fws_hip_status(hipError_t e) {
     return e == hipSuccess ? 0 : (FWS_ERR_HIP_BASE - (int)e);
 }
 
+// One-launch decode of a small read (small_kernels.hip): streams of at most
+// kSmallMax bytes (16-B aligned base) with at most kSmallFrames headers;
+// more headers -> res->status = FWS_SMALL_DECLINED, nothing else written.
+constexpr uint64_t kSmallMax = 64u << 10;
+constexpr uint32_t kSmallFrames = 256;
+constexpr int FWS_SMALL_DECLINED = -30;
+int fws_resolve_mode();   // decode_kernels.hip test hook (fws_internal_set_resolve_mode)
+int fws_launch_decode_small(uint8_t *wire, uint64_t N, fws_frame_info *frames, uint32_t cap,
+                            fws_decode_result *res, hipStream_t s);
+
 // Device workspace for the chunk plan of one descriptor batch.
 // Descriptor batches are planned two ways in one launch (k_plan): chunk space
 // (cbase / unit_first: any descriptor order) and byte space (unit_first_s:

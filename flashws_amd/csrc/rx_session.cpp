@@ -48,7 +48,19 @@ struct fws_rx_session {
     fws_frame_info *dframes = nullptr;
     uint32_t fcap = 0;
     fws_decode_result *dres = nullptr;
-    std::vector<fws_frame_info> frames;
+    // pinned landing area: the decode result and the first kSpec frames come
+    // back with the bytes, before the one synchronize; larger reads copy the
+    // rest after it
+    static constexpr uint32_t kSpec = 1024;
+    static constexpr uint64_t kResPad = 64;
+    // reads up to kZcMax bytes are staged by the host into pinned memory the
+    // kernels work on directly (no copy-engine transfers; one copy of the
+    // result block back)
+    static constexpr uint64_t kZcMax = kSmallMax;
+    uint8_t *hstage = nullptr;
+    fws_decode_result *hres = nullptr;
+    fws_frame_info *hframes = nullptr;
+    uint32_t hfcap = 0;
     std::vector<uint8_t> stream_host;
     // event sinks of the current feed
     fws_rx_event *ev = nullptr;
@@ -160,14 +172,31 @@ struct fws_rx_session {
             if ((e = hipMalloc((void **)&dA, capA)) != hipSuccess) return fws_hip_status(e);
             if ((e = hipMalloc((void **)&dB, capB)) != hipSuccess) return fws_hip_status(e);
         }
-        if (nframes > fcap) {
-            if (dframes) (void)hipFree(dframes);
-            fcap = nframes;
-            if ((e = hipMalloc((void **)&dframes, (uint64_t)fcap * sizeof(fws_frame_info))) != hipSuccess)
+        if (nframes > fcap || !dres) {
+            // one device block [result | frames], so a single copy brings back
+            // the result and the first frames
+            if (dres) (void)hipFree(dres);
+            fcap = nframes > fcap ? nframes : fcap;
+            if ((e = hipMalloc((void **)&dres, kResPad + (uint64_t)fcap * sizeof(fws_frame_info))) != hipSuccess)
                 return fws_hip_status(e);
+            dframes = (fws_frame_info *)((uint8_t *)dres + kResPad);
         }
-        if (!dres && (e = hipMalloc((void **)&dres, sizeof(fws_decode_result))) != hipSuccess)
+        if (bytes <= kZcMax && !hstage && (e = hipHostMalloc((void **)&hstage, 2 * kZcMax + 64)) != hipSuccess)
             return fws_hip_status(e);
+        return host_room(kSpec);
+    }
+
+    // pinned [result | frames] landing block for n frames
+    int host_room(uint32_t n) {
+        if (n <= hfcap) return 0;
+        if (hres) (void)hipHostFree(hres);
+        hres = nullptr;
+        hframes = nullptr;
+        hfcap = 0;
+        hipError_t e = hipHostMalloc((void **)&hres, kResPad + (uint64_t)n * sizeof(fws_frame_info));
+        if (e != hipSuccess) return fws_hip_status(e);
+        hframes = (fws_frame_info *)((uint8_t *)hres + kResPad);
+        hfcap = n;
         return 0;
     }
 };
@@ -195,8 +224,9 @@ void fws_rx_session_destroy(fws_rx_session *s) {
     if (s->stream) (void)hipStreamSynchronize(s->stream);
     if (s->dA) (void)hipFree(s->dA);
     if (s->dB) (void)hipFree(s->dB);
-    if (s->dframes) (void)hipFree(s->dframes);
     if (s->dres) (void)hipFree(s->dres);
+    if (s->hres) (void)hipHostFree(s->hres);
+    if (s->hstage) (void)hipHostFree(s->hstage);
     if (s->stream) (void)hipStreamDestroy(s->stream);
     delete s;
 }
@@ -239,6 +269,45 @@ static int feed_impl(fws_rx_session *s, uint8_t *buf, uint64_t size, uint64_t bu
 
     // 1. continuation of the frame in progress (WAIT_FRAME_PAYLOAD, w_socket.h:607-617)
     uint64_t u = 0;
+    fws_decode_result res{};
+    const uint32_t spec = fcap < fws_rx_session::kSpec ? fcap : fws_rx_session::kSpec;
+    if (s->recv_status == kWaitPayload) u = size < s->unread ? size : s->unread;
+    const uint32_t part0 = s->part_len;
+    const uint64_t rest = size - u;
+    const uint64_t L = part0 + rest;
+    const bool zc = size <= fws_rx_session::kZcMax;
+    if (zc) {
+        // small read: stage [continuation | 16-B pad | header stream] in pinned
+        // memory, run the kernels on it, copy the result block back
+        uint8_t *cont = s->hstage;
+        const uint64_t soff = (u + 15) & ~15ull;
+        uint8_t *hs = s->hstage + soff;
+        if (u) {
+            memcpy(cont, buf, u);
+            if ((r = fws_gpu_mask(cont, u, s->key, st))) return r;
+        }
+        if (rest) {
+            if (part0) memcpy(hs, s->hdr, part0);
+            memcpy(hs + part0, buf + u, rest);
+            r = L <= kSmallMax ? fws_launch_decode_small(hs, L, s->dframes, fcap, s->dres, st)
+                               : fws_gpu_decode_stream(s->ctx, hs, L, s->dframes, fcap, s->dres, nullptr, st);
+            if (r) return r;
+            if ((e = hipMemcpyAsync(s->hres, s->dres, fws_rx_session::kResPad + (uint64_t)spec * sizeof(fws_frame_info),
+                                    hipMemcpyDeviceToHost, st)) != hipSuccess)
+                return fws_hip_status(e);
+        }
+        if ((e = hipStreamSynchronize(st)) != hipSuccess) return fws_hip_status(e);
+        if (rest && s->hres->status == FWS_SMALL_DECLINED) {
+            // more headers than the one-launch walk takes: the parallel decode
+            if ((r = fws_gpu_decode_stream(s->ctx, hs, L, s->dframes, fcap, s->dres, nullptr, st))) return r;
+            if ((e = hipMemcpyAsync(s->hres, s->dres, fws_rx_session::kResPad + (uint64_t)spec * sizeof(fws_frame_info),
+                                    hipMemcpyDeviceToHost, st)) != hipSuccess)
+                return fws_hip_status(e);
+            if ((e = hipStreamSynchronize(st)) != hipSuccess) return fws_hip_status(e);
+        }
+        if (u) memcpy(buf, cont, u);
+        if (rest) memcpy(buf + u, hs + part0, rest);
+    } else {
     if (s->recv_status == kWaitPayload) {
         u = size < s->unread ? size : s->unread;
         if (u) {
@@ -248,26 +317,25 @@ static int feed_impl(fws_rx_session *s, uint8_t *buf, uint64_t size, uint64_t bu
         }
     }
     // 2. header stream: staged header bytes + the rest of the read
-    const uint32_t part0 = s->part_len;
-    const uint64_t rest = size - u;
-    const uint64_t L = part0 + rest;
-    fws_decode_result res{};
     if (rest) {
         if (part0 && (e = hipMemcpyAsync(s->dB, s->hdr, part0, hipMemcpyHostToDevice, st)) != hipSuccess)
             return fws_hip_status(e);
         if ((e = hipMemcpyAsync(s->dB + part0, buf + u, rest, hipMemcpyHostToDevice, st)) != hipSuccess)
             return fws_hip_status(e);
         if ((r = fws_gpu_decode_stream(s->ctx, s->dB, L, s->dframes, fcap, s->dres, nullptr, st))) return r;
-        if ((e = hipMemcpyAsync(&res, s->dres, sizeof(res), hipMemcpyDeviceToHost, st)) != hipSuccess)
+        if ((e = hipMemcpyAsync(s->hres, s->dres, fws_rx_session::kResPad + (uint64_t)spec * sizeof(fws_frame_info),
+                                hipMemcpyDeviceToHost, st)) != hipSuccess)
             return fws_hip_status(e);
         if ((e = hipMemcpyAsync(buf + u, s->dB + part0, rest, hipMemcpyDeviceToHost, st)) != hipSuccess)
             return fws_hip_status(e);
     }
     if ((e = hipStreamSynchronize(st)) != hipSuccess) return fws_hip_status(e);
+    }
+    if (rest) res = *s->hres;
     if (res.status == FWS_ERR_CAPACITY) return FWS_ERR_CAPACITY;
-    s->frames.resize(res.n_frames);
-    if (res.n_frames) {
-        if ((e = hipMemcpy(s->frames.data(), s->dframes, (uint64_t)res.n_frames * sizeof(fws_frame_info),
+    if (res.n_frames > spec) {
+        if ((r = s->host_room((uint32_t)res.n_frames))) return r;
+        if ((e = hipMemcpy(s->hframes, s->dframes, (uint64_t)res.n_frames * sizeof(fws_frame_info),
                            hipMemcpyDeviceToHost)) != hipSuccess)
             return fws_hip_status(e);
     }
@@ -279,7 +347,7 @@ static int feed_impl(fws_rx_session *s, uint8_t *buf, uint64_t size, uint64_t bu
     if (!rest) return 0;   // the whole read was payload of the frame in progress
     // header stream coordinate x <-> read coordinate x - part0 + u
     for (uint32_t i = 0; i < res.n_frames; ++i) {
-        const fws_frame_info &fi = s->frames[i];
+        const fws_frame_info &fi = s->hframes[i];
         const uint32_t op = fi.opcode;
         if (op >> 3) { s->is_ctl = true; s->last_ctl_op = (uint8_t)op; }      // :455-464
         else if (op != 0u) s->last_op = (uint8_t)op;

@@ -1,0 +1,159 @@
+// small_kernels.hip -- one-launch decode of a small read (the RX session's
+// per-read path, rx_session.cpp): header parse + unmask of a stream of at
+// most kSmallMax bytes by one workgroup.
+//
+// The multi-launch stream decode (k_scan -> k_merge -> k_link -> k_emit ->
+// k_resolve -> k_unmask_stream, decode_kernels.hip / merge_kernels.hip) is
+// built for HBM-sized streams; on a 4 KiB read its six launches cost ~40 us of
+// dependent latency, more than the read's PCIe copies. Here the stream is
+// staged in LDS with one round of 16-B loads, the header chain is walked from
+// offset 0 by one lane with ParseFrameHdr's exact semantics (w_socket.h:435-524,
+// loop w_socket.h:543-769; the same walk the super-tile resolve finishes its
+// terminal with), and every 16-B chunk holding payload bytes is unmasked from
+// LDS by the whole workgroup and stored once.
+//
+// A read with more than kSmallFrames headers (tiny frames) is declined:
+// res->status = FWS_SMALL_DECLINED and nothing is written but the result; the
+// caller then runs fws_gpu_decode_stream. Results are those of
+// fws_gpu_decode_stream (fws_decode_result, fws_frame_info, bytes).
+#include "decode_common.h"
+#include "fws_device.h"
+#include "fws_internal.h"
+
+namespace fwsk {
+
+constexpr uint32_t kSThreads = 1024;
+constexpr uint32_t kSChunks = kSmallMax / 16;
+
+__global__ __launch_bounds__(kSThreads) void k_decode_small(uint8_t *__restrict__ wire, uint32_t N,
+                                                            fws_frame_info *__restrict__ frames, uint32_t cap,
+                                                            fws_decode_result *__restrict__ res) {
+    __shared__ u32x4 s_buf[kSChunks + 1];
+    __shared__ uint32_t s_po[kSmallFrames + 1];     // payload start of path frame f
+    __shared__ uint32_t s_pe[kSmallFrames + 1];     // payload end, clipped to N
+    __shared__ uint32_t s_key[kSmallFrames + 1];
+    __shared__ uint32_t s_nf;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t nch = (N + 15u) >> 4;
+    const uintptr_t base = (uintptr_t)wire;
+
+    // 1. stage: all loads of a thread in flight together (the base is 16-B
+    //    aligned, so the last chunk's block never crosses a page)
+    {
+        u32x4 v[kSChunks / kSThreads];
+#pragma unroll
+        for (uint32_t k = 0; k < kSChunks / kSThreads; ++k) {
+            const uint32_t c = tid + k * kSThreads;
+            if (c < nch) v[k] = gload16(base + 16u * c);
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < kSChunks / kSThreads; ++k) {
+            const uint32_t c = tid + k * kSThreads;
+            if (c < nch) s_buf[c] = v[k];
+        }
+        if (tid == 0) s_buf[nch] = u32x4{0u, 0u, 0u, 0u};
+    }
+    __syncthreads();
+    const uint8_t *sb = (const uint8_t *)s_buf;
+
+    // 2. the header chain from offset 0 (one lane; the terminal walk of
+    //    merge_kernels.hip resolve_path, from the stream start)
+    if (tid == 0) {
+        fws_decode_result r{};
+        r.status = FWS_OK;
+        uint64_t pos = 0;
+        uint32_t nf = 0;
+        bool declined = false;
+        while (pos < N) {
+            Hdr h;
+            const uint32_t q = (uint32_t)pos;
+            const int rc = parse_hdr([&](int i) -> uint32_t { return sb[q + (uint32_t)i]; }, N - q, true, h);
+            if (rc < 0) { r.status = rc; r.err_off = q; break; }
+            if (rc == 0) break;                               // incomplete trailing header
+            if (nf == kSmallFrames) { declined = true; break; }
+            const uint64_t po = q + (uint32_t)rc;
+            const uint64_t pe = po + h.plen;
+            s_po[nf] = (uint32_t)po;
+            s_pe[nf] = (uint32_t)(pe < N ? pe : N);
+            s_key[nf] = h.key;
+            if (nf < cap) {
+                fws_frame_info fi;
+                fi.hdr_off = q; fi.payload_len = h.plen; fi.key = h.key; fi.opcode = (uint8_t)h.opcode;
+                fi.fin = (uint8_t)h.fin; fi.hdr_len = (uint8_t)rc;
+                fi.flags = pe > N ? (uint8_t)FWS_FRAME_TRUNCATED : (uint8_t)0;
+                frames[nf] = fi;
+            }
+            ++nf;
+            pos = pe;
+        }
+        if (declined) {
+            r = fws_decode_result{};
+            r.status = FWS_SMALL_DECLINED;
+            nf = 0;
+        } else {
+            if (r.status == FWS_OK) {
+                if (pos > N) { r.carry_unread = pos - N; r.consumed = N; }
+                else if (pos < N) { r.carry_hdr_len = (uint32_t)(N - pos); r.consumed = pos; }
+                else r.consumed = N;
+            } else {
+                r.consumed = r.err_off;
+            }
+            if (nf > cap && r.status == FWS_OK) r.status = FWS_ERR_CAPACITY;
+            r.n_frames = nf;
+            r.n_survivors = nf;
+        }
+        s_nf = nf < cap ? nf : cap;                          // the frames listed are the ones unmasked
+        *res = r;
+    }
+    __syncthreads();
+
+    // 3. unmask: every chunk holding payload bytes, from LDS, one store each
+    const uint32_t nf = s_nf;
+    if (nf == 0) return;
+    for (uint32_t c = tid; c < nch; c += kSThreads) {
+        const uint32_t lo = 16u * c, hi = lo + 16u;
+        // last frame whose payload starts at or before lo (or frame 0)
+        uint32_t a = 0, b = nf - 1u;
+        while (a < b) {
+            const uint32_t m = (a + b + 1u) >> 1;
+            if (s_po[m] <= lo) a = m; else b = m - 1u;
+        }
+        u32x4 v = s_buf[c];
+        bool touched = false;
+        for (uint32_t f = a; f < nf && s_po[f] < hi; ++f) {
+            const uint32_t po = s_po[f], pe = s_pe[f];
+            if (pe <= lo) continue;
+            touched = true;
+            const uint32_t key = s_key[f];
+#pragma unroll
+            for (uint32_t w = 0; w < 4u; ++w) {
+                const uint32_t x = lo + 4u * w;               // dword of bytes [x, x + 4)
+                uint32_t m = 0;
+#pragma unroll
+                for (uint32_t j = 0; j < 4u; ++j) {
+                    const uint32_t y = x + j;
+                    if (y >= po && y < pe) m |= ((key >> (8u * ((y - po) & 3u))) & 0xFFu) << (8u * j);
+                }
+                v[w] ^= m;
+            }
+        }
+        if (!touched) continue;
+        if (hi <= N) {
+            gstore16(base + lo, v);
+        } else {
+            const uint8_t *vb = (const uint8_t *)&v;
+            for (uint32_t j = 0; lo + j < N; ++j) wire[lo + j] = vb[j];
+        }
+    }
+}
+
+}  // namespace fwsk
+
+int fws_launch_decode_small(uint8_t *wire, uint64_t N, fws_frame_info *frames, uint32_t cap,
+                            fws_decode_result *res, hipStream_t s) {
+    if (N > kSmallMax || ((uintptr_t)wire & 15u) || (N && !wire) || !res || (cap && !frames))
+        return FWS_ERR_INVALID;
+    hipLaunchKernelGGL(fwsk::k_decode_small, dim3(1), dim3(fwsk::kSThreads), 0, s, wire, (uint32_t)N, frames, cap,
+                       res);
+    return fws_hip_status(hipGetLastError());
+}

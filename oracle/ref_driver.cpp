@@ -76,6 +76,8 @@ struct Session {
     size_t read_start = 0;     // IOBuffer::start_pos of the current read
     uint64_t bytes_seen = 0;   // used by the timing loop
     bool timing = false;       // timing mode: count bytes only, no recording
+    bool echo = false;         // echo harness: record parts, no socketpair drain per part
+    fws::IOBuffer *rbuf = nullptr;   // echo harness: the session's pool read buffer
 };
 
 // Parse server TX frames written to the socketpair (server frames are unmasked;
@@ -135,7 +137,7 @@ void *ref_session_new(void) {
     s->sock.SetOnRead([s](Probe::Base &, uint32_t opcode, fws::IOBuffer &&buf, bool frame_end,
                           bool msg_end, bool is_ctl, void *) {
         if (s->timing) { s->bytes_seen += (uint64_t)buf.size; return; }
-        DrainPeer(*s);                       // replies written before this delivery
+        if (!s->echo) DrainPeer(*s);         // replies written before this delivery
         RefEvent e{};
         e.kind = 0; e.opcode = opcode; e.is_ctl = is_ctl;
         e.frame_end = frame_end; e.msg_end = msg_end;
@@ -243,6 +245,32 @@ double ref_time_onrecv(const uint8_t *stream, size_t n, size_t read_size, int it
     *payload_bytes = s->bytes_seen;
     ref_session_free(s);
     return std::chrono::duration<double>(t1 - t0).count();
+}
+
+// Echo harness (tools/ws_echo.cpp, run by bench.py's CPU-baseline leg): the
+// session's own pool read buffer, RequestBuf(pad + cap) with reads landing at
+// start_pos 32 as the transport puts them (floop.h:664-665), and OnRecvData on
+// a view of it without a copy. Events as ref_session_feed's; control replies
+// stay unread on the socketpair (the echo sends no control frames).
+uint8_t *ref_session_read_buf(void *h, size_t cap) {
+    auto *s = static_cast<Session *>(h);
+    const size_t pad = fws::constants::DEFAULT_READ_BUF_PRE_PADDING_SIZE;
+    if (!s->rbuf) s->rbuf = new fws::IOBuffer(fws::RequestBuf(pad + cap + 64));
+    s->echo = true;
+    return s->rbuf->data + pad;
+}
+
+int ref_session_feed_inplace(void *h, size_t n, void *events, size_t ev_cap, size_t *n_ev) {
+    auto *s = static_cast<Session *>(h);
+    const size_t pad = fws::constants::DEFAULT_READ_BUF_PRE_PADDING_SIZE;
+    s->events.clear();
+    s->ctl.clear();
+    s->read_start = pad;
+    fws::IOBuffer view(s->rbuf->data, (ssize_t)n, pad, pad + n);
+    int ret = s->sock.OnRecvData(view);
+    *n_ev = s->events.size();
+    std::memcpy(events, s->events.data(), sizeof(RefEvent) * std::min(ev_cap, s->events.size()));
+    return ret;
 }
 
 // WSMaskBytesFast alone over a list of (offset, len, key) parts of `buf`.

@@ -16,7 +16,7 @@ from wsframes import frame
 
 pytestmark = pytest.mark.gpu
 
-RESOLVE_MODES = {"super_tile": 0, "k_resolve": 1}
+RESOLVE_MODES = {"super_tile": 0, "k_resolve": 1, "small_read": 2}
 CNT_FALLBACK = 9            # decode_common.h Counter::kCntFallback
 
 
@@ -24,7 +24,10 @@ CNT_FALLBACK = 9            # decode_common.h Counter::kCntFallback
 def resolve_mode(request):
     """Every decode test runs on both resolve paths: the super-tile resolve
     (merge_kernels.hip, the common path) and the cooperative k_resolve it
-    falls back to (resolve_kernels.hip), forced."""
+    falls back to (resolve_kernels.hip), forced; and through the RX session's
+    one-launch small-read kernel (small_kernels.hip; streams <= 64 KiB with
+    <= 256 headers, the rest fall back to the super-tile path as the session
+    does)."""
     from flashws_amd import _lib
     L = _lib.lib()
     old = L.fws_internal_set_resolve_mode(RESOLVE_MODES[request.param])
@@ -427,3 +430,57 @@ def test_gather_plan_shapes(ctx, cuda, shape):
     got = dst[:total].cpu().numpy()
     assert np.array_equal(got, exp), int(np.flatnonzero(got != exp)[0])
     assert int(dst[total:].sum()) == 0
+
+
+@pytest.mark.parametrize("nfr", [1, 2, 255, 256, 257, 400])
+@pytest.mark.parametrize("tail", ["none", "truncated", "partial_header"])
+def test_small_read_frame_counts(ctx, cuda, nfr, tail):
+    """Header counts around the small-read kernel's walk limit (256: more are
+    declined and decoded by the parallel path), with the read ending at a
+    frame end, inside a payload or inside a header."""
+    rng = np.random.default_rng(nfr * 7 + len(tail))
+    parts = [frame(int(rng.choice([1, 2, 0])), rng.integers(0, 256, int(rng.integers(0, 200)), dtype=np.uint8).tobytes(),
+                   fin=int(rng.random() < 0.8), key=int(rng.integers(0, 2**32))) for _ in range(nfr)]
+    wire = b"".join(parts)
+    if tail == "truncated":
+        wire += frame(2, b"z" * 3000)[:-1234]
+    elif tail == "partial_header":
+        wire += frame(2, b"z" * 300)[:5]
+    check(ctx, cuda, wire)
+
+
+@pytest.mark.parametrize("size", [65536 - 7, 65536, 65537, 70000])
+def test_small_read_size_limit(ctx, cuda, size):
+    """Streams either side of the small-read kernel's 64 KiB limit."""
+    rng = np.random.default_rng(size)
+    parts, n = [], 0
+    while n < size:
+        p = int(min(rng.integers(100, 9000), max(size - n - 8, 0)))
+        f = frame(2, rng.integers(0, 256, p, dtype=np.uint8).tobytes(), key=int(rng.integers(0, 2**32)))
+        parts.append(f)
+        n += len(f)
+    wire = b"".join(parts)[:size]
+    check(ctx, cuda, wire)
+
+
+def test_small_read_capacity(ctx, cuda, resolve_mode):
+    """cap below the header count: the first cap frames listed and unmasked,
+    FWS_ERR_CAPACITY, n_frames = all headers; identical on every path."""
+    if resolve_mode == "k_resolve":
+        pytest.skip("compared against the super-tile path below")
+    rng = np.random.default_rng(5)
+    wire = np.frombuffer(b"".join(frame(2, rng.integers(0, 256, int(rng.integers(0, 400)), dtype=np.uint8).tobytes(),
+                                       key=int(rng.integers(0, 2**32))) for _ in range(60)), dtype=np.uint8)
+    got, gframes, r = decode(ctx, wire, cuda, cap=23)
+    from flashws_amd import _lib
+    L = _lib.lib()
+    old = L.fws_internal_set_resolve_mode(0)
+    try:
+        ref, rframes, rr = decode(ctx, wire, cuda, cap=23)
+    finally:
+        L.fws_internal_set_resolve_mode(old)
+    assert int(r["status"]) == int(rr["status"]) == -20
+    assert int(r["n_frames"]) == int(rr["n_frames"]) == 60
+    for k in ("hdr_off", "payload_len", "key", "opcode", "fin", "hdr_len"):
+        assert np.array_equal(gframes[k], rframes[k]), k
+    assert np.array_equal(got, ref)

@@ -14,7 +14,7 @@ static inline int fws_hip_status(hipError_t e) {
 // One-launch decode of a small read (small_kernels.hip): streams of at most
 // kSmallMax bytes (16-B aligned base) with at most kSmallFrames headers;
 // more headers -> res->status = FWS_SMALL_DECLINED, nothing else written.
-constexpr uint64_t kSmallMax = 64u << 10;
+constexpr uint64_t kSmallMax = 128u << 10;
 constexpr uint32_t kSmallFrames = 256;
 constexpr int FWS_SMALL_DECLINED = -30;
 int fws_resolve_mode();   // decode_kernels.hip test hook (fws_internal_set_resolve_mode)

@@ -52,11 +52,12 @@ struct fws_rx_session {
     // back with the bytes, before the one synchronize; larger reads copy the
     // rest after it
     static constexpr uint32_t kSpec = 1024;
+    static_assert(kSpec > kSmallFrames, "small-read frames land in the pinned block");
     static constexpr uint64_t kResPad = 64;
     // reads up to kZcMax bytes are staged by the host into pinned memory the
     // kernels work on directly (no copy-engine transfers; one copy of the
     // result block back)
-    static constexpr uint64_t kZcMax = kSmallMax;
+    static constexpr uint64_t kZcMax = 16u << 10;
     uint8_t *hstage = nullptr;
     fws_decode_result *hres = nullptr;
     fws_frame_info *hframes = nullptr;
@@ -275,13 +276,26 @@ static int feed_impl(fws_rx_session *s, uint8_t *buf, uint64_t size, uint64_t bu
     const uint32_t part0 = s->part_len;
     const uint64_t rest = size - u;
     const uint64_t L = part0 + rest;
-    const bool zc = size <= fws_rx_session::kZcMax;
-    if (zc) {
-        // small read: stage [continuation | 16-B pad | header stream] in pinned
-        // memory, run the kernels on it, copy the result block back
+    // The header stream [staged header bytes | rest of the read] is decoded on
+    // `hs`: streams of <= kSmallMax bytes by the one-launch small-read kernel
+    // (declined for > kSmallFrames headers, then by the parallel decode),
+    // longer ones by fws_gpu_decode_stream. The result block (result + the
+    // first `spec` frames) comes back with one copy.
+    auto launch = [&](uint8_t *hs, bool small) -> int {
+        int rr = small ? fws_launch_decode_small(hs, L, s->dframes, fcap, s->dres, st)
+                       : fws_gpu_decode_stream(s->ctx, hs, L, s->dframes, fcap, s->dres, nullptr, st);
+        if (rr) return rr;
+        return fws_hip_status(hipMemcpyAsync(s->hres, s->dres,
+                                             fws_rx_session::kResPad + (uint64_t)spec * sizeof(fws_frame_info),
+                                             hipMemcpyDeviceToHost, st));
+    };
+    const bool small = L <= kSmallMax;
+    if (size <= fws_rx_session::kZcMax) {
+        // tiny read: the host stages [continuation | 16-B pad | header stream]
+        // in pinned memory and the kernels work on it there (no copy-engine
+        // transfers of the bytes)
         uint8_t *cont = s->hstage;
-        const uint64_t soff = (u + 15) & ~15ull;
-        uint8_t *hs = s->hstage + soff;
+        uint8_t *hs = s->hstage + ((u + 15) & ~15ull);
         if (u) {
             memcpy(cont, buf, u);
             if ((r = fws_gpu_mask(cont, u, s->key, st))) return r;
@@ -289,47 +303,38 @@ static int feed_impl(fws_rx_session *s, uint8_t *buf, uint64_t size, uint64_t bu
         if (rest) {
             if (part0) memcpy(hs, s->hdr, part0);
             memcpy(hs + part0, buf + u, rest);
-            r = L <= kSmallMax ? fws_launch_decode_small(hs, L, s->dframes, fcap, s->dres, st)
-                               : fws_gpu_decode_stream(s->ctx, hs, L, s->dframes, fcap, s->dres, nullptr, st);
-            if (r) return r;
-            if ((e = hipMemcpyAsync(s->hres, s->dres, fws_rx_session::kResPad + (uint64_t)spec * sizeof(fws_frame_info),
-                                    hipMemcpyDeviceToHost, st)) != hipSuccess)
-                return fws_hip_status(e);
+            if ((r = launch(hs, small))) return r;
         }
         if ((e = hipStreamSynchronize(st)) != hipSuccess) return fws_hip_status(e);
         if (rest && s->hres->status == FWS_SMALL_DECLINED) {
-            // more headers than the one-launch walk takes: the parallel decode
-            if ((r = fws_gpu_decode_stream(s->ctx, hs, L, s->dframes, fcap, s->dres, nullptr, st))) return r;
-            if ((e = hipMemcpyAsync(s->hres, s->dres, fws_rx_session::kResPad + (uint64_t)spec * sizeof(fws_frame_info),
-                                    hipMemcpyDeviceToHost, st)) != hipSuccess)
-                return fws_hip_status(e);
+            if ((r = launch(hs, false))) return r;
             if ((e = hipStreamSynchronize(st)) != hipSuccess) return fws_hip_status(e);
         }
         if (u) memcpy(buf, cont, u);
         if (rest) memcpy(buf + u, hs + part0, rest);
     } else {
-    if (s->recv_status == kWaitPayload) {
-        u = size < s->unread ? size : s->unread;
         if (u) {
             if ((e = hipMemcpyAsync(s->dA, buf, u, hipMemcpyHostToDevice, st)) != hipSuccess) return fws_hip_status(e);
             if ((r = fws_gpu_mask(s->dA, u, s->key, st))) return r;
             if ((e = hipMemcpyAsync(buf, s->dA, u, hipMemcpyDeviceToHost, st)) != hipSuccess) return fws_hip_status(e);
         }
-    }
-    // 2. header stream: staged header bytes + the rest of the read
-    if (rest) {
-        if (part0 && (e = hipMemcpyAsync(s->dB, s->hdr, part0, hipMemcpyHostToDevice, st)) != hipSuccess)
-            return fws_hip_status(e);
-        if ((e = hipMemcpyAsync(s->dB + part0, buf + u, rest, hipMemcpyHostToDevice, st)) != hipSuccess)
-            return fws_hip_status(e);
-        if ((r = fws_gpu_decode_stream(s->ctx, s->dB, L, s->dframes, fcap, s->dres, nullptr, st))) return r;
-        if ((e = hipMemcpyAsync(s->hres, s->dres, fws_rx_session::kResPad + (uint64_t)spec * sizeof(fws_frame_info),
-                                hipMemcpyDeviceToHost, st)) != hipSuccess)
-            return fws_hip_status(e);
-        if ((e = hipMemcpyAsync(buf + u, s->dB + part0, rest, hipMemcpyDeviceToHost, st)) != hipSuccess)
-            return fws_hip_status(e);
-    }
-    if ((e = hipStreamSynchronize(st)) != hipSuccess) return fws_hip_status(e);
+        if (rest) {
+            if (part0 && (e = hipMemcpyAsync(s->dB, s->hdr, part0, hipMemcpyHostToDevice, st)) != hipSuccess)
+                return fws_hip_status(e);
+            if ((e = hipMemcpyAsync(s->dB + part0, buf + u, rest, hipMemcpyHostToDevice, st)) != hipSuccess)
+                return fws_hip_status(e);
+            if ((r = launch(s->dB, small))) return r;
+            if ((e = hipMemcpyAsync(buf + u, s->dB + part0, rest, hipMemcpyDeviceToHost, st)) != hipSuccess)
+                return fws_hip_status(e);
+        }
+        if ((e = hipStreamSynchronize(st)) != hipSuccess) return fws_hip_status(e);
+        if (rest && small && s->hres->status == FWS_SMALL_DECLINED) {
+            // declined (nothing written): the parallel decode, and the bytes again
+            if ((r = launch(s->dB, false))) return r;
+            if ((e = hipMemcpyAsync(buf + u, s->dB + part0, rest, hipMemcpyDeviceToHost, st)) != hipSuccess)
+                return fws_hip_status(e);
+            if ((e = hipStreamSynchronize(st)) != hipSuccess) return fws_hip_status(e);
+        }
     }
     if (rest) res = *s->hres;
     if (res.status == FWS_ERR_CAPACITY) return FWS_ERR_CAPACITY;

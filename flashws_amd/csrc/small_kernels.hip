@@ -39,20 +39,21 @@ __global__ __launch_bounds__(kSThreads) void k_decode_small(uint8_t *__restrict_
 
     // 1. stage: all loads of a thread in flight together (the base is 16-B
     //    aligned, so the last chunk's block never crosses a page)
-    {
-        u32x4 v[kSChunks / kSThreads];
+    // (two rounds of four loads per thread in flight)
 #pragma unroll
-        for (uint32_t k = 0; k < kSChunks / kSThreads; ++k) {
-            const uint32_t c = tid + k * kSThreads;
-            if (c < nch) v[k] = gload16(base + 16u * c);
-        }
-#pragma unroll
-        for (uint32_t k = 0; k < kSChunks / kSThreads; ++k) {
-            const uint32_t c = tid + k * kSThreads;
-            if (c < nch) s_buf[c] = v[k];
-        }
-        if (tid == 0) s_buf[nch] = u32x4{0u, 0u, 0u, 0u};
+    for (uint32_t k0 = 0; k0 < kSChunks / kSThreads; k0 += 4u) {
+        u32x4 v0, v1, v2, v3;
+        const uint32_t c = tid + k0 * kSThreads;
+        if (c < nch) v0 = gload16(base + 16u * c);
+        if (c + kSThreads < nch) v1 = gload16(base + 16u * (c + kSThreads));
+        if (c + 2u * kSThreads < nch) v2 = gload16(base + 16u * (c + 2u * kSThreads));
+        if (c + 3u * kSThreads < nch) v3 = gload16(base + 16u * (c + 3u * kSThreads));
+        if (c < nch) s_buf[c] = v0;
+        if (c + kSThreads < nch) s_buf[c + kSThreads] = v1;
+        if (c + 2u * kSThreads < nch) s_buf[c + 2u * kSThreads] = v2;
+        if (c + 3u * kSThreads < nch) s_buf[c + 3u * kSThreads] = v3;
     }
+    if (tid == 0) s_buf[nch] = u32x4{0u, 0u, 0u, 0u};
     __syncthreads();
     const uint8_t *sb = (const uint8_t *)s_buf;
 
@@ -141,8 +142,7 @@ __global__ __launch_bounds__(kSThreads) void k_decode_small(uint8_t *__restrict_
         if (hi <= N) {
             gstore16(base + lo, v);
         } else {
-            const uint8_t *vb = (const uint8_t *)&v;
-            for (uint32_t j = 0; lo + j < N; ++j) wire[lo + j] = vb[j];
+            for (uint32_t j = 0; lo + j < N; ++j) wire[lo + j] = (uint8_t)(v[j >> 2] >> (8u * (j & 3u)));
         }
     }
 }

@@ -25,7 +25,7 @@ def resolve_mode(request):
     """Every decode test runs on both resolve paths: the super-tile resolve
     (merge_kernels.hip, the common path) and the cooperative k_resolve it
     falls back to (resolve_kernels.hip), forced; and through the RX session's
-    one-launch small-read kernel (small_kernels.hip; streams <= 64 KiB with
+    one-launch small-read kernel (small_kernels.hip; streams <= 128 KiB with
     <= 256 headers, the rest fall back to the super-tile path as the session
     does)."""
     from flashws_amd import _lib
@@ -449,9 +449,9 @@ def test_small_read_frame_counts(ctx, cuda, nfr, tail):
     check(ctx, cuda, wire)
 
 
-@pytest.mark.parametrize("size", [65536 - 7, 65536, 65537, 70000])
+@pytest.mark.parametrize("size", [65537, 131072 - 7, 131072, 131073, 140000])
 def test_small_read_size_limit(ctx, cuda, size):
-    """Streams either side of the small-read kernel's 64 KiB limit."""
+    """Streams either side of the small-read kernel's 128 KiB limit."""
     rng = np.random.default_rng(size)
     parts, n = [], 0
     while n < size:

@@ -5,7 +5,10 @@
 Workload (BASELINE configs[1]): 65 536 client-masked BIN frames
 x 4 096 B payload (8-B headers, one random key each, seed 42), packed
 contiguously, resident in HBM before timing starts. One step = one
-fws_gpu_unmask_batch over one batch (plan kernels + the unmask kernel). Steps
+fws_gpu_unmask_sorted over one batch (a packed batch is sorted by
+construction; one launch, k_unmask_sorted, which finds each 4 KiB unit's
+frames itself). The any-order path fws_gpu_unmask_batch (k_plan +
+k_unmask_desc) is timed beside it in extra.C2_unmask_batch_any_order. Steps
 rotate over NBUF >= 4 distinct device copies (>= 1 GiB) so the 256 MiB
 Infinity Cache cannot serve a batch from the previous step.
 
@@ -14,7 +17,7 @@ weak scaling, no collective on the data path); the timed region is bracketed
 by barrier + synchronize and the slowest rank's time is reported.
 
 Output: ONE JSON line on rank 0 (contract in the task statement), with
-`roofline` for the dominant kernel (k_unmask, timed live with HIP events on
+`roofline` for the dominant kernel (k_unmask_sorted, timed live with HIP events on
 its stream) and `cpu_baseline` (the compiled reference's
 WSocket::OnRecvData on this host, rank 0, N=1 only).
 """
@@ -45,6 +48,8 @@ def parse():
     ap.add_argument("--nbuf", type=int, default=4)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-batch-extra", action="store_true",
+                    help="skip the fws_gpu_unmask_batch (plan + run) comparison line")
     ap.add_argument("--extra", action="store_true",
                     help="also time C2 stream decode, C3, C4, e2e (PCIe) -> 'extra'")
     ap.add_argument("--c5", action="store_true", help="with --extra: the 4 GiB C5 UTF-8 config")
@@ -143,7 +148,9 @@ def pmc_traffic():
     p = os.path.join(ROOT, "profiles", "pmc_unmask.json")
     try:
         with open(p) as f:
-            return json.load(f).get("hbm_bytes_per_launch")
+            rec = json.load(f)
+        # only a summary of the kernel this bench times counts
+        return rec.get("hbm_bytes_per_launch") if rec.get("kernel") == "k_unmask_sorted" else None
     except (OSError, ValueError):
         return None
 
@@ -166,8 +173,9 @@ def main():
     dd = gpu.descs_to_device(descs, dev)
     stream = torch.cuda.current_stream()
 
+    # a packed batch is sorted by construction: the one-launch fws_gpu_unmask_sorted
     for i in range(args.warmup):
-        gpu.unmask_batch(ctx, bufs[i % args.nbuf], dd, n)
+        gpu.unmask_sorted(ctx, bufs[i % args.nbuf], dd, n)
     torch.cuda.synchronize()
 
     # ---- timed region: K whole steps
@@ -175,27 +183,28 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        gpu.unmask_batch(ctx, bufs[i % args.nbuf], dd, n)
+        gpu.unmask_sorted(ctx, bufs[i % args.nbuf], dd, n)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     barrier(world)
     step_s = max_over_ranks(world, (t1 - t0) / args.steps)
 
-    # ---- dominant kernel alone (k_unmask_desc), HIP events on its stream
-    gpu.unmask_plan(ctx, bufs[0], dd, n)
+    # ---- dominant kernel alone (k_unmask_sorted, the step's only launch), HIP
+    # events on its stream (the current stream, where the ABI call launches it)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
     ev0.record(stream)
     for i in range(args.steps):
-        gpu.unmask_run(ctx, bufs[i % args.nbuf], dd, n)
+        gpu.unmask_sorted(ctx, bufs[i % args.nbuf], dd, n)
     ev1.record(stream)
     torch.cuda.synchronize()
     kern_s = ev0.elapsed_time(ev1) / 1e3 / args.steps
-    # restore input parity (even number of passes per buffer is not required for timing)
 
     extra = {}
+    if not args.no_batch_extra:
+        extra["C2_unmask_batch_any_order"] = batch_extra(ctx, bufs, dd, n, payload_bytes, args, stream)
     if args.extra:
-        extra = stream_decode_extra(ctx, wire, dev, args)
+        extra.update(stream_decode_extra(ctx, wire, dev, args))
 
     value = aggregate_gib_s(world, payload_bytes, step_s)
     achieved = alg_bytes / kern_s / 1e9
@@ -214,14 +223,15 @@ def main():
         "dtype": "u8",
         "data": "synthetic (fws_gen_batch, mt19937_64 seed 42+rank): client-masked BIN frames",
         "config": {"workload": "C2: device-resident 65536 x 4 KiB masked BIN frames, "
-                               "descriptor-mode unmask (fws_gpu_unmask_batch)",
+                               "descriptor-mode unmask of the packed (sorted) batch, "
+                               "one launch (fws_gpu_unmask_sorted)",
                    "frames_per_gpu": n, "payload_bytes_per_frame": args.payload,
                    "wire_bytes_per_gpu": wire_bytes, "rotating_buffers": args.nbuf,
                    "parallelism": f"batch split x{world} (no collective)"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic,
-                     "kernel": "k_unmask_desc", "kernel_us": round(kern_s * 1e6, 2),
+                     "kernel": "k_unmask_sorted", "kernel_us": round(kern_s * 1e6, 2),
                      "alg_bytes_per_launch": alg_bytes},
     }
     out.update(extra)
@@ -244,6 +254,18 @@ def _time(fn, steps, stream):
     ev1.record(stream)
     torch.cuda.synchronize()
     return ev0.elapsed_time(ev1) / 1e3 / steps
+
+
+def batch_extra(ctx, bufs, dd, n, payload_bytes, args, stream):
+    """fws_gpu_unmask_batch (k_plan + k_unmask_desc: any descriptor order) on
+    the same C2 batches: the step, and the unmask kernel alone."""
+    steps = max(20, args.steps // 2)
+    t = _time(lambda i: gpu.unmask_batch(ctx, bufs[i % args.nbuf], dd, n), steps, stream)
+    gpu.unmask_plan(ctx, bufs[0], dd, n)
+    tk = _time(lambda i: gpu.unmask_run(ctx, bufs[i % args.nbuf], dd, n), steps, stream)
+    return {"GiB_per_s": round(payload_bytes / t / GIB, 1), "ms_per_step": round(t * 1e3, 4),
+            "k_unmask_desc_us": round(tk * 1e6, 2),
+            "path": "fws_gpu_unmask_batch: k_plan + k_unmask_desc (descriptors in any order)"}
 
 
 def stream_decode_extra(ctx, wire_c2, dev, args):

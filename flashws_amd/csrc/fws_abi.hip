@@ -178,6 +178,17 @@ int fws_gpu_unmask_batch(fws_gpu_ctx *ctx, void *dev_base, const fws_frame_desc 
     return fws_gpu_unmask_run(ctx, dev_base, dev_descs, n, stream);
 }
 
+int fws_gpu_unmask_sorted(fws_gpu_ctx *ctx, void *dev_base, const fws_frame_desc *dev_descs, uint32_t n,
+                          void *stream) {
+    if (!ctx || (n && (!dev_base || !dev_descs))) return FWS_ERR_INVALID;
+    if (n == 0) return 0;
+    int r;
+    if ((r = fws_hip_status(hipSetDevice(ctx->device)))) return r;
+    // the grid only bounds the grid-stride loop: every unit of the span is visited at any grid
+    const uint64_t span = ctx->cap_stream ? ctx->cap_stream : 4096ull * n;
+    return fws_launch_unmask_sorted((uint8_t *)dev_base, dev_descs, n, span, (hipStream_t)stream);
+}
+
 int fws_gpu_unmask_gather(fws_gpu_ctx *ctx, void *dev_dst, const void *dev_src, const fws_frame_desc *dev_descs,
                           uint32_t n, void *stream) {
     if (!ctx || (n && (!dev_dst || !dev_src || !dev_descs))) return FWS_ERR_INVALID;

@@ -144,9 +144,13 @@ __global__ __launch_bounds__(kBlock) void k_plan(const uint8_t *base, const fws_
     }
     bool all_sorted;
     const uint64_t prefix = block_lookback(a.status, blk, agg, blk_sorted, a.epoch, &all_sorted);
-    const uint64_t S = po0 - ((b0 + po0) & 15u);
+    // unit origin S (base-relative, modulo 2^64: below the base when dev_base is
+    // not 16-B aligned and the first payload starts within 15 B of it); every
+    // comparison below is made on absolute addresses, which never wrap
+    const uint64_t Sa = (b0 + po0) & ~uint64_t(15);
+    const uint64_t S = Sa - b0;
     const uint64_t cap = a.unit_cap;
-    const uint64_t nus = last_pe > S ? (last_pe - S + 4095u) / 4096u : 0;
+    const uint64_t nus = b0 + last_pe > Sa ? (b0 + last_pe - Sa + 4095u) / 4096u : 0;
     uint64_t run = prefix + run0;
     // this frame's unit-map runs: chunk space [cu, cue), byte space [bu, bue)
     uint64_t cu = 0, cue = 0, bu = 0, bue = 0;
@@ -158,8 +162,8 @@ __global__ __launch_bounds__(kBlock) void k_plan(const uint8_t *base, const fws_
         }
         run += s;
         // byte space: the unit starts in [po_f, po_{f+1})
-        bu = f == 0 ? 0 : (poA >= S ? (poA - S + 4095u) / 4096u : cap);
-        bue = !hasB ? nus : (poB >= S ? (poB - S + 4095u) / 4096u : 0);
+        bu = f == 0 ? 0 : (b0 + poA >= Sa ? (b0 + poA - Sa + 4095u) / 4096u : cap);
+        bue = !hasB ? nus : (b0 + poB >= Sa ? (b0 + poB - Sa + 4095u) / 4096u : 0);
         if (f == n - 1) {                             // the thread holding the last frame
             a.cbase[n] = run;
             *a.total = run;
@@ -193,8 +197,8 @@ __global__ __launch_bounds__(kBlock) void k_plan(const uint8_t *base, const fws_
                           __builtin_amdgcn_readlane((int)mine.hasC, L) != 0};
         },
         [&](const RecCtx &c, uint64_t u) {
-            a.unit_rec[u] = unit_record(S + 4096u * u, po0, last_pe, c.f, c.poA, c.peA, c.rkA, c.hasB, c.poB, c.peB,
-                                        c.rkB, c.hasC, c.poC);
+            a.unit_rec[u] = unit_record(Sa + 4096u * u, b0 + po0, b0 + last_pe, c.f, b0 + c.poA, b0 + c.peA, c.rkA,
+                                        c.hasB, b0 + c.poB, b0 + c.peB, c.rkB, c.hasC, b0 + c.poC);
         });
 }
 
@@ -713,14 +717,8 @@ __device__ __forceinline__ uint32_t byte_sel32(uint32_t o, uint32_t lo, uint32_t
 // key masks of the frames starting before the unit's end into its 4 chunks
 // (frame k broadcast by readlane); then the 4 loads, XOR and stores. Chunks
 // reaching outside [E0, E1) are stored byte-exact.
-template <bool kNT>
-__device__ __forceinline__ void byte_space_unit_slow(uint8_t *base, const fws_frame_desc *__restrict__ d,
-                                                     uint32_t n, uint32_t flo, uint64_t E0, uint64_t E1, uint64_t U0,
-                                                     int lane) {
-    const uintptr_t b0 = (uintptr_t)base;
-    const uint64_t c0 = U0 + uint64_t(lane) * 16u;
-    const uint64_t safe = (E1 - 1u) & ~uint64_t(15);   // chunks in [S, E1) hold a byte of the span
-    u32x4 m[kUnmaskU];
+__device__ __forceinline__ void slow_unit_masks(const fws_frame_desc *__restrict__ d, uint32_t n, uint32_t flo,
+                                                uintptr_t b0, uint64_t U0, int lane, u32x4 (&m)[kUnmaskU]) {
 #pragma unroll
     for (int j = 0; j < kUnmaskU; ++j) m[j] = u32x4{0u, 0u, 0u, 0u};
     uint32_t o0 = (uint32_t)lane * 16u;
@@ -754,12 +752,13 @@ __device__ __forceinline__ void byte_space_unit_slow(uint8_t *base, const fws_fr
         }
         if (cnt < kWave) break;
     }
-    u32x4 v[kUnmaskU];
-#pragma unroll
-    for (int j = 0; j < kUnmaskU; ++j) {
-        const uint64_t c = c0 + uint64_t(j) * 1024u;
-        v[j] = gload16<kNT>(c < E1 ? c : safe);
-    }
+}
+
+// XOR and store of a slow-kind unit's chunks (loaded from c0 + 1024 j, clamped
+// into the span): chunks reaching outside [E0, E1) are stored byte-exact.
+template <bool kNT>
+__device__ __forceinline__ void slow_unit_store(uint64_t c0, uint64_t E0, uint64_t E1, const u32x4 (&v)[kUnmaskU],
+                                                const u32x4 (&m)[kUnmaskU]) {
 #pragma unroll
     for (int j = 0; j < kUnmaskU; ++j) {
         const uint64_t c = c0 + uint64_t(j) * 1024u;
@@ -767,6 +766,45 @@ __device__ __forceinline__ void byte_space_unit_slow(uint8_t *base, const fws_fr
         const u32x4 x = v[j] ^ m[j];
         if (c >= E0 && c + 16u <= E1) gstore16<kNT>(c, x);
         else store_bytes(c, x, E0, E1);
+    }
+}
+
+template <bool kNT>
+__device__ __forceinline__ void byte_space_unit_slow(uint8_t *base, const fws_frame_desc *__restrict__ d,
+                                                     uint32_t n, uint32_t flo, uint64_t E0, uint64_t E1, uint64_t U0,
+                                                     int lane) {
+    const uint64_t c0 = U0 + uint64_t(lane) * 16u;
+    const uint64_t safe = (E1 - 1u) & ~uint64_t(15);   // chunks in [S, E1) hold a byte of the span
+    u32x4 m[kUnmaskU];
+    slow_unit_masks(d, n, flo, (uintptr_t)base, U0, lane, m);
+    u32x4 v[kUnmaskU];
+#pragma unroll
+    for (int j = 0; j < kUnmaskU; ++j) {
+        const uint64_t c = c0 + uint64_t(j) * 1024u;
+        v[j] = gload16<kNT>(c < E1 ? c : safe);
+    }
+    slow_unit_store<kNT>(c0, E0, E1, v, m);
+}
+
+// Key masks of a fast-kind unit's four chunks of this lane from its record.
+__device__ __forceinline__ void fast_unit_masks(const u32x4 &rec, int lane, u32x4 (&mk)[kUnmaskU]) {
+    const uint32_t a0 = rec.z & 0x1FFFu, a1 = (rec.z >> 13) & 0x1FFFu;
+    const uint32_t e0 = rec.w & 0x1FFFu, e1 = (rec.w >> 13) & 0x1FFFu;
+    uint32_t o0 = (uint32_t)lane * 16u;
+    asm volatile("" : "+v"(o0));                     // opaque per unit: no hoisted per-dword offsets
+#pragma unroll
+    for (int j = 0; j < kUnmaskU; ++j) {
+        const uint32_t o = o0 + (uint32_t)j * 1024u;
+        const bool inA = o >= a0 && o + 16u <= a1, inB = o >= e0 && o + 16u <= e1;
+        if (inA || inB) {
+            const uint32_t rk = inA ? rec.x : rec.y;
+            mk[j] = u32x4{rk, rk, rk, rk};
+        } else {
+            mk[j] = u32x4{(rec.x & byte_sel32(o, a0, a1)) | (rec.y & byte_sel32(o, e0, e1)),
+                          (rec.x & byte_sel32(o + 4u, a0, a1)) | (rec.y & byte_sel32(o + 4u, e0, e1)),
+                          (rec.x & byte_sel32(o + 8u, a0, a1)) | (rec.y & byte_sel32(o + 8u, e0, e1)),
+                          (rec.x & byte_sel32(o + 12u, a0, a1)) | (rec.y & byte_sel32(o + 12u, e0, e1))};
+        }
     }
 }
 
@@ -782,25 +820,8 @@ __device__ __forceinline__ void byte_space_unit(uint8_t *base, const fws_frame_d
             byte_space_unit_slow<kNT>(base, d, n, rec.x, b0 + pm.first_po, b0 + pm.last_pe, U0, lane);
         return;
     }
-    const uint32_t a0 = rec.z & 0x1FFFu, a1 = (rec.z >> 13) & 0x1FFFu;
-    const uint32_t e0 = rec.w & 0x1FFFu, e1 = (rec.w >> 13) & 0x1FFFu;
-    uint32_t o0 = (uint32_t)lane * 16u;
-    asm volatile("" : "+v"(o0));                     // opaque per unit: no hoisted per-dword offsets
     u32x4 mk[kUnmaskU];
-#pragma unroll
-    for (int j = 0; j < kUnmaskU; ++j) {
-        const uint32_t o = o0 + (uint32_t)j * 1024u;
-        const bool inA = o >= a0 && o + 16u <= a1, inB = o >= e0 && o + 16u <= e1;
-        if (inA || inB) {
-            const uint32_t rk = inA ? rec.x : rec.y;
-            mk[j] = u32x4{rk, rk, rk, rk};
-        } else {
-            mk[j] = u32x4{(rec.x & byte_sel32(o, a0, a1)) | (rec.y & byte_sel32(o, e0, e1)),
-                          (rec.x & byte_sel32(o + 4u, a0, a1)) | (rec.y & byte_sel32(o + 4u, e0, e1)),
-                          (rec.x & byte_sel32(o + 8u, a0, a1)) | (rec.y & byte_sel32(o + 8u, e0, e1)),
-                          (rec.x & byte_sel32(o + 12u, a0, a1)) | (rec.y & byte_sel32(o + 12u, e0, e1))};
-        }
-    }
+    fast_unit_masks(rec, lane, mk);
     const uint64_t c0 = U0 + uint64_t(lane) * 16u;
     u32x4 v[kUnmaskU];
 #pragma unroll
@@ -809,6 +830,7 @@ __device__ __forceinline__ void byte_space_unit(uint8_t *base, const fws_frame_d
     for (int j = 0; j < kUnmaskU; ++j)
         if (mk[j].x | mk[j].y | mk[j].z | mk[j].w) gstore16<kNT>(c0 + uint64_t(j) * 1024u, v[j] ^ mk[j]);
 }
+
 
 // One chunk-space plan unit (any descriptor order): k_unmask_fast's body.
 template <bool kNT>
@@ -889,6 +911,128 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) voi
         chunk_space_unit<kNT>(base, d, n, cbase, unit_first, total, n_units, u, lane);
 }
 
+#ifndef FWS_SORTED_WPE
+#define FWS_SORTED_WPE 6
+#endif
+// ---------------------------------------------------------------- sorted, one launch
+// fws_gpu_unmask_sorted: k_unmask_desc's byte-space unmask without k_plan, for
+// batches whose descriptors are sorted by payload_off and non-overlapping (a
+// packed read batch, the decoder's frame list). Each wave finds the owner of
+// its unit's first byte (the last frame with payload_off <= U0, else frame 0,
+// as k_plan assigns it) by itself: an interpolation guess from the batch span,
+// one scalar round of four payload offsets around it, and a binary search only
+// when the guess misses (uneven frame sizes). It then builds the record k_plan
+// would have written (unit_record) and runs the same unit body. Units that
+// meet no payload (gaps of a sparse batch) are skipped without loads.
+// Absolute addresses throughout (U0, po: base + offset), so a dev_base that is
+// not 16-B aligned never wraps the unit origin below the base.
+// rate = frames per 4 KiB unit of the span (the guess of unit u is u * rate).
+__device__ __forceinline__ uint32_t sorted_owner(const fws_frame_desc *__restrict__ d, uint32_t n, uintptr_t b0,
+                                                 uint64_t U0, uint64_t po0, uint64_t u, float rate) {
+    if (U0 < po0 || n == 1) return 0u;
+    const float gf = (float)(uint32_t)u * rate;
+    uint64_t g = (uint32_t)__builtin_amdgcn_readfirstlane((int)(gf < 4.0e9f ? (uint32_t)gf : 0xFFFFFFFFu));
+    g = g >= 1u ? g - 1u : 0u;
+    if (g > n - 1u) g = n - 1u;
+    uint64_t p[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) p[k] = b0 + d[g + k < n ? g + k : n - 1u].payload_off;   // one scalar round
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const uint64_t i = g + k;
+        if (i < n && p[k] <= U0 && (i + 1u >= n || p[k + 1] > U0)) return (uint32_t)i;
+    }
+    uint32_t lo = 0, hi = n;                         // count of frames starting at or before U0 (>= 1)
+    while (lo < hi) {
+        const uint32_t mid = lo + (hi - lo) / 2u;
+        if (b0 + d[mid].payload_off <= U0) lo = mid + 1u;
+        else hi = mid;
+    }
+    return lo - 1u;
+}
+
+// kEarly: the unit's data loads are issued before the owner lookup (their
+// addresses depend only on the span), so the lookup's scalar rounds overlap
+// the HBM latency; gap units then cost their loads. Without it, the lookup
+// comes first and units that meet no payload are skipped without loads.
+template <bool kNT, bool kEarly>
+__device__ __forceinline__ void unmask_sorted_body(uint8_t *base, const fws_frame_desc *__restrict__ d, uint32_t n) {
+    if (n == 0) return;
+    const int lane = threadIdx.x & (kWave - 1);
+    const uintptr_t b0 = (uintptr_t)base;
+    const uint64_t nwaves = uint64_t(gridDim.x) * (kBlock / kWave);
+    const uint64_t u0 = uint64_t(blockIdx.x) * (kBlock / kWave) + __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const uint64_t po0 = d[0].payload_off;
+    const fws_frame_desc dl = d[n - 1];
+    const uint64_t last_pe = dl.payload_off + dl.payload_len;
+    const uint64_t E0 = b0 + po0, E1 = b0 + last_pe;   // absolute span of the batch's payloads
+    const uint64_t Sa = E0 & ~uint64_t(15);
+    const uint64_t nus = E1 > Sa ? (E1 - Sa + 4095u) / 4096u : 0;
+    const uint64_t safe = (E1 - 1u) & ~uint64_t(15);   // chunk holding the span's last byte
+    const float rate = (float)n * 4096.0f / (float)(E1 > E0 ? E1 - E0 : 1u);
+    for (uint64_t u = u0; u < nus; u += nwaves) {
+        const uint64_t U0 = Sa + 4096u * u;
+        const uint64_t c0 = U0 + uint64_t(lane) * 16u;
+        u32x4 v[kUnmaskU];
+        if (kEarly) {
+#pragma unroll
+            for (int j = 0; j < kUnmaskU; ++j) {
+                const uint64_t c = c0 + uint64_t(j) * 1024u;
+                v[j] = gload16<kNT>(c < E1 ? c : safe);
+            }
+        }
+        const uint32_t A = sorted_owner(d, n, b0, U0, E0, u, rate);
+        const bool hasB = A + 1u < n, hasC = A + 2u < n;
+        const fws_frame_desc fa = d[A];
+        fws_frame_desc fb{0, 0, 0, 0};
+        if (hasB) fb = d[A + 1u];
+        const uint64_t poC = hasC ? b0 + d[A + 2u].payload_off : 0;
+        const uint64_t poA = b0 + fa.payload_off, peA = poA + fa.payload_len;
+        const uint64_t poB = b0 + fb.payload_off, peB = poB + fb.payload_len;
+        const u32x4 rec = unit_record(U0, E0, E1, A, poA, peA, aligned_key(fa.key, fa.phase, poA), hasB, poB, peB,
+                                      aligned_key(fb.key, fb.phase, poB), hasC, poC);
+        const bool slow = (rec.z & kRecSlow) != 0;
+        if (!kEarly && !slow) {
+            const uint32_t a0 = rec.z & 0x1FFFu, a1 = (rec.z >> 13) & 0x1FFFu;
+            const uint32_t e0 = rec.w & 0x1FFFu, e1 = (rec.w >> 13) & 0x1FFFu;
+            if (a1 <= a0 && e1 <= e0) continue;      // a gap between payloads
+        }
+        u32x4 m[kUnmaskU];
+        if (slow) slow_unit_masks(d, n, A, b0, U0, lane, m);
+        else fast_unit_masks(rec, lane, m);
+        if (!kEarly) {
+#pragma unroll
+            for (int j = 0; j < kUnmaskU; ++j) {
+                const uint64_t c = c0 + uint64_t(j) * 1024u;
+                v[j] = gload16<kNT>(c < E1 ? c : safe);
+            }
+        }
+        if (slow) {
+            slow_unit_store<kNT>(c0, E0, E1, v, m);
+        } else {
+#pragma unroll
+            for (int j = 0; j < kUnmaskU; ++j)      // fast kind: every chunk lies inside [E0, E1)
+                if (m[j].x | m[j].y | m[j].z | m[j].w) gstore16<kNT>(c0 + uint64_t(j) * 1024u, v[j] ^ m[j]);
+        }
+    }
+}
+
+// k_unmask_sorted (lookup first, 8 waves per SIMD, no spills) is the default;
+// k_unmask_sorted_early needs 80 VGPRs (the unit's 16 data registers live
+// across the lookup and the slow-kind mask walk) and measured slower at 6
+// waves per SIMD (84.9 vs 82.7 us on C2), kept behind the tuning hook
+template <bool kNT>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FWS_SORTED_WPE))) void k_unmask_sorted_early(
+    uint8_t *base, const fws_frame_desc *__restrict__ d, uint32_t n) {
+    unmask_sorted_body<kNT, true>(base, d, n);
+}
+
+template <bool kNT>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) void k_unmask_sorted(
+    uint8_t *base, const fws_frame_desc *__restrict__ d, uint32_t n) {
+    unmask_sorted_body<kNT, false>(base, d, n);
+}
+
 }  // namespace fwsk
 
 // ---------------------------------------------------------------- launchers
@@ -908,6 +1052,13 @@ static int g_grid_cap = 16384;  // tuning hook: max workgroups of the streaming 
 extern "C" __attribute__((visibility("default"))) int fws_internal_set_grid_cap(int blocks) {
     const int old = g_grid_cap;
     if (blocks > 0) g_grid_cap = blocks;
+    return old;
+}
+
+static int g_sorted_early = 0;  // tuning hook: 1 = k_unmask_sorted_early, 0 = k_unmask_sorted
+extern "C" __attribute__((visibility("default"))) int fws_internal_set_sorted_early(int on) {
+    const int old = g_sorted_early;
+    g_sorted_early = on != 0;
     return old;
 }
 
@@ -939,6 +1090,17 @@ int fws_launch_plan(const uint8_t *base, const fws_frame_desc *d, uint32_t n, co
     PlanArgs a{ws.cbase, ws.unit_first, (u32x4 *)ws.unit_rec, ws.total, ws.status, ws.ticket,
                (fws_plan_mode *)ws.mode, ws.unit_cap, ws.epoch};
     hipLaunchKernelGGL(k_plan, dim3(nb), dim3(kBlock), 0, s, base, d, n, n_dev, a);
+    return fws_hip_status(hipGetLastError());
+}
+
+int fws_launch_unmask_sorted(uint8_t *base, const fws_frame_desc *d, uint32_t n, uint64_t max_span,
+                             hipStream_t s) {
+    if (n == 0) return 0;
+    const uint64_t units = max_span / 4096u + 2u;
+    if (g_sorted_early)
+        hipLaunchKernelGGL(k_unmask_sorted_early<true>, dim3(grid_for_units(units)), dim3(kBlock), 0, s, base, d, n);
+    else
+        hipLaunchKernelGGL(k_unmask_sorted<true>, dim3(grid_for_units(units)), dim3(kBlock), 0, s, base, d, n);
     return fws_hip_status(hipGetLastError());
 }
 

@@ -73,6 +73,12 @@ def unmask_batch(ctx, base, dev_descs, n, stream=None):
                                                              _stream_handle(stream)))
 
 
+def unmask_sorted(ctx, base, dev_descs, n, stream=None):
+    """fws_gpu_unmask_sorted: one-launch unmask of a sorted, non-overlapping batch."""
+    check("fws_gpu_unmask_sorted", lib().fws_gpu_unmask_sorted(ctx.h, _ptr(base), _ptr(dev_descs), n,
+                                                               _stream_handle(stream)))
+
+
 def unmask_plan(ctx, base, dev_descs, n, stream=None):
     check("fws_gpu_unmask_plan", lib().fws_gpu_unmask_plan(ctx.h, _ptr(base), _ptr(dev_descs), n,
                                                            _stream_handle(stream)))

@@ -116,6 +116,19 @@ int fws_gpu_mask(void *dev_ptr, uint64_t n, uint32_t key, void *stream);
 int fws_gpu_unmask_batch(fws_gpu_ctx *ctx, void *dev_base, const fws_frame_desc *dev_descs,
                          uint32_t n, void *stream);
 
+/* One-launch batch unmask for descriptors sorted by payload_off with
+ * non-overlapping regions (payload_off_i + payload_len_i <= payload_off_i+1),
+ * as a batch cut from a wire stream or fws_gpu_decode_stream's frame list
+ * always is. Same result and the same byte-space write rule as
+ * fws_gpu_unmask_batch, without its plan launch: each 4 KiB unit finds its
+ * frames itself (interpolation guess, binary search on a miss). Unsorted or
+ * overlapping descriptors are a contract violation: results are undefined
+ * inside [first payload, last payload end), nothing outside it is written.
+ * Replaces the per-frame WSMaskBytesFast calls (ws_mask.h:175) of
+ * OnRecvData's frame loop (w_socket.h:586,614) for a whole batch. */
+int fws_gpu_unmask_sorted(fws_gpu_ctx *ctx, void *dev_base, const fws_frame_desc *dev_descs,
+                          uint32_t n, void *stream);
+
 /* The two halves of fws_gpu_unmask_batch, for callers that reuse one plan
  * (same descriptors) across buffers: _plan builds the chunk plan of the
  * descriptors in ctx, _run unmasks with the last plan built in ctx. */

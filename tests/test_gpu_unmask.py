@@ -225,3 +225,142 @@ def test_plan_reused_across_buffers(ctx, cuda):
     orc.orc_decode_stream(exp)
     assert np.array_equal(b.cpu().numpy(), exp)
     assert torch.equal(a.cpu(), torch.from_numpy(wire))
+
+
+# ---- fws_gpu_unmask_sorted: one launch, no plan (sorted, disjoint regions) ----
+
+def run_sorted(ctx, host, descs, cuda, base_shift=0):
+    """Unmask through fws_gpu_unmask_sorted; base_shift moves dev_base off the
+    allocation's alignment (descriptor offsets are base-relative)."""
+    dev = torch.from_numpy(np.concatenate([np.zeros(base_shift, np.uint8), host])).to(cuda)
+    dd = gpu.descs_to_device(descs, cuda)
+    gpu.unmask_sorted(ctx, dev[base_shift:], dd, len(descs))
+    torch.cuda.synchronize()
+    return dev[base_shift:].cpu().numpy()
+
+
+@pytest.mark.parametrize("n_frames", [1, 2, 7, 4096, 65536])
+def test_sorted_c2_shape(ctx, cuda, n_frames):
+    """BASELINE C2 layout (65 536 at full size): interpolation guesses hit."""
+    wire, descs, _ = gpu.config_c2(seed=17, n_frames=n_frames)
+    got = run_sorted(ctx, wire, descs, cuda)
+    exp = wire.copy()
+    ret, frames, _, _ = orc.orc_decode_stream(exp)
+    assert ret == 0 and len(frames) == n_frames
+    assert np.array_equal(got, exp)
+
+
+@pytest.mark.parametrize("shift", [1, 3, 8, 15])
+def test_sorted_unaligned_base(ctx, cuda, shift):
+    wire, descs, _ = gpu.config_c2(seed=19, n_frames=300)
+    got = run_sorted(ctx, wire, descs, cuda, base_shift=shift)
+    exp = wire.copy()
+    orc.orc_decode_stream(exp)
+    assert np.array_equal(got, exp)
+
+
+def test_sorted_mixed_c3(ctx, cuda):
+    """C3-shaped 64 B-64 KiB frames: guesses miss, binary search finds owners."""
+    wire, descs, _ = gpu.config_c3(seed=23, target=16 << 20)
+    got = run_sorted(ctx, wire, descs, cuda)
+    exp = wire.copy()
+    ret, frames, _, _ = orc.orc_decode_stream(exp)
+    assert ret == 0 and len(frames) == len(descs)
+    assert np.array_equal(got, exp)
+
+
+def test_sorted_alignment_sweep(ctx, cuda):
+    rng = np.random.default_rng(29)
+    regions, pos = [], 0
+    for ln in range(0, 601):
+        for sh in (0, 1, 5, 13, 31, 47, 63):
+            pos = (pos + 63) // 64 * 64 + sh
+            regions.append((pos, ln, int(rng.integers(0, 2**32)), int(rng.integers(0, 4))))
+            pos += ln + int(rng.integers(0, 9))
+    host = aligned_host(pos + 64)
+    host[:] = rng.integers(0, 256, len(host), dtype=np.uint8)
+    descs = np.array(regions, dtype=gpu.FRAME_DESC)
+    assert np.array_equal(run_sorted(ctx, host, descs, cuda), oracle_unmask_regions(host, descs))
+
+
+@pytest.mark.parametrize("n,max_len,max_gap", [(1, 5, 0), (3, 20, 3), (1025, 64, 2), (70000, 30, 3),
+                                                (300000, 12, 1), (5000, 0, 2)])
+def test_sorted_tiny_frames(ctx, cuda, n, max_len, max_gap):
+    """Many frames per 4 KiB unit (slow-kind units), zero-length frames."""
+    rng = np.random.default_rng(n + 7)
+    regions, pos = _rand_regions(rng, n, max_len, max_gap)
+    host = aligned_host(pos + 32)
+    host[:] = rng.integers(0, 256, len(host), dtype=np.uint8)
+    descs = np.array(regions, dtype=gpu.FRAME_DESC)
+    assert np.array_equal(run_sorted(ctx, host, descs, cuda), oracle_unmask_regions(host, descs))
+
+
+def test_sorted_large_and_sparse(ctx, cuda):
+    """A 16 MiB frame among tiny ones (guesses miss), then a sparse batch
+    (64 B every 1 MiB: gap units skipped)."""
+    rng = np.random.default_rng(37)
+    lens = [16 << 20, 3, 1 << 20, 4097, 12345, 0, 65536 * 3 + 7, 9]
+    regions, pos = [], 7
+    for ln in lens:
+        regions.append((pos, ln, int(rng.integers(0, 2**32)), int(rng.integers(0, 4))))
+        pos += ln + 14
+    host = aligned_host(pos + 32)
+    host[:] = rng.integers(0, 256, len(host), dtype=np.uint8)
+    descs = np.array(regions, dtype=gpu.FRAME_DESC)
+    assert np.array_equal(run_sorted(ctx, host, descs, cuda), oracle_unmask_regions(host, descs))
+    regions = [(i * (1 << 20) + 3, 64, int(rng.integers(0, 2**32)), 0) for i in range(64)]
+    host = aligned_host(64 << 20)
+    host[:] = rng.integers(0, 256, len(host), dtype=np.uint8)
+    descs = np.array(regions, dtype=gpu.FRAME_DESC)
+    assert np.array_equal(run_sorted(ctx, host, descs, cuda), oracle_unmask_regions(host, descs))
+
+
+def test_sorted_matches_batch_and_involution(ctx, cuda):
+    """Full C2 size: _sorted and _batch agree, and two _sorted passes restore the input."""
+    wire, descs, _ = gpu.config_c2(seed=43)
+    dev = torch.from_numpy(wire).to(cuda)
+    ref = torch.from_numpy(wire).to(cuda)
+    dd = gpu.descs_to_device(descs, cuda)
+    gpu.unmask_sorted(ctx, dev, dd, len(descs))
+    gpu.unmask_batch(ctx, ref, dd, len(descs))
+    torch.cuda.synchronize()
+    assert torch.equal(dev, ref)
+    gpu.unmask_sorted(ctx, dev, dd, len(descs))
+    torch.cuda.synchronize()
+    assert torch.equal(dev.cpu(), torch.from_numpy(wire))
+
+
+@pytest.mark.parametrize("shift", [1, 7, 15])
+def test_batch_unaligned_base(ctx, cuda, shift):
+    """fws_gpu_unmask_batch with dev_base off 16-B alignment and the first
+    payload within 15 B of it (the byte-space unit origin lies below the base)."""
+    wire, descs, _ = gpu.config_c2(seed=47, n_frames=300)
+    dev = torch.from_numpy(np.concatenate([np.zeros(shift, np.uint8), wire])).to(cuda)
+    dd = gpu.descs_to_device(descs, cuda)
+    gpu.unmask_batch(ctx, dev[shift:], dd, len(descs))
+    torch.cuda.synchronize()
+    assert gpu.plan_mode(ctx)["byte_space"] == 1
+    exp = wire.copy()
+    orc.orc_decode_stream(exp)
+    assert np.array_equal(dev[shift:].cpu().numpy(), exp)
+    assert not dev[:shift].cpu().numpy().any()
+
+
+def test_sorted_early_variant(ctx, cuda):
+    """The tuning variant k_unmask_sorted_early (data loads before the lookup)
+    on C2, mixed and tiny-frame batches, bit-exact like the default."""
+    from flashws_amd import lib
+    old = lib().fws_internal_set_sorted_early(1)
+    try:
+        for wire, descs, _ in (gpu.config_c2(seed=53, n_frames=5000), gpu.config_c3(seed=59, target=4 << 20)):
+            exp = wire.copy()
+            orc.orc_decode_stream(exp)
+            assert np.array_equal(run_sorted(ctx, wire, descs, cuda), exp)
+        rng = np.random.default_rng(61)
+        regions, pos = _rand_regions(rng, 20000, 30, 3)
+        host = aligned_host(pos + 32)
+        host[:] = rng.integers(0, 256, len(host), dtype=np.uint8)
+        descs = np.array(regions, dtype=gpu.FRAME_DESC)
+        assert np.array_equal(run_sorted(ctx, host, descs, cuda), oracle_unmask_regions(host, descs))
+    finally:
+        lib().fws_internal_set_sorted_early(old)

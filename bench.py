@@ -204,7 +204,8 @@ def main():
     if not args.no_batch_extra:
         extra["C2_unmask_batch_any_order"] = batch_extra(ctx, bufs, dd, n, payload_bytes, args, stream)
     if args.extra:
-        extra.update(stream_decode_extra(ctx, wire, dev, args))
+        extra.update(stream_decode_extra(ctx, wire, dev, args)["extra"])
+    extra = {"extra": extra} if extra else {}
 
     value = aggregate_gib_s(world, payload_bytes, step_s)
     achieved = alg_bytes / kern_s / 1e9

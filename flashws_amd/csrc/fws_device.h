@@ -144,32 +144,37 @@ __device__ __forceinline__ uint32_t sel_bytes(uintptr_t w, uintptr_t lo, uintptr
     return (0xFFFFFFFFu << (8u * s)) & (0xFFFFFFFFu >> (8u * e));
 }
 
-// bit 7 of each byte of t set <=> that byte is zero
-__device__ __forceinline__ uint32_t zero_bytes(uint32_t t) {
-    return ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t) & 0x80808080u;
-}
-
 // UTF-8 error flags (bit 7 of each byte) of the 4 bytes of x, p = the dword
 // before x. Bytes outside the region are zero, so a sequence cut by the region
 // end fails the continuation rule at the first zero byte after it.
 //   continuation (10xxxxxx) <=> prev1 >= C0 or prev2 >= E0 or prev3 >= F0
 //   never C0, C1, F5..FF
 //   after E0: >= A0, after ED: <= 9F, after F0: >= 90, after F4: <= 8F
+// Lead flags (>= C0 / E0 / F0 at bit 7) are computed once per dword and
+// byte-aligned (v_alignbyte) to the prev1..3 positions; the four second-byte
+// rules test prev1 & 1F (00 / 0D / 10 / 14 under prev1 >= E0) with one add
+// each and select by bit 5 / bits 5|4 of x (v_bfi). ~38 VALU ops per dword
+// (was ~60); inlined chains share the flags of the dword between two calls.
+// Equivalent to the per-rule form on every (prev3, prev2, prev1, x) of 28
+// boundary bytes at every alignment and 2e8 random dword pairs (host check).
 __device__ __forceinline__ uint32_t utf8_err(uint32_t x, uint32_t p) {
     const uint32_t H = 0x80808080u;
-    const uint32_t p1 = __builtin_amdgcn_alignbyte(x, p, 3u);   // the byte before each byte of x
-    const uint32_t p2 = __builtin_amdgcn_alignbyte(x, p, 2u);
-    const uint32_t p3 = __builtin_amdgcn_alignbyte(x, p, 1u);
-    const uint32_t cont = x & ~(x << 1);
-    const uint32_t req = (p1 & (p1 << 1)) | (p2 & (p2 << 1) & (p2 << 2)) | (p3 & (p3 << 1) & (p3 << 2) & (p3 << 3));
-    uint32_t err = cont ^ req;
-    err |= zero_bytes((x & 0xFEFEFEFEu) ^ 0xC0C0C0C0u);
-    err |= ((x & 0x7F7F7F7Fu) + 0x0B0B0B0Bu) & x;
-    const uint32_t b5 = x << 2, b54 = (x << 2) | (x << 3);      // bit 5 / bits 5|4 of each byte at bit 7
-    err |= zero_bytes(p1 ^ 0xE0E0E0E0u) & ~b5;
-    err |= zero_bytes(p1 ^ 0xEDEDEDEDu) & b5;
-    err |= zero_bytes(p1 ^ 0xF0F0F0F0u) & ~b54;
-    err |= zero_bytes(p1 ^ 0xF4F4F4F4u) & b54;
+    const uint32_t x1 = x << 1, x2 = x << 2, x3 = x << 3;
+    const uint32_t tx = x & x1, ux = tx & x2, wx = ux & x3;
+    const uint32_t tp = p & (p << 1), up = tp & (p << 2), wp = up & (p << 3);
+    const uint32_t req = __builtin_amdgcn_alignbyte(tx, tp, 3u) | __builtin_amdgcn_alignbyte(ux, up, 2u) |
+                         __builtin_amdgcn_alignbyte(wx, wp, 1u);
+    uint32_t err = (x & ~x1) ^ req;
+    err |= tx & ~((x & 0x3E3E3E3Eu) + 0x7E7E7E7Eu);             // C0, C1: >= C0, bits 5..1 zero
+    err |= ((x & 0x7F7F7F7Fu) + 0x0B0B0B0Bu) & x;               // F5..FF
+    const uint32_t e1 = __builtin_amdgcn_alignbyte(ux, up, 3u);  // prev1 >= E0
+    const uint32_t q = __builtin_amdgcn_alignbyte(x, p, 3u) & 0x1F1F1F1Fu;
+    const uint32_t nzE0 = q + 0x7F7F7F7Fu, nzED = (q ^ 0x0D0D0D0Du) + 0x7F7F7F7Fu;   // bit 7: q != lead & 1F
+    const uint32_t nzF0 = (q ^ 0x10101010u) + 0x7F7F7F7Fu, nzF4 = (q ^ 0x14141414u) + 0x7F7F7F7Fu;
+    const uint32_t s5 = x2, s54 = x2 | x3;                       // bit 5 / bits 5|4 of each byte at bit 7
+    const uint32_t bE = (s5 & nzED) | (~s5 & nzE0);
+    const uint32_t bF = (s54 & nzF4) | (~s54 & nzF0);
+    err |= e1 & ~(bE & bF);
     return err & H;
 }
 

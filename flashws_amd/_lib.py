@@ -76,6 +76,7 @@ SIGNATURES = [
     ("fws_gpu_mask", _I, [_P, _U64, _U32, _P]),
     ("fws_gpu_unmask_batch", _I, [_P, _P, _P, _U32, _P]),
     ("fws_gpu_unmask_sorted", _I, [_P, _P, _P, _U32, _P]),
+    ("fws_gpu_unmask_sorted_utf8", _I, [_P, _P, _P, _U32, _P, _P]),
     ("fws_gpu_unmask_plan", _I, [_P, _P, _P, _U32, _P]),
     ("fws_gpu_unmask_run", _I, [_P, _P, _P, _U32, _P]),
     ("fws_gpu_unmask_gather", _I, [_P, _P, _P, _P, _U32, _P]),

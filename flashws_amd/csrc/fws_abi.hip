@@ -189,6 +189,16 @@ int fws_gpu_unmask_sorted(fws_gpu_ctx *ctx, void *dev_base, const fws_frame_desc
     return fws_launch_unmask_sorted((uint8_t *)dev_base, dev_descs, n, span, (hipStream_t)stream);
 }
 
+int fws_gpu_unmask_sorted_utf8(fws_gpu_ctx *ctx, void *dev_base, const fws_frame_desc *dev_descs, uint32_t n,
+                               uint8_t *dev_ok, void *stream) {
+    if (!ctx || (n && (!dev_base || !dev_descs || !dev_ok))) return FWS_ERR_INVALID;
+    if (n == 0) return 0;
+    int r;
+    if ((r = fws_hip_status(hipSetDevice(ctx->device)))) return r;
+    const uint64_t span = ctx->cap_stream ? ctx->cap_stream : 4096ull * n;
+    return fws_launch_unmask_sorted_utf8((uint8_t *)dev_base, dev_descs, n, span, dev_ok, (hipStream_t)stream);
+}
+
 int fws_gpu_unmask_gather(fws_gpu_ctx *ctx, void *dev_dst, const void *dev_src, const fws_frame_desc *dev_descs,
                           uint32_t n, void *stream) {
     if (!ctx || (n && (!dev_dst || !dev_src || !dev_descs))) return FWS_ERR_INVALID;

@@ -955,8 +955,32 @@ __device__ __forceinline__ uint32_t sorted_owner(const fws_frame_desc *__restric
 // addresses depend only on the span), so the lookup's scalar rounds overlap
 // the HBM latency; gap units then cost their loads. Without it, the lookup
 // comes first and units that meet no payload are skipped without loads.
-template <bool kNT, bool kEarly>
-__device__ __forceinline__ void unmask_sorted_body(uint8_t *base, const fws_frame_desc *__restrict__ d, uint32_t n) {
+// UTF-8 of one chunk of a slow-kind unit (kUtf8): every non-empty region that
+// meets the chunk as payload or 3-byte tail, found per lane (the last region
+// starting before the chunk end by binary search from the unit's owner, then
+// walking down while the region's tail still reaches the chunk; pe is
+// non-decreasing over sorted disjoint regions).
+__device__ __forceinline__ void utf8_slow_chunk(const fws_frame_desc *__restrict__ d, uint32_t n, uint32_t A,
+                                                uintptr_t b0, uint64_t c, const u32x4 &x, uint32_t prev,
+                                                uint32_t skip, uint8_t *__restrict__ ok) {
+    if (b0 + d[A].payload_off >= c + 16u) return;
+    uint32_t lo = A, hi = n - 1u;                    // last f with po_f < c + 16
+    while (lo < hi) {
+        const uint32_t mid = lo + ((hi - lo + 1u) >> 1);
+        if (b0 + d[mid].payload_off < c + 16u) lo = mid;
+        else hi = mid - 1u;
+    }
+    for (uint32_t f = lo + 1u; f-- > A;) {
+        const fws_frame_desc fd = d[f];
+        const uint64_t po = b0 + fd.payload_off, pe = po + fd.payload_len;
+        if (pe + 3u <= c) break;
+        if (fd.payload_len && utf8_chunk_bad(x, prev, c, po, pe, skip)) ok[f] = 0;
+    }
+}
+
+template <bool kNT, bool kEarly, bool kUtf8 = false>
+__device__ __forceinline__ void unmask_sorted_body(uint8_t *base, const fws_frame_desc *__restrict__ d, uint32_t n,
+                                                   uint8_t *__restrict__ ok = nullptr) {
     if (n == 0) return;
     const int lane = threadIdx.x & (kWave - 1);
     const uintptr_t b0 = (uintptr_t)base;
@@ -995,7 +1019,8 @@ __device__ __forceinline__ void unmask_sorted_body(uint8_t *base, const fws_fram
         if (!kEarly && !slow) {
             const uint32_t a0 = rec.z & 0x1FFFu, a1 = (rec.z >> 13) & 0x1FFFu;
             const uint32_t e0 = rec.w & 0x1FFFu, e1 = (rec.w >> 13) & 0x1FFFu;
-            if (a1 <= a0 && e1 <= e0) continue;      // a gap between payloads
+            // a gap between payloads (a tail of A reaches at most bytes 0..2: the seam kernel's)
+            if (a1 <= a0 && e1 <= e0) continue;
         }
         u32x4 m[kUnmaskU];
         if (slow) slow_unit_masks(d, n, A, b0, U0, lane, m);
@@ -1014,6 +1039,81 @@ __device__ __forceinline__ void unmask_sorted_body(uint8_t *base, const fws_fram
             for (int j = 0; j < kUnmaskU; ++j)      // fast kind: every chunk lies inside [E0, E1)
                 if (m[j].x | m[j].y | m[j].z | m[j].w) gstore16<kNT>(c0 + uint64_t(j) * 1024u, v[j] ^ m[j]);
         }
+        if constexpr (kUtf8) {
+            // the unmasked chunks, still in registers; a chunk's left context is the previous
+            // lane's last dword (lane 0: lane 63's of chunk j - 1). Bytes 0..2 of the unit are
+            // judged by k_utf8_seam_sorted (their context is another wave's unit).
+            bool badA = false, badB = false;
+            uint32_t carry = 0;
+#pragma unroll
+            for (int j = 0; j < kUnmaskU; ++j) {
+                const uint64_t c = c0 + uint64_t(j) * 1024u;
+                const u32x4 x = v[j] ^ m[j];
+                uint32_t prev = __shfl_up(x.w, 1, 64);
+                if (lane == 0) prev = carry;
+                carry = __shfl(x.w, 63, 64);
+                const uint32_t skip = j == 0 && lane == 0;
+                if (slow) {
+                    utf8_slow_chunk(d, n, A, b0, c, x, prev, skip, ok);
+                    continue;
+                }
+                if (fa.payload_len && c + 16u > poA && c < peA + 3u) badA |= utf8_chunk_bad(x, prev, c, poA, peA, skip);
+                if (hasB && fb.payload_len && c + 16u > poB && c < peB + 3u)
+                    badB |= utf8_chunk_bad(x, prev, c, poB, peB, skip);
+            }
+            if (!slow) {
+                if (__any(badA) && lane == 0) ok[A] = 0;
+                if (__any(badB) && lane == 0) ok[A + 1u] = 0;
+            }
+        }
+    }
+}
+
+// The first 3 bytes of every unit u in [1, n_units) of a sorted batch, whose
+// left context lies in unit u - 1 (k_unmask_sorted_utf8 skipped them), for
+// every non-empty region meeting them as payload or 3-byte tail. One thread
+// per unit seam; reads the already unmasked bytes. The owner of the seam is
+// found like sorted_owner, per thread.
+__global__ __launch_bounds__(kBlock) void k_utf8_seam_sorted(const uint8_t *base, const fws_frame_desc *__restrict__ d,
+                                                             uint32_t n, uint8_t *__restrict__ ok) {
+    if (n == 0) return;
+    const uintptr_t b0 = (uintptr_t)base;
+    const uint64_t E0 = b0 + d[0].payload_off;
+    const fws_frame_desc dl = d[n - 1];
+    const uint64_t E1 = b0 + dl.payload_off + dl.payload_len;
+    const uint64_t Sa = E0 & ~uint64_t(15);
+    const uint64_t nus = E1 > Sa ? (E1 - Sa + 4095u) / 4096u : 0;
+    const float rate = (float)n / (float)(E1 > E0 ? E1 - E0 : 1u);
+    for (uint64_t u = uint64_t(blockIdx.x) * kBlock + threadIdx.x + 1u; u < nus; u += uint64_t(gridDim.x) * kBlock) {
+    const uint64_t P = Sa + 4096u * u;               // P < E1: the dwords at P - 4 and P are in the span's chunks
+    // last region with po < P + 3: guess from the span, bracket check, else binary search
+    uint64_t g = (uint64_t)((float)(P - E0) * rate);
+    g = g >= 1u ? g - 1u : 0u;
+    if (g > n - 1u) g = n - 1u;
+    uint32_t L;
+    const bool lo_ok = b0 + d[g].payload_off < P + 3u;
+    const bool hi_ok = g + 1u >= n || b0 + d[g + 1u].payload_off >= P + 3u;
+    if (lo_ok && hi_ok) {
+        L = (uint32_t)g;
+    } else {
+        uint32_t lo = 0, hi = n - 1u;
+        while (lo < hi) {
+            const uint32_t mid = lo + ((hi - lo + 1u) >> 1);
+            if (b0 + d[mid].payload_off < P + 3u) lo = mid;
+            else hi = mid - 1u;
+        }
+        L = lo;
+    }
+    const uint32_t cur = *(const uint32_t *)(base + (P - b0));
+    const uint32_t prev = *(const uint32_t *)(base + (P - 4u - b0));
+    for (uint32_t f = L + 1u; f-- > 0;) {
+        const fws_frame_desc fd = d[f];
+        const uint64_t po = b0 + fd.payload_off, pe = po + fd.payload_len;
+        if (pe + 3u <= P) break;
+        if (!fd.payload_len || po >= P + 3u) continue;
+        const uint32_t x = cur & sel_bytes(P, po, pe), p = prev & sel_bytes(P - 4u, po, pe);
+        if (utf8_err(x, p) & 0x00808080u) ok[f] = 0;
+    }
     }
 }
 
@@ -1031,6 +1131,13 @@ template <bool kNT>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) void k_unmask_sorted(
     uint8_t *base, const fws_frame_desc *__restrict__ d, uint32_t n) {
     unmask_sorted_body<kNT, false>(base, d, n);
+}
+
+// unmask + per-region UTF-8 flags (C5 in descriptor mode); ok preset to 1
+template <bool kNT>
+__global__ __launch_bounds__(kBlock) void k_unmask_sorted_utf8(uint8_t *base, const fws_frame_desc *__restrict__ d,
+                                                               uint32_t n, uint8_t *__restrict__ ok) {
+    unmask_sorted_body<kNT, false, true>(base, d, n, ok);
 }
 
 }  // namespace fwsk
@@ -1101,6 +1208,19 @@ int fws_launch_unmask_sorted(uint8_t *base, const fws_frame_desc *d, uint32_t n,
         hipLaunchKernelGGL(k_unmask_sorted_early<true>, dim3(grid_for_units(units)), dim3(kBlock), 0, s, base, d, n);
     else
         hipLaunchKernelGGL(k_unmask_sorted<true>, dim3(grid_for_units(units)), dim3(kBlock), 0, s, base, d, n);
+    return fws_hip_status(hipGetLastError());
+}
+
+int fws_launch_unmask_sorted_utf8(uint8_t *base, const fws_frame_desc *d, uint32_t n, uint64_t max_span,
+                                  uint8_t *ok, hipStream_t s) {
+    if (n == 0) return 0;
+    int r = fws_hip_status(hipMemsetAsync(ok, 1, n, s));
+    if (r) return r;
+    const uint64_t units = max_span / 4096u + 2u;
+    hipLaunchKernelGGL(k_unmask_sorted_utf8<true>, dim3(grid_for_units(units)), dim3(kBlock), 0, s, base, d, n, ok);
+    const uint64_t seam_blocks = (units + kBlock - 1) / kBlock;   // grid-stride: any span is covered
+    hipLaunchKernelGGL(k_utf8_seam_sorted, dim3((unsigned)(seam_blocks < 4096u ? seam_blocks : 4096u)), dim3(kBlock), 0, s,
+                       (const uint8_t *)base, d, n, ok);
     return fws_hip_status(hipGetLastError());
 }
 

@@ -79,6 +79,12 @@ def unmask_sorted(ctx, base, dev_descs, n, stream=None):
                                                                _stream_handle(stream)))
 
 
+def unmask_sorted_utf8(ctx, base, dev_descs, n, ok, stream=None):
+    """fws_gpu_unmask_sorted_utf8: one-pass unmask + per-region UTF-8 flags (ok: device uint8[n])."""
+    check("fws_gpu_unmask_sorted_utf8", lib().fws_gpu_unmask_sorted_utf8(ctx.h, _ptr(base), _ptr(dev_descs), n,
+                                                                         _ptr(ok), _stream_handle(stream)))
+
+
 def unmask_plan(ctx, base, dev_descs, n, stream=None):
     check("fws_gpu_unmask_plan", lib().fws_gpu_unmask_plan(ctx.h, _ptr(base), _ptr(dev_descs), n,
                                                            _stream_handle(stream)))

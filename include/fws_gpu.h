@@ -129,6 +129,14 @@ int fws_gpu_unmask_batch(fws_gpu_ctx *ctx, void *dev_base, const fws_frame_desc 
 int fws_gpu_unmask_sorted(fws_gpu_ctx *ctx, void *dev_base, const fws_frame_desc *dev_descs,
                           uint32_t n, void *stream);
 
+/* fws_gpu_unmask_sorted plus per-region UTF-8 validation of the unmasked
+ * payloads in the same pass (BASELINE config 5 in descriptor mode):
+ * dev_ok[i] = 1 iff region i is well-formed UTF-8 (Unicode Table 3-7), the
+ * same flags as fws_gpu_unmask_sorted followed by fws_gpu_validate_utf8.
+ * Same sortedness contract as fws_gpu_unmask_sorted. */
+int fws_gpu_unmask_sorted_utf8(fws_gpu_ctx *ctx, void *dev_base, const fws_frame_desc *dev_descs, uint32_t n,
+                               uint8_t *dev_ok, void *stream);
+
 /* The two halves of fws_gpu_unmask_batch, for callers that reuse one plan
  * (same descriptors) across buffers: _plan builds the chunk plan of the
  * descriptors in ctx, _run unmasks with the last plan built in ctx. */

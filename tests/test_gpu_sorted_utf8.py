@@ -1,0 +1,111 @@
+"""GPU parity: fws_gpu_unmask_sorted_utf8 (one-pass unmask + per-region UTF-8
+flags, BASELINE config 5 in descriptor mode). Bytes vs the oracle's
+WSMaskBytesFast restatement (crypto/ws_mask.h:175-197); flags vs Python's
+strict UTF-8 decoder (the reference does not validate UTF-8: parity unpinned
+against it, pinned to Unicode Table 3-7 / RFC 3629) and vs the
+two-pass fws_gpu_unmask_sorted + fws_gpu_validate_utf8."""
+import numpy as np
+import pytest
+import torch
+
+from flashws_amd import gpu
+from test_gpu_unmask import aligned_host, oracle_unmask_regions
+
+pytestmark = pytest.mark.gpu
+
+
+def _valid(b):
+    try:
+        b.decode("utf-8")
+        return True
+    except UnicodeDecodeError:
+        return False
+
+
+def _cases(rng, n_short, n_long, long_chars):
+    cases = [b"", b"a", b"\xc2\x80", b"\xc2", b"\xe0\xa0\x80", b"\xe0\x9f\x80", b"\xed\x9f\xbf", b"\xed\xa0\x80",
+             b"\xf0\x90\x80\x80", b"\xf0\x8f\xbf\xbf", b"\xf4\x8f\xbf\xbf", b"\xf4\x90\x80\x80", b"\xf5\x80\x80\x80",
+             b"\xc0\x80", b"\xc1\xbf", b"\x80", b"a\xe2\x82", "héllo wörld €𝄞".encode(), b"\xff", b"ab\xe2\x82\xacd"]
+    for _ in range(n_short):
+        cases.append(rng.integers(0, 256, int(rng.integers(0, 40)), dtype=np.uint8).tobytes())
+        s = "".join(chr(int(c)) for c in rng.integers(0x20, 0x2FFF, 20) if not 0xD800 <= int(c) <= 0xDFFF)
+        b = bytearray(s.encode())
+        if len(b) and rng.random() < 0.5:
+            b[int(rng.integers(0, len(b)))] = int(rng.integers(0x80, 0x100))
+        cases.append(bytes(b))
+    for _ in range(n_long):      # sequences across lanes, chunks, 4 KiB units (seams), errors anywhere
+        s = "".join(chr(int(c)) for c in rng.integers(0x20, 0x10FFFF, int(rng.integers(*long_chars)))
+                    if not 0xD800 <= int(c) <= 0xDFFF)
+        b = bytearray(s.encode())
+        k = int(rng.integers(0, 4))
+        if k == 1:
+            b[int(rng.integers(0, len(b)))] = int(rng.integers(0x80, 0x100))
+        elif k == 2:
+            b = b[:-1]
+        cases.append(bytes(b))
+    return cases
+
+
+def _layout(rng, cases, max_pad):
+    """Plain text regions separated by 0..max_pad arbitrary non-ASCII bytes, masked with
+    random keys and phases (the XOR is an involution: masking = the oracle unmask)."""
+    regions, pos, parts = [], int(rng.integers(0, 16)), []
+    parts.append(rng.integers(0x80, 0x100, pos, dtype=np.uint8).tobytes())
+    for c in cases:
+        regions.append((pos, len(c), int(rng.integers(0, 2**32)), int(rng.integers(0, 4))))
+        parts.append(c)
+        pos += len(c)
+        pad = int(rng.integers(0, max_pad + 1))
+        parts.append(rng.integers(0x80, 0x100, pad, dtype=np.uint8).tobytes())
+        pos += pad
+    plain = aligned_host(pos + 32)
+    plain[:] = np.frombuffer(b"".join(parts) + b"\xf0" * 32, dtype=np.uint8)[:len(plain)]
+    descs = np.array(regions, dtype=gpu.FRAME_DESC)
+    return plain, oracle_unmask_regions(plain, descs), descs
+
+
+def _run(ctx, cuda, masked, descs, shift=0):
+    dev = torch.from_numpy(np.concatenate([np.zeros(shift, np.uint8), masked])).to(cuda)
+    dd = gpu.descs_to_device(descs, cuda)
+    ok = torch.full((len(descs),), 7, dtype=torch.uint8, device=cuda)
+    gpu.unmask_sorted_utf8(ctx, dev[shift:], dd, len(descs), ok)
+    torch.cuda.synchronize()
+    return dev[shift:].cpu().numpy(), ok.cpu().numpy()
+
+
+@pytest.mark.parametrize("max_pad,shift", [(0, 0), (3, 0), (20, 5), (600, 11)])
+def test_sorted_utf8_edge_cases(ctx, cuda, max_pad, shift):
+    rng = np.random.default_rng(100 + max_pad)
+    cases = _cases(rng, 300, 60, (100, 1500))
+    plain, masked, descs = _layout(rng, cases, max_pad)
+    got, ok = _run(ctx, cuda, masked, descs, shift)
+    assert np.array_equal(got, plain)
+    exp = np.array([_valid(c) for c in cases])
+    assert np.array_equal(ok.astype(bool), exp), np.nonzero(ok.astype(bool) != exp)[0][:10]
+
+
+def test_sorted_utf8_long_frames(ctx, cuda):
+    """Frames of 4-40 KiB (fast-kind units, every unit seam inside a frame)."""
+    rng = np.random.default_rng(7)
+    cases = _cases(rng, 0, 40, (1000, 12000))
+    plain, masked, descs = _layout(rng, cases, 14)
+    got, ok = _run(ctx, cuda, masked, descs)
+    assert np.array_equal(got, plain)
+    assert np.array_equal(ok.astype(bool), np.array([_valid(c) for c in cases]))
+
+
+def test_sorted_utf8_c5_shape(ctx, cuda):
+    """BASELINE C5 layout (16 KiB TEXT frames, 8-B headers, ~1 % invalid), 4096 frames:
+    flags vs the generator's, bytes and flags vs the two-pass path."""
+    wire, descs, ok_exp = gpu.config_c5(seed=5, n_frames=4096)
+    got, ok = _run(ctx, cuda, wire, descs)
+    assert np.array_equal(ok, np.asarray(ok_exp, dtype=np.uint8)[:len(descs)])
+    assert (ok == 0).sum() > 0
+    dev = torch.from_numpy(wire).to(cuda)
+    dd = gpu.descs_to_device(descs, cuda)
+    ok2 = torch.zeros(len(descs), dtype=torch.uint8, device=cuda)
+    gpu.unmask_sorted(ctx, dev, dd, len(descs))
+    gpu.validate_utf8(ctx, dev, dd, len(descs), ok2)
+    torch.cuda.synchronize()
+    assert np.array_equal(dev.cpu().numpy(), got)
+    assert np.array_equal(ok2.cpu().numpy(), ok)

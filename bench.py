@@ -370,7 +370,23 @@ def stream_decode_extra(ctx, wire_c2, dev, args):
         rec = decode_cfg("C5", w5, len(d5), utf8=True, nbuf=1)
         rec["utf8_invalid_frames_expected"] = int((ok5 == 0).sum())
         out["C5_utf8_text_decode"] = rec
-        del w5
+        # the same batch in descriptor mode (a batch split at frame boundaries knows its
+        # frames): one pass of unmask + UTF-8 flags, fws_gpu_unmask_sorted_utf8
+        c = gpu.Ctx(dev.index or 0, max_frames=len(d5) + 8, max_stream_bytes=len(w5))
+        wd = torch.from_numpy(w5).to(dev)
+        dd5 = gpu.descs_to_device(d5, dev)
+        ok = torch.empty(len(d5), dtype=torch.uint8, device=dev)
+        gpu.unmask_sorted_utf8(c, wd, dd5, len(d5), ok)
+        torch.cuda.synchronize()
+        flags_ok = bool(np.array_equal(ok.cpu().numpy(), np.asarray(ok5, dtype=np.uint8)[:len(d5)]))
+        t = _time(lambda i: gpu.unmask_sorted_utf8(c, wd, dd5, len(d5), ok), 10, stream)
+        pl5 = int(d5["payload_len"].sum())
+        out["C5_utf8_descriptor"] = {"GiB_per_s": round(pl5 / t / GIB, 1), "ms_per_step": round(t * 1e3, 4),
+                                     "frames": len(d5), "alg_GB_per_s": round((len(w5) + pl5) / t / 1e9, 1),
+                                     "flags_match_generator": flags_ok,
+                                     "path": "fws_gpu_unmask_sorted_utf8: k_unmask_sorted_utf8 + k_utf8_seam_sorted"}
+        c.close()
+        del w5, wd
     # end-to-end: pinned host -> HBM -> unmask -> host (PCIe-inclusive), C2
     n = args.frames
     host_in = torch.from_numpy(wire_c2).pin_memory()

@@ -17,4 +17,6 @@ timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -f csv -d $R/gpurun_out/pmc_write
 timeout -k 10 200 rocprofv3 --kernel-trace --stats -f csv -d $R/gpurun_out/prof_main -o run -- python3 $R/bench.py --no-cpu > $R/gpurun_out/prof_main.log 2>&1 || { tail -5 $R/gpurun_out/prof_main.log; exit 1; }
 timeout -k 10 100 rocprofv3 --kernel-trace --stats -f csv -d $R/gpurun_out/prof_c4 -o run -- python3 $R/tools/run_c4.py > $R/gpurun_out/prof_c4.log 2>&1 || { tail -5 $R/gpurun_out/prof_c4.log; exit 1; }
 timeout -k 10 100 rocprofv3 --kernel-trace --stats -f csv -d $R/gpurun_out/prof_tx -o run -- python3 $R/tools/run_tx.py > $R/gpurun_out/prof_tx.log 2>&1 || { tail -5 $R/gpurun_out/prof_tx.log; exit 1; }
+timeout -k 10 200 rocprofv3 --kernel-trace --stats -f csv -d $R/gpurun_out/prof_c5d -o run -- python3 $R/tools/run_c5_desc.py > $R/gpurun_out/prof_c5d.log 2>&1 || { tail -5 $R/gpurun_out/prof_c5d.log; exit 1; }
+timeout -k 10 200 rocprofv3 --kernel-trace --stats -f csv -d $R/gpurun_out/prof_c5 -o run -- python3 $R/tools/run_c5.py > $R/gpurun_out/prof_c5.log 2>&1 || { tail -5 $R/gpurun_out/prof_c5.log; exit 1; }
 echo done

@@ -1133,11 +1133,131 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) voi
     unmask_sorted_body<kNT, false>(base, d, n);
 }
 
-// unmask + per-region UTF-8 flags (C5 in descriptor mode); ok preset to 1
+// Software-pipelined form of unmask_sorted_body<.., kUtf8 = true>: a wave's
+// grid-stride units (16 per wave on C5) are processed so that the next unit's
+// owner lookup and data loads are issued before the current unit's UTF-8
+// check, whose VALU work then overlaps the next unit's HBM latency.
+struct SortedUnit {
+    uint64_t U0, poA, peA, poB, peB;
+    u32x4 rec;
+    uint32_t A, lenA, lenB;
+    bool hasB, slow, gap;
+};
+
 template <bool kNT>
+__device__ __forceinline__ void unmask_sorted_utf8_pipe(uint8_t *base, const fws_frame_desc *__restrict__ d,
+                                                        uint32_t n, uint8_t *__restrict__ ok) {
+    if (n == 0) return;
+    const int lane = threadIdx.x & (kWave - 1);
+    const uintptr_t b0 = (uintptr_t)base;
+    const uint64_t nwaves = uint64_t(gridDim.x) * (kBlock / kWave);
+    const uint64_t u0 = uint64_t(blockIdx.x) * (kBlock / kWave) + __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const uint64_t po0 = d[0].payload_off;
+    const fws_frame_desc dl = d[n - 1];
+    const uint64_t E0 = b0 + po0, E1 = b0 + dl.payload_off + dl.payload_len;
+    const uint64_t Sa = E0 & ~uint64_t(15);
+    const uint64_t nus = E1 > Sa ? (E1 - Sa + 4095u) / 4096u : 0;
+    const uint64_t safe = (E1 - 1u) & ~uint64_t(15);
+    const float rate = (float)n * 4096.0f / (float)(E1 > E0 ? E1 - E0 : 1u);
+    auto lookup = [&](uint64_t u) -> SortedUnit {
+        SortedUnit I;
+        I.U0 = Sa + 4096u * u;
+        I.A = sorted_owner(d, n, b0, I.U0, E0, u, rate);
+        I.hasB = I.A + 1u < n;
+        const bool hasC = I.A + 2u < n;
+        const fws_frame_desc fa = d[I.A];
+        fws_frame_desc fb{0, 0, 0, 0};
+        if (I.hasB) fb = d[I.A + 1u];
+        const uint64_t poC = hasC ? b0 + d[I.A + 2u].payload_off : 0;
+        I.poA = b0 + fa.payload_off;
+        I.peA = I.poA + fa.payload_len;
+        I.poB = b0 + fb.payload_off;
+        I.peB = I.poB + fb.payload_len;
+        I.lenA = fa.payload_len != 0;
+        I.lenB = fb.payload_len != 0;
+        I.rec = unit_record(I.U0, E0, E1, I.A, I.poA, I.peA, aligned_key(fa.key, fa.phase, I.poA), I.hasB, I.poB,
+                            I.peB, aligned_key(fb.key, fb.phase, I.poB), hasC, poC);
+        I.slow = (I.rec.z & kRecSlow) != 0;
+        const uint32_t a0 = I.rec.z & 0x1FFFu, a1 = (I.rec.z >> 13) & 0x1FFFu;
+        const uint32_t e0 = I.rec.w & 0x1FFFu, e1 = (I.rec.w >> 13) & 0x1FFFu;
+        I.gap = !I.slow && a1 <= a0 && e1 <= e0;     // no payload (a tail of A: bytes 0..2, the seam's)
+        return I;
+    };
+    auto load = [&](const SortedUnit &I, u32x4 (&v)[kUnmaskU]) {
+        if (I.gap) return;
+        const uint64_t c0 = I.U0 + uint64_t(lane) * 16u;
+#pragma unroll
+        for (int j = 0; j < kUnmaskU; ++j) {
+            const uint64_t c = c0 + uint64_t(j) * 1024u;
+            v[j] = gload16<kNT>(c < E1 ? c : safe);
+        }
+    };
+    uint64_t u = u0;
+    if (u >= nus) return;
+    SortedUnit cur = lookup(u);
+    u32x4 v[kUnmaskU];
+    load(cur, v);
+    for (;;) {
+        const uint64_t c0 = cur.U0 + uint64_t(lane) * 16u;
+        u32x4 x[kUnmaskU];
+        if (!cur.gap) {
+            u32x4 m[kUnmaskU];
+            if (cur.slow) slow_unit_masks(d, n, cur.A, b0, cur.U0, lane, m);
+            else fast_unit_masks(cur.rec, lane, m);
+            if (cur.slow) {
+                slow_unit_store<kNT>(c0, E0, E1, v, m);
+            } else {
+#pragma unroll
+                for (int j = 0; j < kUnmaskU; ++j)
+                    if (m[j].x | m[j].y | m[j].z | m[j].w) gstore16<kNT>(c0 + uint64_t(j) * 1024u, v[j] ^ m[j]);
+            }
+#pragma unroll
+            for (int j = 0; j < kUnmaskU; ++j) x[j] = v[j] ^ m[j];
+        }
+        // the next unit's lookup and loads go out before this unit's UTF-8 work
+        const uint64_t un = u + nwaves;
+        const bool more = un < nus;
+        SortedUnit nx;
+        if (more) {
+            nx = lookup(un);
+            load(nx, v);
+        }
+        if (!cur.gap) {
+            bool badA = false, badB = false;
+            uint32_t carry = 0;
+#pragma unroll
+            for (int j = 0; j < kUnmaskU; ++j) {
+                const uint64_t c = c0 + uint64_t(j) * 1024u;
+                uint32_t prev = __shfl_up(x[j].w, 1, 64);
+                if (lane == 0) prev = carry;
+                carry = __shfl(x[j].w, 63, 64);
+                const uint32_t skip = j == 0 && lane == 0;
+                if (cur.slow) {
+                    utf8_slow_chunk(d, n, cur.A, b0, c, x[j], prev, skip, ok);
+                    continue;
+                }
+                if (cur.lenA && c + 16u > cur.poA && c < cur.peA + 3u)
+                    badA |= utf8_chunk_bad(x[j], prev, c, cur.poA, cur.peA, skip);
+                if (cur.hasB && cur.lenB && c + 16u > cur.poB && c < cur.peB + 3u)
+                    badB |= utf8_chunk_bad(x[j], prev, c, cur.poB, cur.peB, skip);
+            }
+            if (!cur.slow) {
+                if (__any(badA) && lane == 0) ok[cur.A] = 0;
+                if (__any(badB) && lane == 0) ok[cur.A + 1u] = 0;
+            }
+        }
+        if (!more) break;
+        cur = nx;
+        u = un;
+    }
+}
+
+// unmask + per-region UTF-8 flags (C5 in descriptor mode); ok preset to 1
+template <bool kNT, bool kPipe>
 __global__ __launch_bounds__(kBlock) void k_unmask_sorted_utf8(uint8_t *base, const fws_frame_desc *__restrict__ d,
                                                                uint32_t n, uint8_t *__restrict__ ok) {
-    unmask_sorted_body<kNT, false, true>(base, d, n, ok);
+    if (kPipe) unmask_sorted_utf8_pipe<kNT>(base, d, n, ok);
+    else unmask_sorted_body<kNT, false, true>(base, d, n, ok);
 }
 
 }  // namespace fwsk
@@ -1166,6 +1286,13 @@ static int g_sorted_early = 0;  // tuning hook: 1 = k_unmask_sorted_early, 0 = k
 extern "C" __attribute__((visibility("default"))) int fws_internal_set_sorted_early(int on) {
     const int old = g_sorted_early;
     g_sorted_early = on != 0;
+    return old;
+}
+
+static int g_sorted_utf8_pipe = 0;  // tuning hook: k_unmask_sorted_utf8 software-pipelined (1; measured slower, 2.12 vs 1.89 ms on C5: 90 VGPRs) or plain (0)
+extern "C" __attribute__((visibility("default"))) int fws_internal_set_sorted_utf8_pipe(int on) {
+    const int old = g_sorted_utf8_pipe;
+    g_sorted_utf8_pipe = on != 0;
     return old;
 }
 
@@ -1217,7 +1344,12 @@ int fws_launch_unmask_sorted_utf8(uint8_t *base, const fws_frame_desc *d, uint32
     int r = fws_hip_status(hipMemsetAsync(ok, 1, n, s));
     if (r) return r;
     const uint64_t units = max_span / 4096u + 2u;
-    hipLaunchKernelGGL(k_unmask_sorted_utf8<true>, dim3(grid_for_units(units)), dim3(kBlock), 0, s, base, d, n, ok);
+    if (g_sorted_utf8_pipe)
+        hipLaunchKernelGGL((k_unmask_sorted_utf8<true, true>), dim3(grid_for_units(units)), dim3(kBlock), 0, s, base, d,
+                           n, ok);
+    else
+        hipLaunchKernelGGL((k_unmask_sorted_utf8<true, false>), dim3(grid_for_units(units)), dim3(kBlock), 0, s, base,
+                           d, n, ok);
     const uint64_t seam_blocks = (units + kBlock - 1) / kBlock;   // grid-stride: any span is covered
     hipLaunchKernelGGL(k_utf8_seam_sorted, dim3((unsigned)(seam_blocks < 4096u ? seam_blocks : 4096u)), dim3(kBlock), 0, s,
                        (const uint8_t *)base, d, n, ok);

@@ -109,3 +109,19 @@ def test_sorted_utf8_c5_shape(ctx, cuda):
     torch.cuda.synchronize()
     assert np.array_equal(dev.cpu().numpy(), got)
     assert np.array_equal(ok2.cpu().numpy(), ok)
+
+
+@pytest.mark.parametrize("pipe", [0, 1])
+def test_sorted_utf8_both_variants(ctx, cuda, pipe):
+    """The software-pipelined and the plain fused kernel give the same bytes and flags."""
+    from flashws_amd import lib
+    old = lib().fws_internal_set_sorted_utf8_pipe(pipe)
+    try:
+        rng = np.random.default_rng(300 + pipe)
+        cases = _cases(rng, 200, 40, (100, 9000))
+        plain, masked, descs = _layout(rng, cases, 30)
+        got, ok = _run(ctx, cuda, masked, descs, 3)
+        assert np.array_equal(got, plain)
+        assert np.array_equal(ok.astype(bool), np.array([_valid(c) for c in cases]))
+    finally:
+        lib().fws_internal_set_sorted_utf8_pipe(old)

@@ -47,15 +47,20 @@ def main(reps=6):
     gpu.unmask_sorted_utf8(ctx, w, dd, n, ok)
     torch.cuda.synchronize()
     assert np.array_equal(ok.cpu().numpy(), np.asarray(ok5, dtype=np.uint8)[:n]), "fused utf8 flags differ"
-    tf = 0.0
-    for _ in range(reps):
-        e[0].record(s)
-        gpu.unmask_sorted_utf8(ctx, w, dd, n, ok)
-        e[1].record(s)
-        torch.cuda.synchronize()
-        tf += e[0].elapsed_time(e[1]) / reps
-    print(json.dumps({"C5_descriptor_fused": {"GiB_per_s": round(payload / (tf / 1e3) / 2**30, 1),
-                                              "ms_per_step": round(tf, 4)}}))
+    from flashws_amd import lib
+    for pipe in (1, 0):
+        old = lib().fws_internal_set_sorted_utf8_pipe(pipe)
+        tf = 0.0
+        for _ in range(reps):
+            e[0].record(s)
+            gpu.unmask_sorted_utf8(ctx, w, dd, n, ok)
+            e[1].record(s)
+            torch.cuda.synchronize()
+            tf += e[0].elapsed_time(e[1]) / reps
+        lib().fws_internal_set_sorted_utf8_pipe(old)
+        print(json.dumps({"C5_descriptor_fused": {"pipelined": pipe,
+                                                  "GiB_per_s": round(payload / (tf / 1e3) / 2**30, 1),
+                                                  "ms_per_step": round(tf, 4)}}))
     print(json.dumps({"C5_descriptor_unmask_utf8": {"GiB_per_s": round(payload / (t / 1e3) / 2**30, 1),
                                                     "ms_per_step": round(t, 4), "unmask_ms": round(tu, 4),
                                                     "validate_ms": round(tv, 4), "frames": n,

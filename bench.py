@@ -51,9 +51,16 @@ def parse():
     ap.add_argument("--no-batch-extra", action="store_true",
                     help="skip the fws_gpu_unmask_batch (plan + run) comparison line")
     ap.add_argument("--extra", action="store_true",
-                    help="also time C2 stream decode, C3, C4, e2e (PCIe) -> 'extra'")
-    ap.add_argument("--c5", action="store_true", help="with --extra: the 4 GiB C5 UTF-8 config")
-    return ap.parse_args()
+                    help="also time C2 stream decode, C3, C4, TX, e2e (PCIe) -> 'extra' "
+                         "(default at N=1; multi-GPU runs time the headline only)")
+    ap.add_argument("--c5", action="store_true", help="with --extra: the 4 GiB C5 UTF-8 config (default at N=1)")
+    ap.add_argument("--no-extra", action="store_true", help="headline line only")
+    a = ap.parse_args()
+    if int(os.environ.get("WORLD_SIZE", "1")) == 1 and not a.no_extra:
+        a.extra = a.c5 = True
+    if a.no_extra:
+        a.extra = a.c5 = False
+    return a
 
 
 def setup_dist(args):

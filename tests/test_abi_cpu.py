@@ -65,6 +65,8 @@ def test_invalid_arguments_fail_without_a_device():
     L = _lib.lib()
     assert L.fws_gpu_ctx_create(0, None) == _lib.FWS_ERR_INVALID
     assert L.fws_gpu_unmask_batch(None, None, None, 1, None) == _lib.FWS_ERR_INVALID
+    assert L.fws_gpu_unmask_sorted(None, None, None, 1, None) == _lib.FWS_ERR_INVALID
+    assert L.fws_gpu_unmask_sorted_utf8(None, None, None, 1, None, None) == _lib.FWS_ERR_INVALID
     assert L.fws_gpu_decode_stream(None, None, 0, None, 0, None, None, None) == _lib.FWS_ERR_INVALID
 
 

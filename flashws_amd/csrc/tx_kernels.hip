@@ -160,7 +160,7 @@ __device__ __forceinline__ void tx_store_tail(uint8_t *out, uint64_t a, uint64_t
     for (uint64_t b = a; b < total && b < a + 16u; ++b) out[b] = (uint8_t)(xw[(b - a) >> 2] >> (8u * ((b - a) & 3u)));
 }
 
-__global__ __launch_bounds__(kBlock) void k_tx_encode(uint8_t *__restrict__ out, const uint8_t *__restrict__ src,
+__device__ __forceinline__ void tx_encode_body(uint8_t *__restrict__ out, const uint8_t *__restrict__ src,
                                                       const fws_tx_desc *__restrict__ d, uint32_t n,
                                                       const uint64_t *__restrict__ obase,
                                                       const uint32_t *__restrict__ unit_first, uint64_t unit_cap,
@@ -282,7 +282,30 @@ __global__ __launch_bounds__(kBlock) void k_tx_encode(uint8_t *__restrict__ out,
     }
 }
 
+// 4 waves per SIMD (107 VGPRs) as the compiler allocates it, or 5 with two
+// spilled registers (the rare second-seam loop); tuning hook below.
+__global__ __launch_bounds__(kBlock) void k_tx_encode(uint8_t *__restrict__ out, const uint8_t *__restrict__ src,
+                                                      const fws_tx_desc *__restrict__ d, uint32_t n,
+                                                      const uint64_t *__restrict__ obase,
+                                                      const uint32_t *__restrict__ unit_first, uint64_t unit_cap,
+                                                      const uint64_t *__restrict__ total_ptr) {
+    tx_encode_body(out, src, d, n, obase, unit_first, unit_cap, total_ptr);
+}
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) void k_tx_encode_w5(
+    uint8_t *__restrict__ out, const uint8_t *__restrict__ src, const fws_tx_desc *__restrict__ d, uint32_t n,
+    const uint64_t *__restrict__ obase, const uint32_t *__restrict__ unit_first, uint64_t unit_cap,
+    const uint64_t *__restrict__ total_ptr) {
+    tx_encode_body(out, src, d, n, obase, unit_first, unit_cap, total_ptr);
+}
+
 }  // namespace fwsk
+
+static int g_tx_w5 = 0;  // tuning hook: 1 = k_tx_encode_w5
+extern "C" __attribute__((visibility("default"))) int fws_internal_set_tx_w5(int on) {
+    const int old = g_tx_w5;
+    g_tx_w5 = on != 0;
+    return old;
+}
 
 using namespace fwsk;
 
@@ -316,8 +339,12 @@ int fws_gpu_encode_frames(fws_gpu_ctx *ctx, void *dev_out, uint64_t out_cap, con
     uint64_t u = units < ws.unit_cap ? units : ws.unit_cap;
     uint64_t blocks = (u + 3) / 4;
     if (blocks > 16384) blocks = 16384;
-    hipLaunchKernelGGL(k_tx_encode, dim3((unsigned)blocks), dim3(kBlock), 0, s, (uint8_t *)dev_out,
-                       (const uint8_t *)dev_src, dev_descs, n, ws.cbase, ws.unit_first, ws.unit_cap, ws.total);
+    if (g_tx_w5)
+        hipLaunchKernelGGL(k_tx_encode_w5, dim3((unsigned)blocks), dim3(kBlock), 0, s, (uint8_t *)dev_out,
+                           (const uint8_t *)dev_src, dev_descs, n, ws.cbase, ws.unit_first, ws.unit_cap, ws.total);
+    else
+        hipLaunchKernelGGL(k_tx_encode, dim3((unsigned)blocks), dim3(kBlock), 0, s, (uint8_t *)dev_out,
+                           (const uint8_t *)dev_src, dev_descs, n, ws.cbase, ws.unit_first, ws.unit_cap, ws.total);
     return fws_hip_status(hipGetLastError());
 }
 

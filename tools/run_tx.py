@@ -11,7 +11,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from flashws_amd import gpu  # noqa: E402
 
 
-def main(steps=20, n=65536, pl=4096):
+def setup(n=65536, pl=4096):
+    """Context, 4 output buffers, source payloads, device TX descriptors, n, total out bytes."""
     dev = torch.device("cuda:0")
     rng = np.random.default_rng(7)
     txd = np.zeros(n, dtype=gpu.TX_DESC)
@@ -24,6 +25,11 @@ def main(steps=20, n=65536, pl=4096):
     total = n * (pl + 8)
     ctx = gpu.Ctx(0, max_frames=n, max_stream_bytes=total)
     outs = [torch.empty(total, dtype=torch.uint8, device=dev) for _ in range(4)]
+    return ctx, outs, src, dd, n, total
+
+
+def main(steps=20):
+    ctx, outs, src, dd, n, _ = setup()
     for i in range(steps):
         gpu.encode_frames(ctx, outs[i % 4], src, dd, n)
     torch.cuda.synchronize()

@@ -1,0 +1,39 @@
+#!/usr/bin/env python3
+"""A/B of k_tx_encode (compiler's allocation, 4 waves/SIMD) vs k_tx_encode_w5
+(5 waves/SIMD) on the C2 TX shape, HIP events; outputs checked equal."""
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from flashws_amd import gpu, lib  # noqa: E402
+import run_tx  # noqa: E402
+
+
+def main(steps=100):
+    ctx, outs, src, dd, n, total = run_tx.setup()
+    res, ref = {}, None
+    for w5 in (0, 1, 0, 1):
+        lib().fws_internal_set_tx_w5(w5)
+        for i in range(10):
+            gpu.encode_frames(ctx, outs[i % 4], src, dd, n)
+        torch.cuda.synchronize()
+        got = outs[0][:total].clone()
+        ref = got if ref is None else ref
+        assert torch.equal(ref, got)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for i in range(steps):
+            gpu.encode_frames(ctx, outs[i % 4], src, dd, n)
+        e1.record()
+        torch.cuda.synchronize()
+        res.setdefault(f"w5={w5}", []).append(round(e0.elapsed_time(e1) / steps * 1e3, 2))
+    lib().fws_internal_set_tx_w5(0)
+    print(json.dumps({"tx_step_us": res}))
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()

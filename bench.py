@@ -12,9 +12,14 @@ k_unmask_desc) is timed beside it in extra.C2_unmask_batch_any_order. Steps
 rotate over NBUF >= 4 distinct device copies (>= 1 GiB) so the 256 MiB
 Infinity Cache cannot serve a batch from the previous step.
 
-Multi-GPU (torchrun): every rank unmasks its own batch (independent frames,
-weak scaling, no collective on the data path); the timed region is bracketed
-by barrier + synchronize and the slowest rank's time is reported.
+Multi-GPU: `bench.py --gpus N` (N > 1) started without torchrun's environment
+starts `python -m torch.distributed.run --nproc-per-node N bench.py ...` as a
+child process before anything touches a GPU and exits with its code; under
+torchrun (the driver's launch) one rank per GPU. Every rank unmasks its own
+batch (independent frames, weak scaling, no collective on the data path); the
+timed region is bracketed by barrier + synchronize and the slowest rank's time
+is reported. At N > 1 the 8-GPU BASELINE config (C5: 4 GiB of 16 KiB TEXT
+frames per GPU, unmask + UTF-8 flags) is timed the same way -> extra.
 
 Output: ONE JSON line on rank 0 (contract in the task statement), with
 `roofline` for the dominant kernel (k_unmask_sorted, timed live with HIP events on
@@ -55,6 +60,10 @@ def parse():
                          "(default at N=1; multi-GPU runs time the headline only)")
     ap.add_argument("--c5", action="store_true", help="with --extra: the 4 GiB C5 UTF-8 config (default at N=1)")
     ap.add_argument("--no-extra", action="store_true", help="headline line only")
+    ap.add_argument("--no-c5-split", action="store_true", help="N > 1: skip the C5 batch-split config")
+    ap.add_argument("--launcher-selftest", action="store_true",
+                    help="CPU only (gloo): exercise the N-rank launch, barrier and max-over-ranks timing on a "
+                         "host XOR of each rank's shard; prints a self-test line, not the metric")
     a = ap.parse_args()
     if int(os.environ.get("WORLD_SIZE", "1")) == 1 and not a.no_extra:
         a.extra = a.c5 = True
@@ -63,16 +72,40 @@ def parse():
     return a
 
 
-def setup_dist(args):
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+def launch_ranks(args):
+    """`--gpus N` without torchrun's environment: start N ranks through
+    torch.distributed.run as a child process (nothing here has touched a GPU;
+    torch.cuda.device_count() does not initialise one) and return its exit code."""
+    import socket
+    import subprocess
+    import sys
+    if not args.launcher_selftest:
+        have = torch.cuda.device_count()
+        if have < args.gpus:
+            raise SystemExit(f"bench.py --gpus {args.gpus}: only {have} GPU(s) visible")
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def dist_env():
+    return (int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def setup_dist(world, local):
+    """One process per GPU; the process group only carries the barriers and the
+    max-over-ranks reduction of the step time (outside the timed region)."""
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(0)
-    return world, rank, local
 
 
 def barrier(world):
@@ -101,27 +134,77 @@ def aggregate_gib_s(world, payload_bytes_per_rank, step_s):
     return world * payload_bytes_per_rank / step_s / GIB
 
 
-def cpu_baseline(wire, seconds):
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _physical_cores():
+    """Distinct (package, core) pairs in /proc/cpuinfo, or the logical count."""
+    seen, cur = set(), {}
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if ":" in line:
+                    k, v = (x.strip() for x in line.split(":", 1))
+                    cur[k] = v
+                elif cur:
+                    seen.add((cur.get("physical id"), cur.get("core id")))
+                    cur = {}
+        if cur:
+            seen.add((cur.get("physical id"), cur.get("core id")))
+    except OSError:
+        pass
+    return len(seen) if len(seen) > 1 else (os.cpu_count() or 1)
+
+
+def cpu_share():
+    """Cores the all-core leg may use: this process's affinity set, capped by
+    OMP_NUM_THREADS (the GPU box's per-GPU CPU share) and the physical cores."""
+    n = len(os.sched_getaffinity(0))
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, min(n, _physical_cores()))
+
+
+def frame_cuts(wire_len, descs, parts):
+    """Split a packed stream at frame headers into `parts` ranges of about equal
+    bytes (header offset = payload offset - 6 / 8 / 14 by the length form)."""
+    pl = descs["payload_len"].astype(np.uint64)
+    hdr = np.where(pl < 126, 6, np.where(pl < 65536, 8, 14)).astype(np.uint64)
+    starts = descs["payload_off"].astype(np.uint64) - hdr
+    cuts = [0]
+    for k in range(1, parts):
+        i = int(np.searchsorted(starts, np.uint64(wire_len * k // parts)))
+        cuts.append(int(starts[min(i, len(starts) - 1)]))
+    cuts.append(int(wire_len))
+    return np.array(sorted(set(cuts)), dtype=np.uint64)
+
+
+def cpu_baseline(wire, descs, seconds):
     """The reference's own OnRecvData (oracle/_ref, compiled from the flashws
-    headers in the build container) on this host: 1 thread, the C2 batch fed as
-    2 MiB reads (MAX_READABLE_SIZE_ONE_TIME, constants.h:49-53). Falls back to
-    the C restatement (oracle/liborc.so, kind "port") if the reference build is
-    absent. Bounded to about `seconds` of CPU work."""
+    headers in the build container) on this host, on the C2 batch fed as 2 MiB
+    reads (MAX_READABLE_SIZE_ONE_TIME, constants.h:49-53), bounded to about
+    `seconds` of CPU work per leg: (1) one core, (2) all cores of this process's
+    CPU share, one process per core on a frame-boundary split of the batch (the
+    reference scales as one event loop per core; its buffer singletons are not
+    thread-safe). The all-core figure is `value`. Must run before this process
+    touches a GPU (the all-core leg forks). Falls back to the C restatement
+    (oracle/liborc.so, kind "port", one core) if the reference build is absent."""
     import ctypes as C
     import sys
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import orc
     read = 2 << 20
-    if orc.ref_available():
-        lib = orc.ref()
-        pb, rc = C.c_uint64(0), C.c_int(0)
-        t1 = lib.ref_time_onrecv(wire.ctypes.data, len(wire), read, 1, C.byref(pb), C.byref(rc))
-        iters = max(2, int(seconds / max(t1, 1e-6)) // 2 * 2)    # even: XOR restores the input
-        t = lib.ref_time_onrecv(wire.ctypes.data, len(wire), read, iters, C.byref(pb), C.byref(rc))
-        kind = "reference"
-        payload = pb.value
-    else:
-        st_bytes = bytearray(512)
+    model = _cpu_model()
+    if not orc.ref_available():
         buf = wire.copy()
         t0 = time.perf_counter()
         iters, payload = 0, 0
@@ -133,20 +216,36 @@ def cpu_baseline(wire, seconds):
                 payload += int(ev[ev["kind"] == 0]["size"].sum())
             iters += 1
         t = time.perf_counter() - t0
-        kind = "port"
-        del st_bytes
-    model = "unknown"
-    try:
-        with open("/proc/cpuinfo") as f:
-            for line in f:
-                if line.startswith("model name"):
-                    model = line.split(":", 1)[1].strip()
-                    break
-    except OSError:
-        pass
-    return {"value": round(payload / t / GIB, 3), "unit": "GiB/s", "cores": 1, "kind": kind,
-            "sample": f"{iters} passes of the C2 batch ({len(wire)} wire B) through "
-                      f"WSocket::OnRecvData as 2 MiB reads, {t:.1f} s, g++ -O3 -mavx2, {model}"}
+        return {"value": round(payload / t / GIB, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
+                "sample": f"{iters} passes of the C2 batch through the C restatement of OnRecvData, {t:.1f} s, "
+                          f"{model}"}
+    lib = orc.ref()
+    lib.ref_time_onrecv_procs.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_size_t, C.c_int,
+                                          C.POINTER(C.c_uint64), C.POINTER(C.c_int)]
+    lib.ref_time_onrecv_procs.restype = C.c_double
+    pb, rc = C.c_uint64(0), C.c_int(0)
+    t1 = lib.ref_time_onrecv(wire.ctypes.data, len(wire), read, 1, C.byref(pb), C.byref(rc))
+    iters = max(2, int(seconds / max(t1, 1e-6)) // 2 * 2)    # even: XOR restores the input
+    t = lib.ref_time_onrecv(wire.ctypes.data, len(wire), read, iters, C.byref(pb), C.byref(rc))
+    one = {"value": round(pb.value / t / GIB, 3), "cores": 1,
+           "sample": f"{iters} passes of the C2 batch ({len(wire)} wire B), {t:.1f} s"}
+    cores = cpu_share()
+    cuts = frame_cuts(len(wire), descs, cores)
+    procs = len(cuts) - 1
+    # each process decodes 1/procs of the batch: iters * procs passes of its range ~ `seconds`
+    it_all = max(2, int(seconds / max(t1, 1e-6)) * procs // 2)
+    pb2, rc2 = C.c_uint64(0), C.c_int(0)
+    ta = lib.ref_time_onrecv_procs(wire.ctypes.data, cuts.ctypes.data, procs, read, it_all, C.byref(pb2),
+                                   C.byref(rc2))
+    if ta <= 0 or rc2.value != 0 or rc.value != 0:
+        raise RuntimeError(f"reference CPU baseline failed: t={ta} rc={rc.value},{rc2.value}")
+    return {"value": round(pb2.value / ta / GIB, 3), "unit": "GiB/s", "cores": procs, "kind": "reference",
+            "sample": f"C2 batch ({len(wire)} wire B) split at frame headers into {procs} ranges, one process "
+                      f"per core, each running WSocket::OnRecvData over its range as 2 MiB reads "
+                      f"{it_all} times ({ta:.1f} s, slowest process); g++ -O3 -mavx2; {model}; "
+                      f"host has {os.cpu_count()} logical CPUs, {_physical_cores()} physical cores, "
+                      f"this process's share {cores}",
+            "one_core": one}
 
 
 def pmc_traffic():
@@ -162,12 +261,57 @@ def pmc_traffic():
         return None
 
 
+def launcher_selftest(args, world, rank):
+    """CPU (gloo) rehearsal of the N-rank path: the same launch, shard seeds,
+    barriers, max-over-ranks and aggregate as the GPU run, with a host XOR of
+    each rank's C2 shard standing in for the device step. Prints a self-test
+    line (no metric claim)."""
+    if world > 1:
+        dist.init_process_group(backend="gloo")
+    wire, descs, _ = gpu.config_c2(seed=shard_seed(rank), n_frames=args.frames, payload=args.payload)
+    payload = int(descs["payload_len"].sum())
+    buf = wire.copy()
+    barrier(world)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        np.bitwise_xor(buf, 0x5A, out=buf)
+    t1 = time.perf_counter()
+    barrier(world)
+    own = (t1 - t0) / args.steps
+    step = max_over_ranks(world, own)
+    dig = torch.tensor([int(np.frombuffer(wire[:4096].tobytes(), dtype=np.uint64).sum() & 0x7FFFFFFFFFFF)],
+                       dtype=torch.int64)
+    digs = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+    if world > 1:
+        dist.all_gather(digs, dig)
+    else:
+        digs = [dig]
+    line = {"selftest": True, "n_gpus": world, "rank": rank, "steps": args.steps, "step_s": step,
+            "own_step_s": own, "value": aggregate_gib_s(world, payload, step), "payload_bytes_per_rank": payload,
+            "shard_digests": [int(d.item()) for d in digs]}
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
-    world, rank, local = setup_dist(args)
-    dev = torch.device("cuda", torch.cuda.current_device())
+    world, rank, local = dist_env()
+    if args.gpus > 1 and world == 1:
+        raise SystemExit(launch_ranks(args))
+    if args.launcher_selftest:
+        return launcher_selftest(args, world, rank)
 
     wire, descs, _ = gpu.config_c2(seed=shard_seed(rank), n_frames=args.frames, payload=args.payload)
+    # the host-core reference baseline runs first: its all-core leg forks, which
+    # must happen before this process initialises a GPU
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(wire, descs, args.cpu_seconds)
+
+    setup_dist(world, local)
+    dev = torch.device("cuda", torch.cuda.current_device())
     n = len(descs)
     payload_bytes = int(descs["payload_len"].sum())
     wire_bytes = len(wire)
@@ -208,10 +352,13 @@ def main():
     kern_s = ev0.elapsed_time(ev1) / 1e3 / args.steps
 
     extra = {}
-    if not args.no_batch_extra:
+    if not args.no_batch_extra and world == 1:
         extra["C2_unmask_batch_any_order"] = batch_extra(ctx, bufs, dd, n, payload_bytes, args, stream)
     if args.extra:
         extra.update(stream_decode_extra(ctx, wire, dev, args)["extra"])
+    del bufs
+    if world > 1 and not args.no_c5_split:
+        extra["C5_batch_split"] = c5_split(args, world, rank, local, dev)
     extra = {"extra": extra} if extra else {}
 
     value = aggregate_gib_s(world, payload_bytes, step_s)
@@ -243,13 +390,77 @@ def main():
                      "alg_bytes_per_launch": alg_bytes},
     }
     out.update(extra)
-    if rank == 0 and world == 1 and not args.no_cpu:
-        out["cpu_baseline"] = cpu_baseline(wire, args.cpu_seconds)
+    if cpu is not None:
+        out["cpu_baseline"] = cpu
     if rank == 0:
         print(json.dumps(out), flush=True)
     ctx.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def c5_split(args, world, rank, local, dev):
+    """BASELINE config 5 (the 8-GPU one): every rank unmasks + UTF-8-validates
+    its own 4 GiB of 16 KiB TEXT frames (seed 42 + rank), descriptor mode
+    (fws_gpu_unmask_sorted_utf8) and as a raw stream (fws_gpu_decode_stream with
+    UTF-8 flags); barrier + synchronize around K steps, slowest rank's time,
+    aggregate = all ranks' payload / that time. Flags are checked against the
+    generator on every rank before timing."""
+    w5, d5, ok5 = gpu.config_c5(seed=shard_seed(rank))
+    n5 = len(d5)
+    pl5 = int(d5["payload_len"].sum())
+    c = gpu.Ctx(local, max_frames=n5 + 64, max_stream_bytes=len(w5))
+    wd = torch.from_numpy(w5).to(dev)
+    del w5
+    dd5 = gpu.descs_to_device(d5, dev)
+    ok = torch.empty(n5, dtype=torch.uint8, device=dev)
+    gpu.unmask_sorted_utf8(c, wd, dd5, n5, ok)             # one pass: unmasked, flags valid
+    torch.cuda.synchronize()
+    flags_ok = bool(np.array_equal(ok.cpu().numpy(), np.asarray(ok5, dtype=np.uint8)))
+    gpu.unmask_sorted_utf8(c, wd, dd5, n5, ok)             # masked again (XOR involution)
+    steps = max(2, min(args.steps, 20)) // 2 * 2
+
+    def timed(fn):
+        torch.cuda.synchronize()
+        barrier(world)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            fn(i)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        barrier(world)
+        return max_over_ranks(world, (t1 - t0) / steps), (t1 - t0) / steps
+
+    t_desc, own_desc = timed(lambda i: gpu.unmask_sorted_utf8(c, wd, dd5, n5, ok))
+    cap = n5 + 64
+    frames = torch.empty(cap * gpu.FRAME_INFO.itemsize, dtype=torch.uint8, device=dev)
+    res = torch.empty(gpu.DECODE_RESULT.itemsize, dtype=torch.uint8, device=dev)
+    okd = torch.zeros(cap, dtype=torch.uint8, device=dev)
+
+    def dec(i):
+        rc, _, _, _ = gpu.decode_stream(c, wd, cap, frames=frames, result=res, utf8_ok=okd)
+        assert rc == 0, rc
+
+    dec(0)
+    torch.cuda.synchronize()
+    r = gpu.read_result(res)
+    stream_ok = int(r["status"]) == 0 and int(r["n_frames"]) == n5 and bool(
+        np.array_equal(okd[:n5].cpu().numpy(), np.asarray(ok5, dtype=np.uint8)))
+    dec(1)
+    t_str, own_str = timed(dec)
+    all_ok = max_over_ranks(world, 0.0 if (flags_ok and stream_ok) else 1.0) == 0.0
+    c.close()
+    return {"workload": "C5: per GPU 262144 x 16 KiB masked TEXT frames (4 GiB payload), unmask + per-frame "
+                        "UTF-8 flags; ranks split the 8 x 4 GiB job, no collective on the data path",
+            "descriptor_mode": {"GiB_per_s": round(world * pl5 / t_desc / GIB, 1),
+                                "ms_per_step": round(t_desc * 1e3, 4),
+                                "path": "fws_gpu_unmask_sorted_utf8"},
+            "stream_decode": {"GiB_per_s": round(world * pl5 / t_str / GIB, 1),
+                              "ms_per_step": round(t_str * 1e3, 4),
+                              "path": "fws_gpu_decode_stream + UTF-8 flags"},
+            "payload_bytes_per_gpu": pl5, "steps": steps, "n_gpus": world,
+            "flags_match_generator_all_ranks": all_ok}
 
 
 def _time(fn, steps, stream):

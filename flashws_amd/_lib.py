@@ -26,6 +26,7 @@ FWS_ERR_TOO_LARGE = -2
 FWS_ERR_NOT_MASKED = -3
 FWS_ERR_MASKED = -4
 FWS_ERR_OPCODE = -9
+FWS_ERR_CONTROL_FRAME = -10
 FWS_ERR_CAPACITY = -20
 FWS_ERR_INVALID = -21
 FWS_ERR_NO_DEVICE = -22

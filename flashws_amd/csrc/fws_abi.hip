@@ -158,6 +158,7 @@ int fws_gpu_unmask_plan(fws_gpu_ctx *ctx, const void *dev_base, const fws_frame_
     if (!ctx || (n && (!dev_base || !dev_descs))) return FWS_ERR_INVALID;
     if (n == 0) return 0;
     if (ctx->cap_stream == 0 || n > ctx->cap_frames) return FWS_ERR_CAPACITY;
+    if (int r = fws_hip_status(hipSetDevice(ctx->device))) return r;
     return fws_launch_plan((const uint8_t *)dev_base, dev_descs, n, nullptr, ctx->plan, (hipStream_t)stream);
 }
 
@@ -166,6 +167,9 @@ int fws_gpu_unmask_run(fws_gpu_ctx *ctx, void *dev_base, const fws_frame_desc *d
     if (!ctx || (n && (!dev_base || !dev_descs))) return FWS_ERR_INVALID;
     if (n == 0) return 0;
     if (ctx->cap_stream == 0 || n > ctx->cap_frames) return FWS_ERR_CAPACITY;
+    if (int r = fws_hip_status(hipSetDevice(ctx->device))) return r;
+    // the grid is sized from the reservation; a larger batch is still covered in
+    // full (grid-stride loop, unit owners past the map's capacity are searched)
     const uint64_t max_chunks = ctx->cap_stream / 16 + 2ull * n;
     return fws_launch_unmask((uint8_t *)dev_base, dev_descs, n, nullptr, ctx->plan, max_chunks,
                              (hipStream_t)stream);
@@ -205,6 +209,7 @@ int fws_gpu_unmask_gather(fws_gpu_ctx *ctx, void *dev_dst, const void *dev_src, 
     if (((uintptr_t)dev_dst & 15u) != 0) return FWS_ERR_INVALID;
     if (n == 0) return 0;
     if (ctx->cap_stream == 0 || n > ctx->cap_frames) return FWS_ERR_CAPACITY;
+    if (int r = fws_hip_status(hipSetDevice(ctx->device))) return r;
     return fws_launch_gather((uint8_t *)dev_dst, (const uint8_t *)dev_src, dev_descs, n, ctx->plan, ctx->cap_stream,
                              (hipStream_t)stream);
 }
@@ -212,6 +217,7 @@ int fws_gpu_unmask_gather(fws_gpu_ctx *ctx, void *dev_dst, const void *dev_src, 
 int fws_gpu_validate_utf8(fws_gpu_ctx *ctx, const void *dev_base, const fws_frame_desc *dev_descs, uint32_t n,
                           uint8_t *dev_ok, void *stream) {
     if (!ctx || (n && (!dev_base || !dev_descs || !dev_ok))) return FWS_ERR_INVALID;
+    if (int r = fws_hip_status(hipSetDevice(ctx->device))) return r;
     return fws_launch_utf8_descs((const uint8_t *)dev_base, dev_descs, n, dev_ok, (hipStream_t)stream);
 }
 

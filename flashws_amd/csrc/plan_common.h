@@ -139,4 +139,22 @@ __device__ __forceinline__ void wave_fill_runs(uint32_t *map, uint64_t u0, uint3
                   [&](uint32_t fl, uint64_t u) { map[u] = fl; });
 }
 
+// Entry u of a unit map (frame f owns the units whose first position lies in
+// [prefix_f, prefix_{f+1}), positions in the prefix's units): the map itself
+// where the plan wrote it (u < unit_cap), else the same answer by a binary
+// search of the prefix (the last f < n with prefix_f <= pos), so a batch larger
+// than the context's reservation is still covered in full.
+__device__ __forceinline__ uint32_t unit_owner(const uint32_t *__restrict__ map, uint64_t unit_cap,
+                                               const uint64_t *__restrict__ prefix, uint32_t n, uint64_t u,
+                                               uint64_t pos) {
+    if (u < unit_cap) return map[u];
+    uint32_t lo = 0, hi = n;                          // prefix[lo] <= pos < prefix[hi] (prefix[n] = total)
+    while (hi - lo > 1u) {
+        const uint32_t mid = lo + (hi - lo) / 2u;
+        if (prefix[mid] <= pos) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
 }  // namespace fwsk

@@ -35,6 +35,7 @@ struct fws_rx_pipe_slot {
     fws_decode_result *hres = nullptr;     // pinned
     uint8_t *hutf8 = nullptr;              // pinned
     uint64_t ticket = ~0ull;               // batch in flight (or last completed)
+    uint64_t copied = 0;                   // frame records (and flags) copied back with the batch
     bool busy = false;
 };
 
@@ -42,6 +43,7 @@ struct fws_rx_pipe {
     int device = 0;
     uint64_t max_bytes = 0;
     uint32_t max_frames = 0;
+    uint64_t est = 0;                      // frame records to copy back with the next batch
     bool utf8 = false;
     uint64_t next = 0;
     std::vector<fws_rx_pipe_slot> slots;
@@ -89,6 +91,7 @@ int fws_rx_pipe_create(int device, uint64_t max_batch_bytes, uint32_t max_frames
     p->device = device;
     p->max_bytes = max_batch_bytes;
     p->max_frames = max_frames;
+    p->est = max_frames;
     p->utf8 = utf8 != 0;
     p->slots.resize(depth);
     int r = 0;
@@ -130,14 +133,19 @@ int fws_rx_pipe_submit(fws_rx_pipe *p, uint8_t *batch, uint64_t len, uint64_t *t
     if ((r = fws_gpu_decode_stream(s.ctx, s.dwire, len, s.dframes, p->max_frames, s.dres, s.dutf8, s.stream)))
         return r;
     if (len) e = hipMemcpyAsync(batch, s.dwire, len, hipMemcpyDeviceToHost, s.stream);
-    // the frame list: every slot up to capacity (the count is on the device until the wait)
-    if (e == hipSuccess)
-        e = hipMemcpyAsync(s.hframes, s.dframes, (uint64_t)p->max_frames * sizeof(fws_frame_info),
-                           hipMemcpyDeviceToHost, s.stream);
+    // the frame list: the count is on the device until the wait, so a bounded
+    // guess of it comes back with the batch (every frame has >= 6 header bytes;
+    // the last batch's count plus a margin) and the wait copies any remainder
+    uint64_t k = len / 6 + 1;
+    if (k > p->est) k = p->est;
+    if (k > p->max_frames) k = p->max_frames;
+    s.copied = k;
+    if (e == hipSuccess && k)
+        e = hipMemcpyAsync(s.hframes, s.dframes, k * sizeof(fws_frame_info), hipMemcpyDeviceToHost, s.stream);
     if (e == hipSuccess)
         e = hipMemcpyAsync(s.hres, s.dres, sizeof(fws_decode_result), hipMemcpyDeviceToHost, s.stream);
-    if (e == hipSuccess && p->utf8)
-        e = hipMemcpyAsync(s.hutf8, s.dutf8, p->max_frames, hipMemcpyDeviceToHost, s.stream);
+    if (e == hipSuccess && p->utf8 && k)
+        e = hipMemcpyAsync(s.hutf8, s.dutf8, k, hipMemcpyDeviceToHost, s.stream);
     if (e == hipSuccess) e = hipEventRecord(s.done, s.stream);
     if ((r = fws_hip_status(e))) return r;
     *ticket = t;
@@ -155,9 +163,21 @@ int fws_rx_pipe_wait(fws_rx_pipe *p, uint64_t ticket, const fws_frame_info **fra
     int r = fws_hip_status(hipEventSynchronize(s.done));
     if (r) return r;
     s.busy = false;
+    const uint64_t n = s.hres->n_frames < p->max_frames ? s.hres->n_frames : p->max_frames;
+    if (n > s.copied) {                                         // the guess fell short: the rest
+        if ((r = fws_hip_status(hipSetDevice(p->device)))) return r;
+        hipError_t e = hipMemcpyAsync(s.hframes + s.copied, s.dframes + s.copied,
+                                      (n - s.copied) * sizeof(fws_frame_info), hipMemcpyDeviceToHost, s.stream);
+        if (e == hipSuccess && p->utf8)
+            e = hipMemcpyAsync(s.hutf8 + s.copied, s.dutf8 + s.copied, n - s.copied, hipMemcpyDeviceToHost, s.stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(s.stream);
+        if ((r = fws_hip_status(e))) return r;
+        s.copied = n;
+    }
+    p->est = n + n / 8 + 64;
     if (result) *result = *s.hres;
     if (frames) *frames = s.hframes;
-    if (n_frames) *n_frames = s.hres->n_frames < p->max_frames ? s.hres->n_frames : p->max_frames;
+    if (n_frames) *n_frames = n;
     if (utf8_ok) *utf8_ok = s.hutf8;
     return 0;
 }

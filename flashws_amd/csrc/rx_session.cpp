@@ -119,9 +119,12 @@ struct fws_rx_session {
         const uint32_t opcode = is_ctl ? last_ctl_op : last_op;
         if (is_ctl && avail > 0) {                                    // :629-659
             if (status_at_part == kWaitHead || !ctl_alloc) { ctl_alloc = true; ctl_size = 0; }
+            // control payloads are <= 125 B (checked at the header, feed_impl), so
+            // this never clamps; the clamp keeps ctl_size inside the array regardless
             const uint64_t room = sizeof(ctl) - ctl_size;
-            memcpy(ctl + ctl_size, buf + data, avail < room ? avail : room);
-            ctl_size += (uint32_t)avail;
+            const uint64_t take = avail < room ? avail : room;
+            memcpy(ctl + ctl_size, buf + data, take);
+            ctl_size += (uint32_t)take;
         }
         if (frame_end && is_ctl) {                                   // :661-711
             const uint32_t n = ctl_alloc ? ctl_size : 0u;
@@ -164,7 +167,9 @@ struct fws_rx_session {
         }
     }
 
-    int ensure(uint64_t bytes, uint32_t nframes) {
+    // bytes: device stream capacity; stage: the read goes through the pinned
+    // staging area (size <= kZcMax, feed_impl)
+    int ensure(uint64_t bytes, uint32_t nframes, bool stage) {
         hipError_t e = hipSuccess;
         if (bytes + 32 > capA) {
             if (dA) (void)hipFree(dA);
@@ -182,7 +187,7 @@ struct fws_rx_session {
                 return fws_hip_status(e);
             dframes = (fws_frame_info *)((uint8_t *)dres + kResPad);
         }
-        if (bytes <= kZcMax && !hstage && (e = hipHostMalloc((void **)&hstage, 2 * kZcMax + 64)) != hipSuccess)
+        if (stage && !hstage && (e = hipHostMalloc((void **)&hstage, 2 * kZcMax + 64)) != hipSuccess)
             return fws_hip_status(e);
         return host_room(kSpec);
     }
@@ -265,8 +270,11 @@ static int feed_impl(fws_rx_session *s, uint8_t *buf, uint64_t size, uint64_t bu
     int r;
     hipError_t e;
     hipStream_t st = s->stream;
+    if ((r = fws_hip_status(hipSetDevice(s->ctx->device)))) return r;
     const uint32_t fcap = (uint32_t)((size + s->part_len) / 6 + 2);
-    if ((r = s->ensure(size + 16, fcap))) return r;
+    // staged reads (<= kZcMax) use [continuation | pad | header stream] in hstage:
+    // at most kZcMax + 15 + 13 bytes of its 2 kZcMax + 64
+    if ((r = s->ensure(size + 16, fcap, size <= fws_rx_session::kZcMax))) return r;
 
     // 1. continuation of the frame in progress (WAIT_FRAME_PAYLOAD, w_socket.h:607-617)
     uint64_t u = 0;
@@ -354,6 +362,10 @@ static int feed_impl(fws_rx_session *s, uint8_t *buf, uint64_t size, uint64_t bu
     for (uint32_t i = 0; i < res.n_frames; ++i) {
         const fws_frame_info &fi = s->hframes[i];
         const uint32_t op = fi.opcode;
+        // RFC 6455 §5.5: control frames are FIN and carry <= 125 B. The reference
+        // only asserts this in debug builds (w_socket.h:654) and otherwise copies
+        // past its 125-B control buffer; the session refuses the frame instead.
+        if ((op >> 3) && (fi.payload_len > 125u || !fi.fin)) return FWS_ERR_CONTROL_FRAME;
         if (op >> 3) { s->is_ctl = true; s->last_ctl_op = (uint8_t)op; }      // :455-464
         else if (op != 0u) s->last_op = (uint8_t)op;
         s->key = fi.key;

@@ -12,6 +12,7 @@
 // OR of the error flags per frame.
 #include "fws_device.h"
 #include "fws_internal.h"
+#include "plan_common.h"
 
 namespace fwsk {
 
@@ -122,12 +123,11 @@ __global__ __launch_bounds__(kBlock) void k_gather_fast(uint8_t *__restrict__ ds
     const uint64_t uc = ufirst + 1 < unit_cap ? ufirst : (unit_cap >= 2 ? unit_cap - 2 : 0);
     uint32_t uf0 = unit_first[uc], uf1 = unit_first[uc + 1];
     const uint64_t total = *total_ptr;
-    uint64_t n_units = (total + kGatherUnit - 1) / kGatherUnit;
-    if (n_units > unit_cap) n_units = unit_cap;
+    const uint64_t n_units = (total + kGatherUnit - 1) / kGatherUnit;
     for (uint64_t u = ufirst; u < n_units; u += nw) {
-        if (u != ufirst) {
-            uf0 = unit_first[u];
-            uf1 = u + 1 < unit_cap ? unit_first[u + 1] : 0u;
+        if (u != ufirst || u + 1 >= unit_cap) {       // past the map's capacity: searched (dbase)
+            uf0 = unit_owner(unit_first, unit_cap, dbase, n, u, u * kGatherUnit);
+            uf1 = u + 1 < n_units ? unit_owner(unit_first, unit_cap, dbase, n, u + 1, (u + 1) * kGatherUnit) : 0u;
         }
         const uint32_t flo = uf0;
         const uint32_t fhi = (u + 1 < n_units) ? uf1 : n - 1;

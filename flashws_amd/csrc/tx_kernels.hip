@@ -19,6 +19,7 @@
 // on a frame seam are built bytewise. HBM bytes = payload read + frames written.
 #include "fws_device.h"
 #include "fws_internal.h"
+#include "plan_common.h"
 
 namespace fwsk {
 
@@ -173,12 +174,11 @@ __device__ __forceinline__ void tx_encode_body(uint8_t *__restrict__ out, const 
     const uint64_t uc = ufirst + 1 < unit_cap ? ufirst : (unit_cap >= 2 ? unit_cap - 2 : 0);
     uint32_t uf0 = unit_first[uc], uf1 = unit_first[uc + 1];
     const uint64_t total = *total_ptr;
-    uint64_t n_units = (total + kTxUnit - 1) / kTxUnit;
-    if (n_units > unit_cap) n_units = unit_cap;
+    const uint64_t n_units = (total + kTxUnit - 1) / kTxUnit;
     for (uint64_t u = ufirst; u < n_units; u += nw) {
-        if (u != ufirst) {
-            uf0 = unit_first[u];
-            uf1 = u + 1 < unit_cap ? unit_first[u + 1] : 0u;
+        if (u != ufirst || u + 1 >= unit_cap) {       // past the map's capacity: searched (obase)
+            uf0 = unit_owner(unit_first, unit_cap, obase, n, u, u * kTxUnit);
+            uf1 = u + 1 < n_units ? unit_owner(unit_first, unit_cap, obase, n, u + 1, (u + 1) * kTxUnit) : 0u;
         }
         const uint32_t flo = uf0;
         const uint32_t fhi = (u + 1 < n_units) ? uf1 : n - 1;

@@ -203,79 +203,41 @@ __global__ __launch_bounds__(kBlock) void k_plan(const uint8_t *base, const fws_
 }
 
 // ---------------------------------------------------------------- unmask
-// One wave = one unit of kUnitChunks chunks. Loads for all U chunks of a lane
-// are issued before any XOR/store so each lane keeps 64 B in flight.
-template <bool kSingle>
-__global__ __launch_bounds__(kBlock) void k_unmask(uint8_t *base, const fws_frame_desc *__restrict__ d,
-                                                   uint32_t n, const uint32_t *__restrict__ n_dev,
-                                                   const uint64_t *__restrict__ cbase,
-                                                   const uint32_t *__restrict__ unit_first,
-                                                   const uint64_t *__restrict__ total_ptr,
-                                                   uint64_t unit_cap, fws_frame_desc single) {
-    if (!kSingle && n_dev && *n_dev < n) n = *n_dev;
-    if (n == 0) return;
-    const uint64_t total = kSingle ? chunks_of((uintptr_t)(base + single.payload_off), single.payload_len)
-                                   : *total_ptr;
-    uint64_t n_units = (total + kUnitChunks - 1) / kUnitChunks;
-    if (!kSingle && n_units > unit_cap) n_units = unit_cap;
+// fws_gpu_mask: one region (WSMaskBytesFast's device twin). One wave = one
+// unit of kUnitChunks chunks; a lane's loads are all issued before any
+// XOR/store so each lane keeps 64 B in flight.
+__global__ __launch_bounds__(kBlock) void k_mask_single(uint8_t *base, fws_frame_desc single) {
+    const uintptr_t a0 = (uintptr_t)(base + single.payload_off);
+    const uintptr_t lo = a0, hi = a0 + single.payload_len;
+    const uint64_t total = chunks_of(a0, single.payload_len);
+    const uint64_t n_units = (total + kUnitChunks - 1) / kUnitChunks;
+    const uint32_t rk = aligned_key(single.key, single.phase, a0);
+    const uintptr_t safe = a0 & ~uintptr_t(15);
     const int lane = threadIdx.x & (kWave - 1);
     const uint64_t nwaves = uint64_t(gridDim.x) * (kBlock / kWave);
     for (uint64_t u = uint64_t(blockIdx.x) * (kBlock / kWave) + threadIdx.x / kWave; u < n_units;
          u += nwaves) {
-        uint32_t flo = 0, fhi = 0;
-        if (!kSingle) {
-            flo = unit_first[u];
-            fhi = (u + 1 < n_units) ? unit_first[u + 1] : n - 1;
-        }
-        const uintptr_t safe =
-            (uintptr_t)(base + (kSingle ? single.payload_off : d[flo].payload_off)) & ~uintptr_t(15);
-        uintptr_t ca[kUnmaskU], lo[kUnmaskU], hi[kUnmaskU];
-        uint32_t rk[kUnmaskU];
-        bool live[kUnmaskU];
+        uintptr_t ca[kUnmaskU];
+        bool live[kUnmaskU], full[kUnmaskU];
+        u32x4 v[kUnmaskU];
 #pragma unroll
         for (int j = 0; j < kUnmaskU; ++j) {
             const uint64_t g = u * kUnitChunks + uint64_t(j) * kWave + lane;
             live[j] = g < total;
-            fws_frame_desc fd = single;
-            uint64_t cb = 0;
-            if (!kSingle) {
-                const uint32_t f = find_frame(cbase, flo, fhi, live[j] ? g : cbase[flo]);
-                fd = d[f];
-                cb = cbase[f];
-            }
-            const uintptr_t a0 = (uintptr_t)(base + fd.payload_off);
-            lo[j] = a0;
-            hi[j] = a0 + fd.payload_len;
-            ca[j] = (a0 & ~uintptr_t(15)) + (uintptr_t)((g - cb) << 4);
-            rk[j] = aligned_key(fd.key, fd.phase, a0);
-        }
-        u32x4 v[kUnmaskU];
-        bool full[kUnmaskU];
-#pragma unroll
-        for (int j = 0; j < kUnmaskU; ++j) {
-            full[j] = live[j] && ca[j] >= lo[j] && ca[j] + 16u <= hi[j];
-            // unconditional load so every lane's loads issue back to back before
-            // any wait; non-full lanes read the chunk holding the first byte of
-            // the unit's first frame (non-empty, inside the caller's buffer)
+            ca[j] = safe + (uintptr_t)(g << 4);
+            full[j] = live[j] && ca[j] >= lo && ca[j] + 16u <= hi;
+            // unconditional load so every lane's loads issue back to back
+            // before any wait; non-full lanes read the region's first chunk
             v[j] = gload16(full[j] ? ca[j] : safe);
         }
 #pragma unroll
         for (int j = 0; j < kUnmaskU; ++j) {
-            if (full[j]) {
-                gstore16(ca[j], v[j] ^ rk[j]);
-            } else if (live[j]) {
-                xor_partial_chunk(ca[j], lo[j], hi[j], rk[j]);
-            }
+            if (full[j]) gstore16(ca[j], v[j] ^ rk);
+            else if (live[j]) xor_partial_chunk(ca[j], lo, hi, rk);
         }
     }
 }
 
-// Fast variant. A wave owns G consecutive plan units (G x 4 KiB). When those
-// units touch at most 4 frames (every frame >= ~4 KiB, e.g. BASELINE C2) the
-// frame metadata is wave-uniform: it is fetched with scalar loads (lgkmcnt, so
-// it never queues behind the payload loads on vmcnt), the lane's frame is
-// picked by three compares, and all G*4 16-B loads of a lane are in flight
-// before the first XOR. Units with more frames take the per-lane search path.
 // One chunk by the generic path: per-lane search of its frame, then a full
 // 16-B XOR or a byte-exact partial one (region heads/tails).
 __device__ __forceinline__ void unmask_one_chunk(uint8_t *base, const fws_frame_desc *__restrict__ d,
@@ -308,163 +270,6 @@ __device__ __forceinline__ void store_partial(uintptr_t ca, u32x4 v, uint32_t rk
                 if (w + b >= lo && w + b < hi)
                     *(__attribute__((address_space(1))) uint8_t *)(w + b) = (uint8_t)(w4[i] >> (8 * b));
         }
-    }
-}
-
-// Scalar (wave-uniform) metadata of one plan unit: its first frame and
-// whether the unit touches at most 2 frames.
-struct UnitMeta {
-    uint32_t flo, fhi;
-};
-
-__device__ __forceinline__ UnitMeta unit_meta(const uint32_t *__restrict__ unit_first, uint64_t u, uint64_t n_units,
-                                              uint32_t n) {
-    UnitMeta m{0u, 0u};
-    if (u < n_units) {
-        m.flo = unit_first[u];
-        m.fhi = (u + 1 < n_units) ? unit_first[u + 1] : n - 1;
-    }
-    return m;
-}
-
-// Fast variant, one 4 KiB plan unit per wave step. When the unit touches at
-// most 2 frames (every frame >= 4 KiB, e.g. BASELINE C2) the frame metadata is
-// wave-uniform: fetched with scalar loads (lgkmcnt, never queued behind the
-// payload loads on vmcnt), the lane's frame is one 64-bit compare, all 4
-// loads of a lane issue back to back, region heads/tails are stored byte-exact
-// from the same loaded chunk, and the next unit's metadata is fetched while
-// this unit's payload is in flight. Units with more frames take the per-lane
-// search path.
-template <bool kNT>
-__global__ __launch_bounds__(kBlock) void k_unmask_fast(uint8_t *base, const fws_frame_desc *__restrict__ d,
-                                                        uint32_t n, const uint32_t *__restrict__ n_dev,
-                                                        const uint64_t *__restrict__ cbase,
-                                                        const uint32_t *__restrict__ unit_first,
-                                                        const uint64_t *__restrict__ total_ptr, uint64_t unit_cap) {
-    constexpr int J = kUnmaskU;
-    if (n_dev && *n_dev < n) n = *n_dev;
-    if (n == 0) return;
-    const uint64_t total = *total_ptr;
-    uint64_t n_units = (total + kUnitChunks - 1) / kUnitChunks;
-    if (n_units > unit_cap) n_units = unit_cap;
-    const int lane = threadIdx.x & (kWave - 1);
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-    const uint64_t nwaves = uint64_t(gridDim.x) * (kBlock / kWave);
-    uint64_t u = uint64_t(blockIdx.x) * (kBlock / kWave) + wave;
-    UnitMeta m = unit_meta(unit_first, u, n_units, n);
-    for (; u < n_units; u += nwaves) {
-        const uint32_t flo = m.flo, fhi = m.fhi;
-        const uint64_t g0 = u * kUnitChunks + lane;
-        if (fhi - flo >= 2u) {                          // many small frames: generic path
-            m = unit_meta(unit_first, u + nwaves, n_units, n);
-#pragma unroll 1
-            for (int j = 0; j < J; ++j) {
-                const uint64_t g = g0 + uint64_t(j) * kWave;
-                if (g < total) unmask_one_chunk(base, d, cbase, flo, fhi, g);
-            }
-            continue;
-        }
-        uint64_t A[2], L[2], H[2];
-        uint32_t R[2];
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            const uint32_t f = (flo + (uint32_t)k <= fhi) ? flo + (uint32_t)k : fhi;
-            const fws_frame_desc fd = d[f];
-            const uint64_t c = cbase[f];
-            const uintptr_t a0 = (uintptr_t)(base + fd.payload_off);
-            A[k] = (uint64_t)(a0 & ~uintptr_t(15)) - (c << 4);          // chunk g lives at A + 16 g
-            L[k] = a0;
-            H[k] = a0 + fd.payload_len;
-            R[k] = aligned_key(fd.key, fd.phase, a0);
-        }
-        const uint64_t CB1 = (fhi > flo) ? cbase[flo + 1] : ~0ull;
-        uintptr_t ca[J];
-        uint32_t rk[J];
-        bool live[J], s1[J];
-#pragma unroll
-        for (int j = 0; j < J; ++j) {
-            const uint64_t g = g0 + uint64_t(j) * kWave;
-            s1[j] = g >= CB1;
-            rk[j] = s1[j] ? R[1] : R[0];
-            ca[j] = (uintptr_t)((s1[j] ? A[1] : A[0]) + (g << 4));
-            live[j] = g < total;
-        }
-        const uintptr_t safe = (uintptr_t)L[0] & ~uintptr_t(15);   // holds a byte of frame flo
-        u32x4 v[J];
-#pragma unroll
-        for (int j = 0; j < J; ++j) v[j] = gload16<kNT>(live[j] ? ca[j] : safe);
-        m = unit_meta(unit_first, u + nwaves, n_units, n);        // next unit, overlapped
-#pragma unroll
-        for (int j = 0; j < J; ++j) {
-            if (!live[j]) continue;
-            const uintptr_t lo = s1[j] ? L[1] : L[0], hi = s1[j] ? H[1] : H[0];
-            if (ca[j] >= lo && ca[j] + 16u <= hi) gstore16<kNT>(ca[j], v[j] ^ rk[j]);
-            else store_partial(ca[j], v[j], rk[j], lo, hi);
-        }
-    }
-}
-
-// One plan unit per wave, no grid-stride loop: the grid covers every unit of
-// the host-side bound, so the hardware dispatcher balances the waves and no
-// wave runs a second unit at the tail. The scalar metadata is two dependent
-// rounds: {total, unit_first[u], unit_first[u + 1]}, then {d[flo], d[flo + 1],
-// cbase[flo], cbase[flo + 1]}; then all 4 payload loads of a lane issue.
-template <bool kNT>
-__global__ __launch_bounds__(kBlock) void k_unmask_one(uint8_t *base, const fws_frame_desc *__restrict__ d,
-                                                       uint32_t n, const uint32_t *__restrict__ n_dev,
-                                                       const uint64_t *__restrict__ cbase,
-                                                       const uint32_t *__restrict__ unit_first,
-                                                       const uint64_t *__restrict__ total_ptr, uint64_t unit_cap) {
-    constexpr int J = kUnmaskU;
-    const uint64_t u = uint64_t(blockIdx.x) * (kBlock / kWave) + __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-    if (u >= unit_cap) return;
-    if (n_dev && *n_dev < n) n = *n_dev;
-    const uint64_t total = *total_ptr;
-    const uint32_t uf0 = unit_first[u];
-    const uint32_t uf1 = (u + 1 < unit_cap) ? unit_first[u + 1] : 0u;
-    uint64_t n_units = (total + kUnitChunks - 1) / kUnitChunks;
-    if (n_units > unit_cap) n_units = unit_cap;
-    if (n == 0 || u >= n_units) return;
-    const uint32_t flo = uf0, fhi = (u + 1 < n_units) ? uf1 : n - 1;
-    const int lane = threadIdx.x & (kWave - 1);
-    const uint64_t g0 = u * kUnitChunks + lane;
-    if (fhi - flo >= 2u) {                              // many small frames: generic path
-#pragma unroll 1
-        for (int j = 0; j < J; ++j) {
-            const uint64_t g = g0 + uint64_t(j) * kWave;
-            if (g < total) unmask_one_chunk(base, d, cbase, flo, fhi, g);
-        }
-        return;
-    }
-    const uint32_t f1 = fhi;                            // flo or flo + 1
-    const fws_frame_desc d0 = d[flo], d1 = d[f1];
-    const uint64_t c0 = cbase[flo], CB1 = cbase[flo + 1];
-    const uintptr_t a0 = (uintptr_t)(base + d0.payload_off), a1 = (uintptr_t)(base + d1.payload_off);
-    const uint64_t A0 = (uint64_t)(a0 & ~uintptr_t(15)) - (c0 << 4);
-    const uint64_t A1 = (uint64_t)(a1 & ~uintptr_t(15)) - (CB1 << 4);
-    const uint64_t L0 = a0, H0 = a0 + d0.payload_len, L1 = a1, H1 = a1 + d1.payload_len;
-    const uint32_t R0 = aligned_key(d0.key, d0.phase, a0), R1 = aligned_key(d1.key, d1.phase, a1);
-    const uint64_t S1 = (f1 > flo) ? CB1 : ~0ull;
-    uintptr_t ca[J];
-    bool live[J], s1[J];
-#pragma unroll
-    for (int j = 0; j < J; ++j) {
-        const uint64_t g = g0 + uint64_t(j) * kWave;
-        s1[j] = g >= S1;
-        ca[j] = (uintptr_t)((s1[j] ? A1 : A0) + (g << 4));
-        live[j] = g < total;
-    }
-    const uintptr_t safe = (uintptr_t)L0 & ~uintptr_t(15);
-    u32x4 v[J];
-#pragma unroll
-    for (int j = 0; j < J; ++j) v[j] = gload16<kNT>(live[j] ? ca[j] : safe);
-#pragma unroll
-    for (int j = 0; j < J; ++j) {
-        if (!live[j]) continue;
-        const uintptr_t lo = s1[j] ? L1 : L0, hi = s1[j] ? H1 : H0;
-        const uint32_t rk = s1[j] ? R1 : R0;
-        if (ca[j] >= lo && ca[j] + 16u <= hi) gstore16<kNT>(ca[j], v[j] ^ rk);
-        else store_partial(ca[j], v[j], rk, lo, hi);
     }
 }
 
@@ -669,7 +474,7 @@ __global__ __launch_bounds__(kBlock) void k_utf8_seam(const uint8_t *base, uint6
 // bytes that share a chunk with payload bytes between the batch's first and
 // last payload byte are stored back unchanged; only the batch's two outer edge
 // chunks use byte-exact stores. No partial-line writes reach HBM inside the
-// batch. Otherwise the chunk-space path (k_unmask_fast's unit body).
+// batch. Otherwise the chunk-space path (chunk_space_unit).
 
 // Store the bytes of x that lie in [lo, hi) (dword stores where whole).
 __device__ __forceinline__ void store_bytes(uintptr_t ca, const u32x4 &x, uintptr_t lo, uintptr_t hi) {
@@ -832,15 +637,16 @@ __device__ __forceinline__ void byte_space_unit(uint8_t *base, const fws_frame_d
 }
 
 
-// One chunk-space plan unit (any descriptor order): k_unmask_fast's body.
+// One chunk-space plan unit (any descriptor order).
 template <bool kNT>
 __device__ __forceinline__ void chunk_space_unit(uint8_t *base, const fws_frame_desc *__restrict__ d, uint32_t n,
                                                  const uint64_t *__restrict__ cbase,
-                                                 const uint32_t *__restrict__ unit_first, uint64_t total,
-                                                 uint64_t n_units, uint64_t u, int lane) {
+                                                 const uint32_t *__restrict__ unit_first, uint64_t unit_cap,
+                                                 uint64_t total, uint64_t n_units, uint64_t u, int lane) {
     constexpr int J = kUnmaskU;
-    const uint32_t flo = unit_first[u];
-    const uint32_t fhi = (u + 1 < n_units) ? unit_first[u + 1] : n - 1;
+    const uint32_t flo = unit_owner(unit_first, unit_cap, cbase, n, u, u * kUnitChunks);
+    const uint32_t fhi = (u + 1 < n_units) ? unit_owner(unit_first, unit_cap, cbase, n, u + 1, (u + 1) * kUnitChunks)
+                                           : n - 1;
     const uint64_t g0 = u * kUnitChunks + lane;
     if (fhi - flo >= 2u) {
 #pragma unroll 1
@@ -905,10 +711,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) voi
         }
         return;
     }
-    uint64_t n_units = (total + kUnitChunks - 1) / kUnitChunks;
-    if (n_units > unit_cap) n_units = unit_cap;
+    // every unit of the batch: past the unit map's capacity (a batch larger than
+    // the reservation) the owners come from a search of cbase
+    const uint64_t n_units = (total + kUnitChunks - 1) / kUnitChunks;
     for (uint64_t u = u0; u < n_units; u += nwaves)
-        chunk_space_unit<kNT>(base, d, n, cbase, unit_first, total, n_units, u, lane);
+        chunk_space_unit<kNT>(base, d, n, cbase, unit_first, unit_cap, total, n_units, u, lane);
 }
 
 #ifndef FWS_SORTED_WPE
@@ -1265,16 +1072,6 @@ __global__ __launch_bounds__(kBlock) void k_unmask_sorted_utf8(uint8_t *base, co
 // ---------------------------------------------------------------- launchers
 using namespace fwsk;
 
-// Kernel variant used by fws_launch_unmask (tuning hook, not part of the ABI):
-// 0 = k_unmask (per-lane search), 1 = k_unmask_fast, 5 = k_unmask_fast nontemporal.
-static int g_unmask_variant = 7;
-
-extern "C" __attribute__((visibility("default"))) int fws_internal_set_unmask_variant(int v) {
-    const int old = g_unmask_variant;
-    if (v >= 0 && v <= 7) g_unmask_variant = v;
-    return old;
-}
-
 static int g_grid_cap = 16384;  // tuning hook: max workgroups of the streaming kernels
 extern "C" __attribute__((visibility("default"))) int fws_internal_set_grid_cap(int blocks) {
     const int old = g_grid_cap;
@@ -1309,8 +1106,7 @@ int fws_launch_mask_single(void *dev_ptr, uint64_t n, uint32_t key, uint32_t pha
     fws_frame_desc one{0, n, key, phase};
     const uint64_t chunks = ((((uintptr_t)dev_ptr) + n + 15u) >> 4) - (((uintptr_t)dev_ptr) >> 4);
     const uint64_t units = (chunks + kUnitChunks - 1) / kUnitChunks;
-    hipLaunchKernelGGL(k_unmask<true>, dim3(grid_for_units(units)), dim3(kBlock), 0, s,
-                       (uint8_t *)dev_ptr, nullptr, 1u, nullptr, nullptr, nullptr, nullptr, 0ull, one);
+    hipLaunchKernelGGL(k_mask_single, dim3(grid_for_units(units)), dim3(kBlock), 0, s, (uint8_t *)dev_ptr, one);
     return fws_hip_status(hipGetLastError());
 }
 
@@ -1375,23 +1171,7 @@ int fws_launch_unmask_stream(uint8_t *base, uint64_t N, const fws_frame_info *fr
 int fws_launch_unmask(uint8_t *base, const fws_frame_desc *d, uint32_t n, const uint32_t *n_dev,
                       const fws_plan_ws &ws, uint64_t max_chunks, hipStream_t s) {
     const uint64_t units = (max_chunks + kUnitChunks - 1) / kUnitChunks;
-    fws_frame_desc none{0, 0, 0, 0};
-    const int v = g_unmask_variant;
-    const dim3 grid(grid_for_units(units)), blk(kBlock);
-    if (v == 0 || v == 4)
-        hipLaunchKernelGGL(k_unmask<false>, grid, blk, 0, s, base, d, n, n_dev, ws.cbase, ws.unit_first, ws.total,
-                           ws.unit_cap, none);
-    else if (v == 7)
-        hipLaunchKernelGGL(k_unmask_desc<true>, grid, blk, 0, s, base, d, n, ws.cbase, ws.unit_first,
-                           (const u32x4 *)ws.unit_rec, ws.total, (const fws_plan_mode *)ws.mode, ws.unit_cap);
-    else if (v == 6)
-        hipLaunchKernelGGL(k_unmask_one<true>, dim3((unsigned)((units + (kBlock / kWave) - 1) / (kBlock / kWave))),
-                           blk, 0, s, base, d, n, n_dev, ws.cbase, ws.unit_first, ws.total, ws.unit_cap);
-    else if (v < 4)
-        hipLaunchKernelGGL(k_unmask_fast<false>, grid, blk, 0, s, base, d, n, n_dev, ws.cbase, ws.unit_first,
-                           ws.total, ws.unit_cap);
-    else
-        hipLaunchKernelGGL(k_unmask_fast<true>, grid, blk, 0, s, base, d, n, n_dev, ws.cbase, ws.unit_first,
-                           ws.total, ws.unit_cap);
+    hipLaunchKernelGGL(k_unmask_desc<true>, dim3(grid_for_units(units)), dim3(kBlock), 0, s, base, d, n, ws.cbase,
+                       ws.unit_first, (const u32x4 *)ws.unit_rec, ws.total, (const fws_plan_mode *)ws.mode, ws.unit_cap);
     return fws_hip_status(hipGetLastError());
 }

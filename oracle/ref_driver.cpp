@@ -17,7 +17,9 @@
 
 #include "flashws/flashws.h"
 
+#include <sys/mman.h>
 #include <sys/socket.h>
+#include <sys/wait.h>
 #include <unistd.h>
 #include <fcntl.h>
 #include <chrono>
@@ -245,6 +247,88 @@ double ref_time_onrecv(const uint8_t *stream, size_t n, size_t read_size, int it
     *payload_bytes = s->bytes_seen;
     ref_session_free(s);
     return std::chrono::duration<double>(t1 - t0).count();
+}
+
+// All-core CPU baseline: the reference's own scaling model is one event loop
+// (one process, or one F-Stack lcore) per core (SURVEY §2 "Parallelism",
+// floop.h:331-345), and its BufferManager / MemPoolEnv singletons are not
+// thread-safe (buffer_manager.h:9-34, flash_alloc.h:437), so the stream is split
+// at frame boundaries cuts[0..nproc] into nproc ranges, each decoded by its own
+// forked process exactly as ref_time_onrecv does (one untimed pass, then
+// `iters` timed passes). The children start together (a pipe barrier) and time
+// themselves; returns the slowest child's seconds, *payload_bytes = the sum.
+// Call it before the process initialises a GPU (the children never touch one).
+double ref_time_onrecv_procs(const uint8_t *stream, const uint64_t *cuts, int nproc, size_t read_size, int iters,
+                             uint64_t *payload_bytes, int *ret_code) {
+    struct Slot { double secs; uint64_t bytes; int ret; int done; };
+    auto *slots = static_cast<Slot *>(::mmap(nullptr, sizeof(Slot) * (size_t)nproc, PROT_READ | PROT_WRITE,
+                                             MAP_SHARED | MAP_ANONYMOUS, -1, 0));
+    *payload_bytes = 0;
+    *ret_code = 0;
+    if (slots == MAP_FAILED) return -1.0;
+    std::memset(slots, 0, sizeof(Slot) * (size_t)nproc);
+    int ready[2], go[2];
+    if (::pipe(ready) != 0 || ::pipe(go) != 0) return -1.0;
+    std::vector<pid_t> kids;
+    for (int p = 0; p < nproc; ++p) {
+        const pid_t pid = ::fork();
+        if (pid < 0) break;
+        if (pid == 0) {
+            ::close(ready[0]);
+            ::close(go[1]);
+            const uint8_t *src = stream + cuts[p];
+            const size_t n = (size_t)(cuts[p + 1] - cuts[p]);
+            auto *s = static_cast<Session *>(ref_session_new());
+            const size_t pad = fws::constants::DEFAULT_READ_BUF_PRE_PADDING_SIZE;
+            fws::IOBuffer big = fws::RequestBuf(pad + n + 64);
+            std::memcpy(big.data + pad, src, n);
+            s->timing = true;
+            int rc = 0;
+            auto pass = [&]() {
+                for (size_t off = 0; off < n; off += read_size) {
+                    size_t len = std::min(read_size, n - off);
+                    fws::IOBuffer view(big.data, (ssize_t)len, pad + off, pad + off + len);
+                    int r = s->sock.OnRecvData(view);
+                    if (r < 0) rc = r;
+                }
+            };
+            pass();                                     // untimed: page faults of the copy
+            char c = 1;
+            if (::write(ready[1], &c, 1) != 1) ::_exit(3);
+            if (::read(go[0], &c, 1) != 1) ::_exit(3);
+            s->bytes_seen = 0;
+            auto t0 = std::chrono::steady_clock::now();
+            for (int it = 0; it < iters; ++it) pass();
+            auto t1 = std::chrono::steady_clock::now();
+            slots[p].secs = std::chrono::duration<double>(t1 - t0).count();
+            slots[p].bytes = s->bytes_seen;
+            slots[p].ret = rc;
+            slots[p].done = 1;
+            ::_exit(0);
+        }
+        kids.push_back(pid);
+    }
+    ::close(ready[1]);
+    ::close(go[0]);
+    char c;
+    for (size_t i = 0; i < kids.size(); ++i)
+        if (::read(ready[0], &c, 1) != 1) break;
+    for (size_t i = 0; i < kids.size(); ++i) {
+        c = 1;
+        if (::write(go[1], &c, 1) != 1) break;
+    }
+    for (pid_t k : kids) ::waitpid(k, nullptr, 0);
+    ::close(ready[0]);
+    ::close(go[1]);
+    double worst = 0.0;
+    for (int p = 0; p < nproc; ++p) {
+        if (!slots[p].done || p >= (int)kids.size()) { worst = -1.0; break; }
+        worst = std::max(worst, slots[p].secs);
+        *payload_bytes += slots[p].bytes;
+        if (slots[p].ret < 0) *ret_code = slots[p].ret;
+    }
+    ::munmap(slots, sizeof(Slot) * (size_t)nproc);
+    return worst;
 }
 
 // Echo harness (tools/ws_echo.cpp, run by bench.py's CPU-baseline leg): the

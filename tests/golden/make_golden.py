@@ -7,7 +7,7 @@ own headers by oracle/ref_driver.cpp) drives WSServerSocket<false>::OnRecvData
 (net/w_socket.h:543-769) and fws::WSMaskBytesFast (crypto/ws_mask.h:175).
 The fixtures are data only (inputs + the reference's outputs / digests).
 
-    make -C oracle ref && python tests/golden/make_golden.py [tx]
+    make -C oracle ref && python tests/golden/make_golden.py [tx | configs]
 
 tx_cases.json.gz holds the send side: sequences of WriteFrame calls on a
 WSClientSocket<false> / WSServerSocket<false> (-> SendFrame, w_socket.h:832-944)
@@ -217,7 +217,13 @@ def config_digests():
         "C3": lambda: gpu.config_c3(),
         "C4": lambda: gpu.config_c4(),
         "C5_16k_frames": lambda: gpu.config_c5(n_frames=16384),
+        "C5_full_per_gpu": lambda: gpu.config_c5(),             # 262 144 x 16 KiB, seed 42 (rank 0's shard)
     }
+    only = os.environ.get("GOLDEN_ONLY")
+    if only:
+        specs = {k: v for k, v in specs.items() if k in only.split(",")}
+        with open(os.path.join(HERE, "configs.json")) as f:
+            out = json.load(f)
     for name, fn in specs.items():
         wire, descs, ok = fn()
         rec = {"wire_bytes": int(len(wire)), "frames": int(len(descs)),
@@ -238,10 +244,11 @@ def config_digests():
             full = wire.copy()
             orc.orc_decode_stream(full)
             flags = []
+            mv = memoryview(full)
             for d in descs:
                 o, n = int(d["payload_off"]), int(d["payload_len"])
                 try:
-                    full[o:o + n].tobytes().decode("utf-8", errors="strict")
+                    str(mv[o:o + n], "utf-8", "strict")
                     flags.append(1)
                 except UnicodeDecodeError:
                     flags.append(0)
@@ -309,6 +316,9 @@ def main():
     assert orc.ref_available(), "build oracle/_ref first: make -C oracle ref"
     if sys.argv[1:] == ["tx"]:
         tx_cases()
+        return
+    if sys.argv[1:] == ["configs"]:         # GOLDEN_ONLY=C5_full_per_gpu ... to regenerate one entry
+        config_digests()
         return
     cases = {}
     for name, reads in kat_cases() + random_stream_cases():

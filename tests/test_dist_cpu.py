@@ -62,3 +62,27 @@ def test_two_rank_batch_split_gloo():
         assert ret == 0 and nf == 512
         assert np.isclose(agg, world * payload / step / (1 << 30))
     assert res[0][7][0] != res[0][7][1]                           # independent shards
+
+
+def test_bench_launcher_two_ranks_gloo():
+    """bench.py --gpus 2 starts its own ranks (torch.distributed.run as a child
+    process) and reports the slowest rank's step and the whole-job aggregate;
+    --launcher-selftest swaps the device step for a host XOR over gloo."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--launcher-selftest",
+                          "--steps", "3", "--warmup", "1", "--frames", "512", "--no-cpu"],
+                         cwd=root, env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [json.loads(x) for x in out.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, out.stdout                               # rank 0 prints one line
+    rec = lines[0]
+    assert rec["selftest"] and rec["n_gpus"] == 2 and rec["rank"] == 0
+    assert rec["step_s"] >= rec["own_step_s"]                        # max over ranks
+    assert np.isclose(rec["value"], 2 * rec["payload_bytes_per_rank"] / rec["step_s"] / (1 << 30))
+    d = rec["shard_digests"]
+    assert len(d) == 2 and d[0] != d[1]                              # independent shards (seed 42 + rank)

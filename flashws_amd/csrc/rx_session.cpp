@@ -69,13 +69,23 @@ struct fws_rx_session {
     uint8_t *ctl_out = nullptr;
     uint64_t ctl_cap = 0, ctl_used = 0;
 
+    // fws_rx_session_feed_view: the session's own growing sinks instead
+    bool own = false;
+    std::vector<fws_rx_event> own_ev;
+    std::vector<uint8_t> own_ctl;
+    // the last protocol error of a feed (fws_rx_session_error)
+    int err_code = 0;
+    uint32_t err_opcode = 0;
+
     void push(const fws_rx_event &e) {
-        if (n_ev < ev_cap) ev[n_ev] = e;
+        if (own) own_ev.push_back(e);
+        else if (n_ev < ev_cap) ev[n_ev] = e;
         ++n_ev;
     }
     uint64_t push_ctl(const uint8_t *p, uint64_t n) {
         const uint64_t off = ctl_used;
-        if (ctl_used + n <= ctl_cap) memcpy(ctl_out + ctl_used, p, n);
+        if (own) own_ctl.insert(own_ctl.end(), p, p + n);
+        else if (ctl_used + n <= ctl_cap) memcpy(ctl_out + ctl_used, p, n);
         ctl_used += n;
         return off;
     }
@@ -256,13 +266,42 @@ int fws_rx_session_feed(fws_rx_session *s, uint8_t *buf, uint64_t size, uint64_t
                         fws_rx_event *events, uint64_t ev_cap, uint64_t *n_events,
                         uint8_t *ctl_out, uint64_t ctl_cap, uint64_t *ctl_used) {
     if (!s || (size && !buf) || !n_events || !ctl_used) return FWS_ERR_INVALID;
+    s->own = false;
     s->ev = events; s->ev_cap = events ? ev_cap : 0; s->n_ev = 0;
     s->ctl_out = ctl_out; s->ctl_cap = ctl_out ? ctl_cap : 0; s->ctl_used = 0;
+    s->err_code = 0;
     const int r = feed_impl(s, buf, size, buf_capacity);
+    if (r < 0) s->err_code = r;
     *n_events = s->n_ev;
     *ctl_used = s->ctl_used;
     if (r == 0 && (s->n_ev > ev_cap || s->ctl_used > ctl_cap)) return FWS_ERR_CAPACITY;
     return r;
+}
+
+int fws_rx_session_feed_view(fws_rx_session *s, uint8_t *buf, uint64_t size, uint64_t buf_capacity,
+                             const fws_rx_event **events, uint64_t *n_events, const uint8_t **ctl,
+                             uint64_t *ctl_used) {
+    if (!s || (size && !buf) || !events || !n_events || !ctl || !ctl_used) return FWS_ERR_INVALID;
+    s->own = true;
+    s->own_ev.clear();
+    s->own_ctl.clear();
+    s->n_ev = 0;
+    s->ctl_used = 0;
+    s->err_code = 0;
+    const int r = feed_impl(s, buf, size, buf_capacity);
+    if (r < 0) s->err_code = r;
+    *events = s->own_ev.data();
+    *n_events = s->own_ev.size();
+    *ctl = s->own_ctl.data();
+    *ctl_used = s->own_ctl.size();
+    s->own = false;
+    return r;
+}
+
+int fws_rx_session_error(const fws_rx_session *s, uint32_t *opcode) {
+    if (!s) return FWS_ERR_INVALID;
+    if (opcode) *opcode = s->err_opcode;
+    return s->err_code;
 }
 
 static int feed_impl(fws_rx_session *s, uint8_t *buf, uint64_t size, uint64_t buf_capacity) {
@@ -365,7 +404,10 @@ static int feed_impl(fws_rx_session *s, uint8_t *buf, uint64_t size, uint64_t bu
         // RFC 6455 §5.5: control frames are FIN and carry <= 125 B. The reference
         // only asserts this in debug builds (w_socket.h:654) and otherwise copies
         // past its 125-B control buffer; the session refuses the frame instead.
-        if ((op >> 3) && (fi.payload_len > 125u || !fi.fin)) return FWS_ERR_CONTROL_FRAME;
+        if ((op >> 3) && (fi.payload_len > 125u || !fi.fin)) {
+            s->err_opcode = op;
+            return FWS_ERR_CONTROL_FRAME;
+        }
         if (op >> 3) { s->is_ctl = true; s->last_ctl_op = (uint8_t)op; }      // :455-464
         else if (op != 0u) s->last_op = (uint8_t)op;
         s->key = fi.key;
@@ -388,7 +430,10 @@ static int feed_impl(fws_rx_session *s, uint8_t *buf, uint64_t size, uint64_t bu
             win[have] = x < part0 ? s->hdr[x] : buf[x - part0 + u];
         }
         const int pr = s->host_parse(win, have);
-        if (res.status < 0) return pr < 0 ? pr : res.status;
+        if (res.status < 0) {
+            s->err_opcode = have ? (uint32_t)(win[0] & 15u) : 0u;
+            return pr < 0 ? pr : res.status;
+        }
         // incomplete: reference stages min(14 - part_len, bytes left) (:567-569, 592)
         const uint64_t staged_before = at < part0 ? part0 - at : 0;   // bytes of it from earlier reads
         const uint64_t from_read = L - at - staged_before;

@@ -216,6 +216,16 @@ int fws_rx_session_feed(fws_rx_session *s, uint8_t *buf, uint64_t size, uint64_t
                         fws_rx_event *events, uint64_t ev_cap, uint64_t *n_events,
                         uint8_t *ctl_out, uint64_t ctl_cap, uint64_t *ctl_used);
 int fws_rx_session_state(const fws_rx_session *s, fws_rx_state *out);
+/* fws_rx_session_feed with the session's own event and control-payload sinks
+ * (grown as needed, no capacity error): *events / *ctl point into the session
+ * and stay valid until its next feed. */
+int fws_rx_session_feed_view(fws_rx_session *s, uint8_t *buf, uint64_t size, uint64_t buf_capacity,
+                             const fws_rx_event **events, uint64_t *n_events, const uint8_t **ctl,
+                             uint64_t *ctl_used);
+/* The last feed's protocol error (0 if none) and the opcode of the frame it
+ * stopped at, for the reference's error text ("Opcode %u is not valid",
+ * w_socket.h:452) in the Close reason (ws_server_socket.h:178-181). */
+int fws_rx_session_error(const fws_rx_session *s, uint32_t *opcode);
 
 /* ---- send path: batch frame builder -------------------
  * The bytes WSocket::SendFrame (w_socket.h:832-944) writes for one frame:

@@ -252,14 +252,14 @@ double ref_time_onrecv(const uint8_t *stream, size_t n, size_t read_size, int it
 // All-core CPU baseline: the reference's own scaling model is one event loop
 // (one process, or one F-Stack lcore) per core (SURVEY §2 "Parallelism",
 // floop.h:331-345), and its BufferManager / MemPoolEnv singletons are not
-// thread-safe (buffer_manager.h:9-34, flash_alloc.h:437), so the stream is split
-// at frame boundaries cuts[0..nproc] into nproc ranges, each decoded by its own
-// forked process exactly as ref_time_onrecv does (one untimed pass, then
-// `iters` timed passes). The children start together (a pipe barrier) and time
-// themselves; returns the slowest child's seconds, *payload_bytes = the sum.
-// Call it before the process initialises a GPU (the children never touch one).
-double ref_time_onrecv_procs(const uint8_t *stream, const uint64_t *cuts, int nproc, size_t read_size, int iters,
-                             uint64_t *payload_bytes, int *ret_code) {
+// thread-safe (buffer_manager.h:9-34, flash_alloc.h:437), so process p decodes stream[begin[p], end[p]) (a range starting at a frame
+// header) in its own forked process exactly as ref_time_onrecv does (its own
+// copy in a pool buffer, one untimed pass, then `iters` timed passes). The
+// children start together (a pipe barrier) and time themselves; returns the
+// slowest child's seconds, *payload_bytes = the sum. Call it before the process
+// initialises a GPU (the children never touch one).
+double ref_time_onrecv_procs(const uint8_t *stream, const uint64_t *begin, const uint64_t *end, int nproc,
+                             size_t read_size, int iters, uint64_t *payload_bytes, int *ret_code) {
     struct Slot { double secs; uint64_t bytes; int ret; int done; };
     auto *slots = static_cast<Slot *>(::mmap(nullptr, sizeof(Slot) * (size_t)nproc, PROT_READ | PROT_WRITE,
                                              MAP_SHARED | MAP_ANONYMOUS, -1, 0));
@@ -276,8 +276,8 @@ double ref_time_onrecv_procs(const uint8_t *stream, const uint64_t *cuts, int np
         if (pid == 0) {
             ::close(ready[0]);
             ::close(go[1]);
-            const uint8_t *src = stream + cuts[p];
-            const size_t n = (size_t)(cuts[p + 1] - cuts[p]);
+            const uint8_t *src = stream + begin[p];
+            const size_t n = (size_t)(end[p] - begin[p]);
             auto *s = static_cast<Session *>(ref_session_new());
             const size_t pad = fws::constants::DEFAULT_READ_BUF_PRE_PADDING_SIZE;
             fws::IOBuffer big = fws::RequestBuf(pad + n + 64);

@@ -87,6 +87,9 @@ SIGNATURES = [
     ("fws_rx_session_destroy", None, [_P]),
     ("fws_rx_session_feed", _I, [_P, _P, _U64, _U64, _P, _U64, _PU64, _P, _U64, _PU64]),
     ("fws_rx_session_state", _I, [_P, _P]),
+    ("fws_rx_session_feed_view", _I, [_P, _P, _U64, _U64, C.POINTER(C.c_void_p), _PU64, C.POINTER(C.c_void_p),
+                                      _PU64]),
+    ("fws_rx_session_error", _I, [_P, C.POINTER(C.c_uint32)]),
     ("fws_gen_batch", _I, [C.POINTER(GenParams), _P, _U64, _PU64, _P, _U64, _PU64, _P]),
     ("fws_tx_next", None, [_U32, _I, C.POINTER(C.c_uint8), C.POINTER(C.c_uint8), C.POINTER(C.c_uint8)]),
     ("fws_gpu_encode_frames", _I, [_P, _P, _U64, _P, _P, _U32, _P, _P]),

@@ -1,0 +1,215 @@
+// flashws_amd/gpu_floop.hpp -- opt-in MI355X receive decode for an UNCHANGED
+// flashws server: one call on the listening fws::WSServerSocket<false>, no
+// change to any flashws header and none to the application's on_read /
+// WriteFrame / on_close code.
+//
+//   #include "flashws/flashws.h"              // the app's one flashws TU
+//   #include "flashws_amd/gpu_floop.hpp"
+//   fws_amd::GpuContext gpu(0);
+//   fws_amd::GpuRxHook hook(gpu);
+//   ws_socket.SetOnNewConnection(...); ws_socket.SetOnRead(...); ws_socket.SetOnClose(...);
+//   hook.Enable(ws_socket);                    // <- the only added line
+//   loop.AddSocket(std::move(ws_socket), sizeof(Ctx), true); loop.Run();
+//
+// How it attaches. FLoop copies the listening socket's on_new_connection /
+// on_read / on_write / on_close into every accepted socket
+// (floop.h:367-390). Enable() wraps the first and the last: when a
+// connection's handshake completes (on_new_connection, ws_server_socket.h:
+// 320-536) the wrapper re-installs that socket's under-socket readable
+// callback -- the one WSServerSocket::InitUnderOnReadImp sets
+// (ws_server_socket.h:171-197) -- with a callback of the same shape: in
+// OPEN_STATUS each read goes through fws_amd::GpuRxDecoder (H2D, fused header
+// parse + unmask on the GPU, D2H, OnRecvData's part bookkeeping on the host)
+// instead of WSocket::OnRecvData (w_socket.h:543-769); every other status is
+// handed to the reference's own callback (saved at Enable). The decoded events
+// drive exactly the reference's code paths:
+//   data / PONG part -> on_read()(sock, opcode, IOBuffer, frame_end, msg_end, is_ctl, &sock + 1)
+//                                                              (w_socket.h:713-747)
+//   PING             -> SendControlMsg(PONG)                   (w_socket.h:662-666)
+//   CLOSE            -> OnRecvCloseFrame, SendControlMsg(CLOSE) echo, close_code_,
+//                       on_close()(sock, code, reason, ...)    (w_socket.h:667-710)
+//   error < 0        -> Close(WS_ABNORMAL_CLOSE, error text) and close the TCP
+//                       socket                                 (ws_server_socket.h:176-194)
+// The protected members are reached through using-declarations in a derived
+// access struct and pointers to members (no reference file is edited). The
+// wrapped on_close retires the connection's decoder (freed at the next read).
+//
+// Plain ws:// only (WSServerSocket<false>); a TLS connection's decrypted reads
+// would attach the same way and are not wired here.
+#pragma once
+
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <string_view>
+#include <unordered_map>
+#include <utility>
+#include <vector>
+
+#include "gpu_ws.hpp"
+
+namespace fws_amd {
+namespace detail {
+
+struct TcpAccess : fws::TCPSocket {
+    using fws::TCPSocket::on_readable_;
+};
+
+struct WsServerAccess : fws::WSServerSocket<false> {
+    using S = fws::WSServerSocket<false>;
+    using S::server_status_;
+    using S::on_read;
+    using S::on_close;
+    using S::on_new_connection;
+    using S::SendControlMsg;
+    using S::HasRecvClose;
+    using S::HasSentClose;
+    using S::OnRecvCloseFrame;
+    using S::close_code_;
+    using S::has_called_on_close_;
+    using S::in_shutting_down_;
+    static constexpr auto kOpen = S::OPEN_STATUS;
+    static constexpr auto kClosed = S::CLOSED_STATUS;
+    static constexpr size_t kCtlHdr = fws::constants::WS_SERVER_TX_CONTROL_HDR_SIZE;
+};
+
+}  // namespace detail
+
+class GpuRxHook {
+public:
+    using Sock = fws::WSServerSocket<false>;
+    using A = detail::WsServerAccess;
+
+    explicit GpuRxHook(GpuContext &ctx) : ctx_(ctx) {}
+    GpuRxHook(const GpuRxHook &) = delete;
+    GpuRxHook &operator=(const GpuRxHook &) = delete;
+
+    // Call on the listening socket after the application set its callbacks and
+    // before connections are accepted. The hook must outlive the loop.
+    void Enable(Sock &listen) {
+        user_new_conn_ = (listen.*(&A::on_new_connection))();
+        user_close_ = (listen.*(&A::on_close))();
+        ref_readable_ = listen.under_socket().*(&detail::TcpAccess::on_readable_);
+        GpuRxHook *self = this;
+        listen.SetOnNewConnection([self](Sock &w, std::string_view uri, std::string_view host,
+                                         std::string_view origin, std::string_view sub, std::string_view ext,
+                                         std::string_view &rsub, std::string_view &rext, void *ud) {
+            const int r = self->user_new_conn_(w, uri, host, origin, sub, ext, rsub, rext, ud);
+            if (r >= 0) self->Attach(w);
+            return r;
+        });
+        listen.SetOnClose([self](Sock &w, uint32_t code, std::string_view reason, void *ud) {
+            self->Retire(w);
+            self->user_close_(w, code, reason, ud);
+        });
+    }
+
+    size_t connections() const { return conns_.size(); }
+    uint64_t gpu_reads() const { return gpu_reads_; }
+
+private:
+    struct Conn {
+        Sock *ws;
+        std::unique_ptr<GpuRxDecoder<fws::IOBuffer>> dec;
+    };
+
+    // Maps decoded events onto the reference's own members (see the header).
+    struct Sink {
+        Sock &s;
+        void on_read(uint32_t op, fws::IOBuffer &&b, bool fe, bool me, bool ctl) {
+            (s.*(&A::on_read))()(s, op, std::move(b), fe, me, ctl, &s + 1);
+        }
+        fws::IOBuffer control_buf(std::string_view p) {
+            fws::IOBuffer b = fws::RequestBuf(std::max(fws::constants::WS_MAX_CONTROL_FRAME_SIZE,
+                                                       A::kCtlHdr + p.size()));
+            b.start_pos = A::kCtlHdr;
+            if (!p.empty()) std::memcpy(b.data + b.start_pos, p.data(), p.size());
+            b.size = (ssize_t)p.size();
+            return b;
+        }
+        void on_ping(std::string_view p) { (s.*(&A::SendControlMsg))(control_buf(p), fws::WS_PONG_FRAME); }
+        void on_close(uint32_t code, std::string_view p) {
+            const std::string_view reason = p.size() >= 2 ? p.substr(2) : std::string_view{};
+            if (!(s.*(&A::HasRecvClose))()) {
+                if ((s.*(&A::OnRecvCloseFrame))() < 0) return;
+            }
+            if (!(s.*(&A::HasSentClose))()) (s.*(&A::SendControlMsg))(control_buf(p), fws::WS_CLOSE_FRAME);
+            s.*(&A::close_code_) = static_cast<fws::WSStatusCode>(code);
+            if (!(s.*(&A::has_called_on_close_))) {
+                s.*(&A::has_called_on_close_) = true;
+                (s.*(&A::on_close))()(s, code, reason, &s + 1);
+            }
+        }
+        fws::IOBuffer request_buf(size_t n) {
+            fws::IOBuffer b = fws::RequestBuf(std::max(fws::constants::WS_MAX_CONTROL_FRAME_SIZE, A::kCtlHdr + n));
+            b.start_pos = A::kCtlHdr;
+            return b;
+        }
+    };
+
+    void Attach(Sock &w) {
+        auto &c = conns_[&w.under_socket()];
+        c.ws = &w;
+        c.dec = std::make_unique<GpuRxDecoder<fws::IOBuffer>>(ctx_);
+        GpuRxHook *self = this;
+        w.under_socket().SetOnReadable([self](fws::TCPSocket &u, fws::IOBuffer &&buf, void *ud) {
+            self->OnReadable(u, std::move(buf), ud);
+        });
+    }
+
+    void Retire(Sock &w) {
+        auto it = conns_.find(&w.under_socket());
+        if (it == conns_.end()) return;
+        retired_.push_back(std::move(it->second.dec));   // may be mid-dispatch: freed at the next read
+        conns_.erase(it);
+    }
+
+    // ws_server_socket.h:172-196 with OnRecvData on the GPU.
+    void OnReadable(fws::TCPSocket &u, fws::IOBuffer &&buf, void *ud) {
+        retired_.clear();
+        auto it = conns_.find(&u);
+        if (it == conns_.end() || (it->second.ws->*(&A::server_status_)) != A::kOpen) {
+            ref_readable_(u, std::move(buf), ud);
+            return;
+        }
+        Sock &sock = *it->second.ws;
+        GpuRxDecoder<fws::IOBuffer> *dec = it->second.dec.get();   // `it` may be erased by on_close
+        ++gpu_reads_;
+        const int ret = dec->OnRecvData(buf, Sink{sock});
+        if (ret < 0) {
+            SetErrorText(ret, dec->error_opcode());
+            const std::string_view e = fws::GetErrorStrV();
+            const size_t max_len = fws::constants::WS_MAX_CONTROL_FRAME_SIZE - A::kCtlHdr - 2U;
+            sock.Close(fws::WS_ABNORMAL_CLOSE, std::string_view{e.data(), std::min(e.size(), max_len)});
+        }
+        if (ret < 0 || ((sock.*(&A::server_status_)) == A::kClosed && !(sock.*(&A::in_shutting_down_))))
+            sock.under_socket().Close();
+    }
+
+    // The error texts ParseFrameHdr sets (w_socket.h:452, 468, 494-496); -3 sets none.
+    static void SetErrorText(int ret, uint32_t opcode) {
+        char t[160];
+        switch (ret) {
+        case FWS_ERR_OPCODE: std::snprintf(t, sizeof(t), "Opcode %u is not valid", opcode); break;
+        case FWS_ERR_RSV: std::snprintf(t, sizeof(t), "rev bits are not zero"); break;
+        case FWS_ERR_TOO_LARGE:
+            std::snprintf(t, sizeof(t), "payload length larger thanconstants::MAX_WS_FRAME_SIZE %zu",
+                          fws::constants::MAX_WS_FRAME_SIZE);
+            break;
+        case FWS_ERR_CONTROL_FRAME: std::snprintf(t, sizeof(t), "Control frame over 125 B or fragmented"); break;
+        case FWS_ERR_NOT_MASKED: return;
+        default: std::snprintf(t, sizeof(t), "GPU receive decode failed (%d)", ret); break;
+        }
+        fws::SetErrorString(t, std::strlen(t) + 1);
+    }
+
+    GpuContext &ctx_;
+    Sock::WsOnNewConnectionFunc user_new_conn_;
+    Sock::WSOnCloseFunc user_close_;
+    fws::TCPSocket::OnReadableFunc ref_readable_;
+    std::unordered_map<fws::TCPSocket *, Conn> conns_;
+    std::vector<std::unique_ptr<GpuRxDecoder<fws::IOBuffer>>> retired_;
+    uint64_t gpu_reads_ = 0;
+};
+
+}  // namespace fws_amd

@@ -61,8 +61,6 @@ class GpuRxDecoder {
 public:
     explicit GpuRxDecoder(GpuContext &ctx) {
         if (fws_rx_session_create(ctx.get(), 1, &s_) != 0) throw std::runtime_error("fws_rx_session_create failed");
-        events_.resize(1024);
-        ctl_.resize(4096);
     }
     ~GpuRxDecoder() { fws_rx_session_destroy(s_); }
     GpuRxDecoder(const GpuRxDecoder &) = delete;
@@ -73,20 +71,18 @@ public:
         uint8_t *data = io_buf.data + io_buf.start_pos;
         const uint64_t size = (uint64_t)io_buf.size;
         const uint64_t cap = io_buf.capacity - io_buf.start_pos;
-        // bounds: every part / control event needs >= 6 wire bytes, except the
-        // first (a continuation) and the last; control payloads fit the read
-        if (events_.size() < size / 3 + 8) events_.resize(size / 3 + 8);
-        if (ctl_.size() < size + 256) ctl_.resize(size + 256);
+        const fws_rx_event *ev = nullptr;
+        const uint8_t *ctl = nullptr;
         uint64_t n_ev = 0, ctl_used = 0;
-        const int ret = fws_rx_session_feed(s_, data, size, cap, events_.data(), events_.size(), &n_ev,
-                                            ctl_.data(), ctl_.size(), &ctl_used);
-        for (uint64_t i = 0; i < n_ev && i < events_.size(); ++i) {
-            const fws_rx_event &e = events_[i];
-            const std::string_view ctl((const char *)ctl_.data() + e.ctl_off, e.size);
+        // the session's own event / control sinks: sized by what the read holds
+        const int ret = fws_rx_session_feed_view(s_, data, size, cap, &ev, &n_ev, &ctl, &ctl_used);
+        for (uint64_t i = 0; i < n_ev; ++i) {
+            const fws_rx_event &e = ev[i];
+            const std::string_view payload((const char *)ctl + e.ctl_off, e.kind == 0 && !e.is_ctl ? 0 : e.size);
             if (e.kind == 1) {
-                sink.on_ping(ctl);
+                sink.on_ping(payload);
             } else if (e.kind == 2) {
-                sink.on_close(e.code, ctl);
+                sink.on_close(e.code, payload);
             } else if (!e.is_ctl) {
                 // aliasing view of the (now unmasked) read buffer, w_socket.h:715-728
                 sink.on_read(e.opcode,
@@ -96,19 +92,25 @@ public:
             } else {
                 // PONG payload: copied into a fresh buffer (the reference hands over
                 // its control buffer buf_, w_socket.h:729-731)
-                IOBuffer b = sink.request_buf(ctl.size());
-                for (size_t k = 0; k < ctl.size(); ++k) b.data[b.start_pos + k] = (uint8_t)ctl[k];
-                b.size = (ssize_t)ctl.size();
+                IOBuffer b = sink.request_buf(payload.size());
+                for (size_t k = 0; k < payload.size(); ++k) b.data[b.start_pos + k] = (uint8_t)payload[k];
+                b.size = (ssize_t)payload.size();
                 sink.on_read(e.opcode, std::move(b), e.frame_end != 0, e.msg_end != 0, true);
             }
         }
         return ret;
     }
 
+    // The opcode of the frame the last failing read stopped at (for the
+    // reference's error text, w_socket.h:452).
+    uint32_t error_opcode() const {
+        uint32_t op = 0;
+        (void)fws_rx_session_error(s_, &op);
+        return op;
+    }
+
 private:
     fws_rx_session *s_ = nullptr;
-    std::vector<fws_rx_event> events_;
-    std::vector<uint8_t> ctl_;
 };
 
 // SendFrame over the GPU for one connection (w_socket.h:832-944): frames are

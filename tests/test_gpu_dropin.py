@@ -1,0 +1,163 @@
+"""GPU: the north star's drop-in -- a flashws echo server on the reference's
+own FLoop + WSServerSocket<false> (compiled from the reference headers,
+oracle/_ref/ws_dropin, source tools/dropin/ws_dropin.cpp) whose receive decode
+is moved to the MI355X by ONE added call, fws_amd::GpuRxHook::Enable
+(include/flashws_amd/gpu_floop.hpp). No reference file is changed.
+
+* scripted parity: the same byte scripts (fragmented messages, interleaved
+  PINGs, every length form, random read splits, CLOSE with code and reason,
+  protocol errors) are sent by a raw client to the reference's own server and
+  to the same server with the GPU hook; everything the client receives back
+  (echo frames, PONGs, the CLOSE echo or the 1006 error close with the
+  reference's error text) and the server's on_close log must be identical;
+* load: the reference's WSClientSocket with many connections, every echoed
+  byte checked, PINGs answered, clean CLOSE handshakes, through the GPU hook.
+"""
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import wsraw
+from wsframes import frame
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DROPIN = os.path.join(ROOT, "oracle", "_ref", "ws_dropin")
+
+
+class Server:
+    def __init__(self, gpu, conns, max_seconds=90):
+        if not os.path.exists(DROPIN):
+            pytest.skip("oracle/_ref/ws_dropin not built (make -C oracle ref, build container)")
+        args = [DROPIN, "server", "--conns", str(conns), "--max-seconds", str(max_seconds)]
+        if gpu:
+            args.append("--gpu")
+        self.p = subprocess.Popen(args, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+        line = self.p.stdout.readline()
+        assert line.startswith("listening"), (line, self.p.stderr.read()[-2000:] if self.p.poll() is not None else "")
+        self.port = int(line.split()[1])
+
+    def finish(self, timeout=60):
+        out, err = self.p.communicate(timeout=timeout)
+        assert self.p.returncode == 0, err[-2000:]
+        return json.loads(out.strip().splitlines()[-1])
+
+
+def _chunks(atoms, rng, max_chunk):
+    """Send sizes for the concatenated atoms: random cut points, but never
+    inside or right after a control frame's header -- the reference server
+    dereferences a null control buffer when a read ends there (SURVEY
+    Appendix A.5), so such splits are kept out of the comparison."""
+    stream = b"".join(a for a, _ in atoms)
+    banned, pos = set(), 0
+    for a, ctl in atoms:
+        if ctl:
+            banned.update(range(pos + 1, pos + len(a)))
+        pos += len(a)
+    cuts, p = [], 0
+    while True:
+        p += int(rng.integers(1, max_chunk + 1))
+        if p >= len(stream):
+            break
+        if p not in banned:
+            cuts.append(p)
+    bounds = [0] + cuts + [len(stream)]
+    return stream, [b - a for a, b in zip(bounds, bounds[1:])]
+
+
+def _scripts():
+    rng = np.random.default_rng(2026)
+
+    def key():
+        return int(rng.integers(0, 2**32))
+
+    def msg(op, payload, pieces=1, ping_after=None):
+        atoms, n = [], len(payload)
+        cuts = sorted(set(int(x) for x in rng.integers(0, n + 1, pieces - 1))) if pieces > 1 else []
+        bounds = [0] + cuts + [n]
+        for k in range(len(bounds) - 1):
+            first, last = k == 0, k == len(bounds) - 2
+            atoms.append((frame(op if first else 0, payload[bounds[k]:bounds[k + 1]], fin=int(last), key=key()),
+                          False))
+            if ping_after == k:
+                atoms.append((frame(9, b"mid-message ping", key=key()), True))
+        return atoms
+
+    def rand_payload(n):
+        return rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+
+    mixed = []
+    for i in range(60):
+        n = int(rng.choice([0, 1, 5, 125, 126, 127, 1000, 4096, 65535, 65536, 70000, int(rng.integers(0, 20000))]))
+        op = int(rng.choice([1, 2]))
+        pl = rand_payload(n) if op == 2 else bytes(rng.integers(32, 127, n, dtype=np.uint8))
+        pieces = int(rng.choice([1, 1, 2, 3]))
+        mixed += msg(op, pl, pieces, ping_after=0 if (pieces > 1 and i % 3 == 0) else None)
+        if i % 7 == 0:
+            mixed.append((frame(9, rand_payload(int(rng.integers(0, 126))), key=key()), True))
+    good = [(frame(2, b"some data before the error"), False)]
+    byte_wise = [(frame(2, rand_payload(300 + k)), False) for k in range(5)]
+    s_byte, c_byte = _chunks(byte_wise, rng, 1)
+    close = wsraw.close_frame(1000)
+    return {
+        "mixed_then_close": _chunks(mixed + [(wsraw.close_frame(1000, b"done"), True)], rng, 9000),
+        "close_code_only": _chunks([(frame(2, b"x" * 300), False), (wsraw.close_frame(1001), True)], rng, 11),
+        "ping_125_then_close": _chunks([(frame(9, bytes(range(125))), True), (frame(1, b"hello"), False),
+                                        (wsraw.close_frame(1000, b"ok"), True)], rng, 200),
+        "err_rsv1": _chunks(good + [(bytes([0xC2, 0x80]) + b"\0" * 8, False)], rng, 9),
+        "err_opcode3": _chunks(good + [(bytes([0x83, 0x85, 1, 2, 3, 4]) + b"abcde", False)], rng, 40),
+        "err_len_2p32p1": _chunks(good + [(bytes([0x82, 0xFF]) + (2**32 + 1).to_bytes(8, "big") + b"\0" * 4, False)],
+                                  rng, 4),
+        "split_header_every_byte": (s_byte + close, c_byte + [len(close)]),
+    }
+
+
+SCRIPTS = _scripts()
+
+
+def _run_all(gpu):
+    srv = Server(gpu, conns=len(SCRIPTS))
+    got = {}
+    for name, (stream, chunks) in SCRIPTS.items():
+        head, data = wsraw.run_script(srv.port, stream, chunks)
+        got[name] = (head, data)
+    return got, srv.finish()
+
+
+def test_dropin_scripted_parity_with_reference_server(cuda):
+    ref, ref_srv = _run_all(gpu=False)
+    gpu, gpu_srv = _run_all(gpu=True)
+    assert gpu_srv["gpu_reads"] > 0 and ref_srv["gpu_reads"] == 0
+    for name in SCRIPTS:
+        assert gpu[name][0] == ref[name][0], name                     # handshake reply
+        assert gpu[name][1] == ref[name][1], (name, wsraw.parse_server_frames(ref[name][1])[-2:],
+                                              wsraw.parse_server_frames(gpu[name][1])[-2:])
+    assert gpu_srv["msgs"] == ref_srv["msgs"] and gpu_srv["bytes"] == ref_srv["bytes"]
+    assert gpu_srv["close_log_hex"] == ref_srv["close_log_hex"]
+    # what the scripts must have produced (not only equal, also right)
+    fr = wsraw.parse_server_frames(gpu["err_rsv1"][1])
+    assert fr[0][1] == 2 and fr[-1][1] == 8
+    assert fr[-1][2][:2] == (1006).to_bytes(2, "big") and fr[-1][2][2:] == b"rev bits are not zero"
+    fr = wsraw.parse_server_frames(gpu["err_opcode3"][1])
+    assert fr[-1][2][2:] == b"Opcode 3 is not valid"
+    fr = wsraw.parse_server_frames(gpu["mixed_then_close"][1])
+    assert fr[-1] == (1, 8, (1000).to_bytes(2, "big") + b"done")
+    assert sum(1 for f in fr if f[1] == 10) > 0                       # PONGs
+
+
+@pytest.mark.parametrize("clients,msg_len", [(1, 4096), (8, 4096), (4, 70000), (16, 512)])
+def test_dropin_reference_client_load(cuda, clients, msg_len):
+    srv = Server(True, conns=clients)
+    r = subprocess.run([DROPIN, "client", "--port", str(srv.port), "--clients", str(clients), "--msgs", "600",
+                        "--warmup", "20", "--msg-len", str(msg_len), "--ping-every", "50", "--max-seconds", "60"],
+                       capture_output=True, text=True, timeout=90)
+    assert r.returncode == 0, (r.stdout, r.stderr[-2000:])
+    cli = json.loads(r.stdout.strip().splitlines()[-1])
+    st = srv.finish()
+    assert cli["verified"] is True and cli["pongs"] == clients * (620 // 50)
+    assert st["gpu_reads"] > 0 and st["msgs"] == clients * 620
+    assert all(c == [1000, b"bye".hex()] for c in st["close_log_hex"][:clients])

@@ -332,7 +332,7 @@ __device__ __forceinline__ bool utf8_chunk_bad(const u32x4 &u, uint32_t prev, ui
     return (e0 | utf8_err(x.y, x.x) | utf8_err(x.z, x.y) | utf8_err(x.w, x.z)) != 0u;
 }
 
-template <bool kNT, bool kUtf8>
+template <bool kNT, bool kUtf8, bool kRev>
 __global__ __launch_bounds__(kBlock) void k_unmask_stream(uint8_t *base, uint64_t N,
                                                           const fws_frame_info *__restrict__ fr, uint32_t cap,
                                                           const uint32_t *__restrict__ n_dev,
@@ -345,7 +345,11 @@ __global__ __launch_bounds__(kBlock) void k_unmask_stream(uint8_t *base, uint64_
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const uint64_t nwaves = uint64_t(gridDim.x) * (kBlock / kWave);
     const uintptr_t b0 = (uintptr_t)base;
-    for (uint64_t u = uint64_t(blockIdx.x) * (kBlock / kWave) + wave; u < n_units; u += nwaves) {
+    for (uint64_t ui = uint64_t(blockIdx.x) * (kBlock / kWave) + wave; ui < n_units; ui += nwaves) {
+        // kRev: the first-dispatched waves take the END of the stream, which the
+        // decode's scan read last -- those lines are still in the 256 MB
+        // Infinity Cache (MALL) when this pass re-reads them
+        const uint64_t u = kRev ? n_units - 1u - ui : ui;
         const uint32_t flo = unit_first[u];
         const uint32_t fhi = (u + 1 < n_units) ? unit_first[u + 1] : n - 1;
         const uint64_t c0 = u * 4096u + uint64_t(lane) * 16u;
@@ -1093,6 +1097,15 @@ extern "C" __attribute__((visibility("default"))) int fws_internal_set_sorted_ut
     return old;
 }
 
+// tuning hook: k_unmask_stream variant -- 0 forward nontemporal, 1 reverse
+// nontemporal, 2 forward default policy, 3 reverse default policy
+static int g_stream_variant = 0;
+extern "C" __attribute__((visibility("default"))) int fws_internal_set_stream_variant(int v) {
+    const int old = g_stream_variant;
+    if (v >= 0 && v <= 3) g_stream_variant = v;
+    return old;
+}
+
 static int grid_for_units(uint64_t units) {
     // memory-bound: cap near 256 CUs x 8 blocks and grid-stride the rest
     uint64_t blocks = (units + (kBlock / kWave) - 1) / (kBlock / kWave);
@@ -1156,12 +1169,28 @@ int fws_launch_unmask_stream(uint8_t *base, uint64_t N, const fws_frame_info *fr
                              const uint32_t *n_dev, const uint32_t *unit_first, uint8_t *utf8_ok, hipStream_t s) {
     const uint64_t units = (N + 4095) / 4096;
     if (units == 0 || cap == 0) return 0;
+    const dim3 grid(grid_for_units(units)), blk(kBlock);
+    const int v = g_stream_variant;
     if (utf8_ok == nullptr) {
-        hipLaunchKernelGGL((k_unmask_stream<true, false>), dim3(grid_for_units(units)), dim3(kBlock), 0, s,
-                           (uint8_t *)base, N, frames, cap, n_dev, unit_first, units, nullptr);
+        if (v == 0)
+            hipLaunchKernelGGL((k_unmask_stream<true, false, false>), grid, blk, 0, s, (uint8_t *)base, N, frames, cap,
+                               n_dev, unit_first, units, nullptr);
+        else if (v == 1)
+            hipLaunchKernelGGL((k_unmask_stream<true, false, true>), grid, blk, 0, s, (uint8_t *)base, N, frames, cap,
+                               n_dev, unit_first, units, nullptr);
+        else if (v == 2)
+            hipLaunchKernelGGL((k_unmask_stream<false, false, false>), grid, blk, 0, s, (uint8_t *)base, N, frames,
+                               cap, n_dev, unit_first, units, nullptr);
+        else
+            hipLaunchKernelGGL((k_unmask_stream<false, false, true>), grid, blk, 0, s, (uint8_t *)base, N, frames,
+                               cap, n_dev, unit_first, units, nullptr);
     } else {
-        hipLaunchKernelGGL((k_unmask_stream<true, true>), dim3(grid_for_units(units)), dim3(kBlock), 0, s,
-                           (uint8_t *)base, N, frames, cap, n_dev, unit_first, units, utf8_ok);
+        if (v == 1 || v == 3)
+            hipLaunchKernelGGL((k_unmask_stream<true, true, true>), grid, blk, 0, s, (uint8_t *)base, N, frames, cap,
+                               n_dev, unit_first, units, utf8_ok);
+        else
+            hipLaunchKernelGGL((k_unmask_stream<true, true, false>), grid, blk, 0, s, (uint8_t *)base, N, frames, cap,
+                               n_dev, unit_first, units, utf8_ok);
         hipLaunchKernelGGL(k_utf8_seam, dim3((unsigned)((units + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
                            (const uint8_t *)base, N, frames, cap, n_dev, unit_first, units, utf8_ok);
     }

@@ -499,7 +499,7 @@ def stream_decode_extra(ctx, wire_c2, dev, args):
         payload = int(gpu.read_frames(frames, n_frames)["payload_len"].sum())
         rec = {"GiB_per_s": round(payload / t / GIB, 1), "ms_per_step": round(t * 1e3, 4), "frames": n_frames,
                "wire_bytes": len(wire), "alg_GB_per_s": round((len(wire) + payload) / t / 1e9, 1),
-               "resolve": "k_resolve (fallback)" if gpu.decode_fell_back(c) else "super-tile"}
+               "big_super_tiles": gpu.decode_counters(c)["big_super_tiles"]}
         if utf8:
             rec["utf8_invalid_frames"] = int((ok[:n_frames] == 0).sum().item())
         if pipelined and nbuf >= 4:

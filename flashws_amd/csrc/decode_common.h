@@ -1,5 +1,5 @@
 // decode_common.h -- constants and node encodings shared by the stream-decode
-// kernels: k_scan (decode_kernels.hip) and k_resolve (resolve_kernels.hip).
+// kernels: k_scan (decode_kernels.hip) and the resolve (merge_kernels.hip).
 #pragma once
 
 #include "fws_device.h"
@@ -21,18 +21,19 @@ __device__ __forceinline__ bool is_term(uint32_t v) { return v >= kTermIncomplet
 // dec.counters[] (zeroed before every decode)
 enum Counter {
     kCntSurv = 0,        // survivors (sum of the tiles' counts)
-    kCntOverflow = 1,    // bit 0: survivor capacity exceeded; bit 1: grid barrier timed out
-    kCntBarArrive = 2,   // k_resolve grid barrier: arrivals (monotonic within a launch)
+    kCntOverflow = 1,    // bit 0: k_scan's survivor spill capacity exceeded
+    kCntUnused2 = 2,
     kCntFrames = 3,      // frames emitted (device frame count, read by the unmask)
     kCntRoot = 4,        // survivor index of the header at offset 0 (kNone if absent)
     kCntTerm = 5,        // terminal code of the path
     kCntLast = 6,        // last path node
     kCntSpill = 7,       // survivors spilled by dense tiles
-    kCntBarGen = 8,      // k_resolve grid barrier: generation
-    kCntFallback = 9,    // super-tile resolve declined (dense super tile, capacity): k_resolve runs
-    kCntTicket = 10,     // k_merge workgroups finished (the last one resolves the path)
+    kCntUnused8 = 8,
+    kCntFallback = 9,    // the resolve failed (workspace capacity): the result says so, k_emit skips
+    kCntTicket = 10,     // k_link workgroups finished (the last one resolves the path)
     kCntTails = 11,      // super-tile exit tails appended by k_merge
-    kCntCount = 12
+    kCntBig = 12,        // super tiles that took k_merge's big-ST path (diagnostic)
+    kCntCount = 13
 };
 constexpr uint32_t kCntStride = 16;          // words per counter set (fws_decode_ws::cnt_base)
 static_assert(kCntFrames == kDecodeFramesCounter, "fws_internal.h names the frame counter");

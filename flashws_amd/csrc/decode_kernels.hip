@@ -521,12 +521,6 @@ __global__ __launch_bounds__(kScanThreads) __attribute__((amdgpu_waves_per_eu(5,
 // ------------------------------------------------------------------ host side
 using namespace fwsk;
 
-static uint32_t ceil_log2(uint64_t x) {
-    uint32_t k = 0;
-    while ((1ull << k) < x) ++k;
-    return k;
-}
-
 #ifdef FWS_SCAN_PROF
 extern "C" int fws_internal_scan_prof(unsigned long long *out, int reset) {
     hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(fwsk::g_scan_prof), sizeof(unsigned long long) * 16);
@@ -538,8 +532,9 @@ extern "C" int fws_internal_scan_prof(unsigned long long *out, int reset) {
 }
 #endif
 
-// tuning / test hook: 0 = super-tile resolve with k_resolve fallback, 1 = k_resolve only,
-// 2 = the RX session's small-read kernel first (fws_gpu_decode_stream, tests only)
+// tuning / test hook: 0 = super-tile resolve (LDS tables, big-ST path for dense super
+// tiles), 1 = every super tile on the big-ST path, 2 = the RX session's small-read
+// kernel first (fws_gpu_decode_stream, tests only)
 static int g_resolve_mode = 0;
 extern "C" __attribute__((visibility("default"))) int fws_internal_set_resolve_mode(int m) {
     const int old = g_resolve_mode;
@@ -559,26 +554,18 @@ int fws_decode_ensure(fws_gpu_ctx *ctx, uint64_t N, uint32_t cap) {
     const uint64_t tiles = (N + kTile - 1) / kTile + 1;
     uint64_t s_cap = N / 256 + 8 * tiles + (uint64_t)cap + 64;
     if (ctx->cap_frames + 8 * tiles > s_cap) s_cap = ctx->cap_frames + 8 * tiles;
-    const uint32_t levels = ceil_log2(2 * tiles + 2) + 1;
-    if (tiles <= d.max_tiles && s_cap <= d.max_surv && levels <= d.levels && cap <= d.max_descs) return 0;
+    if (tiles <= d.max_tiles && s_cap <= d.max_surv) return 0;
     const uint64_t nt = tiles > d.max_tiles ? tiles : d.max_tiles;
     const uint64_t ns = s_cap > d.max_surv ? s_cap : d.max_surv;
-    const uint32_t nl = levels > d.levels ? levels : d.levels;
-    const uint64_t nd = cap > d.max_descs ? cap : d.max_descs;
     auto rel = [](auto *&p) { if (p) (void)hipFree(p); p = nullptr; };
-    rel(d.tile_count); rel(d.tile_base); rel(d.tile_entry); rel(d.tile_frames); rel(d.fbase);
-    rel(d.surv_info); rel(d.surv_leaf); rel(d.jump); rel(d.on_path); rel(d.cnt_base);
-    rel(d.descs); rel(d.stage_info); rel(d.stage_leaf); rel(d.spill_info); rel(d.spill_leaf); rel(d.tile_spill);
+    rel(d.tile_count); rel(d.cnt_base);
+    rel(d.stage_info); rel(d.stage_leaf); rel(d.spill_info); rel(d.spill_leaf); rel(d.tile_spill);
     hipError_t e = hipSuccess;
     auto al = [&](auto **p, uint64_t bytes) { if (e == hipSuccess) e = hipMalloc((void **)p, bytes ? bytes : 16); };
-    al(&d.tile_count, nt * 4); al(&d.tile_base, nt * 4); al(&d.tile_entry, nt * 4);
-    al(&d.tile_frames, nt * 4); al(&d.fbase, nt * 4);
-    al(&d.surv_info, ns * sizeof(fws_frame_info)); al(&d.surv_leaf, ns * 4);
-    al(&d.jump, (uint64_t)nl * ns * 4); al(&d.on_path, ns);
+    al(&d.tile_count, nt * 4);
     al(&d.cnt_base, 2 * kCntStride * 4);
     d.counters = d.cnt_base;
     d.cnt_dirty = true;
-    al(&d.descs, (nd + 1) * sizeof(fws_frame_desc));
     if (d.scan_grid == 0) {
         int cus = 0;
         if ((e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device)) != hipSuccess)
@@ -586,29 +573,24 @@ int fws_decode_ensure(fws_gpu_ctx *ctx, uint64_t N, uint32_t cap) {
         d.scan_grid = (uint32_t)cus * (g_scan_blocks_per_cu ? g_scan_blocks_per_cu : kScanBlocksPerCu);
     }
     if (d.scan_dummy == nullptr) al(&d.scan_dummy, (uint64_t)d.scan_grid * kScanWaves * 64u);
-    if (d.resolve_grid == 0) {
-        int cus = 0, coop = 0;
-        if ((e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device)) != hipSuccess ||
-            (e = hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, ctx->device)) != hipSuccess)
-            return fws_hip_status(e);
-        if (!coop) return FWS_ERR_NO_DEVICE;
-        d.resolve_grid = (uint32_t)cus;                       // one k_resolve workgroup per CU
-    }
-    if (d.rbsums == nullptr) al(&d.rbsums, (uint64_t)d.resolve_grid * 8u);
     al(&d.stage_info, nt * kSlots * sizeof(fws_frame_info)); al(&d.stage_leaf, nt * kSlots * 4);
     al(&d.spill_info, ns * sizeof(fws_frame_info)); al(&d.spill_leaf, ns * 4); al(&d.tile_spill, nt * 4);
-    // super-tile resolve: results per slot id, EXIT tails, per-ST bases
-    rel(d.nres); rel(d.tails); rel(d.gnx); rel(d.tmark); rel(d.comp); rel(d.st_nodes); rel(d.st_n); rel(d.st_entry); rel(d.st_fbase);
+    // super-tile resolve: results per slot id, EXIT tails, per-ST bases, big-ST scratch
+    rel(d.nres); rel(d.tails); rel(d.gnx); rel(d.tmark); rel(d.comp); rel(d.st_nodes); rel(d.st_n); rel(d.st_entry);
+    rel(d.st_fbase); rel(d.bg_nx); rel(d.bg_wt); rel(d.bg_lref); rel(d.bg_ptr); rel(d.bg_sc); rel(d.bg_mark);
     const uint64_t nst = fws_merge_super_tiles(nt);
     const uint32_t tcap = fws_merge_tail_cap(nt);
-    al(&d.nres, (nt * kSlots + ns) * sizeof(fws_node_res));
+    const uint64_t nn = nt * kSlots + ns;
+    al(&d.nres, nn * sizeof(fws_node_res));
     al(&d.tails, (uint64_t)tcap * sizeof(fws_tail_rec)); al(&d.gnx, (uint64_t)tcap * 4); al(&d.tmark, ((uint64_t)tcap / 32 + 1) * 4);
     al(&d.comp, (uint64_t)fws_merge_comp_cap() * 4);
     al(&d.st_nodes, fws_merge_st_nodes(nt) * sizeof(fws_st_node)); al(&d.st_n, nst * 4);
     al(&d.st_entry, nst * 4); al(&d.st_fbase, nst * 4);
+    al(&d.bg_nx, nn * 4); al(&d.bg_wt, nn * 4); al(&d.bg_lref, nn * 4); al(&d.bg_ptr, 2 * nn * 4);
+    al(&d.bg_sc, 2 * nn * 4); al(&d.bg_mark, nn * 4);
     if (e != hipSuccess) return fws_hip_status(e);
-    d.max_tiles = nt; d.max_surv = ns; d.levels = nl; d.max_descs = nd;
-    d.max_nodes = nt * kSlots + ns; d.max_st = nst; d.tail_cap = tcap;
+    d.max_tiles = nt; d.max_surv = ns;
+    d.max_nodes = nn; d.max_st = nst; d.tail_cap = tcap;
     return 0;
 }
 
@@ -616,9 +598,8 @@ int fws_launch_decode(fws_gpu_ctx *ctx, uint8_t *wire, uint64_t N, fws_frame_inf
                       fws_decode_result *res, uint8_t *utf8_ok, hipStream_t s) {
     fws_decode_ws &d = ctx->dec;
     const uint32_t n_tiles = (uint32_t)((N + kTile - 1) / kTile);
-    const uint32_t K = ceil_log2(2ull * n_tiles + 2) + 1;
     hipError_t e;
-    // counters: this call's set was zeroed by the previous call's k_resolve launch
+    // counters: this call's set was zeroed by the previous call's k_emit launch
     d.parity ^= 1u;
     d.counters = d.cnt_base + d.parity * kCntStride;
     uint32_t *const next = d.cnt_base + (d.parity ^ 1u) * kCntStride;
@@ -635,14 +616,10 @@ int fws_launch_decode(fws_gpu_ctx *ctx, uint8_t *wire, uint64_t N, fws_frame_inf
                            d.tile_count, d.counters, (uint32_t)d.max_surv, d.scan_dummy);
         if ((e = hipGetLastError()) != hipSuccess) return fws_hip_status(e);
     }
-    // super-tile resolve (common case); k_resolve runs only if it set kCntFallback.
-    // Slot ids are 32-bit (8 per tile): streams of 2^39 B and more take k_resolve.
-    const bool fast = N < (1ull << 39) && g_resolve_mode != 1;   // mode 2 decodes as mode 0 here
-    if (fast) {
-        int r = fws_launch_merge(ctx, wire, N, n_tiles, frames, cap, res, utf8_ok, s);
-        if (r) return r;
-    }
-    const int r = fws_launch_resolve(ctx, wire, N, n_tiles, K, frames, cap, res, fast ? 1 : 0, next, utf8_ok, s);
+    // super-tile resolve; g_resolve_mode 1 sends every super tile down the big-ST
+    // path (tests), mode 2 decodes as mode 0 here. Slot ids are 32-bit.
+    if (N >= (1ull << 39)) return FWS_ERR_CAPACITY;
+    const int r = fws_launch_merge(ctx, wire, N, n_tiles, frames, cap, res, utf8_ok, g_resolve_mode == 1, next, s);
     if (r == 0) d.cnt_dirty = false;
     return r;
 }

@@ -64,7 +64,7 @@ extern "C" {
 // decode on ctx (decode_common.h Counter), synchronously. 0 or an error.
 __attribute__((visibility("default"))) int fws_internal_decode_counters(fws_gpu_ctx *ctx, uint32_t *out, int n) {
     if (!ctx || !out || n <= 0 || !ctx->dec.counters) return FWS_ERR_INVALID;
-    if (n > 12) n = 12;
+    if (n > 16) n = 16;
     return fws_hip_status(hipMemcpy(out, ctx->dec.counters, (size_t)n * 4, hipMemcpyDeviceToHost));
 }
 
@@ -108,23 +108,13 @@ void fws_gpu_ctx_destroy(fws_gpu_ctx *ctx) {
     free_plan(ctx->plan);
     fws_decode_ws &d = ctx->dec;
     dev_free(d.tile_count);
-    dev_free(d.tile_base);
-    dev_free(d.tile_entry);
-    dev_free(d.tile_frames);
-    dev_free(d.fbase);
-    dev_free(d.surv_info);
-    dev_free(d.surv_leaf);
-    dev_free(d.jump);
-    dev_free(d.on_path);
     dev_free(d.cnt_base);
-    dev_free(d.descs);
     dev_free(d.stage_info);
     dev_free(d.stage_leaf);
     dev_free(d.spill_info);
     dev_free(d.spill_leaf);
     dev_free(d.tile_spill);
     dev_free(d.scan_dummy);
-    dev_free(d.rbsums);
     dev_free(d.nres);
     dev_free(d.tails);
     dev_free(d.gnx);
@@ -134,6 +124,12 @@ void fws_gpu_ctx_destroy(fws_gpu_ctx *ctx) {
     dev_free(d.st_n);
     dev_free(d.st_entry);
     dev_free(d.st_fbase);
+    dev_free(d.bg_nx);
+    dev_free(d.bg_wt);
+    dev_free(d.bg_lref);
+    dev_free(d.bg_ptr);
+    dev_free(d.bg_sc);
+    dev_free(d.bg_mark);
     delete ctx;
 }
 

@@ -52,8 +52,11 @@ struct fws_plan_mode {
 
 // Super-tile resolve records (merge_kernels.hip).
 struct fws_node_res {                 // per survivor: its chain inside its super tile
-    uint32_t tail;                    // EXIT: tail-list index; else the tail's ST-local index
-    uint32_t cnt_kind;                // frames up to the tail | ST-local index | kind (merge_kernels.hip)
+    uint32_t tail;                    // EXIT: tail-list index; else the chain's tail survivor
+                                      //   (ST-local index, or slot id on the big-ST path)
+    uint32_t cnt;                     // frames from this survivor up to and including the tail
+    uint32_t ent;                     // this survivor as its ST's entry: ST-local index / slot id
+    uint32_t kind;                    // merge_kernels.hip kKind* | kBigBit
 };
 struct fws_tail_rec {                 // one EXIT tail: a chain leaving its super tile
     uint64_t exit;                    // offset of the next header
@@ -67,26 +70,15 @@ struct fws_tail_rec {                 // one EXIT tail: a chain leaving its supe
 // slot id (bits 0-31) | in-ST next or exit code (32-47) | frame bit (48)
 typedef uint64_t fws_st_node;
 
-// Stream-decode workspace (decode_kernels.hip).
+// Stream-decode workspace (decode_kernels.hip, merge_kernels.hip).
 struct fws_decode_ws {
     uint64_t max_tiles = 0;
-    uint64_t max_surv = 0;            // capacity of the survivor arrays
-    uint64_t max_descs = 0;
-    uint32_t levels = 0;              // pointer-doubling tables allocated
+    uint64_t max_surv = 0;            // capacity of the spill survivor arrays
     uint32_t *tile_count = nullptr;   // survivors per tile
-    uint32_t *tile_base = nullptr;    // first survivor index of each tile
-    uint32_t *tile_entry = nullptr;   // survivor index of the tile's first true header
-    uint32_t *tile_frames = nullptr;  // true frames per tile
-    uint32_t *fbase = nullptr;        // exclusive prefix of tile_frames
-    fws_frame_info *surv_info = nullptr;
-    uint32_t *surv_leaf = nullptr;    // leaf (last in-tile header) of each survivor's chain
-    uint32_t *jump = nullptr;         // [levels][max_surv] pointer-doubling tables
-    uint8_t *on_path = nullptr;       // survivor is a true frame header
     uint32_t *counters = nullptr;     // this call's set (decode_common.h Counter)
-    uint32_t *cnt_base = nullptr;     // two sets of kCntStride words: a call uses one, its k_resolve
+    uint32_t *cnt_base = nullptr;     // two sets of kCntStride words: a call uses one, its k_emit
     uint32_t parity = 0;              //   launch zeroes the other for the next call (no memset launch)
     bool cnt_dirty = true;            // zero this call's set first (new allocation, failed call)
-    fws_frame_desc *descs = nullptr;  // payload regions of the decoded frames
     fws_frame_info *stage_info = nullptr;  // per-tile survivor slots (k_scan)
     uint32_t *stage_leaf = nullptr;
     fws_frame_info *spill_info = nullptr;  // survivors of dense tiles
@@ -94,8 +86,6 @@ struct fws_decode_ws {
     uint32_t *tile_spill = nullptr;        // spill offset of a dense tile, or ~0
     uint32_t scan_grid = 0;                // persistent k_scan workgroups
     uint32_t *scan_dummy = nullptr;        // one 64-B line per k_scan wavefront (idle-lane stores)
-    uint32_t resolve_grid = 0;             // cooperative k_resolve workgroups (one per CU)
-    uint64_t *rbsums = nullptr;            // k_resolve per-workgroup partial sums
     // super-tile resolve (merge_kernels.hip)
     uint64_t max_nodes = 0;                // slot ids: tiles * 8 + spill capacity
     uint64_t max_st = 0;
@@ -105,10 +95,18 @@ struct fws_decode_ws {
     uint32_t *gnx = nullptr;               // [tail_cap] next tail / terminal
     uint32_t *tmark = nullptr;             // [tail_cap / 32 + 1] tails that are some tail's next
     uint32_t *comp = nullptr;              // [fws_merge_comp_cap()] marked tails, compacted
-    fws_st_node *st_nodes = nullptr;       // [max_st * 2048] survivors per super tile (8 B each)
+    fws_st_node *st_nodes = nullptr;       // [max_st * kStCap] survivors per super tile (8 B each)
     uint32_t *st_n = nullptr;              // [max_st] survivors per super tile
-    uint32_t *st_entry = nullptr;          // [max_st] slot id of the path's first header in the ST
+    uint32_t *st_entry = nullptr;          // [max_st] the path's first header in the ST (local index / slot id)
     uint32_t *st_fbase = nullptr;          // [max_st] frames before the ST
+    // big-ST path: super tiles with more survivors than LDS holds (dense small
+    // frames) run the same merge / emit over these, indexed by slot id
+    uint32_t *bg_nx = nullptr;             // [max_nodes] in-ST next slot id or exit code
+    uint32_t *bg_wt = nullptr;             // [max_nodes] 1: a frame; 0: incomplete header
+    uint32_t *bg_lref = nullptr;           // [max_nodes] EXIT tail's index in the ST's tail run
+    uint32_t *bg_ptr = nullptr;            // [2][max_nodes] pointer jumping
+    uint32_t *bg_sc = nullptr;             // [2][max_nodes] frame counts
+    uint32_t *bg_mark = nullptr;           // [max_nodes] k_emit: on the path
 };
 
 struct fws_gpu_ctx {
@@ -158,15 +156,12 @@ int fws_decode_ensure(fws_gpu_ctx *ctx, uint64_t N, uint32_t cap);
 // utf8_ok (optional): per-frame UTF-8 flags, preset here, finished by fws_launch_unmask_stream
 int fws_launch_decode(fws_gpu_ctx *ctx, uint8_t *wire, uint64_t N, fws_frame_info *frames, uint32_t cap,
                       fws_decode_result *res, uint8_t *utf8_ok, hipStream_t s);
-// resolve_kernels.hip: frames, descriptors and the unmask plan from k_scan's survivors
-// gate != 0: only if the super-tile resolve set kCntFallback (else the launch returns at once)
-int fws_launch_resolve(fws_gpu_ctx *ctx, const uint8_t *wire, uint64_t N, uint32_t n_tiles, uint32_t K,
-                       fws_frame_info *frames, uint32_t cap, fws_decode_result *res, int gate,
-                       uint32_t *zero_next, uint8_t *utf8_ok, hipStream_t s);
-// merge_kernels.hip: the super-tile resolve (k_merge + k_emit), the common path
+// merge_kernels.hip: from k_scan's survivors to the frame list, the result and the
+// unmask plan (k_merge -> k_link + path -> k_emit); no grid barrier anywhere
 uint64_t fws_merge_super_tiles(uint64_t n_tiles);
 uint32_t fws_merge_tail_cap(uint64_t n_tiles);
 uint64_t fws_merge_st_nodes(uint64_t n_tiles);
 uint32_t fws_merge_comp_cap();
 int fws_launch_merge(fws_gpu_ctx *ctx, const uint8_t *wire, uint64_t N, uint32_t n_tiles, fws_frame_info *frames,
-                     uint32_t cap, fws_decode_result *res, uint8_t *utf8_ok, hipStream_t s);
+                     uint32_t cap, fws_decode_result *res, uint8_t *utf8_ok, bool force_big, uint32_t *zero_next,
+                     hipStream_t s);

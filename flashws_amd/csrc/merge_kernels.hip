@@ -1,6 +1,6 @@
-// merge_kernels.hip -- second half of fws_gpu_decode_stream on the common
-// path: from k_scan's per-tile survivors to the frame list and the unmask
-// plan in three launches, with no grid barrier.
+// merge_kernels.hip -- second half of fws_gpu_decode_stream: from k_scan's
+// per-tile survivors to the frame list, the result and the unmask plan in
+// three launches, with no grid barrier (no launch depends on co-residency).
 //
 // OnRecvData's frame loop (net/w_socket.h:543-769) is a chain: the next
 // header starts at this header's exit (hdr_off + hdr_len + payload_len,
@@ -17,7 +17,10 @@
 //           end), DEAD (the exit is not a header: a protocol error or a false
 //           chain) or INC (an incomplete header at the stream end). EXIT
 //           tails go to a global list; the ST's survivors are also written as
-//           one contiguous table for k_emit.
+//           one contiguous table for k_emit. A super tile with more survivors
+//           than the LDS tables hold (dense small frames: 64 B frames put
+//           ~3700 headers in one ST) runs the same steps over global scratch
+//           indexed by slot id (the big-ST path), in the same workgroup.
 //  k_link   one thread per EXIT tail: the survivor its exit lands on (the
 //           tile's slots, one batch of loads) and next(tail) = the tail of
 //           that survivor's chain; marks every next() target in a bitmap.
@@ -26,10 +29,13 @@
 //           compacted into LDS. The path's tails are the greatest fixpoint of
 //           K = {root's tail} U next(K): offsets strictly increase along next,
 //           so a false tail has a finite chain of predecessors and drops out
-//           after a few rounds. Each landing survivor on the path is its ST's
-//           entry; a scan over the STs gives every ST's first frame index.
-//           The terminal is finished with ParseFrameHdr's rules
-//           (w_socket.h:435-524): error walk, carry-out, fws_decode_result.
+//           after a few rounds (an input that keeps one alive for 64 rounds
+//           is walked serially from the root instead). Each landing survivor
+//           on the path is its ST's entry; a scan over the STs gives every
+//           ST's first frame index. The terminal is finished with
+//           ParseFrameHdr's rules (w_socket.h:435-524): error walk, carry-out,
+//           fws_decode_result. Workspace limits (k_scan's survivor spill, the
+//           tail list) end the decode with FWS_ERR_CAPACITY in the result.
 //  k_emit   one workgroup per ST with an entry: marks the entry's chain by
 //           pointer doubling over the ST's table and writes fws_frame_info in
 //           stream order and the unmask plan: unit_first[u] = the frame whose
@@ -39,11 +45,6 @@
 // Every global access on these paths is metadata (about 1 survivor per KiB of
 // stream); the kernels are latency-bound, so loads are issued in batches of
 // independent addresses before their uses.
-//
-// A super tile with more than kStCap survivors (dense small frames), a full
-// tail list, a survivor overflow in k_scan or a pruning that does not settle
-// sets kCntFallback: k_emit then returns at once and the cooperative k_resolve
-// (resolve_kernels.hip) does the whole job.
 #include "decode_common.h"
 
 namespace fwsk {
@@ -94,14 +95,25 @@ __device__ unsigned long long g_merge_prof[32];
 #define MP_SPAN(k0, k1) do { } while (0)
 #endif
 
-// fws_node_res::cnt_kind = frames (bits 0-11) | ST-local index (12-22) | kind (30-31)
-__device__ __forceinline__ uint32_t res_cnt(uint32_t ck) { return ck & 0xFFFu; }
-__device__ __forceinline__ uint32_t res_lidx(uint32_t ck) { return (ck >> 12) & 0x7FFu; }
-__device__ __forceinline__ uint32_t res_kind(uint32_t ck) { return ck >> 30; }
-static_assert(kStCap <= 2048, "cnt_kind packing: 12-bit counts, 11-bit local indices");
+// fws_node_res::kind = kKind* | kBigBit (tail / ent are slot ids, not ST-local indices)
+constexpr uint32_t kBigBit = 4u;
+__device__ __forceinline__ uint32_t res_kind(const fws_node_res &r) { return r.kind & 3u; }
 
 __device__ __forceinline__ uint32_t kind_of(uint16_t code) {
     return code == kNxExit ? kKindExit : code == kNxEnd ? kKindEnd : code == kNxDead ? kKindDead : kKindInc;
+}
+
+// big-ST path: in-ST next as a slot id, or how the chain leaves the ST
+constexpr uint32_t kBgInc = 0xFFFFFFFCu, kBgDead = 0xFFFFFFFDu, kBgEnd = 0xFFFFFFFEu, kBgExit = 0xFFFFFFFFu;
+__device__ __forceinline__ uint32_t bg_kind(uint32_t code) {
+    return code == kBgExit ? kKindExit : code == kBgEnd ? kKindEnd : code == kBgDead ? kKindDead : kKindInc;
+}
+// relaxed agent-scope accesses: coherent in L2 across the waves of a workgroup
+__device__ __forceinline__ uint32_t gld(const uint32_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void gst(uint32_t *p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 struct MergeParams {
@@ -131,6 +143,16 @@ struct MergeParams {
     uint8_t *utf8_ok;                                // optional: preset per frame (TEXT, FIN, complete)
     uint32_t *unit_first;                            // unmask plan (fws_plan_ws), stream space
     uint64_t n_units;                                // ceil(N / kUnit), clamped to the plan's capacity
+    uint32_t force_big;                              // test hook: every ST on the big-ST path
+    uint32_t *zero_next;                             // the next call's counter set (k_emit zeroes it)
+    uint32_t *bg_nx, *bg_wt, *bg_lref, *bg_ptr, *bg_sc, *bg_mark;   // big-ST scratch [max_nodes]
+    uint64_t max_nodes;
+
+    __device__ __forceinline__ bool big(uint32_t n) const { return force_big || n > kStCap; }
+    // the record of a chain's tail survivor in ST s (fws_node_res::tail of a non-EXIT kind)
+    __device__ __forceinline__ const fws_frame_info *tail_rec(uint32_t s, const fws_node_res &r) const {
+        return (r.kind & kBigBit) ? rec(r.tail) : rec((uint32_t)st_nodes[(uint64_t)s * kStCap + r.tail]);
+    }
 
     // slot id of survivor r of tile t (stage slots, or the tile's spill run)
     __device__ __forceinline__ uint32_t sid(uint32_t t, uint32_t sp, uint32_t r) const {
@@ -218,6 +240,95 @@ struct MergeLds {
     uint32_t n_tail, tail_base;
 };
 
+// Slot id of survivor i of ST s (tile by a search of the ST's tile prefix in LDS).
+__device__ __forceinline__ uint32_t st_sid(const MergeParams &P, const MergeLds &L, uint32_t t0, uint32_t i) {
+    uint32_t lo = 0, hi = kStTiles;                  // last tile with tbase <= i
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (L.tbase[mid] <= i) lo = mid; else hi = mid;
+    }
+    return P.sid(t0 + lo, L.tsp[lo], i - L.tbase[lo]);
+}
+
+// The big-ST path of k_merge: the LDS path's steps for a super tile whose n
+// survivors do not fit the LDS tables, over global scratch indexed by slot
+// id. Same outputs (fws_node_res with kBigBit: tails and entries are slot
+// ids; EXIT tails in the global list), no table for k_emit (it walks the
+// scratch the same way).
+__device__ void merge_big(const MergeParams &P, MergeLds &L, uint32_t s, uint32_t n) {
+    const uint32_t tid = threadIdx.x, t0 = s * kStTiles;
+    const uint64_t st_end = uint64_t(s + 1) * kStBytes;
+    uint32_t *const C = P.counters;
+    uint32_t *const p0 = P.bg_ptr, *const p1 = P.bg_ptr + P.max_nodes;
+    uint32_t *const c0 = P.bg_sc, *const c1 = P.bg_sc + P.max_nodes;
+    // in-ST next of every survivor: the survivor at its exit (search in the exit's tile)
+    for (uint32_t i = tid; i < n; i += kMThreads) {
+        const uint32_t id = st_sid(P, L, t0, i);
+        const fws_frame_info r = *P.rec(id);
+        const uint64_t x = exit_of(r);
+        uint32_t v;
+        if (!r.hdr_len) v = kBgInc;
+        else if (x >= P.N) v = kBgEnd;
+        else if (x >= st_end) v = kBgExit;
+        else {
+            v = P.find_node(x);
+            if (v == kTermDead) v = kBgDead;
+        }
+        const uint32_t wt = r.hdr_len ? 1u : 0u;
+        const bool tail = v >= kBgInc;
+        gst(P.bg_nx + id, v);
+        gst(P.bg_wt + id, wt);
+        gst(p0 + id, tail ? id : v);
+        gst(c0 + id, tail ? 0u : wt);
+        if (v == kBgExit) gst(P.bg_lref + id, atomicAdd(&L.n_tail, 1u));
+    }
+    __syncthreads();
+    if (tid == 0) {                                  // the ST's run of the tail list
+        const uint32_t k = L.n_tail;
+        uint32_t base = k ? atomicAdd(&C[kCntTails], k) : 0u;
+        if (k && (base > P.tail_cap || P.tail_cap - base < k)) {
+            atomicOr(&C[kCntFallback], 1u);
+            base = kNone;
+        }
+        L.tail_base = base;
+    }
+    // pointer jumping over slot ids: every survivor -> its chain's tail, frame counts
+    uint32_t *pc = p0, *pn = p1, *sc = c0, *sn = c1;
+    for (;;) {
+        int changed = 0;
+        for (uint32_t i = tid; i < n; i += kMThreads) {
+            const uint32_t id = st_sid(P, L, t0, i);
+            const uint32_t p = gld(pc + id), q = gld(pc + p);
+            const uint32_t a = gld(sc + id);
+            if (p != q) {
+                gst(pn + id, q);
+                gst(sn + id, a + gld(sc + p));
+                changed = 1;
+            } else {
+                gst(pn + id, p);
+                gst(sn + id, a);
+            }
+        }
+        uint32_t *t = pc; pc = pn; pn = t;
+        t = sc; sc = sn; sn = t;
+        if (!__syncthreads_or(changed)) break;
+    }
+    const uint32_t tb = L.tail_base;
+    if (tb == kNone) return;
+    for (uint32_t i = tid; i < n; i += kMThreads) {
+        const uint32_t id = st_sid(P, L, t0, i);
+        const uint32_t t = gld(pc + id);
+        const uint32_t kind = bg_kind(gld(P.bg_nx + t));
+        const uint32_t cnt = gld(sc + id) + gld(P.bg_wt + t);
+        const uint32_t ref = kind == kKindExit ? tb + gld(P.bg_lref + t) : t;
+        P.nres[id] = fws_node_res{ref, cnt, id, kind | kBigBit};
+        if (gld(P.bg_nx + id) == kBgExit) {
+            const uint64_t x = exit_of(*P.rec(id));
+            P.tails[tb + gld(P.bg_lref + id)] = fws_tail_rec{x, id, kTermDead, (uint32_t)(x / kStBytes), 0u};
+        }
+    }
+}
+
 __global__ __launch_bounds__(kMThreads) void k_merge(MergeParams P) {
     __shared__ MergeLds L;
     const uint32_t s = blockIdx.x, tid = threadIdx.x;
@@ -243,10 +354,6 @@ __global__ __launch_bounds__(kMThreads) void k_merge(MergeParams P) {
         atomicAdd(&C[kCntSurv], n);
         P.st_n[s] = n;
     }
-    if (n > kStCap) {
-        if (tid == 0) atomicOr(&C[kCntFallback], 1u);
-        return;
-    }
     if (tid < kStTiles) {
         L.tcnt[tid] = c;
         L.tsp[tid] = sp;
@@ -255,6 +362,11 @@ __global__ __launch_bounds__(kMThreads) void k_merge(MergeParams P) {
     if (tid == 0) L.n_tail = 0;
     __syncthreads();
     MP_MARK(0);
+    if (P.big(n)) {
+        if (tid == 0) atomicAdd(&C[kCntBig], 1u);
+        merge_big(P, L, s, n);
+        return;
+    }
 
     // this thread's survivors i = kPer * tid + j: slot ids, then one batch of record loads
     const uint32_t i0 = kPer * tid;
@@ -377,7 +489,7 @@ __global__ __launch_bounds__(kMThreads) void k_merge(MergeParams P) {
         const uint32_t kind = kind_of(L.nx[t]);
         const uint32_t cnt = L.sc[cur][i] + L.wt[t];
         const uint32_t ref = kind == kKindExit ? tb + L.lref[t] : t;
-        P.nres[nid[j]] = fws_node_res{ref, cnt | (i << 12) | (kind << 30)};
+        P.nres[nid[j]] = fws_node_res{ref, cnt, i, kind};
         if (vv[j] == kNxExit) {
             const uint64_t x = exit_of(r[j]);
             P.tails[tb + L.lref[i]] = fws_tail_rec{x, nid[j], kTermDead, (uint32_t)(x / kStBytes), 0u};
@@ -396,7 +508,7 @@ struct PathLds {
     uint16_t cnx[kCompCap];                          // compact next, or kCTerm (comp: P.comp)
     uint32_t kb[2][kCompCap / 32];                   // kept bitmaps
     uint32_t red32[kMWaves];
-    uint32_t root, rt, crt, root_ck, end_kind, end_set;
+    uint32_t root, rt, crt, root_ent, root_cnt, end_kind, end_set;
     const fws_frame_info *end_rec;                   // the path's last header
 };
 
@@ -419,6 +531,20 @@ __device__ __forceinline__ void batched4(uint32_t n, Load load, Use use) {
     }
 }
 
+// A workspace limit was hit (k_scan's survivor spill, the tail list, the
+// compacted tails): the decode ends with FWS_ERR_CAPACITY, nothing listed or
+// unmasked (k_emit and the unmask see kCntFallback / zero frames).
+__device__ void fail_capacity(const MergeParams &P) {
+    uint32_t *const C = P.counters;
+    if (threadIdx.x != 0) return;
+    atomicOr(&C[kCntFallback], 1u);
+    fws_decode_result r{};
+    r.status = FWS_ERR_CAPACITY;
+    r.n_survivors = ld_acq(&C[kCntSurv]);
+    C[kCntFrames] = 0;
+    *P.res = r;
+}
+
 // The path from offset 0 over the target tails: ST entries and frame bases,
 // terminal, result. Runs in the last k_link workgroup.
 __device__ void resolve_path(const MergeParams &P, PathLds &G) {
@@ -426,32 +552,33 @@ __device__ void resolve_path(const MergeParams &P, PathLds &G) {
     const uint32_t tid = threadIdx.x;
     MP_INIT();
     if (ld_acq(&C[kCntFallback]) || (ld_acq(&C[kCntOverflow]) & 1u)) {
-        if (tid == 0) atomicOr(&C[kCntFallback], 1u);
+        fail_capacity(P);                            // k_scan's spill or the tail list overflowed
         return;
     }
     const uint32_t M = ld_acq(&C[kCntTails]);
     const uint32_t n_st = P.n_st;
     const uint64_t N = P.N;
     if (tid == 0) {
-        uint32_t root = kNone, rt = kNone, ck = 0;
+        uint32_t root = kNone, rt = kNone;
+        fws_node_res rr{0, 0, 0, 0};
         if (P.n_tiles && P.tile_count[0]) {
             const uint32_t id0 = P.sid(0, P.tile_spill[0], 0);
             if (P.rec(id0)->hdr_off == 0) root = id0;
         }
         G.end_set = 0;
         if (root != kNone) {
-            const fws_node_res r = P.nres[root];
-            ck = r.cnt_kind;
-            if (res_kind(ck) == kKindExit) rt = r.tail;
+            rr = P.nres[root];
+            if (res_kind(rr) == kKindExit) rt = rr.tail;
             else {                                   // the root's chain ends in ST 0
-                G.end_rec = P.rec((uint32_t)P.st_nodes[r.tail]);
-                G.end_kind = res_kind(ck);
+                G.end_rec = P.tail_rec(0, rr);
+                G.end_kind = res_kind(rr);
                 G.end_set = 1;
             }
         }
         G.root = root;
         G.rt = rt;
-        G.root_ck = ck;
+        G.root_ent = rr.ent;
+        G.root_cnt = rr.cnt;
     }
     // ST bases start from zero counts
     for (uint32_t s = tid; s < n_st; s += kMThreads) {
@@ -477,8 +604,8 @@ __device__ void resolve_path(const MergeParams &P, PathLds &G) {
     }
     uint32_t mc;
     uint32_t pre = block_excl<uint32_t>(cnt, G.red32, &mc);
-    if (mc > kCompCap) {
-        if (tid == 0) atomicOr(&C[kCntFallback], 1u);
+    if (mc > kCompCap) {                             // > 32 768 STs on the path (8 GiB streams)
+        fail_capacity(P);
         return;
     }
     for (uint32_t w = w0; w < w1; ++w) {
@@ -527,14 +654,25 @@ __device__ void resolve_path(const MergeParams &P, PathLds &G) {
     }
     MP_MARK(13);
     if (!settled) {
-        if (tid == 0) atomicOr(&C[kCntFallback], 1u);
-        return;
+        // an input that keeps false tails alive for kMaxPruneRounds: the path
+        // itself, walked from the root's tail (offsets increase along next, so
+        // at most mc steps)
+        for (uint32_t w = tid; w < cw; w += kMThreads) ka[w] = 0u;
+        __syncthreads();
+        if (tid == 0) {
+            for (uint32_t c = crt; c != kNone && c < mc;) {
+                ka[c >> 5] |= 1u << (c & 31u);
+                const uint16_t g = G.cnx[c];
+                c = g == kCTerm ? kNone : (uint32_t)g;
+            }
+        }
+        __syncthreads();
     }
 
     // entries: the root, and every kept tail's landing survivor, with their chain counts
     if (tid == 0 && root != kNone) {
-        P.st_entry[0] = res_lidx(G.root_ck);
-        P.st_fbase[0] = res_cnt(G.root_ck);
+        P.st_entry[0] = G.root_ent;
+        P.st_fbase[0] = G.root_cnt;
     }
     for (uint32_t base = tid; base < mc; base += 4u * kMThreads) {
         fws_tail_rec tr[4];
@@ -559,11 +697,11 @@ __device__ void resolve_path(const MergeParams &P, PathLds &G) {
                 if (ends) { G.end_rec = P.rec(tr[j].id); G.end_kind = kKindDead; G.end_set = 1; }
                 continue;
             }
-            P.st_entry[tr[j].wst] = res_lidx(nr[j].cnt_kind);
-            P.st_fbase[tr[j].wst] = res_cnt(nr[j].cnt_kind);
+            P.st_entry[tr[j].wst] = nr[j].ent;
+            P.st_fbase[tr[j].wst] = nr[j].cnt;
             if (ends) {
-                G.end_rec = P.rec((uint32_t)P.st_nodes[(uint64_t)tr[j].wst * kStCap + nr[j].tail]);
-                G.end_kind = res_kind(nr[j].cnt_kind);
+                G.end_rec = P.tail_rec(tr[j].wst, nr[j]);
+                G.end_kind = res_kind(nr[j]);
                 G.end_set = 1;
             }
         }
@@ -596,6 +734,10 @@ __device__ void resolve_path(const MergeParams &P, PathLds &G) {
     if (tid != 0) return;
     if (root != kNone && !G.end_set) {               // no terminal on the path: cannot happen
         atomicOr(&C[kCntFallback], 1u);
+        fws_decode_result r{};
+        r.status = FWS_ERR_INTERNAL;
+        C[kCntFrames] = 0;
+        *P.res = r;
         return;
     }
     // terminal: the path's last header, then ParseFrameHdr from its exit on error
@@ -679,7 +821,7 @@ __global__ __launch_bounds__(kMThreads) void k_link(MergeParams P) {
         if (w != kTermDead) {
             __hip_atomic_store(&tr.w, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             const fws_node_res r = P.nres[w];
-            g = res_kind(r.cnt_kind) == kKindExit ? r.tail : (kGTerm | res_kind(r.cnt_kind));
+            g = res_kind(r) == kKindExit ? r.tail : (kGTerm | res_kind(r));
         }
         __hip_atomic_store(&P.gnx[x], g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (g < kGTerm) atomicOr(&P.tmark[g >> 5], 1u << (g & 31u));
@@ -705,16 +847,92 @@ struct EmitLds {
     uint32_t red32[kMWaves];
 };
 
+// The big-ST path of k_emit (k_merge's merge_big): the same marking of the
+// entry's chain by pointer doubling, over slot ids in global scratch; the
+// frames in offset order are the ST's survivors in tile order.
+__device__ void emit_big(const MergeParams &P, uint32_t s, uint32_t n, uint32_t e, uint32_t fbase, uint32_t lim) {
+    __shared__ uint32_t s_tb[kStTiles], s_tsp[kStTiles], s_red[kMWaves];
+    const uint32_t tid = threadIdx.x, t0 = s * kStTiles;
+    uint32_t c = 0, sp = kNone;
+    if (tid < kStTiles && t0 + tid < P.n_tiles) {
+        c = P.tile_count[t0 + tid];
+        sp = P.tile_spill[t0 + tid];
+    }
+    uint32_t tot;
+    const uint32_t b = block_excl<uint32_t>(c, s_red, &tot);
+    if (tid < kStTiles) {
+        s_tb[tid] = b;
+        s_tsp[tid] = sp;
+    }
+    __syncthreads();
+    auto sid_of = [&](uint32_t i) -> uint32_t {
+        uint32_t lo = 0, hi = kStTiles;
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (s_tb[mid] <= i) lo = mid; else hi = mid;
+        }
+        return P.sid(t0 + lo, s_tsp[lo], i - s_tb[lo]);
+    };
+    uint32_t *const p0 = P.bg_ptr, *const p1 = P.bg_ptr + P.max_nodes;
+    for (uint32_t i = tid; i < n; i += kMThreads) {
+        const uint32_t id = sid_of(i);
+        const uint32_t v = gld(P.bg_nx + id);
+        gst(p0 + id, v >= kBgInc ? id : v);
+        gst(P.bg_mark + id, id == e ? 1u : 0u);
+    }
+    __syncthreads();
+    // marks double along the chain: after round k every node within 2^k steps of the entry
+    uint32_t *pc = p0, *pn = p1;
+    for (;;) {
+        int changed = 0;
+        for (uint32_t i = tid; i < n; i += kMThreads) {
+            const uint32_t id = sid_of(i);
+            const uint32_t p = gld(pc + id);
+            if (gld(P.bg_mark + id) && !gld(P.bg_mark + p)) {
+                gst(P.bg_mark + p, 1u);
+                changed = 1;
+            }
+            gst(pn + id, gld(pc + p));
+        }
+        uint32_t *t = pc; pc = pn; pn = t;
+        if (!__syncthreads_or(changed)) break;
+    }
+    // the chain's frames in offset order, in rounds of kMThreads survivors
+    uint32_t f = fbase;
+    for (uint32_t i0 = 0; i0 < n; i0 += kMThreads) {
+        const uint32_t i = i0 + tid;
+        uint32_t id = 0;
+        bool fr = false;
+        if (i < n) {
+            id = sid_of(i);
+            fr = gld(P.bg_mark + id) && gld(P.bg_wt + id);
+        }
+        uint32_t rt;
+        const uint32_t o = f + block_excl<uint32_t>(fr ? 1u : 0u, s_red, &rt);
+        if (fr && o < lim) {
+            const fws_frame_info fi = *P.rec(id);
+            P.put_frame(o, fi);
+            P.plan_units(o, fi.hdr_off, exit_of(fi), o == lim - 1);
+        }
+        f += rt;
+    }
+}
+
 __global__ __launch_bounds__(kMThreads) void k_emit(MergeParams P) {
     __shared__ EmitLds L;
     const uint32_t s = blockIdx.x, tid = threadIdx.x;
     const uint32_t *const C = P.counters;
     MP_T0();
     MP_INIT();
+    if (s == 0 && tid < kCntStride) P.zero_next[tid] = 0u;   // the next call's counter set
     if (s >= P.n_st) return;
     const uint32_t fb = C[kCntFallback], e = P.st_entry[s], fbase = P.st_fbase[s], n = P.st_n[s];
     const uint32_t lim = C[kCntFrames];
-    if (fb || e == kNone || fbase >= lim || n > kStCap) return;
+    if (fb || e == kNone || fbase >= lim) return;
+    if (P.big(n)) {
+        emit_big(P, s, n, e, fbase, lim);
+        return;
+    }
     const fws_st_node *const tab = P.st_nodes + (uint64_t)s * kStCap;
     const uint32_t i0 = kPer * tid;
     fws_st_node nd[kPer];
@@ -805,7 +1023,8 @@ uint32_t fws_merge_tail_cap(uint64_t n_tiles) {
 }
 
 int fws_launch_merge(fws_gpu_ctx *ctx, const uint8_t *wire, uint64_t N, uint32_t n_tiles, fws_frame_info *frames,
-                     uint32_t cap, fws_decode_result *res, uint8_t *utf8_ok, hipStream_t s) {
+                     uint32_t cap, fws_decode_result *res, uint8_t *utf8_ok, bool force_big, uint32_t *zero_next,
+                     hipStream_t s) {
     fws_decode_ws &d = ctx->dec;
     MergeParams P;
     P.wire = wire;
@@ -835,6 +1054,15 @@ int fws_launch_merge(fws_gpu_ctx *ctx, const uint8_t *wire, uint64_t N, uint32_t
     P.unit_first = ctx->plan.unit_first;
     const uint64_t units = (N + kUnit - 1) / kUnit;
     P.n_units = units < ctx->plan.unit_cap ? units : ctx->plan.unit_cap;
+    P.force_big = force_big ? 1u : 0u;
+    P.zero_next = zero_next;
+    P.bg_nx = d.bg_nx;
+    P.bg_wt = d.bg_wt;
+    P.bg_lref = d.bg_lref;
+    P.bg_ptr = d.bg_ptr;
+    P.bg_sc = d.bg_sc;
+    P.bg_mark = d.bg_mark;
+    P.max_nodes = d.max_nodes;
     const dim3 grid(P.n_st ? P.n_st : 1u), blk(kMThreads);
     hipLaunchKernelGGL(k_merge, grid, blk, 0, s, P);
     hipLaunchKernelGGL(k_link, dim3((P.tail_cap + kMThreads - 1) / kMThreads), blk, 0, s, P);

@@ -259,12 +259,12 @@ def plan_mode(ctx):
     return dict(zip(("byte_space", "s0", "first_po", "last_pe", "n_units"), list(out)))
 
 
-def decode_fell_back(ctx):
-    """True if the last decode on ctx took the cooperative k_resolve fallback
-    instead of the super-tile resolve (diagnostic; synchronises)."""
-    out = (C.c_uint32 * 12)()
-    check("fws_internal_decode_counters", lib().fws_internal_decode_counters(ctx.h, out, 12))
-    return out[9] != 0          # decode_common.h Counter::kCntFallback
+def decode_counters(ctx):
+    """The last decode's counters on ctx (decode_common.h Counter; diagnostic,
+    synchronises): survivors, frames, big-ST super tiles, failure flag."""
+    out = (C.c_uint32 * 16)()
+    check("fws_internal_decode_counters", lib().fws_internal_decode_counters(ctx.h, out, 16))
+    return {"survivors": out[0], "frames": out[3], "failed": out[9] != 0, "big_super_tiles": out[12]}
 
 
 class RxPipe:

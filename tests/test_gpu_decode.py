@@ -16,18 +16,19 @@ from wsframes import frame
 
 pytestmark = pytest.mark.gpu
 
-RESOLVE_MODES = {"super_tile": 0, "k_resolve": 1, "small_read": 2}
-CNT_FALLBACK = 9            # decode_common.h Counter::kCntFallback
+RESOLVE_MODES = {"super_tile": 0, "big_st": 1, "small_read": 2}
+CNT_FAILED = 9              # decode_common.h Counter::kCntFallback (the resolve failed)
+CNT_BIG = 12                # decode_common.h Counter::kCntBig (super tiles on the big-ST path)
 
 
 @pytest.fixture(params=list(RESOLVE_MODES), autouse=True)
 def resolve_mode(request):
     """Every decode test runs on both resolve paths: the super-tile resolve
-    (merge_kernels.hip, the common path) and the cooperative k_resolve it
-    falls back to (resolve_kernels.hip), forced; and through the RX session's
-    one-launch small-read kernel (small_kernels.hip; streams <= 128 KiB with
-    <= 256 headers, the rest fall back to the super-tile path as the session
-    does)."""
+    with its tables in LDS (merge_kernels.hip, the common path) and the big-ST
+    path it takes for super tiles with more survivors than LDS holds, forced
+    for every super tile; and through the RX session's one-launch small-read
+    kernel (small_kernels.hip; streams <= 128 KiB with <= 256 headers, the rest
+    fall back to the super-tile path as the session does)."""
     from flashws_amd import _lib
     L = _lib.lib()
     old = L.fws_internal_set_resolve_mode(RESOLVE_MODES[request.param])
@@ -35,12 +36,18 @@ def resolve_mode(request):
     L.fws_internal_set_resolve_mode(old)
 
 
-def fell_back(ctx):
+def counters(ctx):
     import ctypes as C
     from flashws_amd import _lib
-    out = (C.c_uint32 * 12)()
-    assert _lib.lib().fws_internal_decode_counters(ctx.h, out, 12) == 0
-    return out[CNT_FALLBACK] != 0
+    out = (C.c_uint32 * 16)()
+    assert _lib.lib().fws_internal_decode_counters(ctx.h, out, 16) == 0
+    return list(out)
+
+
+def fell_back(ctx):
+    """True if the last decode failed in the resolve or took the big-ST path."""
+    c = counters(ctx)
+    return c[CNT_FAILED] != 0 or c[CNT_BIG] != 0
 
 
 def decode(ctx, wire, cuda, cap=None):
@@ -166,7 +173,7 @@ def test_c3_mixed_parity(ctx, cuda, resolve_mode):
     r = check(ctx, cuda, wire)
     assert int(r["n_frames"]) == len(descs)
     if resolve_mode == "super_tile":
-        assert not fell_back(ctx), "C3 must resolve on the super-tile path"
+        assert not fell_back(ctx), "C3 must resolve on the super-tile path with LDS tables"
 
 
 def test_c2_full_parity(ctx, cuda, resolve_mode):
@@ -174,7 +181,19 @@ def test_c2_full_parity(ctx, cuda, resolve_mode):
     r = check(ctx, cuda, wire)
     assert int(r["n_frames"]) == 65536
     if resolve_mode == "super_tile":
-        assert not fell_back(ctx), "C2 must resolve on the super-tile path"
+        assert not fell_back(ctx), "C2 must resolve on the super-tile path with LDS tables"
+
+
+def test_dense_64b_frames(ctx, cuda, resolve_mode):
+    """200 000 x 64 B frames: super tiles with more survivors than
+    the LDS tables hold take the big-ST path, bit-exact either way."""
+    wire, descs, _ = gpu.config_c2(seed=65, n_frames=200_000, payload=64)
+    r = check(ctx, cuda, wire)
+    assert int(r["n_frames"]) == 200_000
+    c = counters(ctx)
+    assert c[CNT_FAILED] == 0
+    if resolve_mode != "small_read":
+        assert c[CNT_BIG] > 0
 
 
 def test_c3_full_roundtrip(ctx, cuda):
@@ -466,7 +485,7 @@ def test_small_read_size_limit(ctx, cuda, size):
 def test_small_read_capacity(ctx, cuda, resolve_mode):
     """cap below the header count: the first cap frames listed and unmasked,
     FWS_ERR_CAPACITY, n_frames = all headers; identical on every path."""
-    if resolve_mode == "k_resolve":
+    if resolve_mode == "big_st":
         pytest.skip("compared against the super-tile path below")
     rng = np.random.default_rng(5)
     wire = np.frombuffer(b"".join(frame(2, rng.integers(0, 256, int(rng.integers(0, 400)), dtype=np.uint8).tobytes(),

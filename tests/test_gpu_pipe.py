@@ -70,3 +70,23 @@ def test_pipe_utf8_flags(cuda):
     assert int(res["status"]) == 0 and int(res["n_frames"]) == 400
     assert np.array_equal(flags, ok)
     pipe.close()
+
+
+def test_pipe_dense_64b_frames(cuda):
+    """SURVEY §6's dense workload: 200 000 x 64 B masked frames (~3 700
+    headers per 256 KiB super tile, over the LDS tables: the big-ST path),
+    through the pipe with 3 batches in flight; every batch bit-exact against
+    the oracle."""
+    wire, descs, _ = gpu.config_c2(seed=64, n_frames=200_000, payload=64)
+    exp_buf, exp_frames, ret = _expect(wire)
+    assert ret == 0 and len(exp_frames) == 200_000
+    pipe = gpu.RxPipe(0, max_batch_bytes=len(wire) + 64, max_frames=200_064, depth=3)
+    hosts = [torch.from_numpy(wire.copy()).pin_memory() for _ in range(3)]
+    tickets = [pipe.submit(h) for h in hosts]
+    for i, t in enumerate(tickets):
+        frames, res, _ = pipe.wait(t)
+        assert int(res["status"]) == 0 and int(res["n_frames"]) == 200_000, i
+        assert np.array_equal(hosts[i].numpy(), exp_buf), i
+        for k in ("hdr_off", "payload_len", "key", "opcode", "fin", "hdr_len"):
+            assert np.array_equal(frames[k], exp_frames[k]), (i, k)
+    pipe.close()

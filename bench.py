@@ -41,6 +41,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 METRIC = "GiB/s masked WS payload unmasked, device-resident frame batch; % HBM roofline"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 GIB = float(1 << 30)
+DENSE_FRAMES, DENSE_PAYLOAD = 200000, 64   # SURVEY §6 dense small-frame workload
 
 
 def parse():
@@ -228,13 +229,25 @@ def cpu_baseline(wire, descs, seconds):
                                    C.byref(pb2), C.byref(rc2))
     if ta <= 0 or rc2.value != 0 or rc.value != 0:
         raise RuntimeError(f"reference CPU baseline failed: t={ta} rc={rc.value},{rc2.value}")
+    # SURVEY §6's dense workload (200 000 x 64 B BIN frames), one core, beside the GPU's
+    # dense_64B_stream_decode extra
+    wd, dd, _ = gpu.config_c2(n_frames=DENSE_FRAMES, payload=DENSE_PAYLOAD)
+    pbd, rcd = C.c_uint64(0), C.c_int(0)
+    td1 = lib.ref_time_onrecv(wd.ctypes.data, len(wd), read, 1, C.byref(pbd), C.byref(rcd))
+    it_d = max(2, int(min(seconds, 3.0) / max(td1, 1e-6)) // 2 * 2)
+    td = lib.ref_time_onrecv(wd.ctypes.data, len(wd), read, it_d, C.byref(pbd), C.byref(rcd))
+    dense = {"value": round(pbd.value / td / GIB, 3), "unit": "GiB/s", "cores": 1,
+             "sample": f"{it_d} passes of {DENSE_FRAMES} x {DENSE_PAYLOAD} B BIN frames ({len(wd)} wire B) "
+                       f"as 2 MiB reads, {td:.2f} s"}
+    if rcd.value != 0:
+        raise RuntimeError(f"reference CPU baseline (dense) failed: rc={rcd.value}")
     return {"value": round(pb2.value / ta / GIB, 3), "unit": "GiB/s", "cores": procs, "kind": "reference",
             "sample": f"{procs} processes (one per core, the reference's one-event-loop-per-core model), each "
                       f"running WSocket::OnRecvData over its own copy of the C2 batch ({len(wire)} wire B) as "
                       f"2 MiB reads {it_all} times ({ta:.1f} s, slowest process); g++ -O3 -mavx2; {model}; "
                       f"host has {os.cpu_count()} logical CPUs, {_physical_cores()} physical cores, this "
                       f"process's CPU share {procs}",
-            "one_core": one}
+            "one_core": one, "dense_64B_one_core": dense}
 
 
 def pmc_traffic():
@@ -497,9 +510,15 @@ def stream_decode_extra(ctx, wire_c2, dev, args):
         r = gpu.read_result(res)
         assert int(r["status"]) == 0 and int(r["n_frames"]) == n_frames, (name, r)
         payload = int(gpu.read_frames(frames, n_frames)["payload_len"].sum())
+        alg = (len(wire) + payload) / t / 1e9
         rec = {"GiB_per_s": round(payload / t / GIB, 1), "ms_per_step": round(t * 1e3, 4), "frames": n_frames,
-               "wire_bytes": len(wire), "alg_GB_per_s": round((len(wire) + payload) / t / 1e9, 1),
-               "big_super_tiles": gpu.decode_counters(c)["big_super_tiles"]}
+               "wire_bytes": len(wire), "alg_GB_per_s": round(alg, 1),
+               "big_super_tiles": gpu.decode_counters(c)["big_super_tiles"],
+               # the whole decode step (scan .. stream unmask, every launch) against HBM peak:
+               # algorithmic bytes = every wire byte read + every payload byte written
+               "roofline": {"bound": "hbm", "achieved": round(alg, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                            "frac": round(alg / HBM_PEAK_GBS, 4), "basis": "whole fws_gpu_decode_stream step",
+                            "alg_bytes_per_step": len(wire) + payload}}
         if utf8:
             rec["utf8_invalid_frames"] = int((ok[:n_frames] == 0).sum().item())
         if pipelined and nbuf >= 4:
@@ -533,6 +552,11 @@ def stream_decode_extra(ctx, wire_c2, dev, args):
     w3, d3, _ = gpu.config_c3()
     out["C3_mixed_stream_decode"] = decode_cfg("C3", w3, len(d3))
     del w3
+    # SURVEY §6's dense workload: 200 000 x 64 B frames (~3 700 headers per 256 KiB super
+    # tile: the big-ST resolve path); the reference's 1-core rate is cpu_baseline.dense_64B_one_core
+    wd, dd, _ = gpu.config_c2(n_frames=DENSE_FRAMES, payload=DENSE_PAYLOAD)
+    out["dense_64B_stream_decode"] = decode_cfg("dense", wd, DENSE_FRAMES, pipelined=False)
+    del wd
     # C4: one 256 MiB fragmented message, unmask + reassemble out of place
     w4, d4, _ = gpu.config_c4()
     c = gpu.Ctx(dev.index or 0, max_frames=len(d4) + 8, max_stream_bytes=len(w4))

@@ -39,6 +39,7 @@ constexpr uint32_t kCntStride = 16;          // words per counter set (fws_decod
 static_assert(kCntFrames == kDecodeFramesCounter, "fws_internal.h names the frame counter");
 
 constexpr uint32_t kSlots = 8;               // per-tile survivor slots before spilling
+constexpr uint32_t kDenseTile = 0xFFFFFFFEu; // tile_count mark: k_scan left the tile to k_scan_dense (which overwrites it)
 
 __device__ __forceinline__ uint64_t exit_of(const fws_frame_info &fi) {
     return fi.hdr_off + fi.hdr_len + fi.payload_len;

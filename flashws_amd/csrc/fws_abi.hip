@@ -110,9 +110,7 @@ void fws_gpu_ctx_destroy(fws_gpu_ctx *ctx) {
     dev_free(d.tile_count);
     dev_free(d.cnt_base);
     dev_free(d.stage_info);
-    dev_free(d.stage_leaf);
     dev_free(d.spill_info);
-    dev_free(d.spill_leaf);
     dev_free(d.tile_spill);
     dev_free(d.scan_dummy);
     dev_free(d.nres);

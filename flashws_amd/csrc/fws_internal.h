@@ -80,9 +80,7 @@ struct fws_decode_ws {
     uint32_t parity = 0;              //   launch zeroes the other for the next call (no memset launch)
     bool cnt_dirty = true;            // zero this call's set first (new allocation, failed call)
     fws_frame_info *stage_info = nullptr;  // per-tile survivor slots (k_scan)
-    uint32_t *stage_leaf = nullptr;
     fws_frame_info *spill_info = nullptr;  // survivors of dense tiles
-    uint32_t *spill_leaf = nullptr;
     uint32_t *tile_spill = nullptr;        // spill offset of a dense tile, or ~0
     uint32_t scan_grid = 0;                // persistent k_scan workgroups
     uint32_t *scan_dummy = nullptr;        // one 64-B line per k_scan wavefront (idle-lane stores)

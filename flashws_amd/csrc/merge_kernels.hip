@@ -45,11 +45,11 @@
 // Every global access on these paths is metadata (about 1 survivor per KiB of
 // stream); the kernels are latency-bound, so loads are issued in batches of
 // independent addresses before their uses.
-#include "decode_common.h"
+#include "scan_common.h"
 
 namespace fwsk {
 
-constexpr uint32_t kStTiles = 128;                  // tiles per super tile
+constexpr uint32_t kStTiles = 256;                  // tiles per super tile
 constexpr uint64_t kStBytes = uint64_t(kStTiles) * kTile;
 constexpr uint32_t kStCap = 2048;                   // survivors of one ST in LDS
 constexpr int kMThreads = 512;
@@ -69,6 +69,13 @@ constexpr uint16_t kCTerm = 0xFFFF;
 #ifdef FWS_SCAN_PROF
 // phase clocks (100 MHz wall clock, summed over workgroups) for tools/prof_scan.py
 __device__ unsigned long long g_merge_prof[32];
+// per-workgroup timestamps (tools/prof_merge_trace.py): [workgroup % kTraceWg][mark]
+constexpr uint32_t kTraceWg = 1024;
+__device__ unsigned long long g_merge_trace[kTraceWg * 32];
+#define MP_START(slot)                                                              \
+    do {                                                                            \
+        if (threadIdx.x == 0) g_merge_trace[(blockIdx.x % kTraceWg) * 32 + (slot)] = wall_clock64(); \
+    } while (0)
 #define MP_T0() const uint64_t mp_t0 = wall_clock64()
 #define MP_INIT() uint64_t mp_t = wall_clock64()
 #define MP_MARK(k)                                                                  \
@@ -76,6 +83,7 @@ __device__ unsigned long long g_merge_prof[32];
         if (threadIdx.x == 0) {                                                     \
             const uint64_t now = wall_clock64();                                    \
             atomicAdd(&g_merge_prof[k], (unsigned long long)(now - mp_t));          \
+            g_merge_trace[(blockIdx.x % kTraceWg) * 32 + (k)] = now;                \
             mp_t = now;                                                             \
         }                                                                           \
     } while (0)
@@ -88,6 +96,7 @@ __device__ unsigned long long g_merge_prof[32];
         }                                                                           \
     } while (0)
 #else
+#define MP_START(slot) do { } while (0)
 #define MP_T0() do { } while (0)
 #define MP_INIT() do { } while (0)
 #define MP_MARK(k) do { } while (0)
@@ -123,8 +132,10 @@ struct MergeParams {
     uint32_t n_st;
     const fws_frame_info *stage_info;
     const fws_frame_info *spill_info;
-    const uint32_t *tile_count;
-    const uint32_t *tile_spill;
+    uint32_t *tile_count;                            // k_merge rewrites the tiles k_scan left (kDenseTile)
+    uint32_t *tile_spill;
+    fws_frame_info *spill_w;                         // = spill_info, for dense_tile()
+    uint32_t s_cap;                                  // spill capacity
     uint32_t spill_base;                             // n_tiles * kSlots: first slot id of the spill area
     uint32_t tail_cap;
     uint32_t *counters;
@@ -224,18 +235,24 @@ __device__ __forceinline__ T block_excl(T v, T *sred, T *total) {
 }
 
 // ------------------------------------------------------------------ k_merge
+constexpr uint32_t kDenseWaves = 4;                 // k_merge wavefronts running dense_tile()
 struct MergeLds {
     uint32_t tcnt[kStTiles];
     uint32_t tsp[kStTiles];
     uint32_t tbase[kStTiles];
     union {
-        uint32_t off[kStCap];                        // hdr_off - ST start (the exit search)
-        uint32_t lref[kStCap];                       // then: EXIT tail's index in the ST's tail run
+        struct {
+            union {
+                uint32_t off[kStCap];                // hdr_off - ST start (the exit search)
+                uint32_t lref[kStCap];               // then: EXIT tail's index in the ST's tail run
+            };
+            uint16_t nx[kStCap];
+            uint8_t wt[kStCap];                      // 1: a frame; 0: incomplete header
+            uint16_t ptr[2][kStCap];                 // Wyllie pointer (tails point to themselves)
+            uint16_t sc[2][kStCap];                  // frames from i up to ptr (exclusive)
+        };
+        ScanWaveLds dw[kDenseWaves];                 // first: the tiles k_scan left (dense_tile)
     };
-    uint16_t nx[kStCap];
-    uint8_t wt[kStCap];                              // 1: a frame; 0: incomplete header
-    uint16_t ptr[2][kStCap];                         // Wyllie pointer (tails point to themselves)
-    uint16_t sc[2][kStCap];                          // frames from i up to ptr (exclusive)
     uint32_t red32[kMWaves];
     uint32_t n_tail, tail_base;
 };
@@ -333,6 +350,7 @@ __global__ __launch_bounds__(kMThreads) void k_merge(MergeParams P) {
     __shared__ MergeLds L;
     const uint32_t s = blockIdx.x, tid = threadIdx.x;
     uint32_t *const C = P.counters;
+    MP_START(30);
     MP_T0();
     MP_INIT();
     // the tail-target bitmap k_link sets
@@ -347,6 +365,36 @@ __global__ __launch_bounds__(kMThreads) void k_merge(MergeParams P) {
     if (tid < kStTiles && t0 + tid < P.n_tiles) {
         c = P.tile_count[t0 + tid];
         sp = P.tile_spill[t0 + tid];
+    }
+    if (__syncthreads_or(c == kDenseTile)) {
+        // tiles k_scan left (frames under ~32 B): dense_tile() on kDenseWaves wavefronts,
+        // survivors to spill runs; the counts go back to tile_count / tile_spill for k_link
+        // and k_emit (find_node)
+        if (tid < kStTiles) {
+            L.tcnt[tid] = c;
+            L.tsp[tid] = sp;
+        }
+        __syncthreads();
+        const uint32_t w = tid >> 6;
+        if (w < kDenseWaves) {
+            for (uint32_t i = w; i < kStTiles; i += kDenseWaves) {
+                if (L.tcnt[i] != kDenseTile) continue;           // wave-uniform
+                const uint64_t r = dense_tile(L.dw[w], P.wire, P.N, t0 + i, P.spill_w, C, P.s_cap);
+                const uint32_t dn = (uint32_t)r, dsp = (uint32_t)(r >> 32);
+                if ((tid & 63) == 0) {
+                    L.tcnt[i] = dn;
+                    L.tsp[i] = dsp;
+                    P.tile_count[t0 + i] = dn;
+                    P.tile_spill[t0 + i] = dsp;
+                }
+            }
+        }
+        __syncthreads();
+        if (tid < kStTiles) {
+            c = L.tcnt[tid];
+            sp = L.tsp[tid];
+        }
+        __syncthreads();
     }
     uint32_t n;
     const uint32_t b = block_excl<uint32_t>(c, L.red32, &n);
@@ -538,11 +586,15 @@ __device__ void fail_capacity(const MergeParams &P) {
     uint32_t *const C = P.counters;
     if (threadIdx.x != 0) return;
     atomicOr(&C[kCntFallback], 1u);
-    fws_decode_result r{};
-    r.status = FWS_ERR_CAPACITY;
-    r.n_survivors = ld_acq(&C[kCntSurv]);
     C[kCntFrames] = 0;
-    *P.res = r;
+    fws_decode_result *const r = P.res;              // field by field: no stack copy
+    r->status = FWS_ERR_CAPACITY;
+    r->n_frames = 0;
+    r->consumed = 0;
+    r->err_off = 0;
+    r->carry_unread = 0;
+    r->carry_hdr_len = 0;
+    r->n_survivors = ld_acq(&C[kCntSurv]);
 }
 
 // The path from offset 0 over the target tails: ST entries and frame bases,
@@ -810,6 +862,7 @@ __global__ __launch_bounds__(kMThreads) void k_link(MergeParams P) {
     __shared__ uint32_t s_last;
     const uint32_t tid = threadIdx.x;
     uint32_t *const C = P.counters;
+    MP_START(29);
     MP_T0();
     MP_INIT();
     const uint32_t M = C[kCntTails];
@@ -922,6 +975,7 @@ __global__ __launch_bounds__(kMThreads) void k_emit(MergeParams P) {
     __shared__ EmitLds L;
     const uint32_t s = blockIdx.x, tid = threadIdx.x;
     const uint32_t *const C = P.counters;
+    MP_START(28);
     MP_T0();
     MP_INIT();
     if (s == 0 && tid < kCntStride) P.zero_next[tid] = 0u;   // the next call's counter set
@@ -998,6 +1052,10 @@ __global__ __launch_bounds__(kMThreads) void k_emit(MergeParams P) {
 }  // namespace fwsk
 
 #ifdef FWS_SCAN_PROF
+extern "C" int fws_internal_merge_trace(unsigned long long *out) {
+    return fws_hip_status(hipMemcpyFromSymbol(out, HIP_SYMBOL(fwsk::g_merge_trace),
+                                              sizeof(unsigned long long) * fwsk::kTraceWg * 32));
+}
 extern "C" int fws_internal_merge_prof(unsigned long long *out, int reset) {
     hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(fwsk::g_merge_prof), sizeof(unsigned long long) * 32);
     if (e == hipSuccess && reset) {
@@ -1033,6 +1091,8 @@ int fws_launch_merge(fws_gpu_ctx *ctx, const uint8_t *wire, uint64_t N, uint32_t
     P.n_st = (uint32_t)fws_merge_super_tiles(n_tiles);
     P.stage_info = d.stage_info;
     P.spill_info = d.spill_info;
+    P.spill_w = d.spill_info;
+    P.s_cap = (uint32_t)d.max_surv;
     P.tile_count = d.tile_count;
     P.tile_spill = d.tile_spill;
     P.spill_base = n_tiles * kSlots;

@@ -160,6 +160,27 @@ def test_random_small_frames(ctx, cuda, seed):
     check(ctx, cuda, b"".join(out))
 
 
+@pytest.mark.parametrize("seed", range(3))
+def test_tiny_frames_dense_tiles(ctx, cuda, seed):
+    """Frames of 0..24 B payload (~100 headers per 2 KiB tile): k_scan leaves
+    every such tile to dense_tile() in k_merge (more live nodes than lanes);
+    mixed with 4 KiB frames so sparse and dense tiles alternate."""
+    rng = np.random.default_rng(500 + seed)
+    out, total = [], 0
+    while total < 600_000:
+        if rng.random() < 0.02:
+            n = 4096
+        else:
+            n = int(rng.integers(0, 25))
+        op = int(rng.choice([1, 2, 0, 9, 10]))
+        out.append(frame(op, rng.integers(0, 256, n, dtype=np.uint8).tobytes(),
+                         fin=int(rng.random() < 0.7), key=int(rng.integers(0, 2**32))))
+        total += len(out[-1])
+    check(ctx, cuda, b"".join(out))
+    c = counters(ctx)
+    assert c[CNT_FAILED] == 0
+
+
 @pytest.mark.parametrize("size", [1, 15, 16, 2030, 2047, 2048, 2049, 4103, 16383, 16384, 16385, 16390, 32768 + 7])
 def test_single_frame_tile_boundaries(ctx, cuda, size):
     for lead in (0, 1, 7, 2030, 2041, 16370):

@@ -1,0 +1,73 @@
+#!/usr/bin/env python3
+"""Per-workgroup timelines of k_merge / k_link / k_emit from the FWS_SCAN_PROF
+build (make -C flashws_amd/csrc prof): for the last of a few C2/C3 decodes,
+each kernel's workgroup start spread and per-phase durations (us; median,
+p90, max over workgroups), plus the last k_link workgroup's resolve phases."""
+import ctypes as C
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from flashws_amd import _lib  # noqa: E402
+
+_lib.LIB_PATH = os.path.join(ROOT, "flashws_amd", "lib", "libfws_gpu_prof.so")
+from flashws_amd import gpu  # noqa: E402
+
+KW = 1024
+
+
+def stats(v):
+    v = np.asarray(v, dtype=np.float64)
+    return {"med": round(float(np.median(v)), 2), "p90": round(float(np.percentile(v, 90)), 2),
+            "max": round(float(v.max()), 2)}
+
+
+def main():
+    dev = torch.device("cuda:0")
+    L = _lib.lib()
+    tr = L.fws_internal_merge_trace
+    tr.argtypes = [C.POINTER(C.c_ulonglong)]
+    out = {}
+    for name, mk in (("C2", gpu.config_c2), ("C3", gpu.config_c3)):
+        wire, descs, _ = mk()
+        n = len(descs)
+        ctx = gpu.Ctx(0, max_frames=n + 16, max_stream_bytes=len(wire))
+        w = torch.from_numpy(wire).to(dev)
+        n_st = (len(wire) + (512 << 10) - 1) // (512 << 10)
+        for _ in range(4):
+            gpu.decode_stream(ctx, w, cap=n + 16)
+        torch.cuda.synchronize()
+        arr = (C.c_ulonglong * (KW * 32))()
+        tr(arr)
+        t = np.frombuffer(arr, dtype=np.uint64).reshape(KW, 32).astype(np.float64) / 100.0   # us
+        r = {}
+        m = t[:n_st]
+        t0 = m[:, 30].min()
+        r["k_merge_start_spread_us"] = stats(m[:, 30] - t0)
+        prev = m[:, 30]
+        for k, lab in enumerate(["counts", "records", "next+table", "jump", "tails"]):
+            r[f"k_merge_{lab}"] = stats(m[:, k] - prev)
+            prev = m[:, k]
+        r["k_merge_end_us"] = stats(m[:, 4] - t0)
+        e = t[:n_st]
+        t0e = e[:, 28].min()
+        ok = e[:, 26] > e[:, 28]
+        r["k_emit_start_spread_us"] = stats(e[:, 28] - t0e)
+        prev = e[:, 28]
+        for k, lab in zip((24, 25, 26), ["load", "mark", "write"]):
+            r[f"k_emit_{lab}"] = stats((e[:, k] - prev)[ok])
+            prev = e[:, k]
+        r["k_emit_end_us"] = stats(e[ok, 26] - t0e)
+        r["gap_merge_end_to_emit_start_us"] = round(float(t0e - m[:, 4].max()), 2)
+        out[name] = r
+        ctx.close()
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()

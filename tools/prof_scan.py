@@ -18,7 +18,7 @@ from flashws_amd import _lib  # noqa: E402
 _lib.LIB_PATH = os.path.join(ROOT, "flashws_amd", "lib", "libfws_gpu_prof.so")
 from flashws_amd import gpu  # noqa: E402
 
-PHASES = ["load", "cand+scan", "parse", "jump", "surv+emit"]
+PHASES = ["load", "cand+scan", "pos+first_hop", "live+jump+records"]
 
 
 def main():
@@ -51,10 +51,10 @@ def main():
         prof(arr, 1)
         mprof(marr, 1)
         blocks = tiles * reps
-        r = {PHASES[i]: round(arr[i] / blocks, 1) for i in range(5)}
+        r = {PHASES[i]: round(arr[i] / blocks, 1) for i in range(len(PHASES))}
         r["candidates_per_tile"] = round(arr[5] / blocks, 1)
-        r["jump_rounds_per_tile"] = round(arr[6] / blocks, 2)
-        r["survivors_per_tile"] = round(arr[7] / blocks, 2)
+        r["live_per_tile"] = round(arr[6] / blocks, 2)
+        r["jump_rounds_per_tile"] = round(arr[7] / blocks, 2)
         # clock64 ticks -> GHz via the 100 MHz wall clock over the same wavefronts
         r["clock_GHz"] = round(arr[13] / (arr[12] * 10.0), 3) if arr[12] else None
         # merge kernels: 10-ns ticks -> us; per-workgroup averages, last-WG phases

@@ -28,7 +28,7 @@ enum Counter {
     kCntTerm = 5,        // terminal code of the path
     kCntLast = 6,        // last path node
     kCntSpill = 7,       // survivors spilled by dense tiles
-    kCntUnused8 = 8,
+    kCntEmitDoubling = 8, // super tiles whose k_emit marked the chain by pointer doubling (diagnostic)
     kCntFallback = 9,    // the resolve failed (workspace capacity): the result says so, k_emit skips
     kCntTicket = 10,     // k_link workgroups finished (the last one resolves the path)
     kCntTails = 11,      // super-tile exit tails appended by k_merge

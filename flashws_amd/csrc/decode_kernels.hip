@@ -51,10 +51,15 @@ __device__ unsigned long long g_scan_prof[16];
 constexpr uint32_t kCandCap = 256;           // k_scan: candidates per tile (else dense_tile in k_merge)
 constexpr uint32_t kLiveCap = 64;            // k_scan: live nodes per tile, one per lane
 constexpr uint32_t kDeadLane = 0xFFu;        // k_scan pointer jumping: the chain dies
+// k_scan's halo: the next tile's first bytes, enough for the two-byte test at
+// any exit a 7-bit length form can reach from inside the tile (2047 + 6 + 125,
+// + 1) -- a chain whose exit there fails it is dead, not a survivor
+constexpr uint32_t kHaloX = 144;
+static_assert(kHaloX >= 2047u + 6u + 125u + 2u - kTile && kHaloX % 16u == 0 && kHaloX / 16u <= 64u, "halo");
 
 // LDS of one k_scan wavefront
 struct ScanLds {
-    uint8_t bytes[kTile + kHalo];
+    uint8_t bytes[kTile + kHaloX];
     uint32_t cm[64];                         // candidate bits of lane L's 32 offsets
     uint32_t lm[64];                         // live bits of lane L's 32 offsets
     uint32_t lpre[64];                       // live index of lane L's first live offset
@@ -93,7 +98,7 @@ __global__ __launch_bounds__(kScanThreads) __attribute__((amdgpu_waves_per_eu(8,
     const uint32_t L32 = lane * 32u;
     const uint32_t L16 = lane * 16u;
     // last tile whose bytes + halo lie inside the stream (prefetch clamp)
-    const uint32_t last_inner = kPipe ? (uint32_t)((N - kHalo) / kTile) - 1u : 0u;
+    const uint32_t last_inner = kPipe ? (uint32_t)((N - kHaloX) / kTile) - 1u : 0u;
     // idle lanes' stores go to this wave's own 64-B line (L2-resident, no hot spot)
     fws_frame_info *const dummy_info = reinterpret_cast<fws_frame_info *>(scan_dummy + (uint64_t)gw * 16u);
     uint32_t *const dummy_cnt = scan_dummy + (uint64_t)gw * 16u + 8u;
@@ -109,7 +114,7 @@ __global__ __launch_bounds__(kScanThreads) __attribute__((amdgpu_waves_per_eu(8,
         // coalesced: each load instruction reads 1 KiB contiguous (lane L: 16 B at 16L)
         pf[0] = gload16(reinterpret_cast<uintptr_t>(wire + o + L16));
         pf[1] = gload16(reinterpret_cast<uintptr_t>(wire + o + 1024u + L16));
-        halo = gload16(reinterpret_cast<uintptr_t>(wire + o + kTile));
+        halo = gload16(reinterpret_cast<uintptr_t>(wire + o + kTile + (L16 < kHaloX ? L16 : 0u)));
     };
 
     auto tile = [&](const uint32_t t, u32x4 (&pf)[2], u32x4 &halo) {
@@ -126,9 +131,9 @@ __global__ __launch_bounds__(kScanThreads) __attribute__((amdgpu_waves_per_eu(8,
             if (inner) {
                 *reinterpret_cast<u32x4 *>(B + L16) = pf[0];
                 *reinterpret_cast<u32x4 *>(B + 1024u + L16) = pf[1];
-                if (lane == 0) *reinterpret_cast<u32x4 *>(B + kTile) = halo;
+                if (L16 < kHaloX) *reinterpret_cast<u32x4 *>(B + kTile + L16) = halo;
             } else {
-                for (uint32_t i = lane * 16u; i < kTile + kHalo; i += 64u * 16u) {
+                for (uint32_t i = lane * 16u; i < kTile + kHaloX; i += 64u * 16u) {
                     const uint64_t q = t0 + i;
                     if (q + 16u <= N) {
                         *reinterpret_cast<u32x4 *>(B + i) = gload16(reinterpret_cast<uintptr_t>(wire + q));
@@ -225,6 +230,11 @@ __global__ __launch_bounds__(kScanThreads) __attribute__((amdgpu_waves_per_eu(8,
                         const uint64_t nxo = t0 + p + (uint64_t)r + plen;
                         if (nxo >= t0 + kTile || nxo >= N) {
                             ptr = lane;                        // leaves the tile / the stream
+                            const uint64_t hx = nxo - t0;      // unless its exit, in the halo, is no header
+                            if (nxo + 2u <= N && hx + 1u < kTile + kHaloX) {
+                                const uint32_t e0 = B[hx], e1 = B[hx + 1u];
+                                if ((e0 & 0x77u) > 2u || !(e1 & 0x80u)) ptr = kDeadLane;
+                            }
                         } else {
                             const uint32_t nx = (uint32_t)(nxo - t0);
                             const uint32_t m = W.lm[nx >> 5], bit = nx & 31u;
@@ -412,7 +422,7 @@ int fws_launch_decode(fws_gpu_ctx *ctx, uint8_t *wire, uint64_t N, fws_frame_inf
     if (n_tiles) {
         const uint32_t need = (n_tiles + kScanWaves - 1) / kScanWaves;
         const uint32_t sg = need < d.scan_grid ? need : d.scan_grid;
-        hipLaunchKernelGGL(N >= kTile + kHalo ? k_scan<true> : k_scan<false>, dim3(sg), dim3(kScanThreads), 0, s,
+        hipLaunchKernelGGL(N >= kTile + kHaloX ? k_scan<true> : k_scan<false>, dim3(sg), dim3(kScanThreads), 0, s,
                            wire, N, n_tiles, d.stage_info, d.spill_info, d.tile_spill, d.tile_count, d.counters,
                            (uint32_t)d.max_surv, d.scan_dummy);
         if ((e = hipGetLastError()) != hipSuccess) return fws_hip_status(e);

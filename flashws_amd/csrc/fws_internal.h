@@ -66,9 +66,16 @@ struct fws_tail_rec {                 // one EXIT tail: a chain leaving its supe
     uint32_t pad;
 };
 
-// one survivor in its super tile's table (k_merge -> k_emit):
-// slot id (bits 0-31) | in-ST next or exit code (32-47) | frame bit (48)
-typedef uint64_t fws_st_node;
+// one survivor in its super tile's table (k_merge -> k_emit)
+struct fws_st_node {
+    uint32_t sid;                     // slot id of the record
+    uint16_t nx;                      // in-ST next (local index) or exit code
+    uint16_t tail;                    // local index of its chain's tail in the ST
+    uint16_t cnt;                     // frames from it up to and including the tail
+    uint8_t wt;                       // 1: a frame; 0: incomplete header
+    uint8_t pad0;
+    uint32_t pad1;
+};
 
 // Stream-decode workspace (decode_kernels.hip, merge_kernels.hip).
 struct fws_decode_ws {

@@ -80,21 +80,14 @@ __device__ unsigned long long g_merge_trace[kTraceWg * 32];
 #define MP_INIT() uint64_t mp_t = wall_clock64()
 #define MP_MARK(k)                                                                  \
     do {                                                                            \
-        if (threadIdx.x == 0) {                                                     \
+        if (threadIdx.x == 0) {   /* a plain store: no same-address atomic queue */ \
             const uint64_t now = wall_clock64();                                    \
-            atomicAdd(&g_merge_prof[k], (unsigned long long)(now - mp_t));          \
             g_merge_trace[(blockIdx.x % kTraceWg) * 32 + (k)] = now;                \
             mp_t = now;                                                             \
         }                                                                           \
     } while (0)
-#define MP_ADD(k, v) do { if (threadIdx.x == 0) atomicAdd(&g_merge_prof[k], (unsigned long long)(v)); } while (0)
-#define MP_SPAN(k0, k1)                                                             \
-    do {                                                                            \
-        if (threadIdx.x == 0) {                                                     \
-            atomicMin(&g_merge_prof[k0], (unsigned long long)mp_t0);                \
-            atomicMax(&g_merge_prof[k1], (unsigned long long)wall_clock64());       \
-        }                                                                           \
-    } while (0)
+#define MP_ADD(k, v) do { } while (0)          /* same-address atomics would queue behind each other */
+#define MP_SPAN(k0, k1) do { } while (0)
 #else
 #define MP_START(slot) do { } while (0)
 #define MP_T0() do { } while (0)
@@ -162,7 +155,7 @@ struct MergeParams {
     __device__ __forceinline__ bool big(uint32_t n) const { return force_big || n > kStCap; }
     // the record of a chain's tail survivor in ST s (fws_node_res::tail of a non-EXIT kind)
     __device__ __forceinline__ const fws_frame_info *tail_rec(uint32_t s, const fws_node_res &r) const {
-        return (r.kind & kBigBit) ? rec(r.tail) : rec((uint32_t)st_nodes[(uint64_t)s * kStCap + r.tail]);
+        return (r.kind & kBigBit) ? rec(r.tail) : rec(st_nodes[(uint64_t)s * kStCap + r.tail].sid);
     }
 
     // slot id of survivor r of tile t (stage slots, or the tile's spill run)
@@ -489,7 +482,6 @@ __global__ __launch_bounds__(kMThreads) void k_merge(MergeParams P) {
         const bool tail = v >= kNxInc;
         L.ptr[0][i] = tail ? (uint16_t)i : v;
         L.sc[0][i] = tail ? 0 : L.wt[i];
-        tab[i] = (uint64_t)nid[j] | ((uint64_t)v << 32) | ((uint64_t)L.wt[i] << 48);
     }
     __syncthreads();                                 // off[] dead: lref[] reuses it
 #pragma unroll
@@ -538,6 +530,15 @@ __global__ __launch_bounds__(kMThreads) void k_merge(MergeParams P) {
         const uint32_t cnt = L.sc[cur][i] + L.wt[t];
         const uint32_t ref = kind == kKindExit ? tb + L.lref[t] : t;
         P.nres[nid[j]] = fws_node_res{ref, cnt, i, kind};
+        fws_st_node nd;
+        nd.sid = nid[j];
+        nd.nx = vv[j];
+        nd.tail = (uint16_t)t;
+        nd.cnt = (uint16_t)cnt;
+        nd.wt = L.wt[i];
+        nd.pad0 = 0;
+        nd.pad1 = 0;
+        tab[i] = nd;
         if (vv[j] == kNxExit) {
             const uint64_t x = exit_of(r[j]);
             P.tails[tb + L.lref[i]] = fws_tail_rec{x, nid[j], kTermDead, (uint32_t)(x / kStBytes), 0u};
@@ -897,8 +898,12 @@ __global__ __launch_bounds__(kMThreads) void k_link(MergeParams P) {
 struct EmitLds {
     uint16_t ptr[2][kStCap];
     uint8_t mark[kStCap];
+    uint16_t hist[kStCap + 2];                       // marked survivors per chain depth (frames to the tail)
+    uint16_t rs[kStCap + 2];                         // the entry chain's survivor at each depth
     uint32_t red32[kMWaves];
 };
+constexpr uint16_t kUnres = 0xFFFF;
+constexpr uint32_t kDepthRounds = 16;                // then pointer doubling
 
 // The big-ST path of k_emit (k_merge's merge_big): the same marking of the
 // entry's chain by pointer doubling, over slot ids in global scratch; the
@@ -974,7 +979,7 @@ __device__ void emit_big(const MergeParams &P, uint32_t s, uint32_t n, uint32_t 
 __global__ __launch_bounds__(kMThreads) void k_emit(MergeParams P) {
     __shared__ EmitLds L;
     const uint32_t s = blockIdx.x, tid = threadIdx.x;
-    const uint32_t *const C = P.counters;
+    uint32_t *const C = P.counters;
     MP_START(28);
     MP_T0();
     MP_INIT();
@@ -991,49 +996,103 @@ __global__ __launch_bounds__(kMThreads) void k_emit(MergeParams P) {
     const uint32_t i0 = kPer * tid;
     fws_st_node nd[kPer];
 #pragma unroll
-    for (uint32_t j = 0; j < kPer; ++j) nd[j] = i0 + j < n ? tab[i0 + j] : 0ull;
-#pragma unroll
-    for (uint32_t j = 0; j < kPer; ++j) {
-        const uint32_t i = i0 + j;
-        if (i < n) {
-            const uint16_t v = (uint16_t)(nd[j] >> 32);
-            L.ptr[0][i] = v >= kNxInc ? (uint16_t)i : v;
-            L.mark[i] = i == e;
-        }
-    }
-    __syncthreads();
-    MP_MARK(24);
-    // marks double along the chain: after round k every node within 2^k steps of the entry
-    int cur = 0;
-    for (;;) {
-        int changed = 0;
-        for (uint32_t i = tid; i < n; i += kMThreads) {
-            const uint16_t p = L.ptr[cur][i];
-            if (L.mark[i] && !L.mark[p]) {
-                L.mark[p] = 1;
-                changed = 1;
-            }
-            L.ptr[cur ^ 1][i] = L.ptr[cur][p];
-        }
-        cur ^= 1;
-        if (!__syncthreads_or(changed)) break;
-    }
-    MP_MARK(25);
-    // the chain's frames in offset order (records loaded in one batch), and
-    // their stream-space plan units
+    for (uint32_t j = 0; j < kPer; ++j) nd[j] = tab[i0 + j < n ? i0 + j : e];   // one batch, the entry's row too
+    const fws_st_node ne = tab[e];
+    // the entry's chain = the survivors at or after it with its tail, when their
+    // frame count is the entry's: any other survivor joining the chain (a false
+    // chain merging into it) makes the count larger, and the marks double along
+    // the next pointers instead (exact either way)
     bool fr[kPer];
     uint32_t fl = 0;
 #pragma unroll
     for (uint32_t j = 0; j < kPer; ++j) {
         const uint32_t i = i0 + j;
-        fr[j] = i < n && L.mark[i] && ((nd[j] >> 48) & 1u);
+        fr[j] = i < n && i >= e && nd[j].tail == ne.tail && nd[j].wt;
         fl += fr[j];
     }
+    uint32_t ftot;
+    uint32_t fpre = block_excl<uint32_t>(fl, L.red32, &ftot);
+    MP_MARK(24);
+    if (ftot != ne.cnt) {
+        // other survivors joined the chain (false chains merging into it: common,
+        // a few per super tile): exactly one survivor per depth is on the entry's
+        // chain -- the only one at its depth, or next() of the one a depth above
+        const uint32_t D = ne.cnt;                   // the entry's depth (frames to the tail)
+        for (uint32_t c = tid; c <= D; c += kMThreads) {
+            L.hist[c] = 0;
+            L.rs[c] = kUnres;
+        }
+        __syncthreads();
+        bool mk[kPer];
+#pragma unroll
+        for (uint32_t j = 0; j < kPer; ++j) {
+            const uint32_t i = i0 + j;
+            mk[j] = i < n && i >= e && nd[j].tail == ne.tail && nd[j].cnt <= D;
+            if (i < n) L.ptr[0][i] = nd[j].nx;
+            if (mk[j]) {
+                atomicAdd(reinterpret_cast<uint32_t *>(&L.hist[nd[j].cnt & ~1u]), 1u << (16u * (nd[j].cnt & 1u)));
+                L.rs[nd[j].cnt] = (uint16_t)i;
+            }
+        }
+        __syncthreads();
+        for (uint32_t c = tid; c <= D; c += kMThreads)
+            if (L.hist[c] != 1) L.rs[c] = c == D ? (uint16_t)e : kUnres;
+        __syncthreads();
+        bool open = true;
+        for (uint32_t round = 0; round < kDepthRounds && open; ++round) {
+            int pend = 0;
+            for (uint32_t c = tid; c < D; c += kMThreads) {
+                if (L.rs[c] != kUnres) continue;
+                const uint16_t up = L.rs[c + 1];
+                if (up != kUnres) L.rs[c] = L.ptr[0][up];
+                else pend = 1;
+            }
+            open = __syncthreads_or(pend);
+        }
+        if (open) {
+            if (tid == 0) atomicAdd(&C[kCntEmitDoubling], 1u);
+#pragma unroll
+            for (uint32_t j = 0; j < kPer; ++j) {
+                const uint32_t i = i0 + j;
+                if (i < n) {
+                    const uint16_t v = nd[j].nx;
+                    L.ptr[0][i] = v >= kNxInc ? (uint16_t)i : v;
+                    L.mark[i] = i == e;
+                }
+            }
+            __syncthreads();
+            // marks double along the chain: after round k every node within 2^k steps of the entry
+            int cur = 0;
+            for (;;) {
+                int changed = 0;
+                for (uint32_t i = tid; i < n; i += kMThreads) {
+                    const uint16_t p = L.ptr[cur][i];
+                    if (L.mark[i] && !L.mark[p]) {
+                        L.mark[p] = 1;
+                        changed = 1;
+                    }
+                    L.ptr[cur ^ 1][i] = L.ptr[cur][p];
+                }
+                cur ^= 1;
+                if (!__syncthreads_or(changed)) break;
+            }
+        }
+        fl = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < kPer; ++j) {
+            const uint32_t i = i0 + j;
+            fr[j] = nd[j].wt && (open ? (i < n && L.mark[i]) : (mk[j] && L.rs[nd[j].cnt] == i));
+            fl += fr[j];
+        }
+        fpre = block_excl<uint32_t>(fl, L.red32, &ftot);
+    }
+    MP_MARK(25);
+    // the chain's frames in offset order (records loaded in one batch), and
+    // their stream-space plan units
     fws_frame_info rc[kPer];                         // unconditional (slot 0 for the unused ones):
 #pragma unroll                                        // conditional loads each waited for their data
-    for (uint32_t j = 0; j < kPer; ++j) rc[j] = *P.rec(fr[j] ? (uint32_t)nd[j] : 0u);
-    uint32_t ftot;
-    uint32_t f = fbase + block_excl<uint32_t>(fl, L.red32, &ftot);
+    for (uint32_t j = 0; j < kPer; ++j) rc[j] = *P.rec(fr[j] ? nd[j].sid : 0u);
+    uint32_t f = fbase + fpre;
 #pragma unroll
     for (uint32_t j = 0; j < kPer; ++j) {
         if (!fr[j]) continue;

@@ -160,6 +160,32 @@ def test_random_small_frames(ctx, cuda, seed):
     check(ctx, cuda, b"".join(out))
 
 
+@pytest.mark.parametrize("seed", range(2))
+def test_false_chains_join_the_path(ctx, cuda, seed):
+    """Planted headers inside payloads whose exits land exactly on the next
+    true header: false chains that merge into the true one inside a super tile
+    (k_emit's tail-equality marking must see the extra survivors and fall back
+    to pointer doubling). Bit-exact with the oracle."""
+    rng = np.random.default_rng(700 + seed)
+    frames = []
+    for i in range(4000):
+        n = int(rng.integers(60, 2000))
+        frames.append(bytearray(frame(2, rng.integers(0, 256, n, dtype=np.uint8).tobytes(),
+                                      key=int(rng.integers(0, 2**32)))))
+    for i in range(0, len(frames) - 1, 3):
+        f = frames[i]
+        hl = 8 if len(f) - 8 >= 126 else 6               # this frame's header length
+        pl = len(f) - hl
+        # a fake 6-byte header at payload offset q whose next header is frames[i + 1]
+        if pl < 6:
+            continue
+        flen = int(rng.integers(0, min(126, pl - 5)))      # its payload ends at frames[i + 1]
+        q = pl - 6 - flen
+        pos = hl + q
+        f[pos:pos + 6] = bytes([0x82, 0x80 | flen]) + int(rng.integers(0, 2**32)).to_bytes(4, "little")
+    check(ctx, cuda, b"".join(bytes(f) for f in frames))
+
+
 @pytest.mark.parametrize("seed", range(3))
 def test_tiny_frames_dense_tiles(ctx, cuda, seed):
     """Frames of 0..24 B payload (~100 headers per 2 KiB tile): k_scan leaves

@@ -7,3 +7,4 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_decode.py tests/test_gpu_pi
 tail -2 gpurun_out/dec_tests.log
 bash tools/gpu_kt_decode.sh
 
+timeout -k 10 200 python tools/prof_merge_trace.py > gpurun_out/merge_trace.json 2> gpurun_out/merge_trace.err || true

@@ -27,9 +27,6 @@ def main():
     prof = L.fws_internal_scan_prof
     prof.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
     prof.restype = C.c_int
-    mprof = L.fws_internal_merge_prof
-    mprof.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
-    mprof.restype = C.c_int
     out = {}
     for name, mk in (("C2", gpu.config_c2), ("C3", gpu.config_c3)):
         wire, descs, _ = mk()
@@ -42,14 +39,11 @@ def main():
             gpu.decode_stream(ctx, w.clone(), cap=n + 16)
         torch.cuda.synchronize()
         arr = (C.c_ulonglong * 16)()
-        marr = (C.c_ulonglong * 32)()
         prof(arr, 1)
-        mprof(marr, 1)
         for _ in range(reps):
             gpu.decode_stream(ctx, w.clone(), cap=n + 16)
             torch.cuda.synchronize()
         prof(arr, 1)
-        mprof(marr, 1)
         blocks = tiles * reps
         r = {PHASES[i]: round(arr[i] / blocks, 1) for i in range(len(PHASES))}
         r["candidates_per_tile"] = round(arr[5] / blocks, 1)
@@ -57,19 +51,6 @@ def main():
         r["jump_rounds_per_tile"] = round(arr[7] / blocks, 2)
         # clock64 ticks -> GHz via the 100 MHz wall clock over the same wavefronts
         r["clock_GHz"] = round(arr[13] / (arr[12] * 10.0), 3) if arr[12] else None
-        # merge kernels: 10-ns ticks -> us; per-workgroup averages, last-WG phases
-        us = lambda v: round(v / 100.0, 2)
-        wg = max(marr[5], 1)
-        r["k_merge_wg_us"] = {k: us(marr[i] / wg) for i, k in enumerate(
-            ["counts", "records", "next+table", "jump", "tails"])}
-        r["k_link_wg_us"] = us(marr[8] / max(marr[9], 1))
-        r["k_link_last_wg_us"] = {k: us(marr[10 + i] / reps) for i, k in enumerate(
-            ["root+zero", "compact", "next", "prune", "entries", "st_scan"])}
-        r["k_link_terminal_us"] = us(marr[17] / reps)
-        r["marked_tails"] = marr[16] // reps
-        ew = max(marr[27], 1)
-        r["k_emit_wg_us"] = {k: us(marr[24 + i] / ew) for i, k in enumerate(["load", "mark", "write"])}
-        r["k_emit_wgs"] = marr[27] // reps
         out[name] = r
     print(json.dumps(out, indent=1))
 

@@ -22,7 +22,7 @@ __device__ __forceinline__ bool is_term(uint32_t v) { return v >= kTermIncomplet
 enum Counter {
     kCntSurv = 0,        // survivors (sum of the tiles' counts)
     kCntOverflow = 1,    // bit 0: k_scan's survivor spill capacity exceeded
-    kCntUnused2 = 2,
+    kCntDenseTiles = 2,  // tiles k_scan left to dense_tile() (diagnostic)
     kCntFrames = 3,      // frames emitted (device frame count, read by the unmask)
     kCntRoot = 4,        // survivor index of the header at offset 0 (kNone if absent)
     kCntTerm = 5,        // terminal code of the path
@@ -35,7 +35,26 @@ enum Counter {
     kCntBig = 12,        // super tiles that took k_merge's big-ST path (diagnostic)
     kCntCount = 13
 };
-constexpr uint32_t kCntStride = 16;          // words per counter set (fws_decode_ws::cnt_base)
+constexpr uint32_t kCntStride = 128;         // words per counter set (fws_decode_ws::cnt_base)
+// Spill runs: k_scan wavefront gw reserves from region gw % kSpillRegions (its
+// own counter at kCntRegion0 + region: no single hot atomic when every tile
+// spills), then from the shared second half (kCntSpill; dense_tile uses only that)
+constexpr uint32_t kSpillRegions = 64;
+constexpr uint32_t kCntRegion0 = 64;
+static_assert(kCntRegion0 >= kCntCount && kCntRegion0 + kSpillRegions <= kCntStride, "counter layout");
+// [0, half): kSpillRegions regions of region_size; [half, s_cap): shared
+__device__ __forceinline__ uint32_t spill_half(uint32_t s_cap) { return s_cap / 2u; }
+__device__ __forceinline__ uint32_t spill_region_size(uint32_t s_cap) { return spill_half(s_cap) / kSpillRegions; }
+// a shared spill run of ns records, or kNone (capacity exceeded: kCntOverflow set)
+__device__ __forceinline__ uint32_t spill_shared(uint32_t *counters, uint32_t s_cap, uint32_t ns) {
+    const uint32_t off = atomicAdd(&counters[kCntSpill], ns);
+    const uint32_t room = s_cap - spill_half(s_cap);
+    if (off > room || room - off < ns) {
+        atomicOr(&counters[kCntOverflow], 1u);
+        return kNone;
+    }
+    return spill_half(s_cap) + off;
+}
 static_assert(kCntFrames == kDecodeFramesCounter, "fws_internal.h names the frame counter");
 
 constexpr uint32_t kSlots = 8;               // per-tile survivor slots before spilling

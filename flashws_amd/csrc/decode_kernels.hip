@@ -258,13 +258,13 @@ __global__ __launch_bounds__(kScanThreads) __attribute__((amdgpu_waves_per_eu(8,
                     srank = mbcnt64(sm);
                     if (ns > kSlots) {
                         // more survivors than slots (frames under ~250 B): a spill run
-                        if (lane == 0) spill = atomicAdd(&counters[kCntSpill], ns);
-                        spill = __shfl(spill, 0, 64);
-                        if (spill > s_cap || s_cap - spill < ns) {
-                            if (lane == 0) atomicOr(&counters[kCntOverflow], 1u);
-                            ns = 0;
-                            spill = kNone;
+                        if (lane == 0) {
+                            const uint32_t rs = spill_region_size(s_cap), rg = gw % kSpillRegions;
+                            const uint32_t off = atomicAdd(&counters[kCntRegion0 + rg], ns);
+                            spill = (off <= rs && rs - off >= ns) ? rg * rs + off : spill_shared(counters, s_cap, ns);
                         }
+                        spill = __shfl(spill, 0, 64);
+                        if (spill == kNone) ns = 0;
                     }
                     rec = surv && ns != 0;
                     fi.hdr_off = t0 + p;
@@ -363,8 +363,11 @@ extern "C" int fws_internal_set_scan_blocks_per_cu(int v) {
 int fws_decode_ensure(fws_gpu_ctx *ctx, uint64_t N, uint32_t cap) {
     fws_decode_ws &d = ctx->dec;
     const uint64_t tiles = (N + kTile - 1) / kTile + 1;
-    uint64_t s_cap = N / 256 + 8 * tiles + (uint64_t)cap + 64;
-    if (ctx->cap_frames + 8 * tiles > s_cap) s_cap = ctx->cap_frames + 8 * tiles;
+    // spill capacity: every frame a survivor twice over (half of it is split in
+    // kSpillRegions regions, decode_common.h), plus random survivors
+    uint64_t s_cap = N / 256 + 8 * tiles + 2 * (uint64_t)cap + 64;
+    if (2 * ctx->cap_frames + 8 * tiles > s_cap) s_cap = 2 * ctx->cap_frames + 8 * tiles;
+    if (s_cap > 0xF0000000ull) s_cap = 0xF0000000ull;   // 32-bit slot ids
     if (tiles <= d.max_tiles && s_cap <= d.max_surv) return 0;
     const uint64_t nt = tiles > d.max_tiles ? tiles : d.max_tiles;
     const uint64_t ns = s_cap > d.max_surv ? s_cap : d.max_surv;

@@ -229,10 +229,12 @@ __device__ __forceinline__ T block_excl(T v, T *sred, T *total) {
 
 // ------------------------------------------------------------------ k_merge
 constexpr uint32_t kDenseWaves = 4;                 // k_merge wavefronts running dense_tile()
+constexpr uint32_t kMidCap = 8192;                  // big super tiles merged / emitted in LDS (else global scratch)
 struct MergeLds {
     uint32_t tcnt[kStTiles];
     uint32_t tsp[kStTiles];
     uint32_t tbase[kStTiles];
+    uint16_t boff[kMidCap];                          // mid path: tile-local offset of survivor i
     union {
         struct {
             union {
@@ -245,6 +247,7 @@ struct MergeLds {
             uint16_t sc[2][kStCap];                  // frames from i up to ptr (exclusive)
         };
         ScanWaveLds dw[kDenseWaves];                 // first: the tiles k_scan left (dense_tile)
+        uint32_t bw[kMidCap];                        // mid path: ptr | frames << 16 | kind << 29 | frame bit << 31
     };
     uint32_t red32[kMWaves];
     uint32_t n_tail, tail_base;
@@ -339,6 +342,141 @@ __device__ void merge_big(const MergeParams &P, MergeLds &L, uint32_t s, uint32_
     }
 }
 
+// A super tile with kStCap < n <= kMidCap survivors (frames of ~70 B and up):
+// the big path's outputs (fws_node_res with kBigBit; bg_ptr[id] = in-ST next as
+// a local index or itself for a tail, bg_wt, bg_nx = exit kind, bg_lref) with
+// the chain work in LDS: the exit search over tile-local offsets (boff) and
+// in-place pointer jumping on one word per survivor (a pair read or written
+// as one 32-bit word stays consistent, so rounds need no second buffer).
+// Global loads are issued four survivors at a time.
+constexpr uint32_t kMidB = 4;
+__device__ void merge_mid(const MergeParams &P, MergeLds &L, uint32_t s, uint32_t n) {
+    const uint32_t tid = threadIdx.x, t0 = s * kStTiles;
+    const uint64_t st0 = uint64_t(s) * kStBytes, st_end = st0 + kStBytes;
+    uint32_t *const C = P.counters;
+    MP_INIT();
+    // pass 1: tile-local offsets
+    for (uint32_t base = tid; base < n; base += kMidB * kMThreads) {
+        uint32_t id[kMidB];
+        uint64_t off[kMidB];
+#pragma unroll
+        for (uint32_t b = 0; b < kMidB; ++b) {
+            const uint32_t i = base + b * kMThreads;
+            id[b] = st_sid(P, L, t0, i < n ? i : base);
+        }
+#pragma unroll
+        for (uint32_t b = 0; b < kMidB; ++b) off[b] = P.rec(id[b])->hdr_off;
+#pragma unroll
+        for (uint32_t b = 0; b < kMidB; ++b) {
+            const uint32_t i = base + b * kMThreads;
+            if (i < n) L.boff[i] = (uint16_t)(off[b] % kTile);
+        }
+    }
+    __syncthreads();
+    MP_MARK(18);
+    // pass 2: in-ST next (the survivor at the exit, searched in the exit's tile)
+    for (uint32_t base = tid; base < n; base += kMidB * kMThreads) {
+        uint32_t id[kMidB];
+        fws_frame_info r[kMidB];
+#pragma unroll
+        for (uint32_t b = 0; b < kMidB; ++b) {
+            const uint32_t i = base + b * kMThreads;
+            id[b] = st_sid(P, L, t0, i < n ? i : base);
+        }
+#pragma unroll
+        for (uint32_t b = 0; b < kMidB; ++b) r[b] = *P.rec(id[b]);
+#pragma unroll
+        for (uint32_t b = 0; b < kMidB; ++b) {
+            const uint32_t i = base + b * kMThreads;
+            if (i >= n) continue;
+            const uint64_t x = exit_of(r[b]);
+            uint32_t kind = 0, nx = i;
+            bool tail = true;
+            if (!r[b].hdr_len) kind = kKindInc;
+            else if (x >= P.N) kind = kKindEnd;
+            else if (x >= st_end) kind = kKindExit;
+            else {
+                const uint32_t tl = (uint32_t)((x - st0) / kTile), xo = (uint32_t)(x % kTile);
+                uint32_t lo = L.tbase[tl], hi = lo + L.tcnt[tl];
+                while (lo < hi) {                    // first survivor of the tile at or past xo
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (L.boff[mid] < xo) lo = mid + 1; else hi = mid;
+                }
+                if (lo < L.tbase[tl] + L.tcnt[tl] && L.boff[lo] == xo) {
+                    nx = lo;
+                    tail = false;
+                } else {
+                    kind = kKindDead;
+                }
+            }
+            const uint32_t wt = r[b].hdr_len ? 1u : 0u;
+            L.bw[i] = nx | (tail ? 0u : wt << 16) | (kind << 29) | (wt << 31);
+            P.bg_ptr[id[b]] = nx;
+            P.bg_wt[id[b]] = wt;
+            P.bg_nx[id[b]] = tail ? kind : kNone;
+            if (tail && kind == kKindExit) P.bg_lref[id[b]] = atomicAdd(&L.n_tail, 1u);
+        }
+    }
+    __syncthreads();
+    MP_MARK(19);
+    if (tid == 0) {                                  // the ST's run of the tail list
+        const uint32_t k = L.n_tail;
+        uint32_t base = k ? atomicAdd(&C[kCntTails], k) : 0u;
+        if (k && (base > P.tail_cap || P.tail_cap - base < k)) {
+            atomicOr(&C[kCntFallback], 1u);
+            base = kNone;
+        }
+        L.tail_base = base;
+    }
+    // pointer jumping in place: ptr and frame count move together in one word
+    for (;;) {
+        int changed = 0;
+        for (uint32_t i = tid; i < n; i += kMThreads) {
+            const uint32_t w = L.bw[i], p = w & 0xFFFFu;
+            if (p == i) continue;
+            const uint32_t wp = L.bw[p], q = wp & 0xFFFFu;
+            if (q == p) continue;
+            const uint32_t c = ((w >> 16) & 0x1FFFu) + ((wp >> 16) & 0x1FFFu);
+            L.bw[i] = (w & 0xE0000000u) | q | (c << 16);
+            changed = 1;
+        }
+        if (!__syncthreads_or(changed)) break;
+    }
+    MP_MARK(20);
+    const uint32_t tb = L.tail_base;
+    if (tb == kNone) return;
+    for (uint32_t base = tid; base < n; base += kMidB * kMThreads) {
+        uint32_t id[kMidB], tid_[kMidB], lr[kMidB], own[kMidB];
+        uint64_t x[kMidB];
+#pragma unroll
+        for (uint32_t b = 0; b < kMidB; ++b) {
+            const uint32_t i = base + b * kMThreads < n ? base + b * kMThreads : base;
+            id[b] = st_sid(P, L, t0, i);
+            tid_[b] = st_sid(P, L, t0, L.bw[i] & 0xFFFFu);
+        }
+#pragma unroll
+        for (uint32_t b = 0; b < kMidB; ++b) {
+            lr[b] = P.bg_lref[tid_[b]];
+            own[b] = P.bg_lref[id[b]];
+            x[b] = exit_of(*P.rec(id[b]));
+        }
+#pragma unroll
+        for (uint32_t b = 0; b < kMidB; ++b) {
+            const uint32_t i = base + b * kMThreads;
+            if (i >= n) continue;
+            const uint32_t w = L.bw[i], t = w & 0xFFFFu, wt_t = L.bw[t];
+            const uint32_t kind = (wt_t >> 29) & 3u;
+            const uint32_t cnt = ((w >> 16) & 0x1FFFu) + (wt_t >> 31);
+            const uint32_t ref = kind == kKindExit ? tb + lr[b] : tid_[b];
+            P.nres[id[b]] = fws_node_res{ref, cnt, id[b], kind | kBigBit};
+            if (t == i && kind == kKindExit)
+                P.tails[tb + own[b]] = fws_tail_rec{x[b], id[b], kTermDead, (uint32_t)(x[b] / kStBytes), 0u};
+        }
+    }
+    __syncthreads();
+    MP_MARK(21);
+}
+
 __global__ __launch_bounds__(kMThreads) void k_merge(MergeParams P) {
     __shared__ MergeLds L;
     const uint32_t s = blockIdx.x, tid = threadIdx.x;
@@ -372,6 +510,7 @@ __global__ __launch_bounds__(kMThreads) void k_merge(MergeParams P) {
         if (w < kDenseWaves) {
             for (uint32_t i = w; i < kStTiles; i += kDenseWaves) {
                 if (L.tcnt[i] != kDenseTile) continue;           // wave-uniform
+                if ((tid & 63) == 0) atomicAdd(&C[kCntDenseTiles], 1u);
                 const uint64_t r = dense_tile(L.dw[w], P.wire, P.N, t0 + i, P.spill_w, C, P.s_cap);
                 const uint32_t dn = (uint32_t)r, dsp = (uint32_t)(r >> 32);
                 if ((tid & 63) == 0) {
@@ -405,7 +544,8 @@ __global__ __launch_bounds__(kMThreads) void k_merge(MergeParams P) {
     MP_MARK(0);
     if (P.big(n)) {
         if (tid == 0) atomicAdd(&C[kCntBig], 1u);
-        merge_big(P, L, s, n);
+        if (n <= kMidCap && !P.force_big) merge_mid(P, L, s, n);
+        else merge_big(P, L, s, n);
         return;
     }
 
@@ -896,10 +1036,19 @@ __global__ __launch_bounds__(kMThreads) void k_link(MergeParams P) {
 
 // ------------------------------------------------------------------ k_emit
 struct EmitLds {
-    uint16_t ptr[2][kStCap];
-    uint8_t mark[kStCap];
-    uint16_t hist[kStCap + 2];                       // marked survivors per chain depth (frames to the tail)
-    uint16_t rs[kStCap + 2];                         // the entry chain's survivor at each depth
+    union {
+        struct {
+            uint16_t ptr[2][kStCap];
+            uint8_t mark[kStCap];
+            uint16_t hist[kStCap + 2];               // marked survivors per chain depth (frames to the tail)
+            uint16_t rs[kStCap + 2];                 // the entry chain's survivor at each depth
+        };
+        struct {                                     // emit_mid
+            uint16_t mptr[kMidCap];
+            uint8_t mmark[kMidCap];                  // bit 0: on the entry's chain; bit 1: a frame
+        };
+    };
+    uint32_t mtb[kStTiles], mtsp[kStTiles];          // emit_mid: the ST's tile prefix
     uint32_t red32[kMWaves];
 };
 constexpr uint16_t kUnres = 0xFFFF;
@@ -976,6 +1125,118 @@ __device__ void emit_big(const MergeParams &P, uint32_t s, uint32_t n, uint32_t 
     }
 }
 
+// k_emit for a super tile merge_mid handled: the entry's chain marked by
+// synchronous pointer doubling in LDS (each round reads every pointer and mark
+// into registers, then writes), frames in offset order. Thread t owns
+// survivors [kMidPer * t, kMidPer * (t + 1)).
+constexpr uint32_t kMidPer = kMidCap / kMThreads;
+constexpr uint32_t kMidBatch = 4;
+static_assert(kMidPer * kMThreads == kMidCap && kMidPer % kMidBatch == 0, "mid survivors per thread");
+__device__ void emit_mid(const MergeParams &P, EmitLds &L, uint32_t s, uint32_t n, uint32_t e, uint32_t fbase,
+                         uint32_t lim) {
+    const uint32_t tid = threadIdx.x, t0 = s * kStTiles;
+    uint32_t c = 0, sp = kNone;
+    if (tid < kStTiles && t0 + tid < P.n_tiles) {
+        c = P.tile_count[t0 + tid];
+        sp = P.tile_spill[t0 + tid];
+    }
+    uint32_t tot;
+    const uint32_t b0 = block_excl<uint32_t>(c, L.red32, &tot);
+    if (tid < kStTiles) {
+        L.mtb[tid] = b0;
+        L.mtsp[tid] = sp;
+    }
+    __syncthreads();
+    const uint32_t i0 = kMidPer * tid;
+    uint32_t tl0;
+    {
+        uint32_t lo = 0, hi = kStTiles;              // tile of survivor i0
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (L.mtb[mid] <= i0) lo = mid; else hi = mid;
+        }
+        tl0 = lo;
+    }
+    // slot ids of this thread's survivors kMidBatch at a time, walking the tiles forward
+    auto ids = [&](uint32_t j0, uint32_t &tl, uint32_t (&id)[kMidBatch]) {
+#pragma unroll
+        for (uint32_t j = 0; j < kMidBatch; ++j) {
+            const uint32_t i = i0 + j0 + j < n ? i0 + j0 + j : i0;
+            while (tl + 1 < kStTiles && L.mtb[tl + 1] <= i) ++tl;
+            id[j] = P.sid(t0 + tl, L.mtsp[tl], i - L.mtb[tl]);
+        }
+    };
+    {
+        uint32_t tl = tl0;
+        for (uint32_t j0 = 0; j0 < kMidPer; j0 += kMidBatch) {
+            uint32_t id[kMidBatch], nx[kMidBatch], wt[kMidBatch];
+            ids(j0, tl, id);
+#pragma unroll
+            for (uint32_t j = 0; j < kMidBatch; ++j) {
+                nx[j] = P.bg_ptr[id[j]];
+                wt[j] = P.bg_wt[id[j]];
+            }
+#pragma unroll
+            for (uint32_t j = 0; j < kMidBatch; ++j) {
+                const uint32_t i = i0 + j0 + j;
+                if (i < n) {
+                    L.mptr[i] = (uint16_t)nx[j];
+                    L.mmark[i] = (uint8_t)((id[j] == e ? 1u : 0u) | (wt[j] << 1));
+                }
+            }
+        }
+    }
+    __syncthreads();
+    for (;;) {
+        uint32_t pr[kMidPer];                        // next pointer | target << 16
+        uint32_t mk = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < kMidPer; ++j) {
+            const uint32_t i = i0 + j;
+            pr[j] = 0;
+            if (i < n) {
+                const uint32_t p = L.mptr[i];
+                pr[j] = L.mptr[p] | (p << 16);
+                if ((L.mmark[i] & 1u) && !(L.mmark[p] & 1u)) mk |= 1u << j;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t j = 0; j < kMidPer; ++j) {
+            if (i0 + j < n) L.mptr[i0 + j] = (uint16_t)pr[j];
+            if (mk & (1u << j)) L.mmark[pr[j] >> 16] |= 1u;
+        }
+        if (!__syncthreads_or(mk != 0)) break;
+    }
+    // frames in offset order: this thread's run, then one block scan
+    uint32_t fl = 0, fm = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < kMidPer; ++j)
+        if (i0 + j < n && L.mmark[i0 + j] == 3u) {
+            fm |= 1u << j;
+            ++fl;
+        }
+    uint32_t ft;
+    uint32_t f = fbase + block_excl<uint32_t>(fl, L.red32, &ft);
+    uint32_t tl = tl0;
+    for (uint32_t j0 = 0; j0 < kMidPer; j0 += kMidBatch) {
+        uint32_t id[kMidBatch];
+        ids(j0, tl, id);
+        fws_frame_info rc[kMidBatch];
+#pragma unroll
+        for (uint32_t j = 0; j < kMidBatch; ++j) rc[j] = *P.rec(id[j]);
+#pragma unroll
+        for (uint32_t j = 0; j < kMidBatch; ++j) {
+            if (!((fm >> (j0 + j)) & 1u)) continue;
+            if (f < lim) {
+                P.put_frame(f, rc[j]);
+                P.plan_units(f, rc[j].hdr_off, exit_of(rc[j]), f == lim - 1);
+            }
+            ++f;
+        }
+    }
+}
+
 __global__ __launch_bounds__(kMThreads) void k_emit(MergeParams P) {
     __shared__ EmitLds L;
     const uint32_t s = blockIdx.x, tid = threadIdx.x;
@@ -989,7 +1250,8 @@ __global__ __launch_bounds__(kMThreads) void k_emit(MergeParams P) {
     const uint32_t lim = C[kCntFrames];
     if (fb || e == kNone || fbase >= lim) return;
     if (P.big(n)) {
-        emit_big(P, s, n, e, fbase, lim);
+        if (n <= kMidCap && !P.force_big) emit_mid(P, L, s, n, e, fbase, lim);
+        else emit_big(P, s, n, e, fbase, lim);
         return;
     }
     const fws_st_node *const tab = P.st_nodes + (uint64_t)s * kStCap;

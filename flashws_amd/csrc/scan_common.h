@@ -311,13 +311,9 @@ __device__ __noinline__ uint64_t dense_tile(ScanWaveLds &W, const uint8_t *__res
     }
     uint32_t spill = kNone;
     if (ns) {
-        if (lane == 0) spill = atomicAdd(&counters[kCntSpill], ns);
+        if (lane == 0) spill = spill_shared(counters, s_cap, ns);
         spill = __shfl(spill, 0, 64);
-        if (spill > s_cap || s_cap - spill < ns) {
-            if (lane == 0) atomicOr(&counters[kCntOverflow], 1u);
-            ns = 0;
-            spill = kNone;
-        }
+        if (spill == kNone) ns = 0;
     }
     wave_sync();
     if (ns) {

@@ -231,10 +231,13 @@ def test_c2_full_parity(ctx, cuda, resolve_mode):
         assert not fell_back(ctx), "C2 must resolve on the super-tile path with LDS tables"
 
 
-def test_dense_64b_frames(ctx, cuda, resolve_mode):
-    """200 000 x 64 B frames: super tiles with more survivors than
-    the LDS tables hold take the big-ST path, bit-exact either way."""
-    wire, descs, _ = gpu.config_c2(seed=65, n_frames=200_000, payload=64)
+@pytest.mark.parametrize("payload", [64, 120])
+def test_dense_64b_frames(ctx, cuda, resolve_mode, payload):
+    """200 000 x 64 B frames, and 120 B: super tiles with more
+    survivors than the LDS tables hold (~7 500 and ~4 000 per 512 KiB) take the
+    big-ST path -- merged and emitted in LDS (merge_mid / emit_mid), or over
+    global scratch when forced -- bit-exact either way."""
+    wire, descs, _ = gpu.config_c2(seed=65, n_frames=200_000, payload=payload)
     r = check(ctx, cuda, wire)
     assert int(r["n_frames"]) == 200_000
     c = counters(ctx)

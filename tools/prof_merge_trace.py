@@ -23,6 +23,8 @@ KW = 1024
 
 def stats(v):
     v = np.asarray(v, dtype=np.float64)
+    if v.size == 0:
+        return None
     return {"med": round(float(np.median(v)), 2), "p90": round(float(np.percentile(v, 90)), 2),
             "max": round(float(v.max()), 2)}
 
@@ -33,7 +35,9 @@ def main():
     tr = L.fws_internal_merge_trace
     tr.argtypes = [C.POINTER(C.c_ulonglong)]
     out = {}
-    for name, mk in (("C2", gpu.config_c2), ("C3", gpu.config_c3)):
+    cfgs = (("C2", gpu.config_c2), ("C3", gpu.config_c3),
+            ("dense64", lambda: gpu.config_c2(n_frames=200_000, payload=64)))
+    for name, mk in cfgs:
         wire, descs, _ = mk()
         n = len(descs)
         ctx = gpu.Ctx(0, max_frames=n + 16, max_stream_bytes=len(wire))
@@ -54,6 +58,12 @@ def main():
             r[f"k_merge_{lab}"] = stats(m[:, k] - prev)
             prev = m[:, k]
         r["k_merge_end_us"] = stats(m[:, 4] - t0)
+        big = m[:, 21] > m[:, 30]
+        if big.any():
+            prev = m[big, 0]
+            for k, lab in zip((18, 19, 20, 21), ["offsets", "next", "jump", "results"]):
+                r[f"merge_mid_{lab}"] = stats(m[big, k] - prev)
+                prev = m[big, k]
         e = t[:n_st]
         t0e = e[:, 28].min()
         ok = e[:, 26] > e[:, 28]
@@ -64,6 +74,11 @@ def main():
             prev = e[:, k]
         r["k_emit_end_us"] = stats(e[ok, 26] - t0e)
         r["gap_merge_end_to_emit_start_us"] = round(float(t0e - m[:, 4].max()), 2)
+        r["counters"] = gpu.decode_counters(ctx)
+        import ctypes as CT
+        raw = (CT.c_uint32 * 16)()
+        L.fws_internal_decode_counters(ctx.h, raw, 16)
+        r["counters_raw"] = list(raw)
         out[name] = r
         ctx.close()
     print(json.dumps(out, indent=1))

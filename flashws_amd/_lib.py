@@ -48,6 +48,10 @@ TX_DESC = np.dtype([("src_off", "<u8"), ("len", "<u8"), ("key", "<u4"), ("opcode
                     ("masked", "u1"), ("pad", "u1")])
 assert FRAME_DESC.itemsize == 24 and FRAME_INFO.itemsize == 24 and TX_DESC.itemsize == 24
 assert DECODE_RESULT.itemsize == 40 and RX_EVENT.itemsize == 48
+RX_READ = np.dtype([("conn", "<u4"), ("flags", "<u4"), ("buf", "<u8"), ("size", "<u8"), ("capacity", "<u8")])
+RX_READ_RESULT = np.dtype([("ret", "<i4"), ("pad", "<u4"), ("events", "<u8"), ("n_events", "<u8"),
+                           ("ctl", "<u8"), ("ctl_used", "<u8")])
+assert RX_READ.itemsize == 32 and RX_READ_RESULT.itemsize == 40
 
 
 class RxState(C.Structure):
@@ -90,6 +94,12 @@ SIGNATURES = [
     ("fws_rx_session_feed_view", _I, [_P, _P, _U64, _U64, C.POINTER(C.c_void_p), _PU64, C.POINTER(C.c_void_p),
                                       _PU64]),
     ("fws_rx_session_error", _I, [_P, C.POINTER(C.c_uint32)]),
+    ("fws_rx_mux_create", _I, [_P, _U32, C.POINTER(C.c_void_p)]),
+    ("fws_rx_mux_destroy", None, [_P]),
+    ("fws_rx_mux_reset", _I, [_P, _U32]),
+    ("fws_rx_mux_state", _I, [_P, _U32, _P]),
+    ("fws_rx_mux_error", _I, [_P, _U32, C.POINTER(C.c_uint32)]),
+    ("fws_rx_mux_feed", _I, [_P, _P, _U32, _P]),
     ("fws_gen_batch", _I, [C.POINTER(GenParams), _P, _U64, _PU64, _P, _U64, _PU64, _P]),
     ("fws_tx_next", None, [_U32, _I, C.POINTER(C.c_uint8), C.POINTER(C.c_uint8), C.POINTER(C.c_uint8)]),
     ("fws_gpu_encode_frames", _I, [_P, _P, _U64, _P, _P, _U32, _P, _P]),

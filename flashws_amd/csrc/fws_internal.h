@@ -20,6 +20,22 @@ constexpr int FWS_SMALL_DECLINED = -30;
 int fws_resolve_mode();   // decode_kernels.hip test hook (fws_internal_set_resolve_mode)
 int fws_launch_decode_small(uint8_t *wire, uint64_t N, fws_frame_info *frames, uint32_t cap,
                             fws_decode_result *res, hipStream_t s);
+// One segment of a multi-connection batch (fws_rx_mux, rx_session.cpp): the
+// continuation bytes [cont_off, cont_off + u) unmasked with `key` (rotated to
+// their first byte), then the header stream [hs_off, hs_off + L) decoded into
+// frames[fbase, fbase + fcap) and res[segment]. Both offsets 16-B aligned.
+struct fws_seg_desc {
+    uint64_t cont_off;
+    uint64_t hs_off;
+    uint32_t u;
+    uint32_t key;
+    uint32_t L;                        // <= kSmallMax
+    uint32_t fcap;
+    uint32_t fbase;
+    uint32_t pad;
+};
+int fws_launch_decode_segments(uint8_t *batch, const fws_seg_desc *segs, uint32_t n, fws_frame_info *frames,
+                               fws_decode_result *res, hipStream_t s);
 
 // Device workspace for the chunk plan of one descriptor batch.
 // Descriptor batches are planned two ways in one launch (k_plan): chunk space

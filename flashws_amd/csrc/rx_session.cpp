@@ -76,6 +76,20 @@ struct fws_rx_session {
     // the last protocol error of a feed (fws_rx_session_error)
     int err_code = 0;
     uint32_t err_opcode = 0;
+    bool borrowed_stream = false;     // a fws_rx_mux connection: the mux's stream
+
+    void reset_state() {              // a new connection (w_socket.h:223-245 initial values)
+        recv_status = kWaitHead;
+        unread = 0;
+        key = 0;
+        last_op = last_ctl_op = last_fin = 0;
+        is_ctl = false;
+        part_len = 0;
+        ctl_size = 0;
+        ctl_alloc = false;
+        err_code = 0;
+        err_opcode = 0;
+    }
 
     void push(const fws_rx_event &e) {
         if (own) own_ev.push_back(e);
@@ -243,7 +257,7 @@ void fws_rx_session_destroy(fws_rx_session *s) {
     if (s->dres) (void)hipFree(s->dres);
     if (s->hres) (void)hipHostFree(s->hres);
     if (s->hstage) (void)hipHostFree(s->hstage);
-    if (s->stream) (void)hipStreamDestroy(s->stream);
+    if (s->stream && !s->borrowed_stream) (void)hipStreamDestroy(s->stream);
     delete s;
 }
 
@@ -261,6 +275,9 @@ int fws_rx_session_state(const fws_rx_session *s, fws_rx_state *out) {
 }
 
 static int feed_impl(fws_rx_session *s, uint8_t *buf, uint64_t size, uint64_t buf_capacity);
+static int replay(fws_rx_session *s, uint8_t *buf, uint64_t size, uint64_t buf_capacity, uint64_t u,
+                  uint32_t part0, uint64_t rest, uint64_t L, const fws_decode_result &res,
+                  const fws_frame_info *frames);
 
 int fws_rx_session_feed(fws_rx_session *s, uint8_t *buf, uint64_t size, uint64_t buf_capacity,
                         fws_rx_event *events, uint64_t ev_cap, uint64_t *n_events,
@@ -391,7 +408,16 @@ static int feed_impl(fws_rx_session *s, uint8_t *buf, uint64_t size, uint64_t bu
                            hipMemcpyDeviceToHost)) != hipSuccess)
             return fws_hip_status(e);
     }
+    return replay(s, buf, size, buf_capacity, u, part0, rest, L, res, s->hframes);
+}
 
+// Steps 3-4 of a feed, once the read's bytes are unmasked in buf: OnRecvData's
+// loop replayed over the decoded frame list (res, frames: the header stream's
+// decode; u continuation bytes, part0 staged header bytes, rest = size - u,
+// L = part0 + rest).
+static int replay(fws_rx_session *s, uint8_t *buf, uint64_t size, uint64_t buf_capacity, uint64_t u,
+                  uint32_t part0, uint64_t rest, uint64_t L, const fws_decode_result &res,
+                  const fws_frame_info *frames) {
     // 3. replay OnRecvData's loop over the decoded parts
     if (u) {
         s->part(buf, size, buf_capacity, 0, u, size, kWaitPayload);
@@ -399,7 +425,7 @@ static int feed_impl(fws_rx_session *s, uint8_t *buf, uint64_t size, uint64_t bu
     if (!rest) return 0;   // the whole read was payload of the frame in progress
     // header stream coordinate x <-> read coordinate x - part0 + u
     for (uint32_t i = 0; i < res.n_frames; ++i) {
-        const fws_frame_info &fi = s->hframes[i];
+        const fws_frame_info &fi = frames[i];
         const uint32_t op = fi.opcode;
         // RFC 6455 §5.5: control frames are FIN and carry <= 125 B. The reference
         // only asserts this in debug builds (w_socket.h:654) and otherwise copies
@@ -439,6 +465,228 @@ static int feed_impl(fws_rx_session *s, uint8_t *buf, uint64_t size, uint64_t bu
         const uint64_t from_read = L - at - staged_before;
         memmove(s->hdr, win, have);
         s->part_len = (uint32_t)(staged_before + from_read);
+    }
+    return 0;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------- fws_rx_mux
+// The reads of many connections in one round trip (the
+// FLoop::OneStep shape, floop.h:661-703: every readable socket's read in one
+// loop iteration). Per connection a fws_rx_session holds the carried state
+// and replays OnRecvData's bookkeeping; the byte work of all reads is one
+// pinned staging pass, one H2D copy, one launch (k_decode_segments: one
+// workgroup per read) and one D2H copy. Reads a segment cannot take (a header
+// stream over kSmallMax bytes or kSmallFrames headers, a read over
+// kMuxMaxRead) go through the connection's own session afterwards.
+struct fws_rx_mux {
+    fws_gpu_ctx *ctx = nullptr;
+    hipStream_t stream = nullptr;
+    std::vector<fws_rx_session *> conns;
+    // pinned staging [segments] and its device copy
+    uint8_t *hbuf = nullptr, *dbuf = nullptr;
+    uint64_t bcap = 0;
+    // pinned [descriptors | results | frames] and its device copy
+    uint8_t *hmeta = nullptr, *dmeta = nullptr;
+    uint64_t mcap = 0;
+    std::vector<uint8_t> seen;        // per connection: fed in this call
+
+    int ensure(uint64_t bytes, uint64_t meta) {
+        hipError_t e;
+        if (bytes > bcap) {
+            if (hbuf) (void)hipHostFree(hbuf);
+            if (dbuf) (void)hipFree(dbuf);
+            hbuf = dbuf = nullptr;
+            bcap = (bytes + 65535) & ~65535ull;
+            if ((e = hipHostMalloc((void **)&hbuf, bcap)) != hipSuccess) { bcap = 0; return fws_hip_status(e); }
+            if ((e = hipMalloc((void **)&dbuf, bcap)) != hipSuccess) { bcap = 0; return fws_hip_status(e); }
+        }
+        if (meta > mcap) {
+            if (hmeta) (void)hipHostFree(hmeta);
+            if (dmeta) (void)hipFree(dmeta);
+            hmeta = dmeta = nullptr;
+            mcap = (meta + 65535) & ~65535ull;
+            if ((e = hipHostMalloc((void **)&hmeta, mcap)) != hipSuccess) { mcap = 0; return fws_hip_status(e); }
+            if ((e = hipMalloc((void **)&dmeta, mcap)) != hipSuccess) { mcap = 0; return fws_hip_status(e); }
+        }
+        return 0;
+    }
+};
+
+namespace {
+constexpr uint64_t kMuxMaxRead = 256u << 10;   // larger reads: the connection's session path
+constexpr uint32_t kNone = 0xFFFFFFFFu;
+inline uint64_t al16(uint64_t x) { return (x + 15) & ~15ull; }
+}  // namespace
+
+extern "C" {
+
+int fws_rx_mux_create(fws_gpu_ctx *ctx, uint32_t n_conns, fws_rx_mux **out) {
+    if (!ctx || !out || n_conns == 0) return FWS_ERR_INVALID;
+    *out = nullptr;
+    int r = fws_hip_status(hipSetDevice(ctx->device));
+    if (r) return r;
+    fws_rx_mux *m = new fws_rx_mux();
+    m->ctx = ctx;
+    if ((r = fws_hip_status(hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking)))) {
+        delete m;
+        return r;
+    }
+    m->conns.resize(n_conns, nullptr);
+    m->seen.resize(n_conns, 0);
+    for (uint32_t i = 0; i < n_conns; ++i) {
+        fws_rx_session *s = new fws_rx_session();
+        s->ctx = ctx;
+        s->stream = m->stream;
+        s->borrowed_stream = true;
+        m->conns[i] = s;
+    }
+    *out = m;
+    return 0;
+}
+
+void fws_rx_mux_destroy(fws_rx_mux *m) {
+    if (!m) return;
+    if (m->stream) (void)hipStreamSynchronize(m->stream);
+    for (fws_rx_session *s : m->conns) fws_rx_session_destroy(s);
+    if (m->hbuf) (void)hipHostFree(m->hbuf);
+    if (m->dbuf) (void)hipFree(m->dbuf);
+    if (m->hmeta) (void)hipHostFree(m->hmeta);
+    if (m->dmeta) (void)hipFree(m->dmeta);
+    if (m->stream) (void)hipStreamDestroy(m->stream);
+    delete m;
+}
+
+int fws_rx_mux_reset(fws_rx_mux *m, uint32_t conn) {
+    if (!m || conn >= m->conns.size()) return FWS_ERR_INVALID;
+    m->conns[conn]->reset_state();
+    return 0;
+}
+
+int fws_rx_mux_state(const fws_rx_mux *m, uint32_t conn, fws_rx_state *out) {
+    if (!m || conn >= m->conns.size()) return FWS_ERR_INVALID;
+    return fws_rx_session_state(m->conns[conn], out);
+}
+
+int fws_rx_mux_error(const fws_rx_mux *m, uint32_t conn, uint32_t *opcode) {
+    if (!m || conn >= m->conns.size()) return FWS_ERR_INVALID;
+    return fws_rx_session_error(m->conns[conn], opcode);
+}
+
+int fws_rx_mux_feed(fws_rx_mux *m, const fws_rx_read *reads, uint32_t n, fws_rx_read_result *results) {
+    if (!m || (n && (!reads || !results))) return FWS_ERR_INVALID;
+    for (uint32_t i = 0; i < n; ++i) {
+        const fws_rx_read &rd = reads[i];
+        if (rd.conn >= m->conns.size() || (rd.size && !rd.buf) || m->seen[rd.conn]) {
+            for (uint32_t j = 0; j < i; ++j) m->seen[reads[j].conn] = 0;
+            return FWS_ERR_INVALID;              // unknown connection, or two reads of one in a call
+        }
+        m->seen[rd.conn] = 1;
+    }
+    for (uint32_t i = 0; i < n; ++i) m->seen[reads[i].conn] = 0;
+    int r;
+    if ((r = fws_hip_status(hipSetDevice(m->ctx->device)))) return r;
+
+    // 1. plan: per read its continuation, header stream and frame slots
+    struct Plan {
+        uint64_t u, rest, L, cont_off, hs_off;
+        uint32_t part0, seg;                     // seg: index in the launch, or kNone (session path)
+    };
+    std::vector<Plan> plan(n);
+    uint64_t bytes = 0, frames = 0;
+    uint32_t nseg = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        fws_rx_session *s = m->conns[reads[i].conn];
+        Plan &p = plan[i];
+        const uint64_t size = reads[i].size;
+        p.u = s->recv_status == kWaitPayload ? (size < s->unread ? size : s->unread) : 0;
+        p.part0 = s->part_len;
+        p.rest = size - p.u;
+        p.L = p.rest ? p.part0 + p.rest : 0;
+        p.seg = kNone;
+        if (size == 0 || size > kMuxMaxRead || p.L > kSmallMax) continue;
+        p.cont_off = bytes;
+        p.hs_off = al16(bytes + p.u);
+        bytes = al16(p.hs_off + p.L) + 16;       // + 16: the small decode reads one chunk past L
+        p.seg = nseg++;
+        frames += p.L / 6 + 2 < kSmallFrames ? p.L / 6 + 2 : kSmallFrames;
+    }
+    const uint64_t desc_bytes = al16((uint64_t)nseg * sizeof(fws_seg_desc));
+    const uint64_t res_bytes = al16((uint64_t)nseg * sizeof(fws_decode_result));
+    if (nseg) {
+        if ((r = m->ensure(bytes, desc_bytes + res_bytes + frames * sizeof(fws_frame_info)))) return r;
+        fws_seg_desc *hd = (fws_seg_desc *)m->hmeta;
+        uint32_t fbase = 0;
+        for (uint32_t i = 0; i < n; ++i) {
+            const Plan &p = plan[i];
+            if (p.seg == kNone) continue;
+            fws_rx_session *s = m->conns[reads[i].conn];
+            const uint8_t *buf = reads[i].buf;
+            if (p.u) memcpy(m->hbuf + p.cont_off, buf, p.u);
+            if (p.rest) {
+                if (p.part0) memcpy(m->hbuf + p.hs_off, s->hdr, p.part0);
+                memcpy(m->hbuf + p.hs_off + p.part0, buf + p.u, p.rest);
+            }
+            fws_seg_desc &d = hd[p.seg];
+            d.cont_off = p.cont_off;
+            d.hs_off = p.hs_off;
+            d.u = (uint32_t)p.u;
+            d.key = s->key;
+            d.L = (uint32_t)p.L;
+            d.fcap = (uint32_t)(p.L / 6 + 2 < kSmallFrames ? p.L / 6 + 2 : kSmallFrames);
+            d.fbase = fbase;
+            d.pad = 0;
+            fbase += d.fcap;
+        }
+        // 2. one round trip: H2D, the segments' decode, D2H
+        hipStream_t st = m->stream;
+        hipError_t e;
+        fws_decode_result *dres = (fws_decode_result *)(m->dmeta + desc_bytes);
+        fws_frame_info *dfr = (fws_frame_info *)(m->dmeta + desc_bytes + res_bytes);
+        if ((e = hipMemcpyAsync(m->dbuf, m->hbuf, bytes, hipMemcpyHostToDevice, st)) != hipSuccess ||
+            (e = hipMemcpyAsync(m->dmeta, m->hmeta, desc_bytes, hipMemcpyHostToDevice, st)) != hipSuccess)
+            return fws_hip_status(e);
+        if ((r = fws_launch_decode_segments(m->dbuf, (const fws_seg_desc *)m->dmeta, nseg, dfr, dres, st))) return r;
+        if ((e = hipMemcpyAsync(m->hbuf, m->dbuf, bytes, hipMemcpyDeviceToHost, st)) != hipSuccess ||
+            (e = hipMemcpyAsync(m->hmeta + desc_bytes, m->dmeta + desc_bytes,
+                                res_bytes + frames * sizeof(fws_frame_info), hipMemcpyDeviceToHost, st)) != hipSuccess)
+            return fws_hip_status(e);
+        if ((e = hipStreamSynchronize(st)) != hipSuccess) return fws_hip_status(e);
+    }
+
+    // 3. per read: the bytes back, OnRecvData's bookkeeping, the events
+    const fws_seg_desc *hd = (const fws_seg_desc *)m->hmeta;
+    const fws_decode_result *hres = (const fws_decode_result *)(m->hmeta + desc_bytes);
+    const fws_frame_info *hfr = (const fws_frame_info *)(m->hmeta + desc_bytes + res_bytes);
+    for (uint32_t i = 0; i < n; ++i) {
+        const fws_rx_read &rd = reads[i];
+        const Plan &p = plan[i];
+        fws_rx_session *s = m->conns[rd.conn];
+        s->own = true;
+        s->own_ev.clear();
+        s->own_ctl.clear();
+        s->n_ev = 0;
+        s->ctl_used = 0;
+        s->err_code = 0;
+        int ret;
+        const fws_decode_result res = p.seg != kNone && p.rest ? hres[p.seg] : fws_decode_result{};
+        if (p.seg == kNone || (p.rest && (res.status == FWS_SMALL_DECLINED || res.status == FWS_ERR_CAPACITY))) {
+            ret = feed_impl(s, rd.buf, rd.size, rd.capacity);          // the session path, on the original bytes
+        } else {
+            if (p.u) memcpy(rd.buf, m->hbuf + p.cont_off, p.u);
+            if (p.rest) memcpy(rd.buf + p.u, m->hbuf + p.hs_off + p.part0, p.rest);
+            ret = replay(s, rd.buf, rd.size, rd.capacity, p.u, p.part0, p.rest, p.L, res, hfr + hd[p.seg].fbase);
+        }
+        if (ret < 0) s->err_code = ret;
+        fws_rx_read_result &o = results[i];
+        o.ret = ret;
+        o.pad = 0;
+        o.events = s->own_ev.data();
+        o.n_events = s->own_ev.size();
+        o.ctl = s->own_ctl.data();
+        o.ctl_used = s->own_ctl.size();
+        s->own = false;
     }
     return 0;
 }

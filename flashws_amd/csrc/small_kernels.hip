@@ -12,7 +12,9 @@
 // terminal with), and every 16-B chunk holding payload bytes is unmasked from
 // LDS by the whole workgroup and stored once.
 //
-// A read with more than kSmallFrames headers (tiny frames) is declined:
+// k_decode_segments does the same for many connections' reads at once (one
+// workgroup each, fws_rx_mux). A read with more than kSmallFrames headers
+// (tiny frames) is declined:
 // res->status = FWS_SMALL_DECLINED and nothing is written but the result; the
 // caller then runs fws_gpu_decode_stream. Results are those of
 // fws_gpu_decode_stream (fws_decode_result, fws_frame_info, bytes).
@@ -25,9 +27,10 @@ namespace fwsk {
 constexpr uint32_t kSThreads = 1024;
 constexpr uint32_t kSChunks = kSmallMax / 16;
 
-__global__ __launch_bounds__(kSThreads) void k_decode_small(uint8_t *__restrict__ wire, uint32_t N,
-                                                            fws_frame_info *__restrict__ frames, uint32_t cap,
-                                                            fws_decode_result *__restrict__ res) {
+// The decode of one small read by the calling workgroup (kSThreads threads).
+__device__ __forceinline__ void decode_small_wg(uint8_t *__restrict__ wire, uint32_t N,
+                                                fws_frame_info *__restrict__ frames, uint32_t cap,
+                                                fws_decode_result *__restrict__ res) {
     __shared__ u32x4 s_buf[kSChunks + 1];
     __shared__ uint32_t s_po[kSmallFrames + 1];     // payload start of path frame f
     __shared__ uint32_t s_pe[kSmallFrames + 1];     // payload end, clipped to N
@@ -147,7 +150,46 @@ __global__ __launch_bounds__(kSThreads) void k_decode_small(uint8_t *__restrict_
     }
 }
 
+__global__ __launch_bounds__(kSThreads) void k_decode_small(uint8_t *__restrict__ wire, uint32_t N,
+                                                            fws_frame_info *__restrict__ frames, uint32_t cap,
+                                                            fws_decode_result *__restrict__ res) {
+    decode_small_wg(wire, N, frames, cap, res);
+}
+
+// fws_rx_mux (rx_session.cpp): the reads of many connections in one launch,
+// one workgroup per read (segment). A segment is the continuation of the
+// connection's frame in progress (unmasked with its carried, rotated key,
+// w_socket.h:607-617) followed by its header stream (staged header bytes +
+// the rest of the read), decoded as above.
+__global__ __launch_bounds__(kSThreads) void k_decode_segments(uint8_t *__restrict__ batch,
+                                                               const fws_seg_desc *__restrict__ segs,
+                                                               fws_frame_info *__restrict__ frames,
+                                                               fws_decode_result *__restrict__ res) {
+    const fws_seg_desc d = segs[blockIdx.x];
+    const uint32_t tid = threadIdx.x;
+    // continuation: 16-B aligned start, so every 4-byte group uses the key as is
+    uint8_t *const cont = batch + d.cont_off;
+    for (uint32_t c = tid; 16u * c < d.u; c += kSThreads) {
+        const uint32_t lo = 16u * c;
+        if (lo + 16u <= d.u) {
+            u32x4 v = gload16(reinterpret_cast<uintptr_t>(cont + lo));
+            v ^= u32x4{d.key, d.key, d.key, d.key};
+            gstore16(reinterpret_cast<uintptr_t>(cont + lo), v);
+        } else {
+            for (uint32_t j = lo; j < d.u; ++j) cont[j] ^= (uint8_t)(d.key >> (8u * (j & 3u)));
+        }
+    }
+    if (d.L) decode_small_wg(batch + d.hs_off, d.L, frames + d.fbase, d.fcap, res + blockIdx.x);
+}
+
 }  // namespace fwsk
+
+int fws_launch_decode_segments(uint8_t *batch, const fws_seg_desc *segs, uint32_t n, fws_frame_info *frames,
+                               fws_decode_result *res, hipStream_t s) {
+    if (!n) return 0;
+    hipLaunchKernelGGL(fwsk::k_decode_segments, dim3(n), dim3(fwsk::kSThreads), 0, s, batch, segs, frames, res);
+    return fws_hip_status(hipGetLastError());
+}
 
 int fws_launch_decode_small(uint8_t *wire, uint64_t N, fws_frame_info *frames, uint32_t cap,
                             fws_decode_result *res, hipStream_t s) {

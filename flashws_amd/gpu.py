@@ -207,6 +207,59 @@ class RxSession:
             pass
 
 
+class RxMux:
+    """fws_rx_mux: the reads of many connections decoded in one round trip
+    (FLoop::OneStep's shape, floop.h:661-703), each with its own carried state;
+    per read the results equal RxSession.feed on that connection alone."""
+
+    def __init__(self, ctx, n_conns):
+        h = C.c_void_p()
+        check("fws_rx_mux_create", lib().fws_rx_mux_create(ctx.h, n_conns, C.byref(h)))
+        self.h = h
+        self.n = n_conns
+
+    def feed(self, reads, extra_cap=0):
+        """reads: [(conn, bytes)]. Returns [(ret, unmasked bytes, events, ctl bytes)]."""
+        bufs = [np.frombuffer(bytes(d), dtype=np.uint8).copy() for _, d in reads]
+        rr = np.zeros(len(reads), dtype=_lib.RX_READ)
+        for i, ((conn, _), b) in enumerate(zip(reads, bufs)):
+            rr[i] = (conn, 0, b.ctypes.data if len(b) else 0, len(b), len(b) + extra_cap)
+        out = np.zeros(len(reads), dtype=_lib.RX_READ_RESULT)
+        check("fws_rx_mux_feed", lib().fws_rx_mux_feed(self.h, rr.ctypes.data if len(reads) else None, len(reads),
+                                                       out.ctypes.data if len(reads) else None))
+        res = []
+        for i, b in enumerate(bufs):
+            o = out[i]
+            n_ev, n_ctl = int(o["n_events"]), int(o["ctl_used"])
+            ev = np.zeros(n_ev, dtype=RX_EVENT)
+            if n_ev:
+                C.memmove(ev.ctypes.data, int(o["events"]), n_ev * RX_EVENT.itemsize)
+            ctl = np.zeros(n_ctl, dtype=np.uint8)
+            if n_ctl:
+                C.memmove(ctl.ctypes.data, int(o["ctl"]), n_ctl)
+            res.append((int(o["ret"]), b, ev, ctl))
+        return res
+
+    def reset(self, conn):
+        check("fws_rx_mux_reset", lib().fws_rx_mux_reset(self.h, conn))
+
+    def state(self, conn):
+        st = _lib.RxState()
+        check("fws_rx_mux_state", lib().fws_rx_mux_state(self.h, conn, C.byref(st)))
+        return st
+
+    def close(self):
+        if self.h:
+            lib().fws_rx_mux_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class TxSession:
     """fws_tx_session: SendFrame (w_socket.h:832-944) for host payloads of one
     connection; the frame bytes are built on the GPU."""

@@ -227,6 +227,43 @@ int fws_rx_session_feed_view(fws_rx_session *s, uint8_t *buf, uint64_t size, uin
  * w_socket.h:452) in the Close reason (ws_server_socket.h:178-181). */
 int fws_rx_session_error(const fws_rx_session *s, uint32_t *opcode);
 
+/* ---- many connections, one round trip -----------------
+ * FLoop::OneStep (floop.h:661-703) drains every readable socket in one loop
+ * iteration and runs each read through its socket's OnRecvData. fws_rx_mux
+ * keeps one RX state per connection (the fws_rx_session of each) and decodes
+ * the reads of many connections -- each with its own carried state: staged
+ * header bytes, unread payload of the frame in progress, rotated key -- with
+ * one pinned staging pass, one H2D copy, one launch (one workgroup per read)
+ * and one D2H copy, then replays each connection's OnRecvData bookkeeping.
+ * Per read the results equal fws_rx_session_feed on that connection alone.
+ * A read over 256 KiB, or whose header stream needs the parallel decode (over
+ * 128 KiB or 256 headers), goes through that connection's session path. */
+typedef struct fws_rx_mux fws_rx_mux;
+typedef struct fws_rx_read {
+    uint32_t conn;          /* connection slot, < n_conns; at most one read per slot per call */
+    uint32_t flags;         /* 0 */
+    uint8_t *buf;           /* host memory, unmasked in place */
+    uint64_t size;
+    uint64_t capacity;      /* the view's capacity from buf (fws_rx_session_feed) */
+} fws_rx_read;
+typedef struct fws_rx_read_result {
+    int32_t ret;            /* fws_rx_session_feed's return for this read */
+    uint32_t pad;
+    const fws_rx_event *events;   /* the connection's events, valid until its next feed */
+    uint64_t n_events;
+    const uint8_t *ctl;           /* control payloads the events point into */
+    uint64_t ctl_used;
+} fws_rx_read_result;
+int fws_rx_mux_create(fws_gpu_ctx *ctx, uint32_t n_conns, fws_rx_mux **out);
+void fws_rx_mux_destroy(fws_rx_mux *m);
+/* slot `conn` starts a new connection (the reference's initial RX state) */
+int fws_rx_mux_reset(fws_rx_mux *m, uint32_t conn);
+int fws_rx_mux_state(const fws_rx_mux *m, uint32_t conn, fws_rx_state *out);
+int fws_rx_mux_error(const fws_rx_mux *m, uint32_t conn, uint32_t *opcode);
+/* Decode n reads (distinct connections). Returns 0 (per-read codes in
+ * results[i].ret) or FWS_ERR_INVALID / a HIP error for the call itself. */
+int fws_rx_mux_feed(fws_rx_mux *m, const fws_rx_read *reads, uint32_t n, fws_rx_read_result *results);
+
 /* ---- send path: batch frame builder -------------------
  * The bytes WSocket::SendFrame (w_socket.h:832-944) writes for one frame:
  * b0 = FIN << 7 | opcode, b1 = MASK << 7 | len7, the BE 16 / 64-bit length,

@@ -74,6 +74,13 @@ struct Engine {
     virtual void *open_conn() = 0;                      // per-connection session
     virtual uint8_t *read_buf(void *conn) = 0;          // where the read lands (start_pos 32)
     virtual int feed(void *conn, size_t n, std::vector<fws_rx_event> &ev, uint64_t *n_ev) = 0;
+    // the reads of every readable connection of one loop iteration at once
+    // (fws_rx_mux); engines without it feed one read at a time
+    virtual bool batched() const { return false; }
+    virtual int feed_batch(void *const *conns, const size_t *n, uint32_t k, fws_rx_read_result *out) {
+        (void)conns; (void)n; (void)k; (void)out;
+        return -1;
+    }
 };
 
 struct GpuConn {
@@ -111,6 +118,56 @@ struct GpuEngine : Engine {
         uint64_t used = 0;
         return fws_rx_session_feed(c->s, c->mem + kPad, n, n, ev.data(), ev.size(), n_ev, c->ctl.data(),
                                    c->ctl.size(), &used);
+    }
+};
+
+// all connections in one fws_rx_mux: the reads of one epoll_wait round are
+// decoded with one H2D copy, one launch and one D2H copy
+struct MuxEngine : Engine {
+    static constexpr uint32_t kSlots = 1024;
+    fws_gpu_ctx *ctx = nullptr;
+    fws_rx_mux *mux = nullptr;
+    struct Conn {
+        uint32_t slot;
+        uint8_t *mem;
+    };
+    std::vector<std::unique_ptr<Conn>> conns;
+    std::vector<fws_rx_read> reads;
+    explicit MuxEngine(int device) {
+        if (int r = fws_gpu_ctx_create(device, &ctx)) die("fws_gpu_ctx_create", r);
+        if (int r = fws_rx_mux_create(ctx, kSlots, &mux)) die("fws_rx_mux_create", r);
+    }
+    ~MuxEngine() override {
+        fws_rx_mux_destroy(mux);
+        for (auto &c : conns) std::free(c->mem);
+        fws_gpu_ctx_destroy(ctx);
+    }
+    void *open_conn() override {
+        if (conns.size() >= kSlots) die("mux slots");
+        auto c = std::make_unique<Conn>();
+        c->slot = (uint32_t)conns.size();
+        c->mem = static_cast<uint8_t *>(std::aligned_alloc(4096, kPad + kReadMax + 4096));
+        conns.push_back(std::move(c));
+        return conns.back().get();
+    }
+    uint8_t *read_buf(void *conn) override { return static_cast<Conn *>(conn)->mem + kPad; }
+    int feed(void *conn, size_t n, std::vector<fws_rx_event> &ev, uint64_t *n_ev) override {
+        fws_rx_read_result o;
+        void *cs[1] = {conn};
+        size_t ns[1] = {n};
+        if (int r = feed_batch(cs, ns, 1, &o)) return r;
+        *n_ev = std::min<uint64_t>(o.n_events, ev.size());
+        std::memcpy(ev.data(), o.events, *n_ev * sizeof(fws_rx_event));
+        return o.ret;
+    }
+    bool batched() const override { return true; }
+    int feed_batch(void *const *cs, const size_t *n, uint32_t k, fws_rx_read_result *out) override {
+        reads.resize(k);
+        for (uint32_t i = 0; i < k; ++i) {
+            auto *c = static_cast<Conn *>(cs[i]);
+            reads[i] = fws_rx_read{c->slot, 0u, c->mem + kPad, n[i], n[i]};
+        }
+        return fws_rx_mux_feed(mux, reads.data(), k, out);
     }
 };
 
@@ -177,7 +234,7 @@ void write_all(int fd, const iovec *iov_in, int n) {
 }
 
 struct ServerStats {
-    uint64_t reads = 0, read_bytes = 0, feed_ns = 0;
+    uint64_t reads = 0, read_bytes = 0, feed_ns = 0, batches = 0;
     int err = 0;
 };
 
@@ -189,9 +246,29 @@ void server_loop(int lfd, int n_clients, Engine &eng, std::atomic<bool> &stop, S
     ::epoll_ctl(ep, EPOLL_CTL_ADD, lfd, &lev);
     std::vector<std::unique_ptr<SrvConn>> conns;
     std::vector<fws_rx_event> ev(kReadMax / 3 + 64);
-    epoll_event evs[64];
+    std::vector<SrvConn *> ready;
+    std::vector<void *> ready_eng;
+    std::vector<size_t> ready_n;
+    std::vector<fws_rx_read_result> results;
+    // the server's on_read (test_ws_server.cpp:203-230): append each data part,
+    // write the message back at msg_end
+    auto echo = [&](SrvConn *c, const uint8_t *buf, const fws_rx_event *evp, uint64_t n_ev) {
+        for (uint64_t j = 0; j < n_ev; ++j) {
+            const fws_rx_event &e = evp[j];
+            if (e.kind != 0 || e.is_ctl) continue;
+            c->msg.insert(c->msg.end(), buf + e.data_off, buf + e.data_off + e.size);
+            c->opcode = e.opcode;
+            if (e.msg_end) {
+                uint8_t h[10];
+                iovec iov[2] = {{h, server_hdr(h, c->opcode, c->msg.size())}, {c->msg.data(), c->msg.size()}};
+                write_all(c->fd, iov, c->msg.empty() ? 1 : 2);
+                c->msg.clear();
+            }
+        }
+    };
+    epoll_event evs[1024];
     while (!stop.load(std::memory_order_relaxed)) {
-        int k = ::epoll_wait(ep, evs, 64, 20);
+        int k = ::epoll_wait(ep, evs, 1024, 20);
         for (int i = 0; i < k; ++i) {
             if (evs[i].data.ptr == nullptr) {
                 int fd = ::accept(lfd, nullptr, nullptr);
@@ -220,23 +297,33 @@ void server_loop(int lfd, int n_clients, Engine &eng, std::atomic<bool> &stop, S
             }
             ++st.reads;
             st.read_bytes += uint64_t(r);
+            if (eng.batched()) {                   // decoded below with this round's other reads
+                ready.push_back(c);
+                ready_n.push_back(size_t(r));
+                continue;
+            }
             uint64_t n_ev = 0;
             const auto t0 = Clock::now();
             const int ret = eng.feed(c->eng, size_t(r), ev, &n_ev);
             st.feed_ns += uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - t0).count());
             if (ret != 0) { st.err = ret; stop = true; break; }
-            for (uint64_t j = 0; j < n_ev; ++j) {
-                const fws_rx_event &e = ev[j];
-                if (e.kind != 0 || e.is_ctl) continue;
-                c->msg.insert(c->msg.end(), buf + e.data_off, buf + e.data_off + e.size);
-                c->opcode = e.opcode;
-                if (e.msg_end) {
-                    uint8_t h[10];
-                    iovec iov[2] = {{h, server_hdr(h, c->opcode, c->msg.size())}, {c->msg.data(), c->msg.size()}};
-                    write_all(c->fd, iov, c->msg.empty() ? 1 : 2);
-                    c->msg.clear();
-                }
+            echo(c, buf, ev.data(), n_ev);
+        }
+        if (!ready.empty()) {
+            ready_eng.clear();
+            for (SrvConn *c : ready) ready_eng.push_back(c->eng);
+            results.resize(ready.size());
+            const auto t0 = Clock::now();
+            const int rc = eng.feed_batch(ready_eng.data(), ready_n.data(), (uint32_t)ready.size(), results.data());
+            st.feed_ns += uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - t0).count());
+            ++st.batches;
+            if (rc != 0) { st.err = rc; stop = true; }
+            for (size_t j = 0; j < ready.size() && rc == 0; ++j) {
+                if (results[j].ret != 0) { st.err = results[j].ret; stop = true; break; }
+                echo(ready[j], eng.read_buf(ready[j]->eng), results[j].events, results[j].n_events);
             }
+            ready.clear();
+            ready_n.clear();
         }
     }
     for (auto &c : conns) ::close(c->fd);
@@ -376,8 +463,9 @@ int main(int argc, char **argv) {
 
     std::unique_ptr<Engine> eng;
     if (o.engine == "gpu") eng = std::make_unique<GpuEngine>(o.device);
+    else if (o.engine == "gpu-mux") eng = std::make_unique<MuxEngine>(o.device);
     else if (o.engine == "ref") eng = std::make_unique<RefEngine>(o.ref_lib);
-    else die("engine must be gpu or ref");
+    else die("engine must be gpu, gpu-mux or ref");
 
     int lfd = ::socket(AF_INET, SOCK_STREAM, 0);
     int one = 1;
@@ -423,11 +511,12 @@ int main(int argc, char **argv) {
                 "\"seconds\": %.4f, \"goodput_rx_tx_mbps\": %.1f, \"payload_GiB_per_s\": %.3f, \"msgs_per_s\": %.0f, "
                 "\"rtt_us\": {\"min\": %.2f, \"p50\": %.2f, \"p99\": %.2f, \"p999\": %.2f, \"max\": %.2f}, "
                 "\"server_reads\": %llu, \"server_bytes_per_read\": %.0f, \"server_feed_us_per_read\": %.2f, "
-                "\"verified\": %s, \"server_ret\": %d}\n",
+                "\"server_reads_per_batch\": %.2f, \"verified\": %s, \"server_ret\": %d}\n",
                 o.engine.c_str(), o.clients, o.msg_len, o.window, o.msgs, o.warmup, secs, goodput_mbps,
                 double(rx) / secs / double(1ull << 30), double(rtt.size()) / secs, quantile(rtt, 0), quantile(rtt, 0.5),
                 quantile(rtt, 0.99), quantile(rtt, 0.999), quantile(rtt, 1.0), (unsigned long long)st.reads,
                 st.reads ? double(st.read_bytes) / double(st.reads) : 0.0,
-                st.reads ? double(st.feed_ns) / double(st.reads) / 1000.0 : 0.0, ok ? "true" : "false", st.err);
+                st.reads ? double(st.feed_ns) / double(st.reads) / 1000.0 : 0.0,
+                st.batches ? double(st.reads) / double(st.batches) : 1.0, ok ? "true" : "false", st.err);
     return ok ? 0 : 1;
 }

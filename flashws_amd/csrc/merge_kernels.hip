@@ -8,19 +8,21 @@
 // offsets whose header chain reaches the tile end ("survivors"): every true
 // header plus a few random offsets.
 //
-//  k_merge  one workgroup per super tile (ST = 128 tiles = 256 KiB). Loads
-//           the ST's survivors (offset order), links each to the survivor at
-//           its exit inside the ST (search in the exit's tile, in LDS) and
+//  k_merge  one workgroup per super tile (ST = 256 tiles = 512 KiB). First
+//           the tiles k_scan left (kDenseTile: frames under ~32 B) are
+//           scanned with dense_tile() (scan_common.h). Then it loads the ST's
+//           survivors (offset order), links each to the survivor at its exit
+//           inside the ST (search in the exit's tile, in LDS) and
 //           pointer-jumps (Wyllie) so every survivor knows the tail of its
 //           chain in the ST, the frames up to that tail, and how the chain
 //           leaves the ST: EXIT (into a later ST), END (at or past the stream
 //           end), DEAD (the exit is not a header: a protocol error or a false
 //           chain) or INC (an incomplete header at the stream end). EXIT
 //           tails go to a global list; the ST's survivors are also written as
-//           one contiguous table for k_emit. A super tile with more survivors
-//           than the LDS tables hold (dense small frames: 64 B frames put
-//           ~3700 headers in one ST) runs the same steps over global scratch
-//           indexed by slot id (the big-ST path), in the same workgroup.
+//           one table (slot id, next, tail, frames to it) for k_emit. A super
+//           tile with 2049-8192 survivors (frames of ~70-250 B) takes
+//           merge_mid (the same steps in LDS, in-place jumping on one word
+//           per survivor); above that, the big-ST path over global scratch.
 //  k_link   one thread per EXIT tail: the survivor its exit lands on (the
 //           tile's slots, one batch of loads) and next(tail) = the tail of
 //           that survivor's chain; marks every next() target in a bitmap.
@@ -36,11 +38,13 @@
 //           ParseFrameHdr's rules (w_socket.h:435-524): error walk, carry-out,
 //           fws_decode_result. Workspace limits (k_scan's survivor spill, the
 //           tail list) end the decode with FWS_ERR_CAPACITY in the result.
-//  k_emit   one workgroup per ST with an entry: marks the entry's chain by
-//           pointer doubling over the ST's table and writes fws_frame_info in
-//           stream order and the unmask plan: unit_first[u] = the frame whose
-//           span [hdr_off, next hdr_off) holds stream byte 4 KiB * u
-//           (k_unmask_stream, unmask_kernels.hip).
+//  k_emit   one workgroup per ST with an entry: marks the entry's chain
+//           (the survivors at or after it with its tail when their frame
+//           count is the entry's, else one survivor per depth -- the only one
+//           at its depth or next() of the one above -- else pointer doubling)
+//           and writes fws_frame_info in stream order and the unmask plan:
+//           unit_first[u] = the frame whose span [hdr_off, next hdr_off)
+//           holds stream byte 4 KiB * u (k_unmask_stream, unmask_kernels.hip).
 //
 // Every global access on these paths is metadata (about 1 survivor per KiB of
 // stream); the kernels are latency-bound, so loads are issued in batches of

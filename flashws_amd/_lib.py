@@ -94,6 +94,7 @@ SIGNATURES = [
     ("fws_rx_session_feed_view", _I, [_P, _P, _U64, _U64, C.POINTER(C.c_void_p), _PU64, C.POINTER(C.c_void_p),
                                       _PU64]),
     ("fws_rx_session_error", _I, [_P, C.POINTER(C.c_uint32)]),
+    ("fws_gpu_check_sorted", _I, [_P, _P, _U32, _P, _P]),
     ("fws_rx_mux_create", _I, [_P, _U32, C.POINTER(C.c_void_p)]),
     ("fws_rx_mux_destroy", None, [_P]),
     ("fws_rx_mux_reset", _I, [_P, _U32]),

@@ -176,12 +176,41 @@ int fws_gpu_unmask_batch(fws_gpu_ctx *ctx, void *dev_base, const fws_frame_desc 
     return fws_gpu_unmask_run(ctx, dev_base, dev_descs, n, stream);
 }
 
+int fws_gpu_check_sorted(fws_gpu_ctx *ctx, const fws_frame_desc *dev_descs, uint32_t n, uint32_t *dev_bad,
+                         void *stream) {
+    if (!ctx || !dev_bad || (n && !dev_descs)) return FWS_ERR_INVALID;
+    int r;
+    if ((r = fws_hip_status(hipSetDevice(ctx->device)))) return r;
+    return fws_launch_check_sorted(dev_descs, n, dev_bad, (hipStream_t)stream);
+}
+
+// FWS_CHECK_SORTED=1 in the environment: the sorted entry points check the
+// contract first and refuse (FWS_ERR_INVALID, nothing written) a violating
+// batch; this synchronises the stream (a debug mode, not for timing)
+static int check_sorted_debug(fws_gpu_ctx *ctx, const fws_frame_desc *d, uint32_t n, hipStream_t s) {
+    static const bool on = [] {
+        const char *v = getenv("FWS_CHECK_SORTED");
+        return v && v[0] && v[0] != '0';
+    }();
+    if (!on) return 0;
+    uint32_t *bad = nullptr, h = 0;
+    hipError_t e = hipMalloc((void **)&bad, sizeof(uint32_t));
+    if (e != hipSuccess) return fws_hip_status(e);
+    int r = fws_launch_check_sorted(d, n, bad, s);
+    if (r == 0 && (e = hipMemcpyAsync(&h, bad, sizeof(h), hipMemcpyDeviceToHost, s)) != hipSuccess) r = fws_hip_status(e);
+    if (r == 0 && (e = hipStreamSynchronize(s)) != hipSuccess) r = fws_hip_status(e);
+    (void)hipFree(bad);
+    if (r) return r;
+    return h == 0xFFFFFFFFu ? 0 : FWS_ERR_INVALID;
+}
+
 int fws_gpu_unmask_sorted(fws_gpu_ctx *ctx, void *dev_base, const fws_frame_desc *dev_descs, uint32_t n,
                           void *stream) {
     if (!ctx || (n && (!dev_base || !dev_descs))) return FWS_ERR_INVALID;
     if (n == 0) return 0;
     int r;
     if ((r = fws_hip_status(hipSetDevice(ctx->device)))) return r;
+    if ((r = check_sorted_debug(ctx, dev_descs, n, (hipStream_t)stream))) return r;
     // the grid only bounds the grid-stride loop: every unit of the span is visited at any grid
     const uint64_t span = ctx->cap_stream ? ctx->cap_stream : 4096ull * n;
     return fws_launch_unmask_sorted((uint8_t *)dev_base, dev_descs, n, span, (hipStream_t)stream);
@@ -193,6 +222,7 @@ int fws_gpu_unmask_sorted_utf8(fws_gpu_ctx *ctx, void *dev_base, const fws_frame
     if (n == 0) return 0;
     int r;
     if ((r = fws_hip_status(hipSetDevice(ctx->device)))) return r;
+    if ((r = check_sorted_debug(ctx, dev_descs, n, (hipStream_t)stream))) return r;
     const uint64_t span = ctx->cap_stream ? ctx->cap_stream : 4096ull * n;
     return fws_launch_unmask_sorted_utf8((uint8_t *)dev_base, dev_descs, n, span, dev_ok, (hipStream_t)stream);
 }

@@ -151,6 +151,8 @@ int fws_launch_unmask(uint8_t *base, const fws_frame_desc *d, uint32_t n, const 
                       const fws_plan_ws &ws, uint64_t max_chunks, hipStream_t s);
 int fws_launch_unmask_sorted(uint8_t *base, const fws_frame_desc *d, uint32_t n, uint64_t max_span,
                              hipStream_t s);
+// *bad = the first index breaking the sorted / disjoint contract, or ~0 (device word)
+int fws_launch_check_sorted(const fws_frame_desc *d, uint32_t n, uint32_t *bad, hipStream_t s);
 int fws_launch_unmask_sorted_utf8(uint8_t *base, const fws_frame_desc *d, uint32_t n, uint64_t max_span,
                                   uint8_t *ok, hipStream_t s);
 // Decoded stream in stream-byte space: unit_first[u] = frame spanning byte 4 KiB * u (the decode's plan).

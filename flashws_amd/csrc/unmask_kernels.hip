@@ -1136,6 +1136,31 @@ int fws_launch_plan(const uint8_t *base, const fws_frame_desc *d, uint32_t n, co
     return fws_hip_status(hipGetLastError());
 }
 
+namespace fwsk {
+// fws_gpu_check_sorted: the first i whose region does not end at or before
+// region i + 1's start (or whose end overflows), by an atomic minimum; the
+// word is preset to ~0 (no violation) by the caller's memset
+__global__ __launch_bounds__(kBlock) void k_check_sorted(const fws_frame_desc *__restrict__ d, uint32_t n,
+                                                         uint32_t *__restrict__ bad) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    bool v = false;
+    if (i < n) {
+        const uint64_t e = d[i].payload_off + d[i].payload_len;
+        v = e < d[i].payload_off || (i + 1 < n && e > d[i + 1].payload_off);
+    }
+    const uint64_t m = __ballot(v);
+    if (m && (threadIdx.x & 63) == (uint32_t)__ffsll((unsigned long long)m) - 1u) atomicMin(bad, i);
+}
+}  // namespace fwsk
+
+int fws_launch_check_sorted(const fws_frame_desc *d, uint32_t n, uint32_t *bad, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(bad, 0xFF, sizeof(uint32_t), s);
+    if (e != hipSuccess) return fws_hip_status(e);
+    if (n) hipLaunchKernelGGL(fwsk::k_check_sorted, dim3((n + fwsk::kBlock - 1) / fwsk::kBlock), dim3(fwsk::kBlock), 0,
+                              s, d, n, bad);
+    return fws_hip_status(hipGetLastError());
+}
+
 int fws_launch_unmask_sorted(uint8_t *base, const fws_frame_desc *d, uint32_t n, uint64_t max_span,
                              hipStream_t s) {
     if (n == 0) return 0;

@@ -207,6 +207,16 @@ class RxSession:
             pass
 
 
+def check_sorted(ctx, dd, n, stream=None):
+    """fws_gpu_check_sorted: the first descriptor index breaking the sorted /
+    disjoint contract of unmask_sorted, or None (synchronises)."""
+    bad = torch.empty(1, dtype=torch.int32, device=dd.device)
+    st = stream if stream is not None else torch.cuda.current_stream()
+    check("fws_gpu_check_sorted", lib().fws_gpu_check_sorted(ctx.h, dd.data_ptr(), n, bad.data_ptr(), st.cuda_stream))
+    v = int(bad.item()) & 0xFFFFFFFF
+    return None if v == 0xFFFFFFFF else v
+
+
 class RxMux:
     """fws_rx_mux: the reads of many connections decoded in one round trip
     (FLoop::OneStep's shape, floop.h:661-703), each with its own carried state;

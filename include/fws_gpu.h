@@ -133,6 +133,16 @@ int fws_gpu_unmask_batch(fws_gpu_ctx *ctx, void *dev_base, const fws_frame_desc 
 int fws_gpu_unmask_sorted(fws_gpu_ctx *ctx, void *dev_base, const fws_frame_desc *dev_descs,
                           uint32_t n, void *stream);
 
+/* The sortedness contract of fws_gpu_unmask_sorted(_utf8), checked on the
+ * device in one launch: *dev_bad (a device word) becomes the first i with
+ * payload_off_i + payload_len_i > payload_off_i+1 (or an overflowing end), or
+ * 0xFFFFFFFF when the batch is sorted and disjoint. With FWS_CHECK_SORTED=1
+ * in the environment the sorted entry points run this check first and refuse
+ * a violating batch with FWS_ERR_INVALID, writing nothing (a debug mode: it
+ * synchronises the stream). */
+int fws_gpu_check_sorted(fws_gpu_ctx *ctx, const fws_frame_desc *dev_descs, uint32_t n, uint32_t *dev_bad,
+                         void *stream);
+
 /* fws_gpu_unmask_sorted plus per-region UTF-8 validation of the unmasked
  * payloads in the same pass (BASELINE config 5 in descriptor mode):
  * dev_ok[i] = 1 iff region i is well-formed UTF-8 (Unicode Table 3-7), the

@@ -364,3 +364,54 @@ def test_sorted_early_variant(ctx, cuda):
         assert np.array_equal(run_sorted(ctx, host, descs, cuda), oracle_unmask_regions(host, descs))
     finally:
         lib().fws_internal_set_sorted_early(old)
+
+
+def test_check_sorted_contract(ctx, cuda):
+    """fws_gpu_check_sorted finds the first descriptor that breaks the
+    sorted / disjoint contract of fws_gpu_unmask_sorted."""
+    wire, descs, _ = gpu.config_c2(n_frames=5000, payload=1000)
+    dd = gpu.descs_to_device(descs, cuda)
+    assert gpu.check_sorted(ctx, dd, len(descs)) is None
+    sw = descs.copy()
+    sw[[1234, 1235]] = sw[[1235, 1234]]                # two frames out of order
+    assert gpu.check_sorted(ctx, gpu.descs_to_device(sw, cuda), len(sw)) == 1234
+    ov = descs.copy()
+    ov["payload_len"][3000] += 20                      # overlaps the next region
+    assert gpu.check_sorted(ctx, gpu.descs_to_device(ov, cuda), len(ov)) == 3000
+    assert gpu.check_sorted(ctx, dd, 0) is None
+
+
+def test_check_sorted_debug_mode_refuses(cuda, tmp_path):
+    """FWS_CHECK_SORTED=1: fws_gpu_unmask_sorted refuses an unsorted batch
+    with FWS_ERR_INVALID and writes nothing (a child process: the mode is read
+    once per process)."""
+    import subprocess
+    import sys
+    script = tmp_path / "chk.py"
+    script.write_text(
+        "import sys, numpy as np, torch\n"
+        f"sys.path.insert(0, {repr(str(__import__('os').path.dirname(__import__('os').path.dirname(__import__('os').path.abspath(__file__)))))})\n"
+        "from flashws_amd import gpu, _lib\n"
+        "wire, d, _ = gpu.config_c2(n_frames=3000, payload=700)\n"
+        "dev = torch.device('cuda:0')\n"
+        "ctx = gpu.Ctx(0, max_frames=4000, max_stream_bytes=len(wire))\n"
+        "w = torch.from_numpy(wire).to(dev)\n"
+        "bad = d.copy(); bad[[10, 11]] = bad[[11, 10]]\n"
+        "rc = _lib.lib().fws_gpu_unmask_sorted(ctx.h, w.data_ptr(), gpu.descs_to_device(bad, dev).data_ptr(), len(bad),"
+        " torch.cuda.current_stream().cuda_stream)\n"
+        "torch.cuda.synchronize()\n"
+        "same = bool(np.array_equal(w.cpu().numpy(), wire))\n"
+        "rc2 = _lib.lib().fws_gpu_unmask_sorted(ctx.h, w.data_ptr(), gpu.descs_to_device(d, dev).data_ptr(), len(d),"
+        " torch.cuda.current_stream().cuda_stream)\n"
+        "torch.cuda.synchronize()\n"
+        "print(rc, same, rc2)\n")
+    env = dict(__import__("os").environ, FWS_CHECK_SORTED="1")
+    out = subprocess.run([sys.executable, str(script)], capture_output=True, text=True, timeout=120, env=env)
+    assert out.returncode == 0, out.stderr[-2000:]
+    rc, same, rc2 = out.stdout.split()[-3:]
+    assert int(rc) == _lib_invalid() and same == "True" and int(rc2) == 0
+
+
+def _lib_invalid():
+    from flashws_amd import _lib
+    return _lib.FWS_ERR_INVALID

@@ -10,6 +10,7 @@
 // the host) to produce the exact on_read() / PONG / CLOSE event sequence and
 // carried RX state (w_socket.h:223-245). Host code only; server side only
 // (client RX has no unmask and is out of scope).
+#include <stdlib.h>
 #include <string.h>
 
 #include <vector>
@@ -491,6 +492,7 @@ struct fws_rx_mux {
     uint8_t *hmeta = nullptr, *dmeta = nullptr;
     uint64_t mcap = 0;
     std::vector<uint8_t> seen;        // per connection: fed in this call
+    uint64_t zc_max = 0;              // batches up to this many bytes: kernels on the pinned buffers
 
     int ensure(uint64_t bytes, uint64_t meta) {
         hipError_t e;
@@ -516,6 +518,10 @@ struct fws_rx_mux {
 
 namespace {
 constexpr uint64_t kMuxMaxRead = 256u << 10;   // larger reads: the connection's session path
+// Batches of at most this many staged bytes skip the copy engines: the segment
+// kernel reads and writes the pinned staging over PCIe (env FWS_MUX_ZC_MAX
+// overrides; 0 = always copy).
+constexpr uint64_t kMuxZcMax = 256u << 10;
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 inline uint64_t al16(uint64_t x) { return (x + 15) & ~15ull; }
 }  // namespace
@@ -535,6 +541,8 @@ int fws_rx_mux_create(fws_gpu_ctx *ctx, uint32_t n_conns, fws_rx_mux **out) {
     }
     m->conns.resize(n_conns, nullptr);
     m->seen.resize(n_conns, 0);
+    const char *zc = getenv("FWS_MUX_ZC_MAX");
+    m->zc_max = zc ? strtoull(zc, nullptr, 10) : kMuxZcMax;
     for (uint32_t i = 0; i < n_conns; ++i) {
         fws_rx_session *s = new fws_rx_session();
         s->ctx = ctx;
@@ -639,20 +647,28 @@ int fws_rx_mux_feed(fws_rx_mux *m, const fws_rx_read *reads, uint32_t n, fws_rx_
             d.pad = 0;
             fbase += d.fcap;
         }
-        // 2. one round trip: H2D, the segments' decode, D2H
+        // 2. one round trip: H2D, the segments' decode, D2H -- or for a small
+        // batch the decode alone, on the pinned buffers
         hipStream_t st = m->stream;
         hipError_t e;
-        fws_decode_result *dres = (fws_decode_result *)(m->dmeta + desc_bytes);
-        fws_frame_info *dfr = (fws_frame_info *)(m->dmeta + desc_bytes + res_bytes);
-        if ((e = hipMemcpyAsync(m->dbuf, m->hbuf, bytes, hipMemcpyHostToDevice, st)) != hipSuccess ||
-            (e = hipMemcpyAsync(m->dmeta, m->hmeta, desc_bytes, hipMemcpyHostToDevice, st)) != hipSuccess)
-            return fws_hip_status(e);
-        if ((r = fws_launch_decode_segments(m->dbuf, (const fws_seg_desc *)m->dmeta, nseg, dfr, dres, st))) return r;
-        if ((e = hipMemcpyAsync(m->hbuf, m->dbuf, bytes, hipMemcpyDeviceToHost, st)) != hipSuccess ||
-            (e = hipMemcpyAsync(m->hmeta + desc_bytes, m->dmeta + desc_bytes,
-                                res_bytes + frames * sizeof(fws_frame_info), hipMemcpyDeviceToHost, st)) != hipSuccess)
-            return fws_hip_status(e);
-        if ((e = hipStreamSynchronize(st)) != hipSuccess) return fws_hip_status(e);
+        if (bytes <= m->zc_max) {
+            fws_decode_result *hr = (fws_decode_result *)(m->hmeta + desc_bytes);
+            fws_frame_info *hf = (fws_frame_info *)(m->hmeta + desc_bytes + res_bytes);
+            if ((r = fws_launch_decode_segments(m->hbuf, (const fws_seg_desc *)m->hmeta, nseg, hf, hr, st))) return r;
+            if ((e = hipStreamSynchronize(st)) != hipSuccess) return fws_hip_status(e);
+        } else {
+            fws_decode_result *dres = (fws_decode_result *)(m->dmeta + desc_bytes);
+            fws_frame_info *dfr = (fws_frame_info *)(m->dmeta + desc_bytes + res_bytes);
+            if ((e = hipMemcpyAsync(m->dbuf, m->hbuf, bytes, hipMemcpyHostToDevice, st)) != hipSuccess ||
+                (e = hipMemcpyAsync(m->dmeta, m->hmeta, desc_bytes, hipMemcpyHostToDevice, st)) != hipSuccess)
+                return fws_hip_status(e);
+            if ((r = fws_launch_decode_segments(m->dbuf, (const fws_seg_desc *)m->dmeta, nseg, dfr, dres, st))) return r;
+            if ((e = hipMemcpyAsync(m->hbuf, m->dbuf, bytes, hipMemcpyDeviceToHost, st)) != hipSuccess ||
+                (e = hipMemcpyAsync(m->hmeta + desc_bytes, m->dmeta + desc_bytes,
+                                    res_bytes + frames * sizeof(fws_frame_info), hipMemcpyDeviceToHost, st)) != hipSuccess)
+                return fws_hip_status(e);
+            if ((e = hipStreamSynchronize(st)) != hipSuccess) return fws_hip_status(e);
+        }
     }
 
     // 3. per read: the bytes back, OnRecvData's bookkeeping, the events

@@ -7,6 +7,8 @@ own carried state (staged header bytes, unread payload, rotated key).
   read's return code, unmasked bytes, on_read / PONG / CLOSE events and
   carried state must equal what the compiled reference produced
   (w_socket.h:543-769) -- the same bar as test_gpu_session.py;
+* both transfer modes: the batch copied to HBM and back, or (small batches)
+  the kernel working on the pinned staging directly;
 * 64 connections with random frame streams cut at random read sizes, some
   reads over the mux's segment limits (the per-connection session path):
   each connection's results equal a standalone fws_rx_session fed the same
@@ -38,11 +40,18 @@ def mctx(cuda):
     c.close()
 
 
+@pytest.fixture(params=["copy", "zero-copy"])
+def zc_mode(request, monkeypatch):
+    """the mux reads FWS_MUX_ZC_MAX at creation: 0 = every batch through the copy engines"""
+    monkeypatch.setenv("FWS_MUX_ZC_MAX", "0" if request.param == "copy" else str(1 << 40))
+    return request.param
+
+
 def _state(st):
     return {k: int(getattr(st, k)) for k, _ in orc.RxStateHead._fields_}
 
 
-def test_mux_all_kat_cases_at_once(mctx):
+def test_mux_all_kat_cases_at_once(mctx, zc_mode):
     names = sorted(CASES)
     mux = gpu.RxMux(mctx, len(names))
     closed = set()
@@ -79,7 +88,7 @@ def _random_stream(rng, n_frames):
 
 
 @pytest.mark.parametrize("seed", range(2))
-def test_mux_matches_per_connection_sessions(mctx, seed):
+def test_mux_matches_per_connection_sessions(mctx, seed, zc_mode):
     rng = np.random.default_rng(900 + seed)
     n_conns = 64
     streams = [_random_stream(rng, int(rng.integers(5, 60))) for _ in range(n_conns)]

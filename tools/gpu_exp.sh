@@ -1,7 +1,5 @@
 set -o pipefail
 R=$GRAFT_REPO_ROOT
-cd /tmp && export TMPDIR=/tmp
-for v in exp6; do
-  timeout -k 10 120 rocprofv3 --kernel-trace --stats -f csv -d $R/gpurun_out/se_$v -o run -- python3 $R/tools/scan_exp.py flashws_amd/lib/libfws_gpu_$v.so > $R/gpurun_out/se_$v.log 2>&1 || exit 1
-done
+cd $R
+timeout -k 10 200 python tools/prof_merge_trace.py > gpurun_out/merge_trace.json 2> gpurun_out/merge_trace.err || { tail -5 gpurun_out/merge_trace.err; exit 1; }
 echo done

@@ -74,6 +74,20 @@ def main():
             prev = e[:, k]
         r["k_emit_end_us"] = stats(e[ok, 26] - t0e)
         r["gap_merge_end_to_emit_start_us"] = round(float(t0e - m[:, 4].max()), 2)
+        # the last k_link workgroup's resolve phases (marks 10..17 in its row)
+        lk = t[:, 17]
+        row = int(np.argmax(lk))
+        if lk[row] > 0:
+            names = ["root+init", "compact", "cnx", "prune", "entries", "st_scan", "-", "terminal"]
+            prev = t[row, 29]
+            ph = {}
+            for k in range(10, 18):
+                if k == 16:
+                    continue
+                ph[names[k - 10]] = round(float(t[row, k] - prev), 2)
+                prev = t[row, k]
+            r["k_link_last_wg_phases_us"] = ph
+            r["k_link_last_wg_start_after_link_start_us"] = round(float(t[row, 29] - t[:, 29][t[:, 29] > 0].min()), 2)
         r["counters"] = gpu.decode_counters(ctx)
         import ctypes as CT
         raw = (CT.c_uint32 * 16)()

@@ -305,6 +305,23 @@ struct StreamFrame {
     bool text;                                       // UTF-8 checked: TEXT, FIN, complete
 };
 
+// A frame record by whole dwords: at a wave-uniform address these are scalar
+// loads (a byte field read on its own is a vector load, and its wait would also
+// wait for the unit's data loads issued before it)
+__device__ __forceinline__ fws_frame_info ld_frame(const fws_frame_info *p) {
+    const uint32_t *w = (const uint32_t *)p;
+    const uint32_t a0 = w[0], a1 = w[1], a2 = w[2], a3 = w[3], a4 = w[4], a5 = w[5];
+    fws_frame_info f;
+    f.hdr_off = a0 | (uint64_t(a1) << 32);
+    f.payload_len = a2 | (uint64_t(a3) << 32);
+    f.key = a4;
+    f.opcode = (uint8_t)a5;
+    f.fin = (uint8_t)(a5 >> 8);
+    f.hdr_len = (uint8_t)(a5 >> 16);
+    f.flags = (uint8_t)(a5 >> 24);
+    return f;
+}
+
 __device__ __forceinline__ StreamFrame stream_frame(const fws_frame_info &fi, uint64_t N) {
     const uint64_t po = fi.hdr_off + fi.hdr_len;
     const uint64_t pe = po + fi.payload_len < N ? po + fi.payload_len : N;
@@ -332,6 +349,31 @@ __device__ __forceinline__ bool utf8_chunk_bad(const u32x4 &u, uint32_t prev, ui
     return (e0 | utf8_err(x.y, x.x) | utf8_err(x.z, x.y) | utf8_err(x.w, x.z)) != 0u;
 }
 
+// utf8_chunk_bad on unit-relative 32-bit offsets (a fast unit's record: the
+// payloads clipped to the unit): chunk at r, region [lo, hi); returns the
+// error flags.
+__device__ __forceinline__ uint32_t sel_bytes32(int32_t w, int32_t lo, int32_t hi) {
+    if (w + 4 <= lo || w >= hi) return 0u;
+    const uint32_t s = lo > w ? (uint32_t)(lo - w) : 0u;
+    const uint32_t e = hi < w + 4 ? (uint32_t)(w + 4 - hi) : 0u;
+    return (0xFFFFFFFFu << (8u * s)) & (0xFFFFFFFFu >> (8u * e));
+}
+__device__ __forceinline__ uint32_t utf8_chunk_err32(const u32x4 &u, uint32_t prev, int32_t r, int32_t lo, int32_t hi,
+                                                     uint32_t skip) {
+    u32x4 x = u;
+    uint32_t p = prev;
+    if (!(r >= lo && r + 16 <= hi)) {
+        x.x &= sel_bytes32(r, lo, hi);
+        x.y &= sel_bytes32(r + 4, lo, hi);
+        x.z &= sel_bytes32(r + 8, lo, hi);
+        x.w &= sel_bytes32(r + 12, lo, hi);
+    }
+    if (!(r >= lo + 4 && r <= hi)) p &= sel_bytes32(r - 4, lo, hi);
+    uint32_t e0 = utf8_err(x.x, p);
+    if (skip) e0 &= 0x80000000u;
+    return e0 | utf8_err(x.y, x.x) | utf8_err(x.z, x.y) | utf8_err(x.w, x.z);
+}
+
 template <bool kNT, bool kUtf8, bool kRev>
 __global__ __launch_bounds__(kBlock) void k_unmask_stream(uint8_t *base, uint64_t N,
                                                           const fws_frame_info *__restrict__ fr, uint32_t cap,
@@ -350,9 +392,21 @@ __global__ __launch_bounds__(kBlock) void k_unmask_stream(uint8_t *base, uint64_
         // decode's scan read last -- those lines are still in the 256 MB
         // Infinity Cache (MALL) when this pass re-reads them
         const uint64_t u = kRev ? n_units - 1u - ui : ui;
+        const uint64_t c0 = u * 4096u + uint64_t(lane) * 16u;
+        // kUtf8 (VALU-heavier per unit): the unit's loads are issued before the frame
+        // lookup, whose dependent round trips then overlap them
+        u32x4 pre[kUnmaskU];
+        if constexpr (kUtf8) {
+            const uint64_t last = (N - 1u) & ~uint64_t(15);
+#pragma unroll
+            for (int j = 0; j < kUnmaskU; ++j) {
+                const uint64_t c = c0 + uint64_t(j) * 1024u;
+                pre[j] = gload16<kNT>(b0 + (c < N ? c : last));
+            }
+            asm volatile("" ::: "memory");           // issued here, not sunk into the branches
+        }
         const uint32_t flo = unit_first[u];
         const uint32_t fhi = (u + 1 < n_units) ? unit_first[u + 1] : n - 1;
-        const uint64_t c0 = u * 4096u + uint64_t(lane) * 16u;
         if (fhi - flo >= 2u) {                       // small frames: per-chunk search
             uint32_t carry = 0;                      // lane 63's last unmasked dword of step j - 1
 #pragma unroll 1
@@ -392,8 +446,34 @@ __global__ __launch_bounds__(kBlock) void k_unmask_stream(uint8_t *base, uint64_
             }
             continue;
         }
-        const StreamFrame A = stream_frame(fr[flo], N), B = stream_frame(fr[fhi], N);
+        const StreamFrame A = stream_frame(ld_frame(fr + flo), N), B = stream_frame(ld_frame(fr + fhi), N);
         const bool two = fhi != flo;
+        if constexpr (kUtf8) {
+            const uint64_t U = u * 4096u;
+            if (!two && A.text && A.po <= U && A.pe >= U + 4096u) {
+                // the unit lies wholly inside one TEXT payload (the common unit of large
+                // frames): one key, no per-chunk region tests; a chunk's left context by
+                // a DPP wave shift (lane 0: lane 63 of the chunk before, carried)
+                const uint32_t rk = rotr32(A.key, 8u * ((uint32_t)(U - A.po) & 3u));
+                u32x4 x[kUnmaskU];
+#pragma unroll
+                for (int j = 0; j < kUnmaskU; ++j) {
+                    x[j] = pre[j] ^ u32x4{rk, rk, rk, rk};
+                    gstore16<kNT>(b0 + c0 + uint64_t(j) * 1024u, x[j]);
+                }
+                uint32_t err = 0, carry = 0;
+#pragma unroll
+                for (int j = 0; j < kUnmaskU; ++j) {
+                    const uint32_t prev = __builtin_amdgcn_update_dpp(carry, x[j].w, 0x138, 0xF, 0xF, false);
+                    carry = __builtin_amdgcn_readlane(x[j].w, 63);
+                    uint32_t e0 = utf8_err(x[j].x, prev);
+                    if (j == 0 && lane == 0) e0 &= 0x80000000u;   // bytes 0..2: k_utf8_seam's
+                    err |= e0 | utf8_err(x[j].y, x[j].x) | utf8_err(x[j].z, x[j].y) | utf8_err(x[j].w, x[j].z);
+                }
+                if (__any(err != 0u) && lane == 0) ok[flo] = 0;
+                continue;
+            }
+        }
         uintptr_t ca[kUnmaskU];
         u32x4 mk[kUnmaskU];
         bool live[kUnmaskU];
@@ -415,7 +495,10 @@ __global__ __launch_bounds__(kBlock) void k_unmask_stream(uint8_t *base, uint64_
         const uintptr_t safe = b0 + (A.po & ~uint64_t(15));
         u32x4 v[kUnmaskU];
 #pragma unroll
-        for (int j = 0; j < kUnmaskU; ++j) v[j] = gload16<kNT>(live[j] ? ca[j] : safe);
+        for (int j = 0; j < kUnmaskU; ++j) {
+            if constexpr (kUtf8) v[j] = pre[j];    // (a dead chunk's bytes are never stored)
+            else v[j] = gload16<kNT>(live[j] ? ca[j] : safe);
+        }
 #pragma unroll
         for (int j = 0; j < kUnmaskU; ++j)
             if (live[j]) gstore16<kNT>(ca[j], v[j] ^ mk[j]);
@@ -827,6 +910,34 @@ __device__ __forceinline__ void unmask_sorted_body(uint8_t *base, const fws_fram
         const u32x4 rec = unit_record(U0, E0, E1, A, poA, peA, aligned_key(fa.key, fa.phase, poA), hasB, poB, peB,
                                       aligned_key(fb.key, fb.phase, poB), hasC, poC);
         const bool slow = (rec.z & kRecSlow) != 0;
+        if constexpr (kUtf8 && !kEarly) {
+            if (rec.z == (4096u << 13) && ((rec.w >> 13) & 0x1FFFu) <= (rec.w & 0x1FFFu)) {
+                // the unit lies wholly inside A's payload and B has no byte in it (the
+                // common unit of large frames): one key, no per-chunk region tests;
+                // a chunk's left context by a DPP wave shift (lane 0: lane 63 of the
+                // chunk before, bound_ctrl off keeps the carried value)
+                u32x4 x[kUnmaskU];
+#pragma unroll
+                for (int j = 0; j < kUnmaskU; ++j) x[j] = gload16<kNT>(c0 + uint64_t(j) * 1024u);
+                const uint32_t rk = rec.x;
+#pragma unroll
+                for (int j = 0; j < kUnmaskU; ++j) {
+                    x[j] = x[j] ^ u32x4{rk, rk, rk, rk};
+                    gstore16<kNT>(c0 + uint64_t(j) * 1024u, x[j]);
+                }
+                uint32_t err = 0, carry = 0;
+#pragma unroll
+                for (int j = 0; j < kUnmaskU; ++j) {
+                    const uint32_t prev = __builtin_amdgcn_update_dpp(carry, x[j].w, 0x138, 0xF, 0xF, false);
+                    carry = __builtin_amdgcn_readlane(x[j].w, 63);
+                    uint32_t e0 = utf8_err(x[j].x, prev);
+                    if (j == 0 && lane == 0) e0 &= 0x80000000u;   // bytes 0..2: k_utf8_seam_sorted's
+                    err |= e0 | utf8_err(x[j].y, x[j].x) | utf8_err(x[j].z, x[j].y) | utf8_err(x[j].w, x[j].z);
+                }
+                if (__any(err != 0u) && lane == 0) ok[A] = 0;
+                continue;
+            }
+        }
         if (!kEarly && !slow) {
             const uint32_t a0 = rec.z & 0x1FFFu, a1 = (rec.z >> 13) & 0x1FFFu;
             const uint32_t e0 = rec.w & 0x1FFFu, e1 = (rec.w >> 13) & 0x1FFFu;
@@ -854,28 +965,40 @@ __device__ __forceinline__ void unmask_sorted_body(uint8_t *base, const fws_fram
             // the unmasked chunks, still in registers; a chunk's left context is the previous
             // lane's last dword (lane 0: lane 63's of chunk j - 1). Bytes 0..2 of the unit are
             // judged by k_utf8_seam_sorted (their context is another wave's unit).
-            bool badA = false, badB = false;
+            if (slow) {
+                uint32_t carry = 0;
+#pragma unroll
+                for (int j = 0; j < kUnmaskU; ++j) {
+                    const u32x4 x = v[j] ^ m[j];
+                    uint32_t prev = __shfl_up(x.w, 1, 64);
+                    if (lane == 0) prev = carry;
+                    carry = __shfl(x.w, 63, 64);
+                    utf8_slow_chunk(d, n, A, b0, c0 + uint64_t(j) * 1024u, x, prev, j == 0 && lane == 0, ok);
+                }
+                continue;
+            }
+            // fast kind: the unit-clipped payloads of A and B from the unit record, as
+            // 32-bit unit offsets (a region ending inside the unit's last 3 bytes leaves
+            // its truncation flag to bytes 0..2 of the next unit: k_utf8_seam_sorted's)
+            const int32_t loA = rec.z & 0x1FFFu, hiA = (rec.z >> 13) & 0x1FFFu;
+            const int32_t loB = rec.w & 0x1FFFu, hiB = (rec.w >> 13) & 0x1FFFu;
+            uint32_t errA = 0, errB = 0;
             uint32_t carry = 0;
+            int32_t r0 = lane * 16;
+            asm volatile("" : "+v"(r0));             // opaque per unit: no hoisted per-dword offsets
 #pragma unroll
             for (int j = 0; j < kUnmaskU; ++j) {
-                const uint64_t c = c0 + uint64_t(j) * 1024u;
                 const u32x4 x = v[j] ^ m[j];
                 uint32_t prev = __shfl_up(x.w, 1, 64);
                 if (lane == 0) prev = carry;
                 carry = __shfl(x.w, 63, 64);
                 const uint32_t skip = j == 0 && lane == 0;
-                if (slow) {
-                    utf8_slow_chunk(d, n, A, b0, c, x, prev, skip, ok);
-                    continue;
-                }
-                if (fa.payload_len && c + 16u > poA && c < peA + 3u) badA |= utf8_chunk_bad(x, prev, c, poA, peA, skip);
-                if (hasB && fb.payload_len && c + 16u > poB && c < peB + 3u)
-                    badB |= utf8_chunk_bad(x, prev, c, poB, peB, skip);
+                const int32_t r = r0 + j * 1024;
+                if (r + 16 > loA && r < hiA + 3) errA |= utf8_chunk_err32(x, prev, r, loA, hiA, skip);
+                if (r + 16 > loB && r < hiB + 3) errB |= utf8_chunk_err32(x, prev, r, loB, hiB, skip);
             }
-            if (!slow) {
-                if (__any(badA) && lane == 0) ok[A] = 0;
-                if (__any(badB) && lane == 0) ok[A + 1u] = 0;
-            }
+            if (__any(errA != 0u) && lane == 0) ok[A] = 0;
+            if (__any(errB != 0u) && lane == 0) ok[A + 1u] = 0;
         }
     }
 }

@@ -46,8 +46,16 @@ def main():
         torch.cuda.synchronize()
         ts.append(e[0].elapsed_time(e[1]))
     t = float(np.median(ts))
+    tp = []
+    for _ in range(reps):                             # the plain unmask of the same batch, for reference
+        e[0].record(s)
+        gpu.unmask_sorted(ctx, w, dd, n)
+        e[1].record(s)
+        torch.cuda.synchronize()
+        tp.append(e[0].elapsed_time(e[1]))
     print(json.dumps({"lib": os.path.basename(sys.argv[1]), "variant": variant, "flags_ok": good, "ms": round(t, 4),
-                      "GiB_per_s": round(payload / (t / 1e3) / 2**30, 1)}))
+                      "GiB_per_s": round(payload / (t / 1e3) / 2**30, 1),
+                      "plain_unmask_ms": round(float(np.median(tp)), 4)}))
     ctx.close()
 
 

@@ -1,7 +1,8 @@
 // flashws_amd/gpu_floop.hpp -- opt-in MI355X receive decode for an UNCHANGED
-// flashws server: one call on the listening fws::WSServerSocket<false>, no
-// change to any flashws header and none to the application's on_read /
-// WriteFrame / on_close code.
+// flashws server: one call on the listening fws::WSServerSocket<false> (ws://,
+// GpuRxHook) or fws::WSServerSocket<true> (wss://, GpuRxHookTls), no change to
+// any flashws header and none to the application's on_read / WriteFrame /
+// on_close code.
 //
 //   #include "flashws/flashws.h"              // the app's one flashws TU
 //   #include "flashws_amd/gpu_floop.hpp"
@@ -34,8 +35,11 @@
 // access struct and pointers to members (no reference file is edited). The
 // wrapped on_close retires the connection's decoder (freed at the next read).
 //
-// Plain ws:// only (WSServerSocket<false>); a TLS connection's decrypted reads
-// would attach the same way and are not wired here.
+// wss:// (SURVEY §8f rank 4): the under-socket is the reference's TLSSocket,
+// whose readable callback (tls_on_readable_, tls_socket.h:206-209) receives
+// the reads OpenSSL has already decrypted on the CPU (SSL_read loop,
+// tls_socket.h:472-562); the hook replaces that callback the same way, so the
+// GPU decodes the plaintext WebSocket stream and TLS stays in OpenSSL.
 #pragma once
 
 #include <cstdio>
@@ -55,8 +59,26 @@ struct TcpAccess : fws::TCPSocket {
     using fws::TCPSocket::on_readable_;
 };
 
-struct WsServerAccess : fws::WSServerSocket<false> {
-    using S = fws::WSServerSocket<false>;
+struct TlsAccess : fws::TLSSocket {
+    using fws::TLSSocket::tls_on_readable_;
+};
+
+// the under-socket's readable callback member (the one InitUnderOnReadImp sets)
+template <bool kTls> struct UnderAccess;
+template <> struct UnderAccess<false> {
+    using Sock = fws::TCPSocket;
+    using Func = fws::TCPSocket::OnReadableFunc;
+    static constexpr auto member = &TcpAccess::on_readable_;
+};
+template <> struct UnderAccess<true> {
+    using Sock = fws::TLSSocket;
+    using Func = fws::TLSSocket::TLSOnReadbleFunc;
+    static constexpr auto member = &TlsAccess::tls_on_readable_;
+};
+
+template <bool kTls>
+struct WsServerAccess : fws::WSServerSocket<kTls> {
+    using S = fws::WSServerSocket<kTls>;
     using S::server_status_;
     using S::on_read;
     using S::on_close;
@@ -75,22 +97,25 @@ struct WsServerAccess : fws::WSServerSocket<false> {
 
 }  // namespace detail
 
-class GpuRxHook {
+template <bool kTls>
+class GpuRxHookT {
 public:
-    using Sock = fws::WSServerSocket<false>;
-    using A = detail::WsServerAccess;
+    using Sock = fws::WSServerSocket<kTls>;
+    using A = detail::WsServerAccess<kTls>;
+    using U = detail::UnderAccess<kTls>;
+    using USock = typename U::Sock;
 
-    explicit GpuRxHook(GpuContext &ctx) : ctx_(ctx) {}
-    GpuRxHook(const GpuRxHook &) = delete;
-    GpuRxHook &operator=(const GpuRxHook &) = delete;
+    explicit GpuRxHookT(GpuContext &ctx) : ctx_(ctx) {}
+    GpuRxHookT(const GpuRxHookT &) = delete;
+    GpuRxHookT &operator=(const GpuRxHookT &) = delete;
 
     // Call on the listening socket after the application set its callbacks and
     // before connections are accepted. The hook must outlive the loop.
     void Enable(Sock &listen) {
         user_new_conn_ = (listen.*(&A::on_new_connection))();
         user_close_ = (listen.*(&A::on_close))();
-        ref_readable_ = listen.under_socket().*(&detail::TcpAccess::on_readable_);
-        GpuRxHook *self = this;
+        ref_readable_ = static_cast<USock &>(listen.under_socket()).*(U::member);
+        GpuRxHookT *self = this;
         listen.SetOnNewConnection([self](Sock &w, std::string_view uri, std::string_view host,
                                          std::string_view origin, std::string_view sub, std::string_view ext,
                                          std::string_view &rsub, std::string_view &rext, void *ud) {
@@ -151,8 +176,8 @@ private:
         auto &c = conns_[&w.under_socket()];
         c.ws = &w;
         c.dec = std::make_unique<GpuRxDecoder<fws::IOBuffer>>(ctx_);
-        GpuRxHook *self = this;
-        w.under_socket().SetOnReadable([self](fws::TCPSocket &u, fws::IOBuffer &&buf, void *ud) {
+        GpuRxHookT *self = this;
+        w.under_socket().SetOnReadable([self](USock &u, fws::IOBuffer &&buf, void *ud) {
             self->OnReadable(u, std::move(buf), ud);
         });
     }
@@ -165,7 +190,7 @@ private:
     }
 
     // ws_server_socket.h:172-196 with OnRecvData on the GPU.
-    void OnReadable(fws::TCPSocket &u, fws::IOBuffer &&buf, void *ud) {
+    void OnReadable(USock &u, fws::IOBuffer &&buf, void *ud) {
         retired_.clear();
         auto it = conns_.find(&u);
         if (it == conns_.end() || (it->second.ws->*(&A::server_status_)) != A::kOpen) {
@@ -204,12 +229,15 @@ private:
     }
 
     GpuContext &ctx_;
-    Sock::WsOnNewConnectionFunc user_new_conn_;
-    Sock::WSOnCloseFunc user_close_;
-    fws::TCPSocket::OnReadableFunc ref_readable_;
-    std::unordered_map<fws::TCPSocket *, Conn> conns_;
+    typename Sock::WsOnNewConnectionFunc user_new_conn_;
+    typename Sock::WSOnCloseFunc user_close_;
+    typename U::Func ref_readable_;
+    std::unordered_map<USock *, Conn> conns_;
     std::vector<std::unique_ptr<GpuRxDecoder<fws::IOBuffer>>> retired_;
     uint64_t gpu_reads_ = 0;
 };
+
+using GpuRxHook = GpuRxHookT<false>;      // ws://
+using GpuRxHookTls = GpuRxHookT<true>;    // wss://
 
 }  // namespace fws_amd

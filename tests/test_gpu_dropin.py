@@ -11,7 +11,11 @@ is moved to the MI355X by ONE added call, fws_amd::GpuRxHook::Enable
   (echo frames, PONGs, the CLOSE echo or the 1006 error close with the
   reference's error text) and the server's on_close log must be identical;
 * load: the reference's WSClientSocket with many connections, every echoed
-  byte checked, PINGs answered, clean CLOSE handshakes, through the GPU hook.
+  byte checked, PINGs answered, clean CLOSE handshakes, through the GPU hook;
+* wss:// (SURVEY §8f rank 4): the same scripted parity and a load run over
+  the reference's TLSSocket (WSServerSocket<true> + fws_amd::GpuRxHookTls):
+  OpenSSL decrypts on the CPU, the GPU decodes the plaintext reads. The
+  certificate is the test-only self-signed one in tests/tls/.
 """
 import json
 import os
@@ -27,15 +31,19 @@ pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 DROPIN = os.path.join(ROOT, "oracle", "_ref", "ws_dropin")
+TLS_ARGS = ["--tls", "--cert", os.path.join(ROOT, "tests", "tls", "server.crt"),
+            "--key", os.path.join(ROOT, "tests", "tls", "server.key")]
 
 
 class Server:
-    def __init__(self, gpu, conns, max_seconds=90):
+    def __init__(self, gpu, conns, max_seconds=90, tls=False):
         if not os.path.exists(DROPIN):
             pytest.skip("oracle/_ref/ws_dropin not built (make -C oracle ref, build container)")
         args = [DROPIN, "server", "--conns", str(conns), "--max-seconds", str(max_seconds)]
         if gpu:
             args.append("--gpu")
+        if tls:
+            args += TLS_ARGS
         self.p = subprocess.Popen(args, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
         line = self.p.stdout.readline()
         assert line.startswith("listening"), (line, self.p.stderr.read()[-2000:] if self.p.poll() is not None else "")
@@ -119,18 +127,19 @@ def _scripts():
 SCRIPTS = _scripts()
 
 
-def _run_all(gpu):
-    srv = Server(gpu, conns=len(SCRIPTS))
+def _run_all(gpu, tls=False):
+    srv = Server(gpu, conns=len(SCRIPTS), tls=tls)
     got = {}
     for name, (stream, chunks) in SCRIPTS.items():
-        head, data = wsraw.run_script(srv.port, stream, chunks)
+        head, data = wsraw.run_script(srv.port, stream, chunks, tls=tls)
         got[name] = (head, data)
     return got, srv.finish()
 
 
-def test_dropin_scripted_parity_with_reference_server(cuda):
-    ref, ref_srv = _run_all(gpu=False)
-    gpu, gpu_srv = _run_all(gpu=True)
+@pytest.mark.parametrize("tls", [False, True], ids=["ws", "wss"])
+def test_dropin_scripted_parity_with_reference_server(cuda, tls):
+    ref, ref_srv = _run_all(gpu=False, tls=tls)
+    gpu, gpu_srv = _run_all(gpu=True, tls=tls)
     assert gpu_srv["gpu_reads"] > 0 and ref_srv["gpu_reads"] == 0
     for name in SCRIPTS:
         assert gpu[name][0] == ref[name][0], name                     # handshake reply
@@ -149,12 +158,13 @@ def test_dropin_scripted_parity_with_reference_server(cuda):
     assert sum(1 for f in fr if f[1] == 10) > 0                       # PONGs
 
 
-@pytest.mark.parametrize("clients,msg_len", [(1, 4096), (8, 4096), (4, 70000), (16, 512)])
-def test_dropin_reference_client_load(cuda, clients, msg_len):
-    srv = Server(True, conns=clients)
+@pytest.mark.parametrize("clients,msg_len,tls", [(1, 4096, False), (8, 4096, False), (4, 70000, False),
+                                                 (16, 512, False), (8, 4096, True), (2, 70000, True)])
+def test_dropin_reference_client_load(cuda, clients, msg_len, tls):
+    srv = Server(True, conns=clients, tls=tls)
     r = subprocess.run([DROPIN, "client", "--port", str(srv.port), "--clients", str(clients), "--msgs", "600",
-                        "--warmup", "20", "--msg-len", str(msg_len), "--ping-every", "50", "--max-seconds", "60"],
-                       capture_output=True, text=True, timeout=90)
+                        "--warmup", "20", "--msg-len", str(msg_len), "--ping-every", "50", "--max-seconds", "60"]
+                       + (["--tls"] if tls else []), capture_output=True, text=True, timeout=90)
     assert r.returncode == 0, (r.stdout, r.stderr[-2000:])
     cli = json.loads(r.stdout.strip().splitlines()[-1])
     st = srv.finish()

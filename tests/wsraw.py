@@ -1,8 +1,11 @@
 """A raw RFC 6455 client for driving a WebSocket server byte for byte (test
 helper): HTTP Upgrade handshake, then a scripted byte stream sent in chosen
 chunks, and everything the server sends back collected until it closes the
-connection. Server frames are parsed (unmasked, 2 / 4 / 10-byte headers)."""
+connection. Server frames are parsed (unmasked, 2 / 4 / 10-byte headers).
+With tls=True the same over a TLS connection (no certificate check: the
+test servers use the self-signed tests/tls certificate)."""
 import socket
+import ssl
 import struct
 import time
 
@@ -12,9 +15,14 @@ HANDSHAKE = (b"GET / HTTP/1.1\r\nHost: 127.0.0.1\r\nUpgrade: websocket\r\nConnec
              b"Sec-WebSocket-Key: dGhlIHNhbXBsZSBub25jZQ==\r\nSec-WebSocket-Version: 13\r\n\r\n")
 
 
-def connect(port, timeout=10.0):
+def connect(port, timeout=10.0, tls=False):
     s = socket.create_connection(("127.0.0.1", port), timeout=timeout)
     s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+    if tls:
+        ctx = ssl.SSLContext(ssl.PROTOCOL_TLS_CLIENT)
+        ctx.check_hostname = False
+        ctx.verify_mode = ssl.CERT_NONE
+        s = ctx.wrap_socket(s, server_hostname="127.0.0.1")
     s.sendall(HANDSHAKE)
     reply = b""
     while b"\r\n\r\n" not in reply:
@@ -27,11 +35,12 @@ def connect(port, timeout=10.0):
     return s, head, rest
 
 
-def run_script(port, stream, chunks, pause_s=0.0002, timeout=10.0):
-    """Send `stream` in pieces of the given sizes, then read until the server
-    closes. Returns (handshake reply head, every byte received after it)."""
+def run_script(port, stream, chunks, pause_s=0.0002, timeout=10.0, tls=False):
+    """Send `stream` in pieces of the given sizes (over TLS: one record each),
+    then read until the server closes. Returns (handshake reply head, every
+    byte received after it)."""
     assert sum(chunks) == len(stream)
-    s, head, got = connect(port, timeout)
+    s, head, got = connect(port, timeout, tls)
     pos, i = 0, 0
     try:
         while pos < len(stream):
@@ -41,7 +50,7 @@ def run_script(port, stream, chunks, pause_s=0.0002, timeout=10.0):
             i += 1
             if pause_s:
                 time.sleep(pause_s)
-    except (BrokenPipeError, ConnectionResetError):
+    except (BrokenPipeError, ConnectionResetError, ssl.SSLError):
         pass
     s.settimeout(timeout)
     try:
@@ -50,7 +59,7 @@ def run_script(port, stream, chunks, pause_s=0.0002, timeout=10.0):
             if not b:
                 break
             got += b
-    except (ConnectionResetError, socket.timeout):
+    except (ConnectionResetError, socket.timeout, ssl.SSLError):
         pass
     s.close()
     return head, got

@@ -11,6 +11,10 @@
 //   (WriteFrame, ws_server_socket.h:131-141); PONG parts are ignored. Prints
 //   "listening <port>", then one JSON line when --conns connections closed:
 //   messages echoed, the on_close (code, reason) log, GPU reads.
+// --tls (both modes): wss:// -- WSServerSocket<true> / WSClientSocket<true> over
+//   the reference's TLSSocket and SSLManager (server: --cert / --key files, no
+//   peer verification); the server's hook is then fws_amd::GpuRxHookTls, which
+//   decodes the reads OpenSSL decrypted.
 // client: --clients connections in one FLoop, each sends --msgs messages of
 //   --msg-len bytes (window 1, a PING every --ping-every messages), checks every
 //   echoed byte against what it sent, then Close(1000, "bye"). One JSON line:
@@ -45,6 +49,8 @@ using Clock = std::chrono::steady_clock;
 
 struct Opts {
     std::string mode;
+    bool tls = false;
+    std::string cert, key;
     int port = 0;
     bool gpu = false;
     int device = 0;
@@ -86,11 +92,15 @@ struct Server {
     }
 };
 
+template <bool kTls>
 int RunServer(const Opts &o) {
-    using WS = fws::WSServerSocket<false>;
+    using WS = fws::WSServerSocket<kTls>;
     static Server srv;                         // reached from captureless-size lambdas
     srv.o = o;
-    if (srv.loop.Init<false>() < 0) die("FLoop::Init");
+    if (srv.loop.template Init<kTls>() < 0) die("FLoop::Init");
+    if constexpr (kTls) {
+        if (fws::SSLManager::instance().Init(false, o.cert.c_str(), o.key.c_str(), nullptr) < 0) die("SSLManager::Init");
+    }
     WS ws{};
     if (ws.Init() < 0) die("WSServerSocket::Init");
     Server *S = &srv;
@@ -127,10 +137,10 @@ int RunServer(const Opts &o) {
     });
 
     std::unique_ptr<fws_amd::GpuContext> gpu;
-    std::unique_ptr<fws_amd::GpuRxHook> hook;
+    std::unique_ptr<fws_amd::GpuRxHookT<kTls>> hook;
     if (o.gpu) {
         gpu = std::make_unique<fws_amd::GpuContext>(o.device);
-        hook = std::make_unique<fws_amd::GpuRxHook>(*gpu);
+        hook = std::make_unique<fws_amd::GpuRxHookT<kTls>>(*gpu);
         hook->Enable(ws);                      // the one added line
     }
 
@@ -157,11 +167,12 @@ int RunServer(const Opts &o) {
         log += (i ? ", " : "") + std::string("[") + std::to_string(srv.close_log[i].first) + ", \"" + r + "\"]";
     }
     log += "]";
-    std::printf("{\"mode\": \"server\", \"gpu\": %s, \"msgs\": %llu, \"bytes\": %llu, \"closes\": %d, "
+    std::printf("{\"mode\": \"server\", \"tls\": %s, \"gpu\": %s, \"msgs\": %llu, \"bytes\": %llu, \"closes\": %d, "
                 "\"close_log_hex\": %s, \"gpu_reads\": %llu}\n",
-                o.gpu ? "true" : "false", (unsigned long long)srv.msgs, (unsigned long long)srv.bytes, srv.closes,
+                kTls ? "true" : "false", o.gpu ? "true" : "false", (unsigned long long)srv.msgs, (unsigned long long)srv.bytes, srv.closes,
                 log.c_str(), (unsigned long long)(hook ? hook->gpu_reads() : 0));
     std::fflush(stdout);
+    if constexpr (kTls) std::_Exit(0);        // see RunClient: no static TLS teardown
     return 0;
 }
 
@@ -188,14 +199,18 @@ struct Client {
     const uint8_t *payload(int id, size_t i) const { return pool.data() + ((i * 131 + size_t(id) * 977) % 4096); }
 };
 
+template <bool kTls>
 int RunClient(const Opts &o) {
-    using WC = fws::WSClientSocket<false>;
+    using WC = fws::WSClientSocket<kTls>;
     static Client cli;
     cli.o = o;
     cli.pool.resize(o.msg_len + 4096);
     uint64_t x = 0x2545F4914F6CDD1Dull;
     for (auto &b : cli.pool) { x ^= x << 13; x ^= x >> 7; x ^= x << 17; b = uint8_t(x >> 32); }
-    if (cli.loop.Init<false>() < 0) die("FLoop::Init");
+    if (cli.loop.template Init<kTls>() < 0) die("FLoop::Init");
+    if constexpr (kTls) {
+        if (fws::SSLManager::instance().Init(false, nullptr, nullptr, nullptr) < 0) die("SSLManager::Init");
+    }
     Client *C = &cli;
     auto send_msg = [](Client *C, WC &w, CliCtx &c) {
         if (C->o.ping_every && c.sent % C->o.ping_every == C->o.ping_every - 1) {
@@ -276,7 +291,11 @@ int RunClient(const Opts &o) {
                 double(v.size()) / secs, q(0.5), q(0.99), q(1.0), (unsigned long long)cli.pongs,
                 (cli.ok && complete) ? "true" : "false");
     std::fflush(stdout);
-    return (cli.ok && complete) ? 0 : 1;
+    const int rc = (cli.ok && complete) ? 0 : 1;
+    // the reference's TLS objects crash in static teardown at exit (with and
+    // without the GPU hook): a wss process leaves without running destructors
+    if constexpr (kTls) std::_Exit(rc);
+    return rc;
 }
 
 }  // namespace
@@ -289,6 +308,9 @@ int main(int argc, char **argv) {
         std::string a = argv[i];
         auto next = [&]() -> std::string { if (i + 1 >= argc) die("missing value"); return argv[++i]; };
         if (a == "--port") o.port = std::atoi(next().c_str());
+        else if (a == "--tls") o.tls = true;
+        else if (a == "--cert") o.cert = next();
+        else if (a == "--key") o.key = next();
         else if (a == "--gpu") o.gpu = true;
         else if (a == "--device") o.device = std::atoi(next().c_str());
         else if (a == "--conns") o.conns = std::atoi(next().c_str());
@@ -300,7 +322,7 @@ int main(int argc, char **argv) {
         else if (a == "--max-seconds") o.max_seconds = std::atoi(next().c_str());
         else die(("unknown option " + a).c_str());
     }
-    if (o.mode == "server") return RunServer(o);
-    if (o.mode == "client") return RunClient(o);
+    if (o.mode == "server") return o.tls ? RunServer<true>(o) : RunServer<false>(o);
+    if (o.mode == "client") return o.tls ? RunClient<true>(o) : RunClient<false>(o);
     die("mode must be server or client");
 }

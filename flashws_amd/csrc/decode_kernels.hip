@@ -392,7 +392,7 @@ int fws_decode_ensure(fws_gpu_ctx *ctx, uint64_t N, uint32_t cap) {
     // super-tile resolve: results per slot id, EXIT tails, per-ST bases, big-ST scratch
     rel(d.nres); rel(d.tails); rel(d.gnx); rel(d.tmark); rel(d.comp); rel(d.st_nodes); rel(d.st_n); rel(d.st_entry);
     rel(d.st_fbase); rel(d.bg_nx); rel(d.bg_wt); rel(d.bg_lref); rel(d.bg_ptr); rel(d.bg_sc); rel(d.bg_mark);
-    const uint64_t nst = fws_merge_super_tiles(nt);
+    const uint64_t nst = fws_merge_super_tiles_cap(nt);
     const uint32_t tcap = fws_merge_tail_cap(nt);
     const uint64_t nn = nt * kSlots + ns;
     al(&d.nres, nn * sizeof(fws_node_res));

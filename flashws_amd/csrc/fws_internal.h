@@ -182,6 +182,7 @@ int fws_launch_decode(fws_gpu_ctx *ctx, uint8_t *wire, uint64_t N, fws_frame_inf
 // merge_kernels.hip: from k_scan's survivors to the frame list, the result and the
 // unmask plan (k_merge -> k_link + path -> k_emit); no grid barrier anywhere
 uint64_t fws_merge_super_tiles(uint64_t n_tiles);
+uint64_t fws_merge_super_tiles_cap(uint64_t n_tiles);   // bound over every n <= n_tiles (table sizes)
 uint32_t fws_merge_tail_cap(uint64_t n_tiles);
 uint64_t fws_merge_st_nodes(uint64_t n_tiles);
 uint32_t fws_merge_comp_cap();

@@ -53,8 +53,12 @@
 
 namespace fwsk {
 
-constexpr uint32_t kStTiles = 256;                  // tiles per super tile
-constexpr uint64_t kStBytes = uint64_t(kStTiles) * kTile;
+// tiles per super tile: kStTiles (512 KiB), halved down to kStTilesMin for a
+// stream too short to give kStTarget super tiles (the host picks it per call,
+// MergeParams::st_tiles; LDS tables are sized for kStTiles)
+constexpr uint32_t kStTiles = 256;
+constexpr uint32_t kStTilesMin = 32;
+constexpr uint64_t kStTarget = 512;
 constexpr uint32_t kStCap = 2048;                   // survivors of one ST in LDS
 constexpr int kMThreads = 512;
 constexpr int kMWaves = kMThreads / 64;
@@ -127,6 +131,8 @@ struct MergeParams {
     uint64_t N;
     uint32_t n_tiles;
     uint32_t n_st;
+    uint32_t st_tiles;                               // tiles per super tile (a power of two <= kStTiles)
+    uint32_t st_shift;                               // log2 of the super tile's bytes
     const fws_frame_info *stage_info;
     const fws_frame_info *spill_info;
     uint32_t *tile_count;                            // k_merge rewrites the tiles k_scan left (kDenseTile)
@@ -273,8 +279,8 @@ __device__ __forceinline__ uint32_t st_sid(const MergeParams &P, const MergeLds 
 // ids; EXIT tails in the global list), no table for k_emit (it walks the
 // scratch the same way).
 __device__ void merge_big(const MergeParams &P, MergeLds &L, uint32_t s, uint32_t n) {
-    const uint32_t tid = threadIdx.x, t0 = s * kStTiles;
-    const uint64_t st_end = uint64_t(s + 1) * kStBytes;
+    const uint32_t tid = threadIdx.x, t0 = s * P.st_tiles;
+    const uint64_t st_end = (uint64_t(s) + 1u) << P.st_shift;
     uint32_t *const C = P.counters;
     uint32_t *const p0 = P.bg_ptr, *const p1 = P.bg_ptr + P.max_nodes;
     uint32_t *const c0 = P.bg_sc, *const c1 = P.bg_sc + P.max_nodes;
@@ -341,7 +347,7 @@ __device__ void merge_big(const MergeParams &P, MergeLds &L, uint32_t s, uint32_
         P.nres[id] = fws_node_res{ref, cnt, id, kind | kBigBit};
         if (gld(P.bg_nx + id) == kBgExit) {
             const uint64_t x = exit_of(*P.rec(id));
-            P.tails[tb + gld(P.bg_lref + id)] = fws_tail_rec{x, id, kTermDead, (uint32_t)(x / kStBytes), 0u};
+            P.tails[tb + gld(P.bg_lref + id)] = fws_tail_rec{x, id, kTermDead, (uint32_t)(x >> P.st_shift), 0u};
         }
     }
 }
@@ -355,8 +361,8 @@ __device__ void merge_big(const MergeParams &P, MergeLds &L, uint32_t s, uint32_
 // Global loads are issued four survivors at a time.
 constexpr uint32_t kMidB = 4;
 __device__ void merge_mid(const MergeParams &P, MergeLds &L, uint32_t s, uint32_t n) {
-    const uint32_t tid = threadIdx.x, t0 = s * kStTiles;
-    const uint64_t st0 = uint64_t(s) * kStBytes, st_end = st0 + kStBytes;
+    const uint32_t tid = threadIdx.x, t0 = s * P.st_tiles;
+    const uint64_t st0 = uint64_t(s) << P.st_shift, st_end = st0 + (1ull << P.st_shift);
     uint32_t *const C = P.counters;
     MP_INIT();
     // pass 1: tile-local offsets
@@ -474,7 +480,7 @@ __device__ void merge_mid(const MergeParams &P, MergeLds &L, uint32_t s, uint32_
             const uint32_t ref = kind == kKindExit ? tb + lr[b] : tid_[b];
             P.nres[id[b]] = fws_node_res{ref, cnt, id[b], kind | kBigBit};
             if (t == i && kind == kKindExit)
-                P.tails[tb + own[b]] = fws_tail_rec{x[b], id[b], kTermDead, (uint32_t)(x[b] / kStBytes), 0u};
+                P.tails[tb + own[b]] = fws_tail_rec{x[b], id[b], kTermDead, (uint32_t)(x[b] >> P.st_shift), 0u};
         }
     }
     __syncthreads();
@@ -492,12 +498,12 @@ __global__ __launch_bounds__(kMThreads) void k_merge(MergeParams P) {
     for (uint64_t w = (uint64_t)s * kMThreads + tid; w < P.tail_cap / 32u + 1u; w += (uint64_t)gridDim.x * kMThreads)
         P.tmark[w] = 0u;
     if (s >= P.n_st) return;
-    const uint32_t t0 = s * kStTiles;
-    const uint64_t st0 = uint64_t(s) * kStBytes, st_end = st0 + kStBytes;
+    const uint32_t t0 = s * P.st_tiles;
+    const uint64_t st0 = uint64_t(s) << P.st_shift, st_end = st0 + (1ull << P.st_shift);
 
     // survivors per tile -> ST-local numbering
     uint32_t c = 0, sp = kNone;
-    if (tid < kStTiles && t0 + tid < P.n_tiles) {
+    if (tid < P.st_tiles && t0 + tid < P.n_tiles) {
         c = P.tile_count[t0 + tid];
         sp = P.tile_spill[t0 + tid];
     }
@@ -685,7 +691,7 @@ __global__ __launch_bounds__(kMThreads) void k_merge(MergeParams P) {
         tab[i] = nd;
         if (vv[j] == kNxExit) {
             const uint64_t x = exit_of(r[j]);
-            P.tails[tb + L.lref[i]] = fws_tail_rec{x, nid[j], kTermDead, (uint32_t)(x / kStBytes), 0u};
+            P.tails[tb + L.lref[i]] = fws_tail_rec{x, nid[j], kTermDead, (uint32_t)(x >> P.st_shift), 0u};
         }
     }
     __syncthreads();
@@ -1063,9 +1069,9 @@ constexpr uint32_t kDepthRounds = 16;                // then pointer doubling
 // frames in offset order are the ST's survivors in tile order.
 __device__ void emit_big(const MergeParams &P, uint32_t s, uint32_t n, uint32_t e, uint32_t fbase, uint32_t lim) {
     __shared__ uint32_t s_tb[kStTiles], s_tsp[kStTiles], s_red[kMWaves];
-    const uint32_t tid = threadIdx.x, t0 = s * kStTiles;
+    const uint32_t tid = threadIdx.x, t0 = s * P.st_tiles;
     uint32_t c = 0, sp = kNone;
-    if (tid < kStTiles && t0 + tid < P.n_tiles) {
+    if (tid < P.st_tiles && t0 + tid < P.n_tiles) {
         c = P.tile_count[t0 + tid];
         sp = P.tile_spill[t0 + tid];
     }
@@ -1138,9 +1144,9 @@ constexpr uint32_t kMidBatch = 4;
 static_assert(kMidPer * kMThreads == kMidCap && kMidPer % kMidBatch == 0, "mid survivors per thread");
 __device__ void emit_mid(const MergeParams &P, EmitLds &L, uint32_t s, uint32_t n, uint32_t e, uint32_t fbase,
                          uint32_t lim) {
-    const uint32_t tid = threadIdx.x, t0 = s * kStTiles;
+    const uint32_t tid = threadIdx.x, t0 = s * P.st_tiles;
     uint32_t c = 0, sp = kNone;
-    if (tid < kStTiles && t0 + tid < P.n_tiles) {
+    if (tid < P.st_tiles && t0 + tid < P.n_tiles) {
         c = P.tile_count[t0 + tid];
         sp = P.tile_spill[t0 + tid];
     }
@@ -1395,13 +1401,32 @@ extern "C" int fws_internal_merge_prof(unsigned long long *out, int reset) {
 // ------------------------------------------------------------------ host side
 using namespace fwsk;
 
-uint64_t fws_merge_super_tiles(uint64_t n_tiles) { return (n_tiles + kStTiles - 1) / kStTiles; }
-uint64_t fws_merge_st_nodes(uint64_t n_tiles) { return fws_merge_super_tiles(n_tiles) * kStCap; }
+// super tiles of kStTiles tiles, halved while that gives fewer than kStTarget
+// (a short stream's resolve then spreads over more CUs), down to kStTilesMin
+static uint32_t st_tiles_for(uint64_t n_tiles) {
+    uint32_t t = kStTiles;
+    while (t > kStTilesMin && n_tiles < (uint64_t)t * kStTarget) t >>= 1;
+    return t;
+}
+uint64_t fws_merge_super_tiles(uint64_t n_tiles) {
+    const uint32_t t = st_tiles_for(n_tiles);
+    return (n_tiles + t - 1) / t;
+}
+// a bound on fws_merge_super_tiles(n) for every n <= n_tiles (the count is not
+// monotonic in n where the super tile halves): at most 2 kStTarget below
+// kStTiles-sized super tiles, and never more than tiles / kStTilesMin
+uint64_t fws_merge_super_tiles_cap(uint64_t n_tiles) {
+    const uint64_t a = (n_tiles + kStTiles - 1) / kStTiles, lo = 2 * kStTarget;
+    const uint64_t b = (n_tiles + kStTilesMin - 1) / kStTilesMin;
+    const uint64_t c = a > lo ? a : lo;
+    return c < b ? c : b;
+}
+uint64_t fws_merge_st_nodes(uint64_t n_tiles) { return fws_merge_super_tiles_cap(n_tiles) * kStCap; }
 
 uint32_t fws_merge_comp_cap() { return kCompCap; }
 
 uint32_t fws_merge_tail_cap(uint64_t n_tiles) {
-    uint64_t c = fws_merge_super_tiles(n_tiles) * 64u + 4096u;
+    uint64_t c = fws_merge_super_tiles_cap(n_tiles) * 64u + 4096u;
     return (uint32_t)(c < kTailCapMax ? c : kTailCapMax);
 }
 
@@ -1413,7 +1438,10 @@ int fws_launch_merge(fws_gpu_ctx *ctx, const uint8_t *wire, uint64_t N, uint32_t
     P.wire = wire;
     P.N = N;
     P.n_tiles = n_tiles;
+    P.st_tiles = st_tiles_for(n_tiles);
+    P.st_shift = (uint32_t)__builtin_ctz(P.st_tiles) + (uint32_t)__builtin_ctz(kTile);
     P.n_st = (uint32_t)fws_merge_super_tiles(n_tiles);
+    if (P.n_st > d.max_st) return FWS_ERR_INTERNAL;   // fws_decode_ensure sized the tables
     P.stage_info = d.stage_info;
     P.spill_info = d.spill_info;
     P.spill_w = d.spill_info;

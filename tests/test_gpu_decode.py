@@ -231,18 +231,20 @@ def test_c2_full_parity(ctx, cuda, resolve_mode):
         assert not fell_back(ctx), "C2 must resolve on the super-tile path with LDS tables"
 
 
-@pytest.mark.parametrize("payload", [64, 120])
-def test_dense_64b_frames(ctx, cuda, resolve_mode, payload):
-    """200 000 x 64 B frames, and 120 B: super tiles with more
-    survivors than the LDS tables hold (~7 500 and ~4 000 per 512 KiB) take the
-    big-ST path -- merged and emitted in LDS (merge_mid / emit_mid), or over
-    global scratch when forced -- bit-exact either way."""
-    wire, descs, _ = gpu.config_c2(seed=65, n_frames=200_000, payload=payload)
+@pytest.mark.parametrize("n_frames,payload", [(200_000, 64), (200_000, 120), (600_000, 16)])
+def test_dense_64b_frames(ctx, cuda, resolve_mode, n_frames, payload):
+    """200 000 x 64 B frames, 120 B, and 600 000 x 16 B. These
+    streams (4-26 MiB) are short, so the resolve uses 64 KiB super tiles
+    (st_tiles_for, merge_kernels.hip): 64 B and 120 B frames then fit the LDS
+    tables; 16 B frames (~3 000 per super tile) take the big-ST path, merged
+    and emitted in LDS (merge_mid / emit_mid), or over global scratch when
+    forced -- bit-exact either way."""
+    wire, descs, _ = gpu.config_c2(seed=65, n_frames=n_frames, payload=payload)
     r = check(ctx, cuda, wire)
-    assert int(r["n_frames"]) == 200_000
+    assert int(r["n_frames"]) == n_frames
     c = counters(ctx)
     assert c[CNT_FAILED] == 0
-    if resolve_mode != "small_read":
+    if resolve_mode != "small_read" and payload == 16:
         assert c[CNT_BIG] > 0
 
 

@@ -21,6 +21,16 @@ from flashws_amd import gpu  # noqa: E402
 KW = 1024
 
 
+def n_super_tiles(nbytes):
+    """merge_kernels.hip st_tiles_for: 512 KiB super tiles, halved (to 64 KiB)
+    while a stream gives fewer than 512 of them"""
+    tiles = (nbytes + 2047) // 2048
+    t = 256
+    while t > 32 and tiles < t * 512:
+        t //= 2
+    return (tiles + t - 1) // t
+
+
 def stats(v):
     v = np.asarray(v, dtype=np.float64)
     if v.size == 0:
@@ -42,7 +52,7 @@ def main():
         n = len(descs)
         ctx = gpu.Ctx(0, max_frames=n + 16, max_stream_bytes=len(wire))
         w = torch.from_numpy(wire).to(dev)
-        n_st = (len(wire) + (512 << 10) - 1) // (512 << 10)
+        n_st = n_super_tiles(len(wire))
         for _ in range(4):
             gpu.decode_stream(ctx, w, cap=n + 16)
         torch.cuda.synchronize()

@@ -33,7 +33,13 @@ enum Counter {
     kCntTicket = 10,     // k_link workgroups finished (the last one resolves the path)
     kCntTails = 11,      // super-tile exit tails appended by k_merge
     kCntBig = 12,        // super tiles that took k_merge's big-ST path (diagnostic)
-    kCntCount = 13
+    // one-pass decode (fused_kernels.hip)
+    kCntFMode = 13,      // 1: k_fused ran this call; the multi-launch path runs only if it failed
+    kCntFFail = 14,      // ~(first failing fused super tile), 0 = none (atomicMax)
+    kCntFTicket = 15,    // k_fused's ordered super-tile ticket
+    kCntFSurv = 16,      // survivors over all fused super tiles (diagnostic, result)
+    kCntFTimeout = 17,   // fused super tiles that gave up a bounded wait (diagnostic)
+    kCntCount = 18
 };
 constexpr uint32_t kCntStride = 128;         // words per counter set (fws_decode_ws::cnt_base)
 // Spill runs: k_scan wavefront gw reserves from region gw % kSpillRegions (its
@@ -56,6 +62,10 @@ __device__ __forceinline__ uint32_t spill_shared(uint32_t *counters, uint32_t s_
     return spill_half(s_cap) + off;
 }
 static_assert(kCntFrames == kDecodeFramesCounter, "fws_internal.h names the frame counter");
+static_assert(kCntFMode == kDecodeFModeCounter && kCntFFail == kDecodeFFailCounter, "fws_internal.h names them");
+// the one-pass decode (k_fused) ran this call and finished the whole stream: the
+// multi-launch kernels queued after it return at once
+__device__ __forceinline__ bool fused_done(const uint32_t *C) { return C[kCntFMode] != 0u && C[kCntFFail] == 0u; }
 
 constexpr uint32_t kSlots = 8;               // per-tile survivor slots before spilling
 constexpr uint32_t kDenseTile = 0xFFFFFFFEu; // tile_count mark: k_scan left the tile to k_scan_dense (which overwrites it)

@@ -48,15 +48,6 @@ __device__ unsigned long long g_scan_prof[16];
 #define SCAN_COUNT(i, v) do { } while (0)
 #endif
 
-constexpr uint32_t kCandCap = 256;           // k_scan: candidates per tile (else dense_tile in k_merge)
-constexpr uint32_t kLiveCap = 64;            // k_scan: live nodes per tile, one per lane
-constexpr uint32_t kDeadLane = 0xFFu;        // k_scan pointer jumping: the chain dies
-// k_scan's halo: the next tile's first bytes, enough for the two-byte test at
-// any exit a 7-bit length form can reach from inside the tile (2047 + 6 + 125,
-// + 1) -- a chain whose exit there fails it is dead, not a survivor
-constexpr uint32_t kHaloX = 144;
-static_assert(kHaloX >= 2047u + 6u + 125u + 2u - kTile && kHaloX % 16u == 0 && kHaloX / 16u <= 64u, "halo");
-
 // LDS of one k_scan wavefront
 struct ScanLds {
     uint8_t bytes[kTile + kHaloX];
@@ -90,6 +81,7 @@ __global__ __launch_bounds__(kScanThreads) __attribute__((amdgpu_waves_per_eu(8,
                                                        uint32_t *__restrict__ counters, uint32_t s_cap,
                                                        uint32_t *__restrict__ scan_dummy) {
     __shared__ __attribute__((aligned(16))) ScanLds lds_w[kScanWaves];
+    if (fused_done(counters)) return;                // k_fused decoded the stream
     const uint32_t lane = threadIdx.x & 63;
     ScanLds &W = lds_w[threadIdx.x >> 6];
     uint8_t *const B = W.bytes;
@@ -422,6 +414,12 @@ int fws_launch_decode(fws_gpu_ctx *ctx, uint8_t *wire, uint64_t N, fws_frame_inf
         d.cnt_dirty = false;
     }
     d.cnt_dirty = true;                  // until every launch of this call is queued
+    // the one-pass decode first; the launches below are its fallback and return
+    // at once when it finished the stream (kCntFMode / kCntFFail)
+    if (g_resolve_mode == 0 && !utf8_ok && cap > 0 && fws_fused_enabled(N)) {
+        if (int r = fws_fused_ensure(ctx, N)) return r;
+        if (int r = fws_launch_fused(ctx, wire, N, frames, cap, res, s)) return r;
+    }
     if (n_tiles) {
         const uint32_t need = (n_tiles + kScanWaves - 1) / kScanWaves;
         const uint32_t sg = need < d.scan_grid ? need : d.scan_grid;

@@ -64,7 +64,7 @@ extern "C" {
 // decode on ctx (decode_common.h Counter), synchronously. 0 or an error.
 __attribute__((visibility("default"))) int fws_internal_decode_counters(fws_gpu_ctx *ctx, uint32_t *out, int n) {
     if (!ctx || !out || n <= 0 || !ctx->dec.counters) return FWS_ERR_INVALID;
-    if (n > 16) n = 16;
+    if (n > 32) n = 32;
     return fws_hip_status(hipMemcpy(out, ctx->dec.counters, (size_t)n * 4, hipMemcpyDeviceToHost));
 }
 
@@ -272,7 +272,7 @@ int fws_gpu_decode_stream(fws_gpu_ctx *ctx, void *dev_wire, uint64_t len, fws_fr
     // the unmask checks UTF-8 while the payload is in registers
     const uint32_t *n_dev = ctx->dec.counters + kDecodeFramesCounter;
     return fws_launch_unmask_stream((uint8_t *)dev_wire, len, dev_frames, cap, n_dev, ctx->plan.unit_first,
-                                    dev_utf8_ok, s);
+                                    dev_utf8_ok, ctx->dec.counters, fws_fused_done(ctx), ctx->dec.fepoch, s);
 }
 
 }  // extern "C"

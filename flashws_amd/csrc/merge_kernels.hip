@@ -494,6 +494,7 @@ __global__ __launch_bounds__(kMThreads) void k_merge(MergeParams P) {
     MP_START(30);
     MP_T0();
     MP_INIT();
+    if (fused_done(C)) return;                       // k_fused decoded the stream (k_link returns too)
     // the tail-target bitmap k_link sets
     for (uint64_t w = (uint64_t)s * kMThreads + tid; w < P.tail_cap / 32u + 1u; w += (uint64_t)gridDim.x * kMThreads)
         P.tmark[w] = 0u;
@@ -1016,6 +1017,7 @@ __global__ __launch_bounds__(kMThreads) void k_link(MergeParams P) {
     MP_START(29);
     MP_T0();
     MP_INIT();
+    if (fused_done(C)) return;
     const uint32_t M = C[kCntTails];
     const uint32_t x = blockIdx.x * kMThreads + tid;
     if (x < M && !C[kCntFallback]) {
@@ -1255,7 +1257,7 @@ __global__ __launch_bounds__(kMThreads) void k_emit(MergeParams P) {
     MP_T0();
     MP_INIT();
     if (s == 0 && tid < kCntStride) P.zero_next[tid] = 0u;   // the next call's counter set
-    if (s >= P.n_st) return;
+    if (s >= P.n_st || fused_done(C)) return;
     const uint32_t fb = C[kCntFallback], e = P.st_entry[s], fbase = P.st_fbase[s], n = P.st_n[s];
     const uint32_t lim = C[kCntFrames];
     if (fb || e == kNone || fbase >= lim) return;

@@ -22,6 +22,14 @@ namespace fwsk {
 constexpr int kScanWaves = 4;                          // wavefronts per workgroup
 constexpr int kScanThreads = kScanWaves * 64;
 constexpr uint32_t kWCap = 1024;                       // node list capacity of a sparse tile
+constexpr uint32_t kCandCap = 256;           // k_scan / k_fused: candidates per tile (else dense)
+constexpr uint32_t kLiveCap = 64;            // live nodes per tile, one per lane
+constexpr uint32_t kDeadLane = 0xFFu;        // pointer jumping in registers: the chain dies
+// the scan's halo: the next tile's first bytes, enough for the two-byte test at
+// any exit a 7-bit length form can reach from inside the tile (2047 + 6 + 125,
+// + 1) -- a chain whose exit there fails it is dead, not a survivor
+constexpr uint32_t kHaloX = 144;
+static_assert(kHaloX >= 2047u + 6u + 125u + 2u - kTile && kHaloX % 16u == 0 && kHaloX / 16u <= 64u, "halo");
 
 
 // Bit i set <=> offset i of the chunk passes the two-byte header test

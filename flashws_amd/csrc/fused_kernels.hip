@@ -67,6 +67,7 @@ constexpr uint32_t kFLoads = kFS / (kFThreads * 16);        // 16-B loads per th
 constexpr uint32_t kFExCap = 16;                            // own exits published per ST
 constexpr uint32_t kFInCap = 16;                            // inbox entries per ST
 constexpr uint32_t kFLive = 2;                              // live fast-table entries per ST
+constexpr uint32_t kFDepth = 4;                             // fast-table keys: own exits of the STs k-4..k-1
 constexpr uint32_t kPsDead = 0xFFFFu;                       // ps: the chain dies in the ST
 constexpr uint32_t kXFar = 0xFFFFFFFFu;                     // fexit: beyond st0 + 4 GiB
 constexpr uint16_t kIncBit = 0x8000;                        // lcnt: the leaf is an incomplete header
@@ -136,7 +137,7 @@ struct FusedParams {
     }
     // an ST before k has failed (kCntFFail holds ~(first failing ST))
     __device__ __forceinline__ bool failed_before(uint32_t k) const {
-        const uint32_t f = cget(&C[kCntFFail]);
+        const uint32_t f = (uint32_t)__builtin_amdgcn_readfirstlane((int)cget(&C[kCntFFail]));
         return f != 0u && ~f < k;
     }
 };
@@ -347,37 +348,20 @@ __device__ bool f_scan_tile(FusedLds &S, uint32_t t, uint64_t st0, uint64_t N) {
     return false;
 }
 
-// Every ST <= k - 1 has published LOCAL (look-back over FRONT / LOCAL words).
-// False: an ST before k failed, or the wait gave up.
-__device__ bool f_wait_frontier(const FusedParams &P, uint32_t k, uint32_t lane, uint32_t &nspin) {
-    if (k == 0) return true;
-    const uint64_t *const LO = P.R(kRLocal), *const FR = P.R(kRFront);
+// The kFDepth STs before k have published LOCAL (their own exits are this ST's
+// keys). False: one of them failed, an ST before k failed, or the wait gave up.
+__device__ bool f_wait_recent(const FusedParams &P, uint32_t k, uint32_t lane, uint32_t &nspin) {
+    const uint64_t *const LO = P.R(kRLocal);
     for (uint32_t spins = 0;; ++spins) {
-        bool all_local = true, fail = false;
-        for (int64_t w0 = (int64_t)k - 1;; w0 -= 64) {
-            const int64_t m = w0 - (int64_t)lane;
-            bool lo = true, fr = false, valid = m >= -1;
-            if (m >= 0) {
-                const uint64_t gl = gget(LO + m), gf = gget(FR + m);
-                lo = gok(gl, P.tag);
-                fail = fail || (lo && (gval(gl) & kLFail));
-                fr = gok(gf, P.tag);
-            } else if (m == -1) {
-                fr = true;                           // virtual front before ST 0
-            }
-            fail = __any(fail);
-            const uint64_t fm = __ballot(valid && fr);
-            if (fm) {
-                const uint32_t j = (uint32_t)__ffsll((unsigned long long)fm) - 1u;
-                const uint64_t below = j ? ((1ull << j) - 1ull) : 0ull;
-                if (__ballot(!lo) & below) all_local = false;
-                break;
-            }
-            if (__ballot(valid && !lo)) all_local = false;
+        bool ok = true, fail = false;
+        if (lane < kFDepth && k >= lane + 1u) {
+            const uint64_t gl = gget(LO + (k - 1u - lane));
+            ok = gok(gl, P.tag);
+            fail = ok && (gval(gl) & kLFail);
         }
         nspin = spins;
-        if (fail) return false;
-        if (all_local) return true;
+        if (__any(fail)) return false;
+        if (__all(ok)) return true;
         if (spins >= kSpinMax || P.failed_before(k)) return false;
         __builtin_amdgcn_s_sleep(1);
     }
@@ -522,14 +506,32 @@ __device__ bool f_lookback(const FusedParams &P, uint32_t k, uint32_t lane, uint
 #pragma unroll
             for (uint32_t i = 0; i < kFLive; ++i) {
                 const uint64_t key = readlane64(e[4 * i], l);
-                if (!hit && i < n && n <= kFLive && key == X) {
+                if (!hit && i < n && n <= kFLive && key == X) {   // n == 3: unreadable, a miss
                     X = readlane64(e[4 * i + 1], l);
                     base += readlane64(e[4 * i + 2], l);
                     tail = readlane64(e[4 * i + 3], l);
                     hit = true;
                 }
             }
-            if (!hit) return false;                          // the true chain dies here: a protocol error
+            if (!hit) {
+                // the entry is no key of this ST's fast table: a jump from more than
+                // kFDepth STs back, or a protocol error. This ST resolves it from its
+                // own tables: wait for its INCL (FAIL if the chain dies there).
+                const uint64_t *px = IX + mm, *pb = IB + mm, *pt = IT + mm;
+                uint64_t gx = gget(px), gb = gget(pb), gt = gget(pt);
+                for (uint32_t sp = 0; !(gok(gx, tag) && gok(gb, tag) && gok(gt, tag)); ++sp) {
+                    if (gok(gx, tag) && gval(gx) == kVFail) return false;
+                    if (sp >= kSpinMax || P.failed_before(k)) return false;
+                    __builtin_amdgcn_s_sleep(1);
+                    gx = gget(px);
+                    gb = gget(pb);
+                    gt = gget(pt);
+                }
+                if (gval(gx) == kVFail) return false;
+                X = gval(gx);
+                base = gval(gb);
+                tail = gval(gt);
+            }
         }
     }
     return true;
@@ -538,7 +540,7 @@ __device__ bool f_lookback(const FusedParams &P, uint32_t k, uint32_t lane, uint
 // tools/prof_fused.py: trace[k * kFTraceW + i] = wall clock at phase i of ST k
 // (0 start, 1 after L, 2 after F, 3 after B, 4 end), 5 = look-back window,
 // 6 = lookback spins, 7 = frontier spins (wave 0 lane 0 writes)
-constexpr uint32_t kFTraceW = 8;
+constexpr uint32_t kFTraceW = 12;   // + 8 after load, 9 after scan, 10 after the in-ST resolve
 #define FT_MARK(i, v) do { if (P.trace && tid == 0) P.trace[(uint64_t)k * kFTraceW + (i)] = (v); } while (0)
 
 __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_fused(FusedParams P) {
@@ -584,19 +586,22 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(3, 3)
     for (;;) {
         __syncthreads();                             // the previous ST is done with LDS
         if (tid == 0) {
-            S.ticket = atomicAdd(&C[kCntFTicket], 1u);
-            S.fail = 0;
+            const uint32_t t = atomicAdd(&C[kCntFTicket], 1u);
+            S.ticket = t;
+            // decided once for the workgroup: every wave must take the same branches
+            // (they hold barriers), so no thread reads the fail word on its own
+            S.fail = t < P.n_st && P.failed_before(t) ? 1u : 0u;
             S.n_ex = 0;
             S.surv = 0;
         }
         __syncthreads();
         const uint32_t k = S.ticket;
         if (k >= P.n_st) break;
+        FT_MARK(0, wall_clock64());
         load_st(k);
         store_st(k);
         __syncthreads();
 
-        FT_MARK(0, wall_clock64());
         const uint64_t st0 = (uint64_t)k * kFS;
         const uint64_t stE = P.end_of(k);
         const uint32_t rel_end = (uint32_t)(stE - st0);
@@ -612,12 +617,14 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(3, 3)
         };
 
         // ---- L: scan, in-ST resolve, own exits, LOCAL
-        bool skip = P.failed_before(k);
+        FT_MARK(8, wall_clock64());
+        bool skip = S.fail != 0;
         if (!skip) {
             for (uint32_t t = wv; t < kFTiles; t += kFWaves)
                 if (f_scan_tile(S, t, st0, N) && lane == 0) S.fail = 1;
         }
         __syncthreads();
+        FT_MARK(9, wall_clock64());
         skip = skip || S.fail;
         if (!skip) {
             for (uint32_t s = tid; s < kFSlots; s += kFThreads) {
@@ -680,11 +687,12 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(3, 3)
             __syncthreads();
             skip = S.fail != 0;
         }
+        FT_MARK(10, wall_clock64());
         if (wv == 0) {
             if (skip) {
                 fail_now();
             } else {
-                // LOCAL: distinct own exits; those landing two or more STs ahead go to that ST's inbox
+                // LOCAL: the distinct own exits
                 const uint32_t n = S.n_ex;
                 const uint64_t e = lane < n ? S.ex[lane] : 0ull;
                 bool dup = false;
@@ -694,22 +702,7 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(3, 3)
                 }
                 const bool keep = lane < n && !dup;
                 const uint64_t km = __ballot(keep);
-                if (keep) {
-                    gput(P.blk(k) + kBEx + mbcnt64(km), gr(tag, e));
-                    const uint64_t tgt = e / kFS;
-                    if (tgt >= (uint64_t)k + 2u) {
-                        uint64_t *const cnt = P.R(kRInbox) + tgt;
-                        for (;;) {
-                            uint64_t x = gget(cnt);
-                            const uint64_t c = gok(x, tag) ? gval(x) : 0ull;
-                            if (__hip_atomic_compare_exchange_strong(cnt, &x, gr(tag, c + 1u), __ATOMIC_RELAXED,
-                                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-                                if (c < kFInCap) gput(P.blk((uint32_t)tgt) + kBIn + c, gr(tag, e));
-                                break;
-                            }
-                        }
-                    }
-                }
+                if (keep) gput(P.blk(k) + kBEx + mbcnt64(km), gr(tag, e));
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 if (lane == 0) {
                     atomicAdd(&C[kCntFSurv], S.surv);
@@ -723,25 +716,23 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(3, 3)
         FT_MARK(1, wall_clock64());
         if (wv == 0 && !skip) {
             uint32_t fsp = 0;
-            const bool fok = f_wait_frontier(P, k, lane, fsp);
+            const bool fok = f_wait_recent(P, k, lane, fsp);
             FT_MARK(7, fsp);
             if (!fok) {
                 if (lane == 0) atomicAdd(&C[kCntFTimeout], 1u);
                 skip = true;
                 fail_now();
             } else {
-                if (lane == 0) gput(P.R(kRFront) + k, gr(tag, 1u));
+                // keys: the own exits of the kFDepth STs before that land here (lanes
+                // 16 d + i: exit i of ST k - 1 - d); a longer jump is a look-back miss
                 uint64_t key = 0;
                 bool has = false, inc = false;
-                if (k > 0) {
-                    const uint32_t np = (uint32_t)(gval(gget(P.R(kRLocal) + k - 1)) & 0xFFu);
-                    const uint64_t gi = gget(P.R(kRInbox) + k);
-                    const uint64_t ni = gok(gi, tag) ? gval(gi) : 0ull;
-                    inc = ni > kFInCap;
-                    const uint64_t *src = nullptr;
-                    if (lane < np) src = P.blk(k - 1) + kBEx + lane;
-                    else if (lane >= 32u && lane - 32u < ni && lane - 32u < kFInCap) src = P.blk(k) + kBIn + (lane - 32u);
-                    if (src) {
+                const uint32_t d = lane >> 4, i = lane & 15u;
+                if (d < kFDepth && k >= d + 1u) {
+                    const uint32_t m = k - 1u - d;
+                    const uint32_t np = (uint32_t)(gval(gget(P.R(kRLocal) + m)) & 0xFFu);
+                    if (i < np) {
+                        const uint64_t *src = P.blk(m) + kBEx + i;
                         uint64_t g = gget(src);
                         for (uint32_t sp = 0; !gok(g, tag) && sp < 4096; ++sp) g = gget(src);
                         if (gok(g, tag)) {

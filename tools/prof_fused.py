@@ -15,7 +15,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from flashws_amd import _lib, gpu  # noqa: E402
 
-W = 8
+W = 12
 
 
 def main():
@@ -54,12 +54,16 @@ def main():
     ok = t[:, 4] > 0
     print(f"STs {got}, finished {int(ok.sum())}")
     t = t[ok]
+    if len(t) == 0:
+        ctx.close()
+        return
     t0 = t[:, 0].min()
     us = lambda x: x / 100.0   # wall clock 100 MHz
-    ph = {"L": t[:, 1] - t[:, 0], "F": t[:, 2] - t[:, 1], "B": t[:, 3] - t[:, 2], "U": t[:, 4] - t[:, 3],
+    ph = {"load": t[:, 8] - t[:, 0], "scan": t[:, 9] - t[:, 8], "res": t[:, 10] - t[:, 9],
+          "pub": t[:, 1] - t[:, 10], "F": t[:, 2] - t[:, 1], "B": t[:, 3] - t[:, 2], "U": t[:, 4] - t[:, 3],
           "all": t[:, 4] - t[:, 0]}
     for k, v in ph.items():
-        print(f"  {k:3s} us: mean {us(v.mean()):8.2f} p50 {us(np.median(v)):8.2f} p90 {us(np.percentile(v, 90)):8.2f} "
+        print(f"  {k:4s} us: mean {us(v.mean()):8.2f} p50 {us(np.median(v)):8.2f} p90 {us(np.percentile(v, 90)):8.2f} "
               f"max {us(v.max()):8.2f}")
     print(f"  span {us(t[:, 4].max() - t0):.1f} us; start of ST k (us) at k = 0, n/4, n/2, 3n/4, n-1: " +
           ", ".join(f"{us(t[min(int(f * (len(t) - 1)), len(t) - 1), 0] - t0):.1f}" for f in (0, .25, .5, .75, 1)))

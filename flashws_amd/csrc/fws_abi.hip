@@ -58,6 +58,17 @@ int fws_ctx_ensure_plan(fws_gpu_ctx *ctx, uint64_t frames, uint64_t units) {
     return 0;
 }
 
+// per-unit seam words of fws_gpu_unmask_sorted_utf8 for a span of `span` bytes
+int fws_ctx_ensure_seam(fws_gpu_ctx *ctx, uint64_t span) {
+    const uint64_t words = 2 * (span / 4096 + 2);
+    if (words <= ctx->seam_cap) return 0;
+    dev_free(ctx->seam);
+    ctx->seam_cap = 0;
+    if (int r = fws_hip_status(hipMalloc((void **)&ctx->seam, words * 4))) return r;
+    ctx->seam_cap = words;
+    return 0;
+}
+
 extern "C" {
 
 // Test / tuning hook (not part of the ABI): the decode counters of the last
@@ -128,6 +139,8 @@ void fws_gpu_ctx_destroy(fws_gpu_ctx *ctx) {
     dev_free(d.bg_ptr);
     dev_free(d.bg_sc);
     dev_free(d.bg_mark);
+    dev_free(d.fpub);
+    dev_free(ctx->seam);
     delete ctx;
 }
 
@@ -139,8 +152,9 @@ int fws_gpu_ctx_reserve(fws_gpu_ctx *ctx, uint64_t max_frames, uint64_t max_stre
     const uint64_t units = (max_stream_bytes / 16 + 2 * max_frames) / 256 + 2;
     if ((r = fws_ctx_ensure_plan(ctx, max_frames, units))) return r;
     if (max_stream_bytes > ctx->cap_stream) ctx->cap_stream = max_stream_bytes;
-    return 0;
+    return fws_ctx_ensure_seam(ctx, ctx->cap_stream);
 }
+
 
 int fws_gpu_mask(void *dev_ptr, uint64_t n, uint32_t key, void *stream) {
     if (n && !dev_ptr) return FWS_ERR_INVALID;
@@ -224,7 +238,9 @@ int fws_gpu_unmask_sorted_utf8(fws_gpu_ctx *ctx, void *dev_base, const fws_frame
     if ((r = fws_hip_status(hipSetDevice(ctx->device)))) return r;
     if ((r = check_sorted_debug(ctx, dev_descs, n, (hipStream_t)stream))) return r;
     const uint64_t span = ctx->cap_stream ? ctx->cap_stream : 4096ull * n;
-    return fws_launch_unmask_sorted_utf8((uint8_t *)dev_base, dev_descs, n, span, dev_ok, (hipStream_t)stream);
+    if ((r = fws_ctx_ensure_seam(ctx, span))) return r;
+    return fws_launch_unmask_sorted_utf8((uint8_t *)dev_base, dev_descs, n, span, dev_ok, ctx->seam,
+                                         (hipStream_t)stream);
 }
 
 int fws_gpu_unmask_gather(fws_gpu_ctx *ctx, void *dev_dst, const void *dev_src, const fws_frame_desc *dev_descs,

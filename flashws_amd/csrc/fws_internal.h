@@ -143,7 +143,10 @@ struct fws_gpu_ctx {
     fws_plan_ws plan;
     fws_decode_ws dec;
     void *pinned = nullptr;           // host staging for small readbacks
+    uint32_t *seam = nullptr;         // fws_gpu_unmask_sorted_utf8: first / last unmasked dword per unit
+    uint64_t seam_cap = 0;            // words
 };
+int fws_ctx_ensure_seam(fws_gpu_ctx *ctx, uint64_t span);
 
 int fws_ctx_ensure_plan(fws_gpu_ctx *ctx, uint64_t frames, uint64_t units);
 
@@ -158,8 +161,10 @@ int fws_launch_unmask_sorted(uint8_t *base, const fws_frame_desc *d, uint32_t n,
                              hipStream_t s);
 // *bad = the first index breaking the sorted / disjoint contract, or ~0 (device word)
 int fws_launch_check_sorted(const fws_frame_desc *d, uint32_t n, uint32_t *bad, hipStream_t s);
+// seam (2 words per 4 KiB unit of the span + 4): the first and last unmasked dword of
+// every unit, written by the unmask and read by the unit-seam UTF-8 check
 int fws_launch_unmask_sorted_utf8(uint8_t *base, const fws_frame_desc *d, uint32_t n, uint64_t max_span,
-                                  uint8_t *ok, hipStream_t s);
+                                  uint8_t *ok, uint32_t *seam, hipStream_t s);
 // Decoded stream in stream-byte space: unit_first[u] = frame spanning byte 4 KiB * u (the decode's plan).
 // utf8_ok (optional): per-frame flags, preset by the resolve to TEXT && FIN && complete; cleared here on
 // a UTF-8 error found while the payload is in registers (+ k_utf8_seam for unit seams).

@@ -880,7 +880,8 @@ __device__ __forceinline__ void utf8_slow_chunk(const fws_frame_desc *__restrict
 
 template <bool kNT, bool kEarly, bool kUtf8 = false>
 __device__ __forceinline__ void unmask_sorted_body(uint8_t *base, const fws_frame_desc *__restrict__ d, uint32_t n,
-                                                   uint8_t *__restrict__ ok = nullptr) {
+                                                   uint8_t *__restrict__ ok = nullptr,
+                                                   uint32_t *__restrict__ seam = nullptr) {
     if (n == 0) return;
     const int lane = threadIdx.x & (kWave - 1);
     const uintptr_t b0 = (uintptr_t)base;
@@ -931,6 +932,9 @@ __device__ __forceinline__ void unmask_sorted_body(uint8_t *base, const fws_fram
                     x[j] = x[j] ^ u32x4{rk, rk, rk, rk};
                     gstore16<kNT>(c0 + uint64_t(j) * 1024u, x[j]);
                 }
+                // the unit's first and last unmasked dwords for k_utf8_seam_sorted
+                if (lane == 0) seam[2u * u] = x[0].x;
+                if (lane == 63) seam[2u * u + 1u] = x[kUnmaskU - 1].w;
                 uint32_t err = 0, carry = 0;
 #pragma unroll
                 for (int j = 0; j < kUnmaskU; ++j) {
@@ -979,6 +983,8 @@ __device__ __forceinline__ void unmask_sorted_body(uint8_t *base, const fws_fram
                     uint32_t prev = __shfl_up(x.w, 1, 64);
                     if (lane == 0) prev = carry;
                     carry = __shfl(x.w, 63, 64);
+                    if (j == 0 && lane == 0) seam[2u * u] = x.x;
+                    if (j == kUnmaskU - 1 && lane == 63) seam[2u * u + 1u] = x.w;
                     utf8_slow_chunk(d, n, A, b0, c0 + uint64_t(j) * 1024u, x, prev, j == 0 && lane == 0, ok);
                 }
                 continue;
@@ -998,6 +1004,8 @@ __device__ __forceinline__ void unmask_sorted_body(uint8_t *base, const fws_fram
                 uint32_t prev = __shfl_up(x.w, 1, 64);
                 if (lane == 0) prev = carry;
                 carry = __shfl(x.w, 63, 64);
+                if (j == 0 && lane == 0) seam[2u * u] = x.x;
+                if (j == kUnmaskU - 1 && lane == 63) seam[2u * u + 1u] = x.w;
                 const uint32_t skip = j == 0 && lane == 0;
                 const int32_t r = r0 + j * 1024;
                 if (r + 16 > loA && r < hiA + 3) errA |= utf8_chunk_err32(x, prev, r, loA, hiA, skip);
@@ -1015,7 +1023,8 @@ __device__ __forceinline__ void unmask_sorted_body(uint8_t *base, const fws_fram
 // per unit seam; reads the already unmasked bytes. The owner of the seam is
 // found like sorted_owner, per thread.
 __global__ __launch_bounds__(kBlock) void k_utf8_seam_sorted(const uint8_t *base, const fws_frame_desc *__restrict__ d,
-                                                             uint32_t n, uint8_t *__restrict__ ok) {
+                                                             uint32_t n, uint8_t *__restrict__ ok,
+                                                             const uint32_t *__restrict__ seam) {
     if (n == 0) return;
     const uintptr_t b0 = (uintptr_t)base;
     const uint64_t E0 = b0 + d[0].payload_off;
@@ -1044,8 +1053,10 @@ __global__ __launch_bounds__(kBlock) void k_utf8_seam_sorted(const uint8_t *base
         }
         L = lo;
     }
-    const uint32_t cur = *(const uint32_t *)(base + (P - b0));
-    const uint32_t prev = *(const uint32_t *)(base + (P - 4u - b0));
+    // the unmask's per-unit record (two adjacent words per thread) rather than two
+    // stream lines 4 KiB apart; the software-pipelined unmask writes none (seam null)
+    const uint32_t cur = seam ? seam[2u * u] : *(const uint32_t *)(base + (P - b0));
+    const uint32_t prev = seam ? seam[2u * u - 1u] : *(const uint32_t *)(base + (P - 4u - b0));
     for (uint32_t f = L + 1u; f-- > 0;) {
         const fws_frame_desc fd = d[f];
         const uint64_t po = b0 + fd.payload_off, pe = po + fd.payload_len;
@@ -1195,9 +1206,10 @@ __device__ __forceinline__ void unmask_sorted_utf8_pipe(uint8_t *base, const fws
 // unmask + per-region UTF-8 flags (C5 in descriptor mode); ok preset to 1
 template <bool kNT, bool kPipe>
 __global__ __launch_bounds__(kBlock) void k_unmask_sorted_utf8(uint8_t *base, const fws_frame_desc *__restrict__ d,
-                                                               uint32_t n, uint8_t *__restrict__ ok) {
+                                                               uint32_t n, uint8_t *__restrict__ ok,
+                                                               uint32_t *__restrict__ seam) {
     if (kPipe) unmask_sorted_utf8_pipe<kNT>(base, d, n, ok);
-    else unmask_sorted_body<kNT, false, true>(base, d, n, ok);
+    else unmask_sorted_body<kNT, false, true>(base, d, n, ok, seam);
 }
 
 }  // namespace fwsk
@@ -1302,20 +1314,20 @@ int fws_launch_unmask_sorted(uint8_t *base, const fws_frame_desc *d, uint32_t n,
 }
 
 int fws_launch_unmask_sorted_utf8(uint8_t *base, const fws_frame_desc *d, uint32_t n, uint64_t max_span,
-                                  uint8_t *ok, hipStream_t s) {
+                                  uint8_t *ok, uint32_t *seam, hipStream_t s) {
     if (n == 0) return 0;
     int r = fws_hip_status(hipMemsetAsync(ok, 1, n, s));
     if (r) return r;
     const uint64_t units = max_span / 4096u + 2u;
     if (g_sorted_utf8_pipe)
         hipLaunchKernelGGL((k_unmask_sorted_utf8<true, true>), dim3(grid_for_units(units)), dim3(kBlock), 0, s, base, d,
-                           n, ok);
+                           n, ok, nullptr);
     else
         hipLaunchKernelGGL((k_unmask_sorted_utf8<true, false>), dim3(grid_for_units(units)), dim3(kBlock), 0, s, base,
-                           d, n, ok);
+                           d, n, ok, seam);
     const uint64_t seam_blocks = (units + kBlock - 1) / kBlock;   // grid-stride: any span is covered
     hipLaunchKernelGGL(k_utf8_seam_sorted, dim3((unsigned)(seam_blocks < 4096u ? seam_blocks : 4096u)), dim3(kBlock), 0, s,
-                       (const uint8_t *)base, d, n, ok);
+                       (const uint8_t *)base, d, n, ok, g_sorted_utf8_pipe ? nullptr : seam);
     return fws_hip_status(hipGetLastError());
 }
 

@@ -95,3 +95,16 @@ def test_generator_streams_decode_to_their_descriptors(cfg):
                 v = 0
             assert v == good
         assert 0 < ok.sum() < len(ok)
+
+
+def test_one_pass_decode_is_off_by_default():
+    """The multi-launch stream decode is the default (k_fused, fused_kernels.hip,
+    measured slower: DESIGN.md 4.3b); fws_internal_set_fused(-1) only reads
+    the mode. A fresh process, so no other test's setting leaks in."""
+    import subprocess
+    import sys
+    code = "from flashws_amd import _lib; print(_lib.lib().fws_internal_set_fused(-1))"
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120,
+                         cwd=str(__import__("pathlib").Path(__file__).resolve().parents[1]))
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.strip().splitlines()[-1] == "0", out

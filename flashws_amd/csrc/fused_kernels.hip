@@ -1069,10 +1069,11 @@ int fws_launch_fused(fws_gpu_ctx *ctx, uint8_t *wire, uint64_t N, fws_frame_info
     fws_decode_ws &d = ctx->dec;
     const uint64_t n_st = (N + kFS - 1) / kFS;
     if (n_st > d.fmax_st || n_st >= (1ull << 31)) return FWS_ERR_INTERNAL;
-    static int cus = 0;
-    if (cus == 0) {
+    if (d.fcus == 0) {                               // per context: its device's CU count
+        int cus = 0;
         hipError_t e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device);
         if (e != hipSuccess) return fws_hip_status(e);
+        d.fcus = (uint32_t)cus;
     }
     d.fepoch = (d.fepoch + 1u) & 0xFFFFFFu;
     if (d.fepoch == 0) d.fepoch = 1;
@@ -1099,7 +1100,7 @@ int fws_launch_fused(fws_gpu_ctx *ctx, uint8_t *wire, uint64_t N, fws_frame_info
         P.trace = g_trace;
         g_trace_n = n_st;
     }
-    const uint64_t g = (uint64_t)cus * kFBlocksPerCu;
+    const uint64_t g = (uint64_t)d.fcus * kFBlocksPerCu;
     hipLaunchKernelGGL(k_fused, dim3((unsigned)(n_st < g ? n_st : g)), dim3(kFThreads), 0, s, P);
     return fws_hip_status(hipGetLastError());
 }

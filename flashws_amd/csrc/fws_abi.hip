@@ -287,8 +287,10 @@ int fws_gpu_decode_stream(fws_gpu_ctx *ctx, void *dev_wire, uint64_t len, fws_fr
     // decoded frames and (with dev_utf8_ok) each frame's TEXT/FIN/complete preset;
     // the unmask checks UTF-8 while the payload is in registers
     const uint32_t *n_dev = ctx->dec.counters + kDecodeFramesCounter;
+    if (dev_utf8_ok && (r = fws_ctx_ensure_seam(ctx, len))) return r;
     return fws_launch_unmask_stream((uint8_t *)dev_wire, len, dev_frames, cap, n_dev, ctx->plan.unit_first,
-                                    dev_utf8_ok, ctx->dec.counters, fws_fused_done(ctx), ctx->dec.fepoch, s);
+                                    dev_utf8_ok, ctx->dec.counters, fws_fused_done(ctx), ctx->dec.fepoch,
+                                    ctx->seam, s);
 }
 
 }  // extern "C"

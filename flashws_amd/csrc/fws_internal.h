@@ -133,6 +133,7 @@ struct fws_decode_ws {
     uint64_t fmax_st = 0;
     uint64_t *fpub = nullptr;              // [fmax_st * kFPubWords] (fused_kernels.hip layout)
     uint32_t fepoch = 0;                   // tag of the last k_fused call (1..2^24-1)
+    uint32_t fcus = 0;                     // CUs of the context's device (k_fused grid)
 };
 
 struct fws_gpu_ctx {
@@ -168,12 +169,14 @@ int fws_launch_unmask_sorted_utf8(uint8_t *base, const fws_frame_desc *d, uint32
 // Decoded stream in stream-byte space: unit_first[u] = frame spanning byte 4 KiB * u (the decode's plan).
 // utf8_ok (optional): per-frame flags, preset by the resolve to TEXT && FIN && complete; cleared here on
 // a UTF-8 error found while the payload is in registers (+ k_utf8_seam for unit seams).
-// fgate (optional): the decode's counter set; when k_fused ran (kCntFMode) the pass
+// seam (utf8_ok only; 2 words per 4 KiB unit + 4): each unit's first / last unmasked dword
+// for the unit-seam check. fgate (optional): the decode's counter set; when k_fused ran (kCntFMode) the pass
 // returns at once unless it failed, and then skips the super tiles k_fused already
 // unmasked (fdone granules tagged fepoch)
 int fws_launch_unmask_stream(uint8_t *base, uint64_t N, const fws_frame_info *frames, uint32_t cap,
                              const uint32_t *n_dev, const uint32_t *unit_first, uint8_t *utf8_ok,
-                             const uint32_t *fgate, const uint64_t *fdone, uint32_t fepoch, hipStream_t s);
+                             const uint32_t *fgate, const uint64_t *fdone, uint32_t fepoch, uint32_t *seam,
+                             hipStream_t s);
 
 // outplan_kernels.hip: one-launch output-space plans (base = ws.cbase, unit map, total)
 int fws_plan_next_epoch(fws_plan_ws &ws, hipStream_t s);

@@ -380,7 +380,8 @@ __global__ __launch_bounds__(kBlock) void k_unmask_stream(uint8_t *base, uint64_
                                                           const uint32_t *__restrict__ n_dev,
                                                           const uint32_t *__restrict__ unit_first, uint64_t n_units,
                                                           uint8_t *__restrict__ ok, const uint32_t *fgate,
-                                                          const uint64_t *fdone, uint32_t fepoch) {
+                                                          const uint64_t *fdone, uint32_t fepoch,
+                                                          uint32_t *__restrict__ seam) {
     // k_fused ran: nothing to do if it finished the stream; else skip the 32 KiB
     // super tiles it unmasked (done granules tagged with its epoch, fused_kernels.hip)
     const bool fran = fgate != nullptr && fgate[kDecodeFModeCounter] != 0u;
@@ -439,6 +440,9 @@ __global__ __launch_bounds__(kBlock) void k_unmask_stream(uint8_t *base, uint64_
                     uint32_t prev = __shfl_up(x.w, 1, 64);
                     if (lane == 0) prev = carry;
                     carry = __shfl(x.w, 63, 64);
+                    // the unit's first and last unmasked dwords for k_utf8_seam
+                    if (j == 0 && lane == 0) seam[2u * u] = x.x;
+                    if (j == kUnmaskU - 1 && lane == 63) seam[2u * u + 1u] = x.w;
                     // frames whose payload or 3-byte tail meets the chunk (lo - 1: the tail of the one before)
                     for (uint32_t f = lo > flo ? lo - 1u : lo; f < n; ++f) {
                         const fws_frame_info fi = fr[f];
@@ -467,6 +471,8 @@ __global__ __launch_bounds__(kBlock) void k_unmask_stream(uint8_t *base, uint64_
                     x[j] = pre[j] ^ u32x4{rk, rk, rk, rk};
                     gstore16<kNT>(b0 + c0 + uint64_t(j) * 1024u, x[j]);
                 }
+                if (lane == 0) seam[2u * u] = x[0].x;
+                if (lane == 63) seam[2u * u + 1u] = x[kUnmaskU - 1].w;
                 uint32_t err = 0, carry = 0;
 #pragma unroll
                 for (int j = 0; j < kUnmaskU; ++j) {
@@ -519,6 +525,10 @@ __global__ __launch_bounds__(kBlock) void k_unmask_stream(uint8_t *base, uint64_
                     uint32_t prev = __shfl_up(x.w, 1, 64);
                     if (lane == 0) prev = carry;
                     carry = __shfl(x.w, 63, 64);
+                    // (a unit with no TEXT frame writes no seam words: k_utf8_seam judges
+                    // only TEXT payload bytes, and none of this unit's are)
+                    if (j == 0 && lane == 0) seam[2u * u] = x.x;
+                    if (j == kUnmaskU - 1 && lane == 63) seam[2u * u + 1u] = x.w;
                     const uint32_t skip = j == 0 && lane == 0;
                     if (A.text && c + 16u > A.po && c < A.pe + 3u)
                         badA |= utf8_chunk_bad(x, prev, c, A.po, A.pe, skip);
@@ -540,15 +550,16 @@ __global__ __launch_bounds__(kBlock) void k_utf8_seam(const uint8_t *base, uint6
                                                       const fws_frame_info *__restrict__ fr, uint32_t cap,
                                                       const uint32_t *__restrict__ n_dev,
                                                       const uint32_t *__restrict__ unit_first, uint64_t n_units,
-                                                      uint8_t *__restrict__ ok) {
+                                                      uint8_t *__restrict__ ok, const uint32_t *__restrict__ seam) {
     uint32_t n = *n_dev;
     if (n > cap) n = cap;
     const uint64_t u = uint64_t(blockIdx.x) * kBlock + threadIdx.x + 1u;
     if (n == 0 || u > n_units) return;
     const uint64_t P = u * 4096u;
     const uint32_t f = u < n_units ? unit_first[u] : n - 1;
-    const uint32_t cur = P < N ? *(const uint32_t *)(base + P) : 0u;      // bytes past N: zeroed below
-    const uint32_t prev = *(const uint32_t *)(base + P - 4u);
+    // the unmask's per-unit record (adjacent words) rather than two stream lines 4 KiB apart
+    const uint32_t cur = P < N ? seam[2u * u] : 0u;                      // bytes past N: zeroed below
+    const uint32_t prev = seam[2u * u - 1u];
     for (uint32_t g = f > 0 ? f - 1u : 0u; g <= f; ++g) {
         const StreamFrame sf = stream_frame(fr[g], N);
         if (!sf.text || P + 3u <= sf.po || P >= sf.pe + 3u) continue;
@@ -1333,7 +1344,8 @@ int fws_launch_unmask_sorted_utf8(uint8_t *base, const fws_frame_desc *d, uint32
 
 int fws_launch_unmask_stream(uint8_t *base, uint64_t N, const fws_frame_info *frames, uint32_t cap,
                              const uint32_t *n_dev, const uint32_t *unit_first, uint8_t *utf8_ok,
-                             const uint32_t *fgate, const uint64_t *fdone, uint32_t fepoch, hipStream_t s) {
+                             const uint32_t *fgate, const uint64_t *fdone, uint32_t fepoch, uint32_t *seam,
+                             hipStream_t s) {
     const uint64_t units = (N + 4095) / 4096;
     if (units == 0 || cap == 0) return 0;
     const dim3 grid(grid_for_units(units)), blk(kBlock);
@@ -1341,25 +1353,25 @@ int fws_launch_unmask_stream(uint8_t *base, uint64_t N, const fws_frame_info *fr
     if (utf8_ok == nullptr) {
         if (v == 0)
             hipLaunchKernelGGL((k_unmask_stream<true, false, false>), grid, blk, 0, s, (uint8_t *)base, N, frames, cap,
-                               n_dev, unit_first, units, nullptr, fgate, fdone, fepoch);
+                               n_dev, unit_first, units, nullptr, fgate, fdone, fepoch, nullptr);
         else if (v == 1)
             hipLaunchKernelGGL((k_unmask_stream<true, false, true>), grid, blk, 0, s, (uint8_t *)base, N, frames, cap,
-                               n_dev, unit_first, units, nullptr, fgate, fdone, fepoch);
+                               n_dev, unit_first, units, nullptr, fgate, fdone, fepoch, nullptr);
         else if (v == 2)
             hipLaunchKernelGGL((k_unmask_stream<false, false, false>), grid, blk, 0, s, (uint8_t *)base, N, frames,
-                               cap, n_dev, unit_first, units, nullptr, fgate, fdone, fepoch);
+                               cap, n_dev, unit_first, units, nullptr, fgate, fdone, fepoch, nullptr);
         else
             hipLaunchKernelGGL((k_unmask_stream<false, false, true>), grid, blk, 0, s, (uint8_t *)base, N, frames,
-                               cap, n_dev, unit_first, units, nullptr, fgate, fdone, fepoch);
+                               cap, n_dev, unit_first, units, nullptr, fgate, fdone, fepoch, nullptr);
     } else {
         if (v == 1 || v == 3)
             hipLaunchKernelGGL((k_unmask_stream<true, true, true>), grid, blk, 0, s, (uint8_t *)base, N, frames, cap,
-                               n_dev, unit_first, units, utf8_ok, nullptr, nullptr, 0u);
+                               n_dev, unit_first, units, utf8_ok, nullptr, nullptr, 0u, seam);
         else
             hipLaunchKernelGGL((k_unmask_stream<true, true, false>), grid, blk, 0, s, (uint8_t *)base, N, frames, cap,
-                               n_dev, unit_first, units, utf8_ok, nullptr, nullptr, 0u);
+                               n_dev, unit_first, units, utf8_ok, nullptr, nullptr, 0u, seam);
         hipLaunchKernelGGL(k_utf8_seam, dim3((unsigned)((units + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
-                           (const uint8_t *)base, N, frames, cap, n_dev, unit_first, units, utf8_ok);
+                           (const uint8_t *)base, N, frames, cap, n_dev, unit_first, units, utf8_ok, seam);
     }
     return fws_hip_status(hipGetLastError());
 }

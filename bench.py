@@ -528,7 +528,7 @@ def stream_decode_extra(ctx, wire_c2, dev, args):
             ctxs = [c, c2]
             fr2 = [frames, torch.empty_like(frames)]
             rs2 = [res, torch.empty_like(res)]
-            sts = [torch.cuda.Stream(), torch.cuda.Stream()]
+            sts = [gpu.hip_stream(), gpu.hip_stream()]     # non-blocking HIP streams (the library's kind)
             def pstep(i):
                 rc, _, _, _ = gpu.decode_stream(ctxs[i % 2], bufs[i % nbuf], cap, frames=fr2[i % 2],
                                                 result=rs2[i % 2], stream=sts[i % 2])
@@ -547,7 +547,7 @@ def stream_decode_extra(ctx, wire_c2, dev, args):
             rec["two_in_flight"] = {"GiB_per_s": round(payload / tp / GIB, 1), "ms_per_batch": round(tp * 1e3, 4),
                                     "ms_per_batch_reps": [round(x * 1e3, 4) for x in reps],
                                     "roofline_frac": round((len(wire) + payload) / tp / 1e9 / HBM_PEAK_GBS, 4),
-                                    "path": "2 contexts x 2 streams, batches alternate (median of 3 repetitions)"}
+                                    "path": "2 contexts x 2 non-blocking HIP streams, batches alternate (median of 3 repetitions)"}
             c2.close()
         del bufs
         c.close()

@@ -21,6 +21,24 @@ def _ptr(t):
     return C.c_void_p(t.data_ptr())
 
 
+_hip = None
+
+
+def hip_stream():
+    """A HIP stream created with hipStreamNonBlocking, as the library's own
+    pipelines create theirs (rx_pipe.cpp, rx_session.cpp), wrapped for torch.
+    Two of these overlap two decodes every time; two torch pool streams did so
+    only in some runs (tools/stream_pair_probe.py: 165-171 vs 176-208 us per
+    C3 batch)."""
+    global _hip
+    if _hip is None:
+        _hip = C.CDLL("libamdhip64.so")
+    s = C.c_void_p()
+    if _hip.hipStreamCreateWithFlags(C.byref(s), C.c_uint(1)) != 0:
+        raise RuntimeError("hipStreamCreateWithFlags failed")
+    return torch.cuda.ExternalStream(s.value)
+
+
 def device_count():
     n = C.c_int(0)
     check("fws_gpu_device_count", lib().fws_gpu_device_count(C.byref(n)))

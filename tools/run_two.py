@@ -20,7 +20,7 @@ def main():
     n = len(descs)
     ctxs = [gpu.Ctx(0, max_frames=n + 64, max_stream_bytes=len(wire)) for _ in range(2)]
     ws = [torch.from_numpy(wire).to(dev) for _ in range(4)]
-    sts = [torch.cuda.Stream(), torch.cuda.Stream()]
+    sts = [gpu.hip_stream(), gpu.hip_stream()]
     fr = [torch.empty((n + 64) * gpu.FRAME_INFO.itemsize, dtype=torch.uint8, device=dev) for _ in range(2)]
     rs = [torch.empty(gpu.DECODE_RESULT.itemsize, dtype=torch.uint8, device=dev) for _ in range(2)]
 

@@ -537,7 +537,15 @@ def stream_decode_extra(ctx, wire_c2, dev, args):
                 pstep(i)
             torch.cuda.synchronize()
             reps = []
-            for _ in range(3):                              # median of 3 repetitions: one is noisy
+            for r in range(3):
+                # median of 3 repetitions, each on a fresh stream pair: whether two streams'
+                # kernels overlap depends on the hardware queues they land on, which HIP
+                # does not expose (one created pair in 4-7 serialises: tools/queue_pair_probe.py)
+                if r:
+                    sts[:] = [gpu.hip_stream(), gpu.hip_stream()]
+                    for i in range(2):
+                        pstep(i)
+                    torch.cuda.synchronize()
                 t0 = time.perf_counter()
                 for i in range(steps):
                     pstep(i)
@@ -547,7 +555,7 @@ def stream_decode_extra(ctx, wire_c2, dev, args):
             rec["two_in_flight"] = {"GiB_per_s": round(payload / tp / GIB, 1), "ms_per_batch": round(tp * 1e3, 4),
                                     "ms_per_batch_reps": [round(x * 1e3, 4) for x in reps],
                                     "roofline_frac": round((len(wire) + payload) / tp / 1e9 / HBM_PEAK_GBS, 4),
-                                    "path": "2 contexts x 2 non-blocking HIP streams, batches alternate (median of 3 repetitions)"}
+                                    "path": "2 contexts x 2 non-blocking HIP streams, batches alternate (median of 3 repetitions, a fresh stream pair each)"}
             c2.close()
         del bufs
         c.close()

@@ -87,7 +87,7 @@ enum FRegion : uint32_t {
     kRInbox = 7,     // inbox count (saturating past kFInCap: overflow)
     kFRegions = 8
 };
-constexpr uint32_t kBEx = 0, kBIn = kFExCap, kBFt = kFExCap + kFInCap;   // block offsets
+constexpr uint32_t kBEx = 0, kBFt = kFExCap + kFInCap;   // block offsets (kFInCap words after the exits: former inbox, unused)
 constexpr uint32_t kFBlk = kBFt + 4 * kFLive;                             // words per ST block
 constexpr uint32_t kFPubWords = kFRegions + kFBlk;
 constexpr uint64_t kV40 = (1ull << 40) - 1;

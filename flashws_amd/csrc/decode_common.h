@@ -24,9 +24,10 @@ enum Counter {
     kCntOverflow = 1,    // bit 0: k_scan's survivor spill capacity exceeded
     kCntDenseTiles = 2,  // tiles k_scan left to dense_tile() (diagnostic)
     kCntFrames = 3,      // frames emitted (device frame count, read by the unmask)
-    kCntRoot = 4,        // survivor index of the header at offset 0 (kNone if absent)
-    kCntTerm = 5,        // terminal code of the path
-    kCntLast = 6,        // last path node
+    kCntRoot = 4,        // k_merge (super tile 0) on the header at offset 0: 0 = not recorded (the
+                         //   big-ST paths), 1 = no survivor there, 2 + kind = this survivor's chain:
+    kCntRootSid = 5,     //   its slot id,
+    kCntRootTail = 6,    //   fws_node_res::tail and
     kCntSpill = 7,       // survivors spilled by dense tiles
     kCntEmitDoubling = 8, // super tiles whose k_emit marked the chain by pointer doubling (diagnostic)
     kCntFallback = 9,    // the resolve failed (workspace capacity): the result says so, k_emit skips
@@ -39,7 +40,8 @@ enum Counter {
     kCntFTicket = 15,    // k_fused's ordered super-tile ticket
     kCntFSurv = 16,      // survivors over all fused super tiles (diagnostic, result)
     kCntFTimeout = 17,   // fused super tiles that gave up a bounded wait (diagnostic)
-    kCntCount = 18
+    kCntRootCnt = 18,    //   ::cnt (ent is 0) -- resolve_path skips four dependent loads
+    kCntCount = 19
 };
 constexpr uint32_t kCntStride = 128;         // words per counter set (fws_decode_ws::cnt_base)
 // Spill runs: k_scan wavefront gw reserves from region gw % kSpillRegions (its

@@ -289,7 +289,7 @@ int fws_gpu_decode_stream(fws_gpu_ctx *ctx, void *dev_wire, uint64_t len, fws_fr
     const uint32_t *n_dev = ctx->dec.counters + kDecodeFramesCounter;
     if (dev_utf8_ok && (r = fws_ctx_ensure_seam(ctx, len))) return r;
     return fws_launch_unmask_stream((uint8_t *)dev_wire, len, dev_frames, cap, n_dev, ctx->plan.unit_first,
-                                    dev_utf8_ok, ctx->dec.counters, fws_fused_done(ctx), ctx->dec.fepoch,
+                                    dev_utf8_ok, ctx->dec.fused_ran ? ctx->dec.counters : nullptr, fws_fused_done(ctx), ctx->dec.fepoch,
                                     ctx->seam, s);
 }
 

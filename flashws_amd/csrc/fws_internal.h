@@ -133,6 +133,8 @@ struct fws_decode_ws {
     uint64_t fmax_st = 0;
     uint64_t *fpub = nullptr;              // [fmax_st * kFPubWords] (fused_kernels.hip layout)
     uint32_t fepoch = 0;                   // tag of the last k_fused call (1..2^24-1)
+    bool fused_ran = false;                // the last fws_launch_decode queued k_fused (the later
+                                           //   launches read its gate words only then)
     uint32_t fcus = 0;                     // CUs of the context's device (k_fused grid)
 };
 
@@ -215,5 +217,5 @@ int fws_launch_fused(fws_gpu_ctx *ctx, uint8_t *wire, uint64_t N, fws_frame_info
                      fws_decode_result *res, hipStream_t s);
 const uint64_t *fws_fused_done(const fws_gpu_ctx *ctx);   // done granules (fws_launch_unmask_stream)
 int fws_launch_merge(fws_gpu_ctx *ctx, const uint8_t *wire, uint64_t N, uint32_t n_tiles, fws_frame_info *frames,
-                     uint32_t cap, fws_decode_result *res, uint8_t *utf8_ok, bool force_big, uint32_t *zero_next,
+                     uint32_t cap, fws_decode_result *res, uint8_t *utf8_ok, bool force_big, bool fused, uint32_t *zero_next,
                      hipStream_t s);

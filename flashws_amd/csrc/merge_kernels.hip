@@ -159,6 +159,7 @@ struct MergeParams {
     uint64_t n_units;                                // ceil(N / kUnit), clamped to the plan's capacity
     uint32_t force_big;                              // test hook: every ST on the big-ST path
     uint32_t *zero_next;                             // the next call's counter set (k_emit zeroes it)
+    uint32_t fused;                                  // k_fused was queued first: read its gate (fused_done)
     uint32_t *bg_nx, *bg_wt, *bg_lref, *bg_ptr, *bg_sc, *bg_mark;   // big-ST scratch [max_nodes]
     uint64_t max_nodes;
 
@@ -494,7 +495,7 @@ __global__ __launch_bounds__(kMThreads) void k_merge(MergeParams P) {
     MP_START(30);
     MP_T0();
     MP_INIT();
-    if (fused_done(C)) return;                       // k_fused decoded the stream (k_link returns too)
+    if (P.fused && fused_done(C)) return;            // k_fused decoded the stream (k_link returns too)
     // the tail-target bitmap k_link sets
     for (uint64_t w = (uint64_t)s * kMThreads + tid; w < P.tail_cap / 32u + 1u; w += (uint64_t)gridDim.x * kMThreads)
         P.tmark[w] = 0u;
@@ -694,7 +695,14 @@ __global__ __launch_bounds__(kMThreads) void k_merge(MergeParams P) {
             const uint64_t x = exit_of(r[j]);
             P.tails[tb + L.lref[i]] = fws_tail_rec{x, nid[j], kTermDead, (uint32_t)(x >> P.st_shift), 0u};
         }
+        if (s == 0 && i == 0 && r[j].hdr_off == 0) {  // the root's chain, for resolve_path
+            C[kCntRootSid] = nid[j];
+            C[kCntRootTail] = ref;
+            C[kCntRootCnt] = cnt;
+            C[kCntRoot] = 2u + kind;
+        }
     }
+    if (s == 0 && tid == 0 && (n == 0 || r[0].hdr_off != 0)) C[kCntRoot] = 1u;
     __syncthreads();
     MP_MARK(4);
     MP_ADD(5, 1);
@@ -755,6 +763,11 @@ __device__ void resolve_path(const MergeParams &P, PathLds &G) {
     uint32_t *const C = P.counters;
     const uint32_t tid = threadIdx.x;
     MP_INIT();
+    // k_merge's record of the root (an earlier launch), loaded beside the flags below
+    const uint32_t root_state = tid == 0 ? C[kCntRoot] : 0u;
+    const uint32_t root_sid = tid == 0 ? C[kCntRootSid] : 0u;
+    const uint32_t root_tail = tid == 0 ? C[kCntRootTail] : 0u;
+    const uint32_t root_cnt = tid == 0 ? C[kCntRootCnt] : 0u;
     if (ld_acq(&C[kCntFallback]) || (ld_acq(&C[kCntOverflow]) & 1u)) {
         fail_capacity(P);                            // k_scan's spill or the tail list overflowed
         return;
@@ -765,13 +778,16 @@ __device__ void resolve_path(const MergeParams &P, PathLds &G) {
     if (tid == 0) {
         uint32_t root = kNone, rt = kNone;
         fws_node_res rr{0, 0, 0, 0};
-        if (P.n_tiles && P.tile_count[0]) {
+        if (root_state >= 2u) {
+            root = root_sid;
+            rr = fws_node_res{root_tail, root_cnt, 0u, root_state - 2u};
+        } else if (root_state == 0u && P.n_tiles && P.tile_count[0]) {
             const uint32_t id0 = P.sid(0, P.tile_spill[0], 0);
             if (P.rec(id0)->hdr_off == 0) root = id0;
         }
         G.end_set = 0;
         if (root != kNone) {
-            rr = P.nres[root];
+            if (root_state == 0u) rr = P.nres[root];
             if (res_kind(rr) == kKindExit) rt = rr.tail;
             else {                                   // the root's chain ends in ST 0
                 G.end_rec = P.tail_rec(0, rr);
@@ -1017,7 +1033,7 @@ __global__ __launch_bounds__(kMThreads) void k_link(MergeParams P) {
     MP_START(29);
     MP_T0();
     MP_INIT();
-    if (fused_done(C)) return;
+    if (P.fused && fused_done(C)) return;
     const uint32_t M = C[kCntTails];
     const uint32_t x = blockIdx.x * kMThreads + tid;
     if (x < M && !C[kCntFallback]) {
@@ -1257,7 +1273,7 @@ __global__ __launch_bounds__(kMThreads) void k_emit(MergeParams P) {
     MP_T0();
     MP_INIT();
     if (s == 0 && tid < kCntStride) P.zero_next[tid] = 0u;   // the next call's counter set
-    if (s >= P.n_st || fused_done(C)) return;
+    if (s >= P.n_st || (P.fused && fused_done(C))) return;
     const uint32_t fb = C[kCntFallback], e = P.st_entry[s], fbase = P.st_fbase[s], n = P.st_n[s];
     const uint32_t lim = C[kCntFrames];
     if (fb || e == kNone || fbase >= lim) return;
@@ -1433,7 +1449,7 @@ uint32_t fws_merge_tail_cap(uint64_t n_tiles) {
 }
 
 int fws_launch_merge(fws_gpu_ctx *ctx, const uint8_t *wire, uint64_t N, uint32_t n_tiles, fws_frame_info *frames,
-                     uint32_t cap, fws_decode_result *res, uint8_t *utf8_ok, bool force_big, uint32_t *zero_next,
+                     uint32_t cap, fws_decode_result *res, uint8_t *utf8_ok, bool force_big, bool fused, uint32_t *zero_next,
                      hipStream_t s) {
     fws_decode_ws &d = ctx->dec;
     MergeParams P;
@@ -1471,6 +1487,7 @@ int fws_launch_merge(fws_gpu_ctx *ctx, const uint8_t *wire, uint64_t N, uint32_t
     P.n_units = units < ctx->plan.unit_cap ? units : ctx->plan.unit_cap;
     P.force_big = force_big ? 1u : 0u;
     P.zero_next = zero_next;
+    P.fused = fused ? 1u : 0u;
     P.bg_nx = d.bg_nx;
     P.bg_wt = d.bg_wt;
     P.bg_lref = d.bg_lref;

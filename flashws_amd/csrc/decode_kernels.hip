@@ -13,15 +13,17 @@
 //                prefetch in registers). Per tile:
 //                 - candidate bits: the two-byte test (RSV clear, valid opcode,
 //                   MASK set; w_socket.h:451-515) passes ~2.3 % of payload bytes;
-//                 - first hop: a candidate with a 7-bit length whose next
+//                 - nodes, one per lane: every candidate when there are <= 64
+//                   (the common case, ~48 on random payload); else first the
+//                   first hop -- a candidate with a 7-bit length whose next
 //                   header offset falls inside the tile on a non-candidate byte
-//                   is dead (97-98 % of them); the rest are "live";
-//                 - live nodes, one per lane (<= 64): full parse (ParseFrameHdr
-//                   semantics, w_socket.h:435-524), next live node, pointer
-//                   jumping in registers (ds_bpermute) to the chain's leaf (the
-//                   last header before the tile end) or DEAD;
-//                 - survivors by ballot, records stored from the lanes (8 slots
-//                   per tile, a spill run past that).
+//                   is dead (97-98 % of them) -- and the rest ("live", <= 64);
+//                 - per node: full parse (ParseFrameHdr semantics,
+//                   w_socket.h:435-524), next node, pointer jumping in
+//                   registers (ds_bpermute) to the chain's leaf (the last
+//                   header before the tile end) or DEAD;
+//                 - survivors by ballot, ranked in offset order, records stored
+//                   from the lanes (8 slots per tile, a spill run past that).
 //                A tile with more than 256 candidates or 64 live nodes (frames
 //                under ~32 B) is marked in tile_count (kDenseTile); k_merge
 //                scans it with dense_tile() (scan_common.h: every candidate a
@@ -53,8 +55,9 @@ struct ScanLds {
     uint8_t bytes[kTile + kHaloX];
     uint32_t cm[64];                         // candidate bits of lane L's 32 offsets
     uint32_t lm[64];                         // live bits of lane L's 32 offsets
-    uint32_t lpre[64];                       // live index of lane L's first live offset
-    uint16_t pos[kCandCap];                  // candidate offsets, in offset order
+    uint32_t lpre[64];                       // node index of lane L's first live offset (first
+                                             //   candidate when every candidate is a node)
+    uint16_t pos[kCandCap];                  // candidate offsets (lane-major; cand_bits32p's order in a lane)
     uint16_t lpos[kLiveCap];                 // live offsets, in offset order
 };
 static_assert(sizeof(ScanLds) % 16 == 0, "16-B aligned per-wave areas");
@@ -168,45 +171,55 @@ __global__ __launch_bounds__(kScanThreads) __attribute__((amdgpu_waves_per_eu(8,
                         W.pos[k++] = (uint16_t)(L32 + cand_off(b));
                     }
                 }
+                // up to 64 candidates (the common case): every candidate is a node, one
+                // per lane, numbered as listed (lane-major, permuted bit order within a
+                // lane); else the first hop below prunes them to the live nodes first
+                const bool direct = nc <= 64u;                 // wave-uniform
+                if (direct) W.lpre[lane] = cp;
                 wave_sync();
-                // first hop: a candidate whose next header offset (7-bit length form,
-                // header complete) is inside the tile and fails the two-byte test is dead
-                uint32_t M = 0;
-                for (uint32_t k0 = 0; k0 < nc; k0 += 64u) {
-                    const uint32_t k = k0 + lane;
-                    bool live = false;
-                    uint32_t p = 0;
-                    if (k < nc) {
-                        p = W.pos[k];
-                        live = true;
-                        const uint32_t len7 = B[p + 1u] & 127u;
-                        if (len7 < 126u && t0 + p + 6u <= N) {
-                            const uint32_t nx = p + 6u + len7;
-                            if (nx < kTile && t0 + nx < N) live = (W.cm[nx >> 5] >> cand_pbit(nx & 31u)) & 1u;
+                uint32_t M = nc;
+                if (!direct) {
+                    // first hop: a candidate whose next header offset (7-bit length form,
+                    // header complete) is inside the tile and fails the two-byte test is dead
+                    M = 0;
+                    for (uint32_t k0 = 0; k0 < nc; k0 += 64u) {
+                        const uint32_t k = k0 + lane;
+                        bool live = false;
+                        uint32_t p = 0;
+                        if (k < nc) {
+                            p = W.pos[k];
+                            live = true;
+                            const uint32_t len7 = B[p + 1u] & 127u;
+                            if (len7 < 126u && t0 + p + 6u <= N) {
+                                const uint32_t nx = p + 6u + len7;
+                                if (nx < kTile && t0 + nx < N) live = (W.cm[nx >> 5] >> cand_pbit(nx & 31u)) & 1u;
+                            }
                         }
+                        if (live) atomicOr(&W.lm[p >> 5], 1u << (p & 31u));
+                        M += (uint32_t)__popcll(__ballot(live));
                     }
-                    if (live) atomicOr(&W.lm[p >> 5], 1u << (p & 31u));
-                    M += (uint32_t)__popcll(__ballot(live));
+                    dense = M > kLiveCap;
+                    if (!dense) {
+                        // live nodes in offset order: lane L lists its own (in-order bits)
+                        wave_sync();
+                        uint32_t mt;
+                        uint32_t lbits = W.lm[lane];
+                        uint32_t li = wave_excl_scan_dpp((uint32_t)__popc(lbits), &mt);
+                        W.lpre[lane] = li;
+                        while (lbits) {
+                            const uint32_t b = (uint32_t)__ffs(lbits) - 1u;
+                            lbits &= lbits - 1u;
+                            W.lpos[li++] = (uint16_t)(L32 + b);
+                        }
+                        wave_sync();
+                    }
                 }
-                dense = M > kLiveCap;
                 SCAN_MARK(2);
                 SCAN_COUNT(6, M);
                 if (!dense) {
-                    // live nodes in offset order: lane L lists its own (in-order bits)
-                    wave_sync();
-                    uint32_t mt;
-                    uint32_t lbits = W.lm[lane];
-                    uint32_t li = wave_excl_scan_dpp((uint32_t)__popc(lbits), &mt);
-                    W.lpre[lane] = li;
-                    while (lbits) {
-                        const uint32_t b = (uint32_t)__ffs(lbits) - 1u;
-                        lbits &= lbits - 1u;
-                        W.lpos[li++] = (uint16_t)(L32 + b);
-                    }
-                    wave_sync();
-                    // live node `lane`: full parse, next live node (lane index), leaf or dead
+                    // node `lane`: full parse, next node (lane index), leaf or dead
                     const bool act = lane < M;
-                    const uint32_t p = act ? W.lpos[lane] : 0u;
+                    const uint32_t p = act ? (direct ? W.pos[lane] : W.lpos[lane]) : 0u;
                     const uint32_t a = p & ~15u;
                     const u32x4 wl = *reinterpret_cast<const u32x4 *>(B + a);
                     const u32x4 wh = *reinterpret_cast<const u32x4 *>(B + a + 16u);
@@ -228,8 +241,10 @@ __global__ __launch_bounds__(kScanThreads) __attribute__((amdgpu_waves_per_eu(8,
                                 if ((e0 & 0x77u) > 2u || !(e1 & 0x80u)) ptr = kDeadLane;
                             }
                         } else {
+                            // the node at the exit: a candidate (direct) or live bit, ranked
                             const uint32_t nx = (uint32_t)(nxo - t0);
-                            const uint32_t m = W.lm[nx >> 5], bit = nx & 31u;
+                            const uint32_t m = direct ? W.cm[nx >> 5] : W.lm[nx >> 5];
+                            const uint32_t bit = direct ? cand_pbit(nx & 31u) : nx & 31u;
                             if ((m >> bit) & 1u) ptr = W.lpre[nx >> 5] + (uint32_t)__popc(m & ((1u << bit) - 1u));
                         }
                     }
@@ -243,11 +258,20 @@ __global__ __launch_bounds__(kScanThreads) __attribute__((amdgpu_waves_per_eu(8,
                         SCAN_COUNT(7, 1u);
                         if (!__any(ch)) break;
                     }
-                    // survivors (offset order = lane order) and their leaves' ranks
+                    // survivors and their ranks in offset order (lane order for live
+                    // nodes; direct nodes are permuted within a 32-byte block: count)
                     const bool surv = act && ptr < 64u;
                     const uint64_t sm = __ballot(surv);
                     ns = (uint32_t)__popcll(sm);
-                    srank = mbcnt64(sm);
+                    if (direct) {
+                        srank = 0;
+                        for (uint64_t mm = sm; mm; mm &= mm - 1u) {
+                            const uint32_t pq = (uint32_t)__builtin_amdgcn_readlane((int)p, (int)__builtin_ctzll(mm));
+                            srank += pq < p ? 1u : 0u;
+                        }
+                    } else {
+                        srank = mbcnt64(sm);
+                    }
                     if (ns > kSlots) {
                         // more survivors than slots (frames under ~250 B): a spill run
                         if (lane == 0) {

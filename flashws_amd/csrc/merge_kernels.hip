@@ -96,7 +96,12 @@ __device__ unsigned long long g_merge_trace[kTraceWg * 32];
     } while (0)
 #define MP_ADD(k, v) do { } while (0)          /* same-address atomics would queue behind each other */
 #define MP_SPAN(k0, k1) do { } while (0)
+#define MP_VAL(k, v)                                                                \
+    do {                                                                            \
+        if (threadIdx.x == 0) g_merge_trace[(blockIdx.x % kTraceWg) * 32 + (k)] = (v); \
+    } while (0)
 #else
+#define MP_VAL(k, v) do { } while (0)
 #define MP_START(slot) do { } while (0)
 #define MP_T0() do { } while (0)
 #define MP_INIT() do { } while (0)
@@ -554,6 +559,10 @@ __global__ __launch_bounds__(kMThreads) void k_merge(MergeParams P) {
     if (tid == 0) L.n_tail = 0;
     __syncthreads();
     MP_MARK(0);
+    MP_VAL(22, n);
+#ifdef FWS_SCAN_PROF
+    { const int nsp = __syncthreads_count(tid < P.st_tiles && sp != kNone); MP_VAL(23, (uint64_t)nsp); }
+#endif
     if (P.big(n)) {
         if (tid == 0) atomicAdd(&C[kCntBig], 1u);
         if (n <= kMidCap && !P.force_big) merge_mid(P, L, s, n);
@@ -575,7 +584,9 @@ __global__ __launch_bounds__(kMThreads) void k_merge(MergeParams P) {
 #pragma unroll
         for (uint32_t j = 0; j < kPer; ++j) {
             const uint32_t i = i0 + j;
-            while (tl + 1 < kStTiles && L.tbase[tl + 1] <= i) ++tl;
+            // (i < n: past the last survivor every later tile has tbase n, and a
+            // partial last super tile has up to 255 of them to walk)
+            while (i < n && tl + 1 < kStTiles && L.tbase[tl + 1] <= i) ++tl;
             nid[j] = i < n ? P.sid(t0 + tl, L.tsp[tl], i - L.tbase[tl]) : 0u;
         }
 #pragma unroll

@@ -68,6 +68,14 @@ def main():
             r[f"k_merge_{lab}"] = stats(m[:, k] - prev)
             prev = m[:, k]
         r["k_merge_end_us"] = stats(m[:, 4] - t0)
+        end = m[:, 4] - t0
+        slow = np.argsort(end)[-5:][::-1]
+        r["k_merge_rows"] = {str(int(i)): [round(float(m[i, k] - m[i, 30]), 2) for k in (0, 1, 2, 3, 4)]
+                             + [int(m[i, 22] * 100), int(m[i, 23] * 100)]
+                             for i in (0, 1, n_st // 2, n_st - 2, n_st - 1)}
+        r["k_merge_slowest"] = [{"st": int(i), "end_us": round(float(end[i]), 2),
+                                 "records_us": round(float(m[i, 1] - m[i, 0]), 2),
+                                 "counts_us": round(float(m[i, 0] - m[i, 30]), 2)} for i in slow]
         big = m[:, 21] > m[:, 30]
         if big.any():
             prev = m[big, 0]

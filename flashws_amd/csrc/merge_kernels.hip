@@ -1045,11 +1045,12 @@ __global__ __launch_bounds__(kMThreads) void k_link(MergeParams P) {
     MP_T0();
     MP_INIT();
     if (P.fused && fused_done(C)) return;
-    const uint32_t M = C[kCntTails];
     const uint32_t x = blockIdx.x * kMThreads + tid;
+    const uint64_t tx = P.tails[x < P.tail_cap ? x : 0u].exit;   // with the counters (read past M: unused)
+    const uint32_t M = C[kCntTails];
     if (x < M && !C[kCntFallback]) {
         fws_tail_rec &tr = P.tails[x];
-        const uint32_t w = P.find_node(tr.exit);
+        const uint32_t w = P.find_node(tx);
         uint32_t g = kGTerm | kKindDead;
         if (w != kTermDead) {
             __hip_atomic_store(&tr.w, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1293,6 +1294,8 @@ __global__ __launch_bounds__(kMThreads) void k_emit(MergeParams P) {
         else emit_big(P, s, n, e, fbase, lim);
         return;
     }
+    // (loading all kStCap rows with the words above, before n is known, measured
+    // 9.4 -> 13.6 us on C3: 16 MB of rows instead of ~1 MB)
     const fws_st_node *const tab = P.st_nodes + (uint64_t)s * kStCap;
     const uint32_t i0 = kPer * tid;
     fws_st_node nd[kPer];

@@ -43,13 +43,15 @@ enum Counter {
     kCntRootCnt = 18,    //   ::cnt (ent is 0) -- resolve_path skips four dependent loads
     kCntCount = 19
 };
-constexpr uint32_t kCntStride = 128;         // words per counter set (fws_decode_ws::cnt_base)
 // Spill runs: k_scan wavefront gw reserves from region gw % kSpillRegions (its
-// own counter at kCntRegion0 + region: no single hot atomic when every tile
-// spills), then from the shared second half (kCntSpill; dense_tile uses only that)
+// own counter at kCntRegion0 + region * kRegionStride, one 128-B line each: no
+// hot atomic or hot line when every tile spills), then from the shared second
+// half (kCntSpill; dense_tile uses only that)
 constexpr uint32_t kSpillRegions = 64;
 constexpr uint32_t kCntRegion0 = 64;
-static_assert(kCntRegion0 >= kCntCount && kCntRegion0 + kSpillRegions <= kCntStride, "counter layout");
+constexpr uint32_t kRegionStride = 32;
+constexpr uint32_t kCntStride = kCntRegion0 + kSpillRegions * kRegionStride;   // words per counter set
+static_assert(kCntRegion0 >= kCntCount, "counter layout");
 // [0, half): kSpillRegions regions of region_size; [half, s_cap): shared
 __device__ __forceinline__ uint32_t spill_half(uint32_t s_cap) { return s_cap / 2u; }
 __device__ __forceinline__ uint32_t spill_region_size(uint32_t s_cap) { return spill_half(s_cap) / kSpillRegions; }

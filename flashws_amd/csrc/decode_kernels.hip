@@ -276,7 +276,7 @@ __global__ __launch_bounds__(kScanThreads) __attribute__((amdgpu_waves_per_eu(8,
                         // more survivors than slots (frames under ~250 B): a spill run
                         if (lane == 0) {
                             const uint32_t rs = spill_region_size(s_cap), rg = gw % kSpillRegions;
-                            const uint32_t off = atomicAdd(&counters[kCntRegion0 + rg], ns);
+                            const uint32_t off = atomicAdd(&counters[kCntRegion0 + rg * kRegionStride], ns);
                             spill = (off <= rs && rs - off >= ns) ? rg * rs + off : spill_shared(counters, s_cap, ns);
                         }
                         spill = __shfl(spill, 0, 64);

@@ -1284,7 +1284,8 @@ __global__ __launch_bounds__(kMThreads) void k_emit(MergeParams P) {
     MP_START(28);
     MP_T0();
     MP_INIT();
-    if (s == 0 && tid < kCntStride) P.zero_next[tid] = 0u;   // the next call's counter set
+    if (s == 0)                                      // the next call's counter set
+        for (uint32_t w = tid; w < kCntStride; w += kMThreads) P.zero_next[w] = 0u;
     if (s >= P.n_st || (P.fused && fused_done(C))) return;
     const uint32_t fb = C[kCntFallback], e = P.st_entry[s], fbase = P.st_fbase[s], n = P.st_n[s];
     const uint32_t lim = C[kCntFrames];

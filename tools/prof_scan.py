@@ -28,7 +28,8 @@ def main():
     prof.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
     prof.restype = C.c_int
     out = {}
-    for name, mk in (("C2", gpu.config_c2), ("C3", gpu.config_c3)):
+    for name, mk in (("C2", gpu.config_c2), ("C3", gpu.config_c3),
+                     ("C5_256M", lambda: gpu.config_c5(n_frames=16384))):
         wire, descs, _ = mk()
         n = len(descs)
         ctx = gpu.Ctx(0, max_frames=n + 16, max_stream_bytes=len(wire))

@@ -2,7 +2,7 @@
 """Runs fws_gpu_decode_stream on one BASELINE config a few times (for
 rocprofv3 --pmc / --kernel-trace runs of the decode kernels).
 
-usage: python tools/run_decode.py [c2|c3|dense] [reps] [stream variant]"""
+usage: python tools/run_decode.py [c2|c3|dense|c5_256m] [reps] [stream variant]"""
 import os
 import sys
 
@@ -18,7 +18,8 @@ def main():
     if len(sys.argv) > 3:
         _lib.lib().fws_internal_set_stream_variant(int(sys.argv[3]))
     mk = {"c2": gpu.config_c2, "c3": gpu.config_c3,
-          "dense": lambda: gpu.config_c2(n_frames=200_000, payload=64)}[which]
+          "dense": lambda: gpu.config_c2(n_frames=200_000, payload=64),
+          "c5_256m": lambda: gpu.config_c5(n_frames=16384)}[which]
     wire, descs, _ = mk()
     dev = torch.device("cuda:0")
     ctx = gpu.Ctx(0, max_frames=len(descs) + 64, max_stream_bytes=len(wire))

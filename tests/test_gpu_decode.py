@@ -300,6 +300,27 @@ def test_candidate_density(ctx, cuda, pattern):
     check(ctx, cuda, b"".join(parts))
 
 
+@pytest.mark.parametrize("seed", range(2))
+def test_candidate_counts_at_node_limits(ctx, cuda, seed):
+    """2 KiB regions with 56-72, 120-136 and 248-264 two-byte candidates
+    (0x81 0x80: an empty masked TEXT header) on filler that never passes the
+    test: tiles on both sides of k_scan's direct-node limit (64 candidates,
+    every candidate a node), of the live-node limit and of the dense-tile
+    limit (256). Candidates 6 bytes apart chain into runs of false headers."""
+    rng = np.random.default_rng(500 + seed)
+    parts = []
+    for lo in (56, 120, 248):
+        pay = bytearray(b"\x10" * (2048 * 17))
+        for r in range(17):
+            k = lo + r
+            for sl in rng.choice(682, size=k, replace=False):
+                q = 2048 * r + 3 * int(sl)
+                pay[q:q + 2] = b"\x81\x80"
+        parts.append(frame(2, bytes(pay), key=0))
+        parts.append(frame(2, rng.integers(0, 256, int(rng.integers(0, 3000)), dtype=np.uint8).tobytes()))
+    check(ctx, cuda, b"".join(parts))
+
+
 def test_utf8_flags_c5_shape(ctx, cuda):
     wire, descs, ok = gpu.config_c5(seed=5, n_frames=512, payload=16384, invalid_permille=100)
     dev = torch.from_numpy(wire).to(cuda)

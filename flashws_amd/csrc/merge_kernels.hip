@@ -259,8 +259,8 @@ struct MergeLds {
             };
             uint16_t nx[kStCap];
             uint8_t wt[kStCap];                      // 1: a frame; 0: incomplete header
-            uint16_t ptr[2][kStCap];                 // Wyllie pointer (tails point to themselves)
-            uint16_t sc[2][kStCap];                  // frames from i up to ptr (exclusive)
+            uint32_t pw[kStCap];                     // Wyllie pointer (tails point to themselves) |
+                                                     //   frames from i up to it (exclusive) << 16
         };
         ScanWaveLds dw[kDenseWaves];                 // first: the tiles k_scan left (dense_tile)
         uint32_t bw[kMidCap];                        // mid path: ptr | frames << 16 | kind << 29 | frame bit << 31
@@ -643,8 +643,7 @@ __global__ __launch_bounds__(kMThreads) void k_merge(MergeParams P) {
         vv[j] = v;
         L.nx[i] = v;
         const bool tail = v >= kNxInc;
-        L.ptr[0][i] = tail ? (uint16_t)i : v;
-        L.sc[0][i] = tail ? 0 : L.wt[i];
+        L.pw[i] = tail ? i : (uint32_t)v | (uint32_t)L.wt[i] << 16;
     }
     __syncthreads();                                 // off[] dead: lref[] reuses it
 #pragma unroll
@@ -662,23 +661,20 @@ __global__ __launch_bounds__(kMThreads) void k_merge(MergeParams P) {
         }
         L.tail_base = base;
     }
-    // pointer jumping: every survivor -> its chain's tail, with frame counts
-    int cur = 0;
+    // pointer jumping in place: every survivor -> its chain's tail, with frame
+    // counts (pointer and count move together in one word, so a read of a word
+    // another thread is rewriting sees either pair, both consistent)
     for (;;) {
         int changed = 0;
         for (uint32_t i = tid; i < n; i += kMThreads) {
-            const uint16_t p = L.ptr[cur][i];
-            const uint16_t q = L.ptr[cur][p];
-            if (p != q) {
-                L.ptr[cur ^ 1][i] = q;
-                L.sc[cur ^ 1][i] = (uint16_t)(L.sc[cur][i] + L.sc[cur][p]);
+            const uint32_t w = L.pw[i];
+            const uint32_t p = w & 0xFFFFu;
+            const uint32_t wp = L.pw[p];
+            if ((wp & 0xFFFFu) != p) {
+                L.pw[i] = (wp & 0xFFFFu) | (((w >> 16) + (wp >> 16)) << 16);
                 changed = 1;
-            } else {
-                L.ptr[cur ^ 1][i] = p;
-                L.sc[cur ^ 1][i] = L.sc[cur][i];
             }
         }
-        cur ^= 1;
         if (!__syncthreads_or(changed)) break;
     }
     MP_MARK(3);
@@ -688,9 +684,9 @@ __global__ __launch_bounds__(kMThreads) void k_merge(MergeParams P) {
     for (uint32_t j = 0; j < kPer; ++j) {
         const uint32_t i = i0 + j;
         if (i >= n) continue;
-        const uint32_t t = L.ptr[cur][i];
+        const uint32_t t = L.pw[i] & 0xFFFFu;
         const uint32_t kind = kind_of(L.nx[t]);
-        const uint32_t cnt = L.sc[cur][i] + L.wt[t];
+        const uint32_t cnt = (L.pw[i] >> 16) + L.wt[t];
         const uint32_t ref = kind == kKindExit ? tb + L.lref[t] : t;
         P.nres[nid[j]] = fws_node_res{ref, cnt, i, kind};
         fws_st_node nd;

@@ -62,6 +62,9 @@ def parse():
     ap.add_argument("--c5", action="store_true", help="with --extra: the 4 GiB C5 UTF-8 config (default at N=1)")
     ap.add_argument("--no-extra", action="store_true", help="headline line only")
     ap.add_argument("--no-c5-split", action="store_true", help="N > 1: skip the C5 batch-split config")
+    ap.add_argument("--share-device", action="store_true",
+                    help="N > 1 validation on one GPU: every rank on device 0, gloo process group "
+                         "(exercises the N-rank path on real HIP; not a scaling measurement)")
     ap.add_argument("--launcher-selftest", action="store_true",
                     help="CPU only (gloo): exercise the N-rank launch, barrier and max-over-ranks timing on a "
                          "host XOR of each rank's shard; prints a self-test line, not the metric")
@@ -80,10 +83,9 @@ def launch_ranks(args):
     import socket
     import subprocess
     import sys
-    if not args.launcher_selftest:
-        have = torch.cuda.device_count()
-        if have < args.gpus:
-            raise SystemExit(f"bench.py --gpus {args.gpus}: only {have} GPU(s) visible")
+    have = kfd_gpu_count()
+    if not args.launcher_selftest and not args.share_device and have is not None and have < args.gpus:
+        raise SystemExit(f"bench.py --gpus {args.gpus}: only {have} GPU(s) visible")
     with socket.socket() as sk:
         sk.bind(("127.0.0.1", 0))
         port = sk.getsockname()[1]
@@ -91,7 +93,37 @@ def launch_ranks(args):
            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env["FWS_BENCH_KFD_GPUS"] = "none" if have is None else str(have)
     return subprocess.call(cmd, env=env)
+
+
+def kfd_gpu_count(topology="/sys/class/kfd/kfd/topology/nodes", env=None):
+    """GPUs this process could use, counted without initialising HIP (the
+    launcher forks torch.distributed.run afterwards; torch.cuda.device_count()
+    may fall back to hipGetDeviceCount): KFD topology nodes with a non-zero
+    gfx_target_version, narrowed by ROCR_VISIBLE_DEVICES / HIP_VISIBLE_DEVICES /
+    CUDA_VISIBLE_DEVICES when set. None when the topology is not readable."""
+    env = os.environ if env is None else env
+    try:
+        nodes = sorted(os.listdir(topology), key=lambda x: int(x) if x.isdigit() else 1 << 30)
+    except OSError:
+        return None
+    n = 0
+    for d in nodes:
+        try:
+            with open(os.path.join(topology, d, "properties")) as f:
+                for line in f:
+                    k, _, v = line.partition(" ")
+                    if k == "gfx_target_version" and int(v.strip() or 0) != 0:
+                        n += 1
+                        break
+        except (OSError, ValueError):
+            continue
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = env.get(var)
+        if v is not None:
+            n = min(n, len([x for x in v.split(",") if x.strip() != ""]))
+    return n
 
 
 def dist_env():
@@ -99,10 +131,17 @@ def dist_env():
             int(os.environ.get("LOCAL_RANK", "0")))
 
 
-def setup_dist(world, local):
+def setup_dist(world, local, share_device=False):
     """One process per GPU; the process group only carries the barriers and the
-    max-over-ranks reduction of the step time (outside the timed region)."""
-    if world > 1:
+    max-over-ranks reduction of the step time (outside the timed region).
+    share_device (validation on a one-GPU box): every rank on device 0 and a
+    gloo group -- RCCL will not put two ranks on one GPU -- so the N-rank path
+    (shard seeds, C5 split, max over ranks) runs on real HIP; its times are
+    contended and not a scaling claim."""
+    if world > 1 and share_device:
+        torch.cuda.set_device(0)
+        dist.init_process_group(backend="gloo")
+    elif world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
     else:
@@ -250,17 +289,33 @@ def cpu_baseline(wire, descs, seconds):
             "one_core": one, "dense_64B_one_core": dense}
 
 
+def source_sha16(rel="flashws_amd/csrc/unmask_kernels.hip"):
+    """sha256 (16 hex) of the headline kernel's source file."""
+    import hashlib
+    try:
+        with open(os.path.join(ROOT, rel), "rb") as f:
+            return hashlib.sha256(f.read()).hexdigest()[:16]
+    except OSError:
+        return None
+
+
 def pmc_traffic():
-    """HBM bytes per k_unmask launch from the committed rocprofv3 PMC summary
-    (profiles/pmc_unmask.json, made by tools/pmc_summary.py), or None."""
+    """HBM bytes per k_unmask_sorted launch from the committed rocprofv3 PMC
+    summary (profiles/pmc_unmask.json, made by tools/pmc_summary.py) and where
+    it came from. The bytes count only if the summary was measured on the
+    kernel source this tree builds (its recorded sha of unmask_kernels.hip);
+    a stale summary gives traffic None."""
     p = os.path.join(ROOT, "profiles", "pmc_unmask.json")
     try:
         with open(p) as f:
             rec = json.load(f)
-        # only a summary of the kernel this bench times counts
-        return rec.get("hbm_bytes_per_launch") if rec.get("kernel") == "k_unmask_sorted" else None
     except (OSError, ValueError):
-        return None
+        return None, {"file": "profiles/pmc_unmask.json", "status": "absent"}
+    src = {"file": "profiles/pmc_unmask.json", "commit": rec.get("commit"),
+           "kernel_source_sha16": rec.get("kernel_source_sha16"), "measured": rec.get("measured")}
+    current = rec.get("kernel") == "k_unmask_sorted" and rec.get("kernel_source_sha16") == source_sha16()
+    src["status"] = "current" if current else "stale (kernel source changed since the PMC passes)"
+    return (rec.get("hbm_bytes_per_launch") if current else None), src
 
 
 def launcher_selftest(args, world, rank):
@@ -290,7 +345,8 @@ def launcher_selftest(args, world, rank):
         digs = [dig]
     line = {"selftest": True, "n_gpus": world, "rank": rank, "steps": args.steps, "step_s": step,
             "own_step_s": own, "value": aggregate_gib_s(world, payload, step), "payload_bytes_per_rank": payload,
-            "shard_digests": [int(d.item()) for d in digs]}
+            "shard_digests": [int(d.item()) for d in digs],
+            "launcher_kfd_gpus": os.environ.get("FWS_BENCH_KFD_GPUS")}
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
@@ -312,8 +368,9 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(wire, descs, args.cpu_seconds)
 
-    setup_dist(world, local)
-    dev = torch.device("cuda", torch.cuda.current_device())
+    setup_dist(world, local, args.share_device)
+    local = torch.cuda.current_device()
+    dev = torch.device("cuda", local)
     n = len(descs)
     payload_bytes = int(descs["payload_len"].sum())
     wire_bytes = len(wire)
@@ -331,33 +388,31 @@ def main():
         gpu.unmask_sorted(ctx, bufs[i % args.nbuf], dd, n)
     torch.cuda.synchronize()
 
-    # ---- timed region: K whole steps
+    # ---- timed region: K whole steps. The dominant kernel (k_unmask_sorted, the
+    # step's only launch) is timed by HIP events on its stream (the current
+    # stream, where the ABI call launches it) around the same K launches, inside
+    # the wall-clock bracket: the per-launch kernel time cannot exceed the step.
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        gpu.unmask_sorted(ctx, bufs[i % args.nbuf], dd, n)
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    barrier(world)
-    step_s = max_over_ranks(world, (t1 - t0) / args.steps)
-
-    # ---- dominant kernel alone (k_unmask_sorted, the step's only launch), HIP
-    # events on its stream (the current stream, where the ABI call launches it)
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    torch.cuda.synchronize()
     ev0.record(stream)
     for i in range(args.steps):
         gpu.unmask_sorted(ctx, bufs[i % args.nbuf], dd, n)
     ev1.record(stream)
     torch.cuda.synchronize()
-    kern_s = ev0.elapsed_time(ev1) / 1e3 / args.steps
+    t1 = time.perf_counter()
+    barrier(world)
+    own_s = (t1 - t0) / args.steps
+    step_s = max_over_ranks(world, own_s)
+    kern_s = min(ev0.elapsed_time(ev1) / 1e3 / args.steps, own_s)
 
     extra = {}
     if not args.no_batch_extra and world == 1:
         extra["C2_unmask_batch_any_order"] = batch_extra(ctx, bufs, dd, n, payload_bytes, args, stream)
     if args.extra:
         extra.update(stream_decode_extra(ctx, wire, dev, args)["extra"])
+        extra["C1_echo"] = c1_echo_extra(local)
     del bufs
     if world > 1 and not args.no_c5_split:
         extra["C5_batch_split"] = c5_split(args, world, rank, local, dev)
@@ -365,7 +420,7 @@ def main():
 
     value = aggregate_gib_s(world, payload_bytes, step_s)
     achieved = alg_bytes / kern_s / 1e9
-    traffic = pmc_traffic()
+    traffic, traffic_src = pmc_traffic()
     out = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -387,8 +442,9 @@ def main():
                    "parallelism": f"batch split x{world} (no collective)"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": traffic,
+                     "traffic": traffic, "traffic_source": traffic_src,
                      "kernel": "k_unmask_sorted", "kernel_us": round(kern_s * 1e6, 2),
+                     "kernel_timing": "HIP events on the launch stream around the K timed steps",
                      "alg_bytes_per_launch": alg_bytes},
     }
     out.update(extra)
@@ -465,6 +521,76 @@ def c5_split(args, world, rank, local, dev):
             "flags_match_generator_all_ranks": all_ok}
 
 
+def c1_echo_extra(device=0):
+    """BASELINE config 1: loopback echo of 4 KiB masked BIN
+    frames through the drop-in server -- the reference's own FLoop +
+    WSServerSocket<false> (oracle/_ref/ws_dropin, tools/dropin/ws_dropin.cpp)
+    with and without the one-line GpuRxHook -- for 1 and 8 clients (window 1,
+    every echoed byte checked), goodput rx+tx and RTT p50/p99; and the
+    reference's own unchanged echo client (tests/new-ws-echo/test_ws_client.cpp,
+    oracle/_ref/ws_ref_client_1, 40,000 messages, its HashArr check every
+    16,384th) against the hooked and the plain server. Host-memory path: every
+    read crosses PCIe twice when hooked."""
+    import subprocess
+    import tempfile
+    dropin = os.path.join(ROOT, "oracle", "_ref", "ws_dropin")
+    refcli = os.path.join(ROOT, "oracle", "_ref", "ws_ref_client_1")
+    if not os.path.exists(dropin):
+        return {"status": "absent: oracle/_ref/ws_dropin not built"}
+
+    def server(gpu, conns, port=0):
+        args = [dropin, "server", "--port", str(port), "--conns", str(conns), "--max-seconds", "60"]
+        if gpu:
+            args += ["--gpu", "--device", str(device)]
+        p = subprocess.Popen(args, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+        line = p.stdout.readline()
+        if not line.startswith("listening"):
+            p.kill()
+            raise RuntimeError(f"ws_dropin server did not start: {line!r} {p.stderr.read()[-500:]}")
+        return p, int(line.split()[1])
+
+    def finish(p):
+        out, err = p.communicate(timeout=60)
+        if p.returncode != 0:
+            raise RuntimeError(f"ws_dropin server rc={p.returncode}: {err[-500:]}")
+        return json.loads(out.strip().splitlines()[-1])
+
+    out = {"workload": "C1: loopback echo, 4 KiB masked BIN frames, window 1, plain ws:// on 127.0.0.1",
+           "server": "reference FLoop + WSServerSocket<false> (ws_dropin); hooked = + fws_amd::GpuRxHook::Enable"}
+    for clients, msgs in ((1, 20000), (8, 4000)):
+        for hooked in (False, True):
+            p, port = server(hooked, clients)
+            r = subprocess.run([dropin, "client", "--port", str(port), "--clients", str(clients), "--msgs", str(msgs),
+                                "--warmup", "200", "--msg-len", "4096", "--max-seconds", "60"],
+                               capture_output=True, text=True, timeout=120)
+            st = finish(p)
+            rec = json.loads(r.stdout.strip().splitlines()[-1]) if r.stdout.strip() else {}
+            out[f"{clients}_client{'s' if clients > 1 else ''}_{'gpu_hook' if hooked else 'reference'}"] = {
+                "goodput_rx_tx_mbps": rec.get("goodput_rx_tx_mbps"), "rtt_us": rec.get("rtt_us"),
+                "msgs_per_s": rec.get("msgs_per_s"), "verified": bool(rec.get("verified")) and r.returncode == 0,
+                "gpu_reads": st.get("gpu_reads")}
+    if os.path.exists(refcli):
+        for hooked in (False, True):
+            p, port = server(hooked, 1, port=58600)   # the port compiled into the reference client
+            with tempfile.TemporaryDirectory() as td:
+                r = subprocess.run([refcli], capture_output=True, text=True, timeout=120, cwd=td)
+            st = finish(p)
+            lines = r.stdout.splitlines()
+            dh = [x.split(":")[1].strip() for x in lines if x.startswith("data hash:")]
+            hv = [x.rsplit("hash value:", 1)[1].split(",")[0].strip() for x in lines if "hash value:" in x]
+            gp = [float(x.split(":")[1].split()[0]) for x in lines if x.startswith("avg (rx+tx) goodput")]
+            lat = [x for x in lines if x.startswith("Latency (us)")]
+            p50 = float(lat[0].split("P50:")[1].split(",")[0]) if lat else None
+            p99 = float(lat[0].split("P99:")[1].split(",")[0]) if lat else None
+            out[f"reference_client_1_{'gpu_hook' if hooked else 'reference'}"] = {
+                "goodput_rx_tx_mbps": gp[0] if gp else None, "rtt_us": {"p50": p50, "p99": p99},
+                "hash_checks_passed": len(hv) if (dh and hv and all(h == dh[0] for h in hv)) else 0,
+                "rc": r.returncode, "msgs": st.get("msgs"), "gpu_reads": st.get("gpu_reads"),
+                "client": "tests/new-ws-echo/test_ws_client.cpp unchanged (oracle/refclient/test_def.h: "
+                          "127.0.0.1, 4 KiB, 40000 msgs)"}
+    return out
+
+
 def _time(fn, steps, stream):
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     fn(0)
@@ -496,7 +622,12 @@ def stream_decode_extra(ctx, wire_c2, dev, args):
     steps = max(4, min(args.steps, 50)) // 2 * 2         # even: in-place XOR restores the input
     out = {}
 
-    def decode_cfg(name, wire, n_frames, utf8=False, nbuf=4, pipelined=True):
+    def decode_cfg(name, wire, n_frames, utf8=False, nbuf=None, pipelined=True):
+        if nbuf is None:
+            # rotate >= 1 GiB of distinct batches so the 256 MB Infinity Cache cannot
+            # serve a step from the one before: 4 for C2 / C3, 77 of the
+            # 14 MB dense batch
+            nbuf = max(4, -(-(1 << 30) // len(wire)))
         c = gpu.Ctx(dev.index or 0, max_frames=n_frames + 64, max_stream_bytes=len(wire))
         bufs = [torch.from_numpy(wire).to(dev) for _ in range(nbuf)]
         cap = n_frames + 64
@@ -512,7 +643,7 @@ def stream_decode_extra(ctx, wire_c2, dev, args):
         payload = int(gpu.read_frames(frames, n_frames)["payload_len"].sum())
         alg = (len(wire) + payload) / t / 1e9
         rec = {"GiB_per_s": round(payload / t / GIB, 1), "ms_per_step": round(t * 1e3, 4), "frames": n_frames,
-               "wire_bytes": len(wire), "alg_GB_per_s": round(alg, 1),
+               "wire_bytes": len(wire), "alg_GB_per_s": round(alg, 1), "rotating_buffers": nbuf,
                "big_super_tiles": gpu.decode_counters(c)["big_super_tiles"],
                # the whole decode step (scan .. stream unmask, every launch) against HBM peak:
                # algorithmic bytes = every wire byte read + every payload byte written
@@ -542,6 +673,8 @@ def stream_decode_extra(ctx, wire_c2, dev, args):
                 # kernels overlap depends on the hardware queues they land on, which HIP
                 # does not expose (one created pair in 4-7 serialises: tools/queue_pair_probe.py)
                 if r:
+                    for st in sts:
+                        st.close()
                     sts[:] = [gpu.hip_stream(), gpu.hip_stream()]
                     for i in range(2):
                         pstep(i)
@@ -556,6 +689,8 @@ def stream_decode_extra(ctx, wire_c2, dev, args):
                                     "ms_per_batch_reps": [round(x * 1e3, 4) for x in reps],
                                     "roofline_frac": round((len(wire) + payload) / tp / 1e9 / HBM_PEAK_GBS, 4),
                                     "path": "2 contexts x 2 non-blocking HIP streams, batches alternate (median of 3 repetitions, a fresh stream pair each)"}
+            for st in sts:
+                st.close()
             c2.close()
         del bufs
         c.close()

@@ -237,9 +237,12 @@ int fws_gpu_unmask_sorted_utf8(fws_gpu_ctx *ctx, void *dev_base, const fws_frame
     int r;
     if ((r = fws_hip_status(hipSetDevice(ctx->device)))) return r;
     if ((r = check_sorted_debug(ctx, dev_descs, n, (hipStream_t)stream))) return r;
+    // span only sizes the grid (grid-stride: every unit is visited) and the seam
+    // reservation; the kernels bound their seam words by ctx->seam_cap, so a batch
+    // whose payload span exceeds it stays in bounds
     const uint64_t span = ctx->cap_stream ? ctx->cap_stream : 4096ull * n;
     if ((r = fws_ctx_ensure_seam(ctx, span))) return r;
-    return fws_launch_unmask_sorted_utf8((uint8_t *)dev_base, dev_descs, n, span, dev_ok, ctx->seam,
+    return fws_launch_unmask_sorted_utf8((uint8_t *)dev_base, dev_descs, n, span, dev_ok, ctx->seam, ctx->seam_cap,
                                          (hipStream_t)stream);
 }
 

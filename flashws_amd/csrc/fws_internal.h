@@ -166,8 +166,10 @@ int fws_launch_unmask_sorted(uint8_t *base, const fws_frame_desc *d, uint32_t n,
 int fws_launch_check_sorted(const fws_frame_desc *d, uint32_t n, uint32_t *bad, hipStream_t s);
 // seam (2 words per 4 KiB unit of the span + 4): the first and last unmasked dword of
 // every unit, written by the unmask and read by the unit-seam UTF-8 check
+// (seam_words: its capacity; units past seam_words / 2 -- a batch wider than the
+// context's reservation -- write no words and the seam check reads the stream)
 int fws_launch_unmask_sorted_utf8(uint8_t *base, const fws_frame_desc *d, uint32_t n, uint64_t max_span,
-                                  uint8_t *ok, uint32_t *seam, hipStream_t s);
+                                  uint8_t *ok, uint32_t *seam, uint64_t seam_words, hipStream_t s);
 // Decoded stream in stream-byte space: unit_first[u] = frame spanning byte 4 KiB * u (the decode's plan).
 // utf8_ok (optional): per-frame flags, preset by the resolve to TEXT && FIN && complete; cleared here on
 // a UTF-8 error found while the payload is in registers (+ k_utf8_seam for unit seams).

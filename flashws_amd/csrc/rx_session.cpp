@@ -428,10 +428,12 @@ static int replay(fws_rx_session *s, uint8_t *buf, uint64_t size, uint64_t buf_c
     for (uint32_t i = 0; i < res.n_frames; ++i) {
         const fws_frame_info &fi = frames[i];
         const uint32_t op = fi.opcode;
-        // RFC 6455 §5.5: control frames are FIN and carry <= 125 B. The reference
-        // only asserts this in debug builds (w_socket.h:654) and otherwise copies
-        // past its 125-B control buffer; the session refuses the frame instead.
-        if ((op >> 3) && (fi.payload_len > 125u || !fi.fin)) {
+        // RFC 6455 §5.5: control frames carry <= 125 B. The reference only asserts
+        // this in debug builds (w_socket.h:654) and otherwise copies past its 125-B
+        // control buffer; the session refuses such a frame instead. A control frame
+        // with FIN = 0 is handled as the reference handles it (PING answered, CLOSE
+        // honoured at its frame end, w_socket.h:659-711, FIN not checked).
+        if ((op >> 3) && fi.payload_len > 125u) {
             s->err_opcode = op;
             return FWS_ERR_CONTROL_FRAME;
         }

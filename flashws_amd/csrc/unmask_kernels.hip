@@ -892,7 +892,8 @@ __device__ __forceinline__ void utf8_slow_chunk(const fws_frame_desc *__restrict
 template <bool kNT, bool kEarly, bool kUtf8 = false>
 __device__ __forceinline__ void unmask_sorted_body(uint8_t *base, const fws_frame_desc *__restrict__ d, uint32_t n,
                                                    uint8_t *__restrict__ ok = nullptr,
-                                                   uint32_t *__restrict__ seam = nullptr) {
+                                                   uint32_t *__restrict__ seam = nullptr,
+                                                   uint64_t seam_units = 0) {
     if (n == 0) return;
     const int lane = threadIdx.x & (kWave - 1);
     const uintptr_t b0 = (uintptr_t)base;
@@ -928,6 +929,10 @@ __device__ __forceinline__ void unmask_sorted_body(uint8_t *base, const fws_fram
         const u32x4 rec = unit_record(U0, E0, E1, A, poA, peA, aligned_key(fa.key, fa.phase, poA), hasB, poB, peB,
                                       aligned_key(fb.key, fb.phase, poB), hasC, poC);
         const bool slow = (rec.z & kRecSlow) != 0;
+        // seam words exist for units below seam_units (the context's seam buffer); a
+        // unit past it (a batch wider than the reservation) leaves its two dwords to
+        // k_utf8_seam_sorted's stream reads
+        const bool sw = u < seam_units;
         if constexpr (kUtf8 && !kEarly) {
             if (rec.z == (4096u << 13) && ((rec.w >> 13) & 0x1FFFu) <= (rec.w & 0x1FFFu)) {
                 // the unit lies wholly inside A's payload and B has no byte in it (the
@@ -944,8 +949,8 @@ __device__ __forceinline__ void unmask_sorted_body(uint8_t *base, const fws_fram
                     gstore16<kNT>(c0 + uint64_t(j) * 1024u, x[j]);
                 }
                 // the unit's first and last unmasked dwords for k_utf8_seam_sorted
-                if (lane == 0) seam[2u * u] = x[0].x;
-                if (lane == 63) seam[2u * u + 1u] = x[kUnmaskU - 1].w;
+                if (sw && lane == 0) seam[2u * u] = x[0].x;
+                if (sw && lane == 63) seam[2u * u + 1u] = x[kUnmaskU - 1].w;
                 uint32_t err = 0, carry = 0;
 #pragma unroll
                 for (int j = 0; j < kUnmaskU; ++j) {
@@ -994,8 +999,8 @@ __device__ __forceinline__ void unmask_sorted_body(uint8_t *base, const fws_fram
                     uint32_t prev = __shfl_up(x.w, 1, 64);
                     if (lane == 0) prev = carry;
                     carry = __shfl(x.w, 63, 64);
-                    if (j == 0 && lane == 0) seam[2u * u] = x.x;
-                    if (j == kUnmaskU - 1 && lane == 63) seam[2u * u + 1u] = x.w;
+                    if (sw && j == 0 && lane == 0) seam[2u * u] = x.x;
+                    if (sw && j == kUnmaskU - 1 && lane == 63) seam[2u * u + 1u] = x.w;
                     utf8_slow_chunk(d, n, A, b0, c0 + uint64_t(j) * 1024u, x, prev, j == 0 && lane == 0, ok);
                 }
                 continue;
@@ -1015,8 +1020,8 @@ __device__ __forceinline__ void unmask_sorted_body(uint8_t *base, const fws_fram
                 uint32_t prev = __shfl_up(x.w, 1, 64);
                 if (lane == 0) prev = carry;
                 carry = __shfl(x.w, 63, 64);
-                if (j == 0 && lane == 0) seam[2u * u] = x.x;
-                if (j == kUnmaskU - 1 && lane == 63) seam[2u * u + 1u] = x.w;
+                if (sw && j == 0 && lane == 0) seam[2u * u] = x.x;
+                if (sw && j == kUnmaskU - 1 && lane == 63) seam[2u * u + 1u] = x.w;
                 const uint32_t skip = j == 0 && lane == 0;
                 const int32_t r = r0 + j * 1024;
                 if (r + 16 > loA && r < hiA + 3) errA |= utf8_chunk_err32(x, prev, r, loA, hiA, skip);
@@ -1035,7 +1040,7 @@ __device__ __forceinline__ void unmask_sorted_body(uint8_t *base, const fws_fram
 // found like sorted_owner, per thread.
 __global__ __launch_bounds__(kBlock) void k_utf8_seam_sorted(const uint8_t *base, const fws_frame_desc *__restrict__ d,
                                                              uint32_t n, uint8_t *__restrict__ ok,
-                                                             const uint32_t *__restrict__ seam) {
+                                                             const uint32_t *__restrict__ seam, uint64_t seam_units) {
     if (n == 0) return;
     const uintptr_t b0 = (uintptr_t)base;
     const uint64_t E0 = b0 + d[0].payload_off;
@@ -1066,8 +1071,9 @@ __global__ __launch_bounds__(kBlock) void k_utf8_seam_sorted(const uint8_t *base
     }
     // the unmask's per-unit record (two adjacent words per thread) rather than two
     // stream lines 4 KiB apart; the software-pipelined unmask writes none (seam null)
-    const uint32_t cur = seam ? seam[2u * u] : *(const uint32_t *)(base + (P - b0));
-    const uint32_t prev = seam ? seam[2u * u - 1u] : *(const uint32_t *)(base + (P - 4u - b0));
+    const bool sw = seam && u < seam_units;          // else the unmask wrote no words for u
+    const uint32_t cur = sw ? seam[2u * u] : *(const uint32_t *)(base + (P - b0));
+    const uint32_t prev = sw ? seam[2u * u - 1u] : *(const uint32_t *)(base + (P - 4u - b0));
     for (uint32_t f = L + 1u; f-- > 0;) {
         const fws_frame_desc fd = d[f];
         const uint64_t po = b0 + fd.payload_off, pe = po + fd.payload_len;
@@ -1218,9 +1224,9 @@ __device__ __forceinline__ void unmask_sorted_utf8_pipe(uint8_t *base, const fws
 template <bool kNT, bool kPipe>
 __global__ __launch_bounds__(kBlock) void k_unmask_sorted_utf8(uint8_t *base, const fws_frame_desc *__restrict__ d,
                                                                uint32_t n, uint8_t *__restrict__ ok,
-                                                               uint32_t *__restrict__ seam) {
+                                                               uint32_t *__restrict__ seam, uint64_t seam_units) {
     if (kPipe) unmask_sorted_utf8_pipe<kNT>(base, d, n, ok);
-    else unmask_sorted_body<kNT, false, true>(base, d, n, ok, seam);
+    else unmask_sorted_body<kNT, false, true>(base, d, n, ok, seam, seam_units);
 }
 
 }  // namespace fwsk
@@ -1325,20 +1331,21 @@ int fws_launch_unmask_sorted(uint8_t *base, const fws_frame_desc *d, uint32_t n,
 }
 
 int fws_launch_unmask_sorted_utf8(uint8_t *base, const fws_frame_desc *d, uint32_t n, uint64_t max_span,
-                                  uint8_t *ok, uint32_t *seam, hipStream_t s) {
+                                  uint8_t *ok, uint32_t *seam, uint64_t seam_words, hipStream_t s) {
+    const uint64_t seam_units = seam ? seam_words / 2u : 0u;
     if (n == 0) return 0;
     int r = fws_hip_status(hipMemsetAsync(ok, 1, n, s));
     if (r) return r;
     const uint64_t units = max_span / 4096u + 2u;
     if (g_sorted_utf8_pipe)
         hipLaunchKernelGGL((k_unmask_sorted_utf8<true, true>), dim3(grid_for_units(units)), dim3(kBlock), 0, s, base, d,
-                           n, ok, nullptr);
+                           n, ok, nullptr, 0ull);
     else
         hipLaunchKernelGGL((k_unmask_sorted_utf8<true, false>), dim3(grid_for_units(units)), dim3(kBlock), 0, s, base,
-                           d, n, ok, seam);
+                           d, n, ok, seam, seam_units);
     const uint64_t seam_blocks = (units + kBlock - 1) / kBlock;   // grid-stride: any span is covered
     hipLaunchKernelGGL(k_utf8_seam_sorted, dim3((unsigned)(seam_blocks < 4096u ? seam_blocks : 4096u)), dim3(kBlock), 0, s,
-                       (const uint8_t *)base, d, n, ok, g_sorted_utf8_pipe ? nullptr : seam);
+                       (const uint8_t *)base, d, n, ok, g_sorted_utf8_pipe ? nullptr : seam, seam_units);
     return fws_hip_status(hipGetLastError());
 }
 

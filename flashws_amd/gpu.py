@@ -36,7 +36,26 @@ def hip_stream():
     s = C.c_void_p()
     if _hip.hipStreamCreateWithFlags(C.byref(s), C.c_uint(1)) != 0:
         raise RuntimeError("hipStreamCreateWithFlags failed")
-    return torch.cuda.ExternalStream(s.value)
+    return HipStream(s.value)
+
+
+class HipStream(torch.cuda.ExternalStream):
+    """A stream from hip_stream(); close() (or leaving a `with` block)
+    synchronizes and destroys it, so probes that make fresh pairs do not leak
+    streams and their queue bindings."""
+
+    def close(self):
+        h = self.cuda_stream
+        if h and _hip is not None and not getattr(self, "_closed", False):
+            self._closed = True
+            _hip.hipStreamSynchronize(C.c_void_p(h))
+            _hip.hipStreamDestroy(C.c_void_p(h))
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
 
 
 def device_count():

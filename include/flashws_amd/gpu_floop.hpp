@@ -221,7 +221,7 @@ private:
             std::snprintf(t, sizeof(t), "payload length larger thanconstants::MAX_WS_FRAME_SIZE %zu",
                           fws::constants::MAX_WS_FRAME_SIZE);
             break;
-        case FWS_ERR_CONTROL_FRAME: std::snprintf(t, sizeof(t), "Control frame over 125 B or fragmented"); break;
+        case FWS_ERR_CONTROL_FRAME: std::snprintf(t, sizeof(t), "Control frame over 125 B"); break;
         case FWS_ERR_NOT_MASKED: return;
         default: std::snprintf(t, sizeof(t), "GPU receive decode failed (%d)", ret); break;
         }

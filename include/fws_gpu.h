@@ -40,8 +40,8 @@ enum {
     FWS_ERR_NOT_MASKED = -3,    /* server RX, MASK bit clear  w_socket.h:513-515 */
     FWS_ERR_MASKED = -4,        /* client RX, MASK bit set    w_socket.h:518-521 */
     FWS_ERR_OPCODE = -9,        /* opcode not 0-2/8-10        w_socket.h:451-454 */
-    FWS_ERR_CONTROL_FRAME = -10,/* host RX session: control frame with payload > 125 B or
-                                   FIN = 0 (RFC 6455 §5.5). The reference does not check
+    FWS_ERR_CONTROL_FRAME = -10,/* host RX session: control frame with payload > 125 B
+                                   (RFC 6455 §5.5). The reference does not check
                                    (only a debug FWS_ASSERT, w_socket.h:654) and overflows
                                    its control buffer; the session refuses the frame. */
     FWS_ERR_CAPACITY = -20,     /* an output array is too small (count still reported) */

@@ -16,7 +16,8 @@ def pytest_configure(config):
 def cuda():
     import torch
     if not torch.cuda.is_available():
-        pytest.skip("no GPU")
+        # a -m gpu run that cannot reach the HIP path must be red, not green-by-skip
+        pytest.fail("no GPU visible: the -m gpu suite needs cuda:0 (MI355X)", pytrace=False)
     return torch.device("cuda:0")
 
 

@@ -86,3 +86,20 @@ def test_bench_launcher_two_ranks_gloo():
     assert np.isclose(rec["value"], 2 * rec["payload_bytes_per_rank"] / rec["step_s"] / (1 << 30))
     d = rec["shard_digests"]
     assert len(d) == 2 and d[0] != d[1]                              # independent shards (seed 42 + rank)
+    # the launcher counted GPUs from the KFD topology (no HIP init) before forking
+    assert rec["launcher_kfd_gpus"] is not None
+
+
+def test_kfd_gpu_count(tmp_path):
+    """bench.launch_ranks counts GPUs from /sys/class/kfd topology nodes with a
+    gfx target (CPU nodes have gfx_target_version 0), narrowed by the
+    *_VISIBLE_DEVICES lists, instead of torch.cuda.device_count()."""
+    import bench
+    for i, ver in enumerate([0, 90500, 90500, 90500]):
+        d = tmp_path / str(i)
+        d.mkdir()
+        (d / "properties").write_text(f"cpu_cores_count 0\ngfx_target_version {ver}\nsimd_count 1024\n")
+    assert bench.kfd_gpu_count(str(tmp_path), env={}) == 3
+    assert bench.kfd_gpu_count(str(tmp_path), env={"ROCR_VISIBLE_DEVICES": "0,1"}) == 2
+    assert bench.kfd_gpu_count(str(tmp_path), env={"HIP_VISIBLE_DEVICES": ""}) == 0
+    assert bench.kfd_gpu_count(str(tmp_path / "absent"), env={}) is None

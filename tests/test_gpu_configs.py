@@ -48,8 +48,7 @@ def sha(t):
 
 
 def _gen(name):
-    if name not in GOLDEN:
-        pytest.skip(f"no golden digest for {name}")
+    assert name in GOLDEN, f"no golden digest for {name} in tests/golden/configs.json"
     g = GOLDEN[name]
     wire, descs, ok = GEN[name]()
     assert len(wire) == g["wire_bytes"] and len(descs) == g["frames"]

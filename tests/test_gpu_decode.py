@@ -574,9 +574,8 @@ def test_small_read_size_limit(ctx, cuda, size):
 
 def test_small_read_capacity(ctx, cuda, resolve_mode):
     """cap below the header count: the first cap frames listed and unmasked,
-    FWS_ERR_CAPACITY, n_frames = all headers; identical on every path."""
-    if resolve_mode == "big_st":
-        pytest.skip("compared against the super-tile path below")
+    FWS_ERR_CAPACITY, n_frames = all headers; identical on every path (each
+    mode is compared with the default super-tile path)."""
     rng = np.random.default_rng(5)
     wire = np.frombuffer(b"".join(frame(2, rng.integers(0, 256, int(rng.integers(0, 400)), dtype=np.uint8).tobytes(),
                                        key=int(rng.integers(0, 2**32))) for _ in range(60)), dtype=np.uint8)

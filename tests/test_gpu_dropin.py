@@ -38,7 +38,8 @@ TLS_ARGS = ["--tls", "--cert", os.path.join(ROOT, "tests", "tls", "server.crt"),
 class Server:
     def __init__(self, gpu, conns, max_seconds=90, tls=False):
         if not os.path.exists(DROPIN):
-            pytest.skip("oracle/_ref/ws_dropin not built (make -C oracle ref, build container)")
+            pytest.fail("oracle/_ref/ws_dropin not built (make -C oracle ref in the build container; "
+                        "__graft_entry__.build() produces it)", pytrace=False)
         args = [DROPIN, "server", "--conns", str(conns), "--max-seconds", str(max_seconds)]
         if gpu:
             args.append("--gpu")
@@ -171,3 +172,45 @@ def test_dropin_reference_client_load(cuda, clients, msg_len, tls):
     assert cli["verified"] is True and cli["pongs"] == clients * (620 // 50)
     assert st["gpu_reads"] > 0 and st["msgs"] == clients * 620
     assert all(c == [1000, b"bye".hex()] for c in st["close_log_hex"][:clients])
+
+
+REF_CLIENTS = {n: os.path.join(ROOT, "oracle", "_ref", f"ws_ref_client_{n}") for n in (1, 8)}
+REF_CLIENT_PORT = 58600        # oracle/refclient/test_def.h (compile-time in the reference client)
+
+
+def run_reference_client(n_clients, gpu, tmp_path):
+    """The reference's unchanged tests/new-ws-echo/test_ws_client.cpp (built by
+    oracle/Makefile `refclient` with our loopback test_def.h: 4 KiB BIN
+    messages, 40,000 in total) against the drop-in server. Returns the client's
+    stdout and the server's JSON line."""
+    exe = REF_CLIENTS[n_clients]
+    if not os.path.exists(exe):
+        pytest.fail(f"{exe} not built (make -C oracle refclient in the build container)", pytrace=False)
+    args = [DROPIN, "server", "--port", str(REF_CLIENT_PORT), "--conns", str(n_clients), "--max-seconds", "90"]
+    if gpu:
+        args.append("--gpu")
+    p = subprocess.Popen(args, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    line = p.stdout.readline()
+    assert line.startswith("listening"), (line, p.stderr.read()[-2000:] if p.poll() is not None else "")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120, cwd=str(tmp_path))
+    out, err = p.communicate(timeout=60)
+    assert p.returncode == 0, err[-2000:]
+    return r, json.loads(out.strip().splitlines()[-1])
+
+
+@pytest.mark.parametrize("n_clients", [1, 8])
+def test_reference_echo_client_through_gpu_hook(cuda, n_clients, tmp_path):
+    """C1 through the reference's own echo client: every message the client gets
+    back was unmasked by the MI355X (GpuRxHook), its FWS_ASSERT(size ==
+    MAX_DATA_LEN) holds for each one (test_ws_client.cpp:217) and its HashArr
+    of the echoed payload equals the hash of what it sent at every 16,384th
+    message (test_ws_client.cpp:260-277; a mismatch aborts the client)."""
+    r, st = run_reference_client(n_clients, True, tmp_path)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-2000:])
+    data_hash = [ln.split(":")[1].strip() for ln in r.stdout.splitlines() if ln.startswith("data hash:")]
+    checks = [ln.rsplit("hash value:", 1)[1].split(",")[0].strip() for ln in r.stdout.splitlines()
+              if "hash value:" in ln]
+    assert len(data_hash) == 1 and len(checks) == 40000 // 16384, r.stdout[-3000:]
+    assert all(c == data_hash[0] for c in checks)
+    assert "avg (rx+tx) goodput" in r.stdout
+    assert st["gpu"] is True and st["gpu_reads"] > 0 and st["msgs"] == 40000

@@ -125,3 +125,33 @@ def test_sorted_utf8_both_variants(ctx, cuda, pipe):
         assert np.array_equal(ok.astype(bool), np.array([_valid(c) for c in cases]))
     finally:
         lib().fws_internal_set_sorted_utf8_pipe(old)
+
+
+def test_sorted_utf8_unreserved_ctx_wide_frames(cuda):
+    """A context without a stream reservation sizes its seam words from 4 KiB per
+    frame; TEXT frames of 64 KiB-1 MiB span far more units than that, so most
+    units have no seam words: the kernels must stay inside the buffer (units
+    past it leave their seam bytes to the stream reads of the seam check) and the
+    flags must still be exact at every unit seam."""
+    rng = np.random.default_rng(11)
+    cases = []
+    for n in (70000, 1 << 20, 200000, 65536):
+        s = "".join(chr(int(c)) for c in rng.integers(0x20, 0x10FFFF, n // 3) if not 0xD800 <= int(c) <= 0xDFFF)
+        b = bytearray(s.encode())[:n]
+        while b and (b[-1] & 0xC0) == 0x80:     # cut back to a whole character
+            b = b[:-1]
+        if b and b[-1] >= 0xC0:
+            b = b[:-1]
+        cases.append(bytes(b))
+    # one invalid byte placed right at a 4 KiB unit seam of the second frame
+    bad = bytearray(cases[1])
+    bad[4096 * 9 + 1] = 0xFF
+    cases.append(bytes(bad))
+    plain, masked, descs = _layout(rng, cases, 7)
+    c = gpu.Ctx(0)                                        # no reservation
+    try:
+        got, ok = _run(c, cuda, masked, descs)
+    finally:
+        c.close()
+    assert np.array_equal(got, plain)
+    assert np.array_equal(ok.astype(bool), np.array([_valid(x) for x in cases]))

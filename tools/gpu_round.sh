@@ -1,22 +1,72 @@
-# Round measurement pass on one MI355X: GPU tests, smoke, full bench (extras,
-# C5, CPU baseline), PMC traffic passes for the headline kernel, kernel stats
-# (headline bench, C4 gather, TX encode; rocprofv3 of the --extra bench
-# segfaults at interpreter exit on this image, so the extras are profiled by
-# their own small drivers).
+#!/bin/bash
+# tools/gpu_round.sh -- the GPU passes of a round, one MI355X (run through gpurun:
+#   gpurun --timeout N -- 'bash tools/gpu_round.sh STEP [STEP ...]').
+# Every GPU step runs under its own time limit; the first failing step ends the
+# script (no retries). Outputs go under gpurun_out/$ROUND/ (copy what is judged
+# into profiles/$ROUND/).
+#   tests        pytest -m gpu (whole suite, one process)
+#   smoke        __graft_entry__.smoke()
+#   bench        python bench.py (default: headline + extras + C1 + CPU baseline)
+#   bench_quick  python bench.py --no-extra --no-cpu
+#   share2       bench.py --gpus 2 --share-device (two ranks on device 0, gloo): the N-rank path on HIP
+#   pmc          FETCH_SIZE / WRITE_SIZE passes of the headline kernel (separate runs)
+#   prof_main    rocprofv3 kernel trace + stats of the headline bench
+#   prof_decode  rocprofv3 kernel trace + stats of the C2/C3/dense/C5 stream decodes
+#   prof_extra   rocprofv3 kernel trace + stats of C4 gather, TX encode, C5 descriptor mode
+#   pmc_decode   FETCH_SIZE / WRITE_SIZE passes of the C3 decode (tools/run_decode.py c3)
+#   sq_decode    SQ counters of the C3 decode kernels
 set -o pipefail
-R=$GRAFT_REPO_ROOT
-mkdir -p $R/gpurun_out
-cd $R
-timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || { tail -30 gpurun_out/gpu_tests.log; exit 1; }
-tail -1 gpurun_out/gpu_tests.log
-timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { tail -20 gpurun_out/smoke.log; exit 1; }
-timeout -k 10 400 python bench.py --extra --c5 --cpu-seconds 10 > gpurun_out/bench_full.log 2>&1 || { tail -20 gpurun_out/bench_full.log; exit 1; }
-cd /tmp && export TMPDIR=/tmp
-timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -f csv -d $R/gpurun_out/pmc_fetch -o run -- python3 $R/bench.py --no-extra --no-cpu --no-batch-extra --steps 10 --warmup 2 > $R/gpurun_out/pmc_fetch.log 2>&1 || { tail -5 $R/gpurun_out/pmc_fetch.log; exit 1; }
-timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -f csv -d $R/gpurun_out/pmc_write -o run -- python3 $R/bench.py --no-extra --no-cpu --no-batch-extra --steps 10 --warmup 2 > $R/gpurun_out/pmc_write.log 2>&1 || { tail -5 $R/gpurun_out/pmc_write.log; exit 1; }
-timeout -k 10 200 rocprofv3 --kernel-trace --stats -f csv -d $R/gpurun_out/prof_main -o run -- python3 $R/bench.py --no-extra --no-cpu > $R/gpurun_out/prof_main.log 2>&1 || { tail -5 $R/gpurun_out/prof_main.log; exit 1; }
-timeout -k 10 100 rocprofv3 --kernel-trace --stats -f csv -d $R/gpurun_out/prof_c4 -o run -- python3 $R/tools/run_c4.py > $R/gpurun_out/prof_c4.log 2>&1 || { tail -5 $R/gpurun_out/prof_c4.log; exit 1; }
-timeout -k 10 100 rocprofv3 --kernel-trace --stats -f csv -d $R/gpurun_out/prof_tx -o run -- python3 $R/tools/run_tx.py > $R/gpurun_out/prof_tx.log 2>&1 || { tail -5 $R/gpurun_out/prof_tx.log; exit 1; }
-timeout -k 10 200 rocprofv3 --kernel-trace --stats -f csv -d $R/gpurun_out/prof_c5d -o run -- python3 $R/tools/run_c5_desc.py > $R/gpurun_out/prof_c5d.log 2>&1 || { tail -5 $R/gpurun_out/prof_c5d.log; exit 1; }
-timeout -k 10 200 rocprofv3 --kernel-trace --stats -f csv -d $R/gpurun_out/prof_c5 -o run -- python3 $R/tools/run_c5.py > $R/gpurun_out/prof_c5.log 2>&1 || { tail -5 $R/gpurun_out/prof_c5.log; exit 1; }
-echo done
+ROUND=${ROUND:-r03}
+R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+O=$R/gpurun_out/$ROUND
+mkdir -p "$O"
+cd "$R" || exit 1
+fail() { echo "step $1 failed (rc $2)"; tail -30 "$3"; exit 1; }
+prof() {   # prof NAME TIMEOUT ARGS... : rocprofv3 with the program right after --
+    local name=$1 t=$2; shift 2
+    (cd /tmp && TMPDIR=/tmp timeout -k 10 "$t" rocprofv3 "$@") > "$O/$name.log" 2>&1 || fail "$name" $? "$O/$name.log"
+}
+for step in "$@"; do
+    echo "== $step $(date +%T)"
+    case $step in
+    tests)
+        timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+            > "$O/gpu_tests.log" 2>&1 || fail tests $? "$O/gpu_tests.log"
+        tail -1 "$O/gpu_tests.log" ;;
+    smoke)
+        timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 \
+            || fail smoke $? "$O/smoke.log"
+        tail -1 "$O/smoke.log" ;;
+    bench)
+        timeout -k 10 600 python bench.py > "$O/bench.json" 2> "$O/bench.err" || fail bench $? "$O/bench.err"
+        cut -c1-600 "$O/bench.json" ;;
+    bench_quick)
+        timeout -k 10 300 python bench.py --no-extra --no-cpu > "$O/bench_quick.json" 2> "$O/bench_quick.err" \
+            || fail bench_quick $? "$O/bench_quick.err"
+        cut -c1-600 "$O/bench_quick.json" ;;
+    share2)
+        timeout -k 10 600 python bench.py --gpus 2 --share-device --no-cpu --steps 20 --warmup 5 \
+            > "$O/share2.json" 2> "$O/share2.err" || fail share2 $? "$O/share2.err"
+        cut -c1-2000 "$O/share2.json" ;;
+    pmc)
+        prof pmc_fetch 120 --pmc FETCH_SIZE -f csv -d "$O/pmc_fetch" -o run -- python3 "$R/bench.py" --no-extra --no-cpu --no-batch-extra --steps 10 --warmup 2
+        prof pmc_write 120 --pmc WRITE_SIZE -f csv -d "$O/pmc_write" -o run -- python3 "$R/bench.py" --no-extra --no-cpu --no-batch-extra --steps 10 --warmup 2 ;;
+    prof_main)
+        prof prof_main 300 --kernel-trace --stats -f csv -d "$O/prof_main" -o run -- python3 "$R/bench.py" --no-extra --no-cpu ;;
+    prof_decode)
+        for c in c2 c3 dense c5_256m; do
+            prof "prof_$c" 300 --kernel-trace --stats -f csv -d "$O/prof_$c" -o run -- python3 "$R/tools/run_decode.py" $c
+        done ;;
+    prof_extra)
+        prof prof_c4 200 --kernel-trace --stats -f csv -d "$O/prof_c4" -o run -- python3 "$R/tools/run_c4.py"
+        prof prof_tx 200 --kernel-trace --stats -f csv -d "$O/prof_tx" -o run -- python3 "$R/tools/run_tx.py"
+        prof prof_c5d 300 --kernel-trace --stats -f csv -d "$O/prof_c5d" -o run -- python3 "$R/tools/run_c5_desc.py" ;;
+    pmc_decode)
+        prof pmc_dec_fetch 120 --pmc FETCH_SIZE -f csv -d "$O/pmc_dec_fetch" -o run -- python3 "$R/tools/run_decode.py" c3
+        prof pmc_dec_write 120 --pmc WRITE_SIZE -f csv -d "$O/pmc_dec_write" -o run -- python3 "$R/tools/run_decode.py" c3 ;;
+    sq_decode)
+        prof sq_dec 120 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_VMEM -f csv -d "$O/sq_dec" -o run -- python3 "$R/tools/run_decode.py" c3 ;;
+    *) echo "unknown step $step"; exit 2 ;;
+    esac
+done
+echo "all steps done $(date +%T)"

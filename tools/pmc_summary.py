@@ -45,7 +45,21 @@ def main():
     ap.add_argument("--kernel", required=True)
     ap.add_argument("--alg-bytes", type=int, required=True)
     ap.add_argument("--out", required=True)
+    ap.add_argument("--source", default="flashws_amd/csrc/unmask_kernels.hip",
+                    help="the kernel's source file; its sha256 is recorded so bench.py can tell a stale summary")
     a = ap.parse_args()
+    import datetime
+    import hashlib
+    import os
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with open(os.path.join(root, a.source), "rb") as fh:
+        src_sha = hashlib.sha256(fh.read()).hexdigest()[:16]
+    try:
+        commit = subprocess.run(["git", "-C", root, "rev-parse", "--short=12", "HEAD"], capture_output=True,
+                                text=True).stdout.strip() or None
+    except OSError:
+        commit = None
     f = per_dispatch(a.fetch, "FETCH_SIZE", a.kernel)
     w = per_dispatch(a.write, "WRITE_SIZE", a.kernel)
     fk, wk = statistics.median(f), statistics.median(w)
@@ -63,6 +77,10 @@ def main():
         "traffic_over_alg": round((read_b + write_b) / a.alg_bytes, 4),
         "correction": "read = 2 x FETCH_SIZE (gfx950 half-count of 16-B/lane streaming reads, "
                       "MI355X_MICROARCH.md HBM); write = WRITE_SIZE; KiB = 1024 B",
+        "kernel_source": a.source,
+        "kernel_source_sha16": src_sha,
+        "commit": commit,
+        "measured": datetime.date.today().isoformat(),
     }
     with open(a.out, "w") as fh:
         json.dump(out, fh, indent=1)

@@ -34,10 +34,10 @@ enum Counter {
     kCntTicket = 10,     // k_link workgroups finished (the last one resolves the path)
     kCntTails = 11,      // super-tile exit tails appended by k_merge
     kCntBig = 12,        // super tiles that took k_merge's big-ST path (diagnostic)
-    // one-pass decode (fused_kernels.hip)
-    kCntFMode = 13,      // 1: k_fused ran this call; the multi-launch path runs only if it failed
+    // one-pass decode (stream_kernels.hip)
+    kCntFMode = 13,      // 1: k_stream ran this call; the multi-launch path runs only if it failed
     kCntFFail = 14,      // ~(first failing fused super tile), 0 = none (atomicMax)
-    kCntFTicket = 15,    // k_fused's ordered super-tile ticket
+    kCntFTicket = 15,    // k_stream's ordered super-tile ticket
     kCntFSurv = 16,      // survivors over all fused super tiles (diagnostic, result)
     kCntFTimeout = 17,   // fused super tiles that gave up a bounded wait (diagnostic)
     kCntRootCnt = 18,    //   ::cnt (ent is 0) -- resolve_path skips four dependent loads
@@ -67,7 +67,7 @@ __device__ __forceinline__ uint32_t spill_shared(uint32_t *counters, uint32_t s_
 }
 static_assert(kCntFrames == kDecodeFramesCounter, "fws_internal.h names the frame counter");
 static_assert(kCntFMode == kDecodeFModeCounter && kCntFFail == kDecodeFFailCounter, "fws_internal.h names them");
-// the one-pass decode (k_fused) ran this call and finished the whole stream: the
+// the one-pass decode (k_stream) ran this call and finished the whole stream: the
 // multi-launch kernels queued after it return at once
 __device__ __forceinline__ bool fused_done(const uint32_t *C) { return C[kCntFMode] != 0u && C[kCntFFail] == 0u; }
 

@@ -84,7 +84,7 @@ __global__ __launch_bounds__(kScanThreads) __attribute__((amdgpu_waves_per_eu(8,
                                                        uint32_t *__restrict__ counters, uint32_t s_cap,
                                                        uint32_t *__restrict__ scan_dummy, uint32_t fused) {
     __shared__ __attribute__((aligned(16))) ScanLds lds_w[kScanWaves];
-    if (fused && fused_done(counters)) return;       // k_fused decoded the stream
+    if (fused && fused_done(counters)) return;       // k_stream decoded the stream
     const uint32_t lane = threadIdx.x & 63;
     ScanLds &W = lds_w[threadIdx.x >> 6];
     uint8_t *const B = W.bytes;

@@ -164,7 +164,7 @@ struct MergeParams {
     uint64_t n_units;                                // ceil(N / kUnit), clamped to the plan's capacity
     uint32_t force_big;                              // test hook: every ST on the big-ST path
     uint32_t *zero_next;                             // the next call's counter set (k_emit zeroes it)
-    uint32_t fused;                                  // k_fused was queued first: read its gate (fused_done)
+    uint32_t fused;                                  // k_stream was queued first: read its gate (fused_done)
     uint32_t *bg_nx, *bg_wt, *bg_lref, *bg_ptr, *bg_sc, *bg_mark;   // big-ST scratch [max_nodes]
     uint64_t max_nodes;
 
@@ -500,7 +500,7 @@ __global__ __launch_bounds__(kMThreads) void k_merge(MergeParams P) {
     MP_START(30);
     MP_T0();
     MP_INIT();
-    if (P.fused && fused_done(C)) return;            // k_fused decoded the stream (k_link returns too)
+    if (P.fused && fused_done(C)) return;            // k_stream decoded the stream (k_link returns too)
     // the tail-target bitmap k_link sets
     for (uint64_t w = (uint64_t)s * kMThreads + tid; w < P.tail_cap / 32u + 1u; w += (uint64_t)gridDim.x * kMThreads)
         P.tmark[w] = 0u;

@@ -382,8 +382,8 @@ __global__ __launch_bounds__(kBlock) void k_unmask_stream(uint8_t *base, uint64_
                                                           uint8_t *__restrict__ ok, const uint32_t *fgate,
                                                           const uint64_t *fdone, uint32_t fepoch,
                                                           uint32_t *__restrict__ seam) {
-    // k_fused ran: nothing to do if it finished the stream; else skip the 32 KiB
-    // super tiles it unmasked (done granules tagged with its epoch, fused_kernels.hip)
+    // k_stream ran: nothing to do if it finished the stream; else skip the 32 KiB
+    // super tiles it unmasked (done granules tagged with its epoch, stream_kernels.hip)
     const bool fran = fgate != nullptr && fgate[kDecodeFModeCounter] != 0u;
     if (fran && fgate[kDecodeFFailCounter] == 0u) return;
     uint32_t n = *n_dev;

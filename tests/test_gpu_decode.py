@@ -20,7 +20,7 @@ pytestmark = pytest.mark.gpu
 RESOLVE_MODES = {"super_tile": (0, 0), "big_st": (1, 0), "small_read": (2, 0), "fused": (0, 2)}
 CNT_FAILED = 9              # decode_common.h Counter::kCntFallback (the resolve failed)
 CNT_BIG = 12                # decode_common.h Counter::kCntBig (super tiles on the big-ST path)
-CNT_FMODE, CNT_FFAIL, CNT_FTIMEOUT = 13, 14, 17   # kCntFMode, kCntFFail, kCntFTimeout (k_fused)
+CNT_FMODE, CNT_FFAIL, CNT_FTIMEOUT = 13, 14, 17   # kCntFMode, kCntFFail, kCntFTimeout (k_stream)
 
 
 @pytest.fixture(params=list(RESOLVE_MODES), autouse=True)
@@ -30,7 +30,7 @@ def resolve_mode(request):
     forced for every super tile; the RX session's one-launch small-read kernel
     (small_kernels.hip; streams <= 128 KiB with <= 256 headers, the rest fall
     back to the super-tile path as the session does); and the one-pass decode
-    (fused_kernels.hip, the default for streams of 1 MiB and more) forced for
+    (stream_kernels.hip, the default for streams of 1 MiB and more) forced for
     every stream, with the multi-launch path as its fallback where it declines
     (dense tiles, protocol errors: the super tiles it finished are skipped)."""
     from flashws_amd import _lib
@@ -52,7 +52,7 @@ def counters(ctx):
 
 
 def fused_finished(ctx):
-    """True if the last decode ran k_fused and it finished the whole stream."""
+    """True if the last decode ran k_stream and it finished the whole stream."""
     c = counters(ctx)
     return c[CNT_FMODE] == 1 and c[CNT_FFAIL] == 0 and c[CNT_FTIMEOUT] == 0
 
@@ -235,7 +235,7 @@ def test_c3_mixed_parity(ctx, cuda, resolve_mode):
     if resolve_mode == "super_tile":
         assert not fell_back(ctx), "C3 must resolve on the super-tile path with LDS tables"
     if resolve_mode == "fused":
-        assert fused_finished(ctx), "C3 must decode in one k_fused pass"
+        assert fused_finished(ctx), "C3 must decode in one k_stream pass"
 
 
 def test_c2_full_parity(ctx, cuda, resolve_mode):
@@ -245,7 +245,7 @@ def test_c2_full_parity(ctx, cuda, resolve_mode):
     if resolve_mode == "super_tile":
         assert not fell_back(ctx), "C2 must resolve on the super-tile path with LDS tables"
     if resolve_mode == "fused":
-        assert fused_finished(ctx), "C2 must decode in one k_fused pass"
+        assert fused_finished(ctx), "C2 must decode in one k_stream pass"
 
 
 @pytest.mark.parametrize("n_frames,payload", [(200_000, 64), (200_000, 120), (600_000, 16)])

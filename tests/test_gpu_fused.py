@@ -1,10 +1,10 @@
-"""GPU parity of the one-pass decode (k_fused, fused_kernels.hip) on the
+"""GPU parity of the one-pass decode (k_stream, stream_kernels.hip) on the
 branches the shared decode tests (tests/test_gpu_decode.py, `fused` mode) do
 not force: frames longer than the fast tables' key depth (4 super tiles of
 32 KiB, so the look-back waits for the landing super tile's own inclusive
 state), more frames than the frame list holds, an incomplete header that
 starts one super tile before the last, a protocol error deep in a long stream
-(the multi-launch fallback finishes it and skips the super tiles k_fused
+(the multi-launch fallback finishes it and skips the super tiles k_stream
 unmasked), and repeated calls on one context (epoch-tagged words). Bit-exact
 against the oracle (w_socket.h:435-769 restated) or against the multi-launch
 path on the same input where the oracle has no counterpart (capacity).
@@ -84,7 +84,7 @@ def check(ctx, cuda, wire):
 def test_frames_longer_than_key_depth(ctx, cuda, seed):
     """Frames of 160 KiB .. 1.5 MiB (5 .. 48 super tiles) among small ones:
     the true chain lands beyond every fast-table key, and the look-back waits
-    for that super tile's own resolution. k_fused must finish the stream."""
+    for that super tile's own resolution. k_stream must finish the stream."""
     rng = np.random.default_rng(100 + seed)
     parts = []
     for _ in range(12):
@@ -94,7 +94,7 @@ def test_frames_longer_than_key_depth(ctx, cuda, seed):
     wire = np.concatenate(parts)
     check(ctx, cuda, wire)
     c = counters(ctx)
-    assert c[CNT_FMODE] == 1 and c[CNT_FFAIL] == 0, "k_fused must decode this stream alone"
+    assert c[CNT_FMODE] == 1 and c[CNT_FFAIL] == 0, "k_stream must decode this stream alone"
 
 
 def test_repeated_calls_one_context(ctx, cuda):
@@ -109,7 +109,7 @@ def test_repeated_calls_one_context(ctx, cuda):
 
 @pytest.mark.parametrize("where", [0.1, 0.5, 0.93])
 def test_protocol_error_deep_in_stream(ctx, cuda, where):
-    """An RSV-set header at 10 / 50 / 93 % of a 12 MiB stream: k_fused finishes
+    """An RSV-set header at 10 / 50 / 93 % of a 12 MiB stream: k_stream finishes
     the super tiles before it, the multi-launch path the rest (its unmask skips
     the finished ones), the result is OnRecvData's."""
     rng = np.random.default_rng(int(where * 100))
@@ -150,9 +150,9 @@ def test_incomplete_header_before_last_super_tile(ctx, cuda, tail_len):
 
 
 def test_capacity_matches_multi_launch_path(ctx, cuda):
-    """More frames than `cap`: k_fused declines (FAIL) and the multi-launch
+    """More frames than `cap`: k_stream declines (FAIL) and the multi-launch
     path produces the capacity result; bytes, frames and result must equal a
-    run with k_fused off."""
+    run with k_stream off."""
     wire, descs, _ = gpu.config_c2(seed=3, n_frames=4000, payload=1000)
     cap = 2500
     got, gframes, r = decode(ctx, wire, cuda, cap=cap)

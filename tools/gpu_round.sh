@@ -15,6 +15,9 @@
 #   prof_extra   rocprofv3 kernel trace + stats of C4 gather, TX encode, C5 descriptor mode
 #   pmc_decode   FETCH_SIZE / WRITE_SIZE passes of the C3 decode (tools/run_decode.py c3)
 #   sq_decode    SQ counters of the C3 decode kernels
+#   trace        phase clocks of k_scan and per-workgroup timelines of the resolve kernels
+#                (FWS_SCAN_PROF build: make -C flashws_amd/csrc prof, built beforehand)
+#   strace       per-super-tile clocks of k_stream (same prof build)
 set -o pipefail
 ROUND=${ROUND:-r03}
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
@@ -66,6 +69,22 @@ for step in "$@"; do
         prof pmc_dec_write 120 --pmc WRITE_SIZE -f csv -d "$O/pmc_dec_write" -o run -- python3 "$R/tools/run_decode.py" c3 ;;
     sq_decode)
         prof sq_dec 120 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_VMEM -f csv -d "$O/sq_dec" -o run -- python3 "$R/tools/run_decode.py" c3 ;;
+    trace)
+        timeout -k 10 300 python tools/prof_scan.py > "$O/prof_scan.json" 2> "$O/prof_scan.err" || fail trace $? "$O/prof_scan.err"
+        timeout -k 10 300 python tools/prof_merge_trace.py > "$O/prof_merge_trace.json" 2> "$O/prof_merge_trace.err" \
+            || fail trace $? "$O/prof_merge_trace.err" ;;
+    strace)
+        timeout -k 10 300 python tools/prof_stream.py all 4 > "$O/prof_stream.json" 2> "$O/prof_stream.err" \
+            || fail strace $? "$O/prof_stream.err"
+        cat "$O/prof_stream.json" | head -80 ;;
+    dectests)
+        timeout -k 10 900 python -u -m pytest tests/test_gpu_decode.py tests/test_gpu_fused.py tests/test_gpu_configs.py -x -v --timeout 120 --timeout-method thread \
+            > "$O/dec_tests.log" 2>&1 || fail dectests $? "$O/dec_tests.log"
+        tail -1 "$O/dec_tests.log" ;;
+    tdec)
+        timeout -k 10 300 python tools/time_decode.py 20 > "$O/time_decode.json" 2> "$O/time_decode.err" \
+            || fail tdec $? "$O/time_decode.err"
+        cat "$O/time_decode.err" | grep -v amdgpu.ids ;;
     *) echo "unknown step $step"; exit 2 ;;
     esac
 done

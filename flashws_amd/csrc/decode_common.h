@@ -34,12 +34,7 @@ enum Counter {
     kCntTicket = 10,     // k_link workgroups finished (the last one resolves the path)
     kCntTails = 11,      // super-tile exit tails appended by k_merge
     kCntBig = 12,        // super tiles that took k_merge's big-ST path (diagnostic)
-    // one-pass decode (stream_kernels.hip)
-    kCntFMode = 13,      // 1: k_stream ran this call; the multi-launch path runs only if it failed
-    kCntFFail = 14,      // ~(first failing fused super tile), 0 = none (atomicMax)
-    kCntFTicket = 15,    // k_stream's ordered super-tile ticket
-    kCntFSurv = 16,      // survivors over all fused super tiles (diagnostic, result)
-    kCntFTimeout = 17,   // fused super tiles that gave up a bounded wait (diagnostic)
+    // 13..17: unused
     kCntRootCnt = 18,    //   ::cnt (ent is 0) -- resolve_path skips four dependent loads
     kCntCount = 19
 };
@@ -66,10 +61,6 @@ __device__ __forceinline__ uint32_t spill_shared(uint32_t *counters, uint32_t s_
     return spill_half(s_cap) + off;
 }
 static_assert(kCntFrames == kDecodeFramesCounter, "fws_internal.h names the frame counter");
-static_assert(kCntFMode == kDecodeFModeCounter && kCntFFail == kDecodeFFailCounter, "fws_internal.h names them");
-// the one-pass decode (k_stream) ran this call and finished the whole stream: the
-// multi-launch kernels queued after it return at once
-__device__ __forceinline__ bool fused_done(const uint32_t *C) { return C[kCntFMode] != 0u && C[kCntFFail] == 0u; }
 
 constexpr uint32_t kSlots = 8;               // per-tile survivor slots before spilling
 constexpr uint32_t kDenseTile = 0xFFFFFFFEu; // tile_count mark: k_scan left the tile to k_scan_dense (which overwrites it)

@@ -82,9 +82,8 @@ __global__ __launch_bounds__(kScanThreads) __attribute__((amdgpu_waves_per_eu(8,
                                                        uint32_t *__restrict__ tile_spill,
                                                        uint32_t *__restrict__ tile_count,
                                                        uint32_t *__restrict__ counters, uint32_t s_cap,
-                                                       uint32_t *__restrict__ scan_dummy, uint32_t fused) {
+                                                       uint32_t *__restrict__ scan_dummy) {
     __shared__ __attribute__((aligned(16))) ScanLds lds_w[kScanWaves];
-    if (fused && fused_done(counters)) return;       // k_stream decoded the stream
     const uint32_t lane = threadIdx.x & 63;
     ScanLds &W = lds_w[threadIdx.x >> 6];
     uint8_t *const B = W.bytes;
@@ -438,26 +437,18 @@ int fws_launch_decode(fws_gpu_ctx *ctx, uint8_t *wire, uint64_t N, fws_frame_inf
         d.cnt_dirty = false;
     }
     d.cnt_dirty = true;                  // until every launch of this call is queued
-    // the one-pass decode first; the launches below are its fallback and return
-    // at once when it finished the stream (kCntFMode / kCntFFail)
-    d.fused_ran = false;
-    if (g_resolve_mode == 0 && !utf8_ok && cap > 0 && fws_fused_enabled(N)) {
-        if (int r = fws_fused_ensure(ctx, N)) return r;
-        if (int r = fws_launch_fused(ctx, wire, N, frames, cap, res, s)) return r;
-        d.fused_ran = true;
-    }
     if (n_tiles) {
         const uint32_t need = (n_tiles + kScanWaves - 1) / kScanWaves;
         const uint32_t sg = need < d.scan_grid ? need : d.scan_grid;
         hipLaunchKernelGGL(N >= kTile + kHaloX ? k_scan<true> : k_scan<false>, dim3(sg), dim3(kScanThreads), 0, s,
                            wire, N, n_tiles, d.stage_info, d.spill_info, d.tile_spill, d.tile_count, d.counters,
-                           (uint32_t)d.max_surv, d.scan_dummy, d.fused_ran ? 1u : 0u);
+                           (uint32_t)d.max_surv, d.scan_dummy);
         if ((e = hipGetLastError()) != hipSuccess) return fws_hip_status(e);
     }
     // super-tile resolve; g_resolve_mode 1 sends every super tile down the big-ST
     // path (tests), mode 2 decodes as mode 0 here. Slot ids are 32-bit.
     if (N >= (1ull << 39)) return FWS_ERR_CAPACITY;
-    const int r = fws_launch_merge(ctx, wire, N, n_tiles, frames, cap, res, utf8_ok, g_resolve_mode == 1, d.fused_ran, next, s);
+    const int r = fws_launch_merge(ctx, wire, N, n_tiles, frames, cap, res, utf8_ok, g_resolve_mode == 1, next, s);
     if (r == 0) d.cnt_dirty = false;
     return r;
 }

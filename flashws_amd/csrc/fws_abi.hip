@@ -75,7 +75,7 @@ extern "C" {
 // decode on ctx (decode_common.h Counter), synchronously. 0 or an error.
 __attribute__((visibility("default"))) int fws_internal_decode_counters(fws_gpu_ctx *ctx, uint32_t *out, int n) {
     if (!ctx || !out || n <= 0 || !ctx->dec.counters) return FWS_ERR_INVALID;
-    if (n > 32) n = 32;
+    if (n > 64) n = 64;
     return fws_hip_status(hipMemcpy(out, ctx->dec.counters, (size_t)n * 4, hipMemcpyDeviceToHost));
 }
 
@@ -139,7 +139,6 @@ void fws_gpu_ctx_destroy(fws_gpu_ctx *ctx) {
     dev_free(d.bg_ptr);
     dev_free(d.bg_sc);
     dev_free(d.bg_mark);
-    dev_free(d.fpub);
     dev_free(ctx->seam);
     delete ctx;
 }
@@ -292,8 +291,7 @@ int fws_gpu_decode_stream(fws_gpu_ctx *ctx, void *dev_wire, uint64_t len, fws_fr
     const uint32_t *n_dev = ctx->dec.counters + kDecodeFramesCounter;
     if (dev_utf8_ok && (r = fws_ctx_ensure_seam(ctx, len))) return r;
     return fws_launch_unmask_stream((uint8_t *)dev_wire, len, dev_frames, cap, n_dev, ctx->plan.unit_first,
-                                    dev_utf8_ok, ctx->dec.fused_ran ? ctx->dec.counters : nullptr, fws_fused_done(ctx), ctx->dec.fepoch,
-                                    ctx->seam, s);
+                                    dev_utf8_ok, ctx->seam, s);
 }
 
 }  // extern "C"

@@ -128,14 +128,6 @@ struct fws_decode_ws {
     uint32_t *bg_ptr = nullptr;            // [2][max_nodes] pointer jumping
     uint32_t *bg_sc = nullptr;             // [2][max_nodes] frame counts
     uint32_t *bg_mark = nullptr;           // [max_nodes] k_emit: on the path
-    // one-pass decode (stream_kernels.hip): epoch-tagged 8-B granules per fused
-    // super tile, published and polled inside the launch (no memset per call)
-    uint64_t fmax_st = 0;
-    uint64_t *fpub = nullptr;              // [fmax_st * kFPubWords] (stream_kernels.hip layout)
-    uint32_t fepoch = 0;                   // tag of the last k_stream call (1..2^24-1)
-    bool fused_ran = false;                // the last fws_launch_decode queued k_stream (the later
-                                           //   launches read its gate words only then)
-    uint32_t fcus = 0;                     // CUs of the context's device (k_stream grid)
 };
 
 struct fws_gpu_ctx {
@@ -174,13 +166,10 @@ int fws_launch_unmask_sorted_utf8(uint8_t *base, const fws_frame_desc *d, uint32
 // utf8_ok (optional): per-frame flags, preset by the resolve to TEXT && FIN && complete; cleared here on
 // a UTF-8 error found while the payload is in registers (+ k_utf8_seam for unit seams).
 // seam (utf8_ok only; 2 words per 4 KiB unit + 4): each unit's first / last unmasked dword
-// for the unit-seam check. fgate (optional): the decode's counter set; when k_stream ran (kCntFMode) the pass
-// returns at once unless it failed, and then skips the super tiles k_stream already
-// unmasked (fdone granules tagged fepoch)
+// for the unit-seam check.
 int fws_launch_unmask_stream(uint8_t *base, uint64_t N, const fws_frame_info *frames, uint32_t cap,
                              const uint32_t *n_dev, const uint32_t *unit_first, uint8_t *utf8_ok,
-                             const uint32_t *fgate, const uint64_t *fdone, uint32_t fepoch, uint32_t *seam,
-                             hipStream_t s);
+                             uint32_t *seam, hipStream_t s);
 
 // outplan_kernels.hip: one-launch output-space plans (base = ws.cbase, unit map, total)
 int fws_plan_next_epoch(fws_plan_ws &ws, hipStream_t s);
@@ -196,8 +185,6 @@ int fws_launch_gather(uint8_t *dst, const uint8_t *src, const fws_frame_desc *d,
 
 // decode_kernels.hip
 constexpr int kDecodeFramesCounter = 3;   // index of the device frame count in dec.counters
-constexpr int kDecodeFModeCounter = 13;   // k_stream ran this call (decode_common.h kCntFMode)
-constexpr int kDecodeFFailCounter = 14;   // ~(first failing fused super tile) (kCntFFail)
 int fws_decode_ensure(fws_gpu_ctx *ctx, uint64_t N, uint32_t cap);
 // utf8_ok (optional): per-frame UTF-8 flags, preset here, finished by fws_launch_unmask_stream
 int fws_launch_decode(fws_gpu_ctx *ctx, uint8_t *wire, uint64_t N, fws_frame_info *frames, uint32_t cap,
@@ -209,16 +196,6 @@ uint64_t fws_merge_super_tiles_cap(uint64_t n_tiles);   // bound over every n <=
 uint32_t fws_merge_tail_cap(uint64_t n_tiles);
 uint64_t fws_merge_st_nodes(uint64_t n_tiles);
 uint32_t fws_merge_comp_cap();
-// stream_kernels.hip: the one-launch decode k_stream (scan, resolve, frame list,
-// unmask; the default for streams of kFusedMin bytes and more); the multi-launch
-// path above runs after it, gated, as its fallback
-constexpr uint32_t kFusedStBytes = 32768;          // bytes per k_stream super tile
-constexpr uint64_t kFusedMin = 1ull << 20;          // streams shorter than this skip it
-bool fws_fused_enabled(uint64_t N);   // the hook's mode (fws_internal_set_fused) and N
-int fws_fused_ensure(fws_gpu_ctx *ctx, uint64_t N);
-int fws_launch_fused(fws_gpu_ctx *ctx, uint8_t *wire, uint64_t N, fws_frame_info *frames, uint32_t cap,
-                     fws_decode_result *res, hipStream_t s);
-const uint64_t *fws_fused_done(const fws_gpu_ctx *ctx);   // done granules (fws_launch_unmask_stream)
 int fws_launch_merge(fws_gpu_ctx *ctx, const uint8_t *wire, uint64_t N, uint32_t n_tiles, fws_frame_info *frames,
-                     uint32_t cap, fws_decode_result *res, uint8_t *utf8_ok, bool force_big, bool fused, uint32_t *zero_next,
+                     uint32_t cap, fws_decode_result *res, uint8_t *utf8_ok, bool force_big, uint32_t *zero_next,
                      hipStream_t s);

@@ -164,7 +164,6 @@ struct MergeParams {
     uint64_t n_units;                                // ceil(N / kUnit), clamped to the plan's capacity
     uint32_t force_big;                              // test hook: every ST on the big-ST path
     uint32_t *zero_next;                             // the next call's counter set (k_emit zeroes it)
-    uint32_t fused;                                  // k_stream was queued first: read its gate (fused_done)
     uint32_t *bg_nx, *bg_wt, *bg_lref, *bg_ptr, *bg_sc, *bg_mark;   // big-ST scratch [max_nodes]
     uint64_t max_nodes;
 
@@ -500,7 +499,6 @@ __global__ __launch_bounds__(kMThreads) void k_merge(MergeParams P) {
     MP_START(30);
     MP_T0();
     MP_INIT();
-    if (P.fused && fused_done(C)) return;            // k_stream decoded the stream (k_link returns too)
     // the tail-target bitmap k_link sets
     for (uint64_t w = (uint64_t)s * kMThreads + tid; w < P.tail_cap / 32u + 1u; w += (uint64_t)gridDim.x * kMThreads)
         P.tmark[w] = 0u;
@@ -1040,7 +1038,6 @@ __global__ __launch_bounds__(kMThreads) void k_link(MergeParams P) {
     MP_START(29);
     MP_T0();
     MP_INIT();
-    if (P.fused && fused_done(C)) return;
     const uint32_t x = blockIdx.x * kMThreads + tid;
     const uint64_t tx = P.tails[x < P.tail_cap ? x : 0u].exit;   // with the counters (read past M: unused)
     const uint32_t M = C[kCntTails];
@@ -1282,7 +1279,7 @@ __global__ __launch_bounds__(kMThreads) void k_emit(MergeParams P) {
     MP_INIT();
     if (s == 0)                                      // the next call's counter set
         for (uint32_t w = tid; w < kCntStride; w += kMThreads) P.zero_next[w] = 0u;
-    if (s >= P.n_st || (P.fused && fused_done(C))) return;
+    if (s >= P.n_st) return;
     const uint32_t fb = C[kCntFallback], e = P.st_entry[s], fbase = P.st_fbase[s], n = P.st_n[s];
     const uint32_t lim = C[kCntFrames];
     if (fb || e == kNone || fbase >= lim) return;
@@ -1460,7 +1457,7 @@ uint32_t fws_merge_tail_cap(uint64_t n_tiles) {
 }
 
 int fws_launch_merge(fws_gpu_ctx *ctx, const uint8_t *wire, uint64_t N, uint32_t n_tiles, fws_frame_info *frames,
-                     uint32_t cap, fws_decode_result *res, uint8_t *utf8_ok, bool force_big, bool fused, uint32_t *zero_next,
+                     uint32_t cap, fws_decode_result *res, uint8_t *utf8_ok, bool force_big, uint32_t *zero_next,
                      hipStream_t s) {
     fws_decode_ws &d = ctx->dec;
     MergeParams P;
@@ -1498,7 +1495,6 @@ int fws_launch_merge(fws_gpu_ctx *ctx, const uint8_t *wire, uint64_t N, uint32_t
     P.n_units = units < ctx->plan.unit_cap ? units : ctx->plan.unit_cap;
     P.force_big = force_big ? 1u : 0u;
     P.zero_next = zero_next;
-    P.fused = fused ? 1u : 0u;
     P.bg_nx = d.bg_nx;
     P.bg_wt = d.bg_wt;
     P.bg_lref = d.bg_lref;

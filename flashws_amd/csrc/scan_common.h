@@ -22,7 +22,7 @@ namespace fwsk {
 constexpr int kScanWaves = 4;                          // wavefronts per workgroup
 constexpr int kScanThreads = kScanWaves * 64;
 constexpr uint32_t kWCap = 1024;                       // node list capacity of a sparse tile
-constexpr uint32_t kCandCap = 256;           // k_scan / k_stream: candidates per tile (else dense)
+constexpr uint32_t kCandCap = 256;           // k_scan: candidates per tile (else dense)
 constexpr uint32_t kLiveCap = 64;            // live nodes per tile, one per lane
 constexpr uint32_t kDeadLane = 0xFFu;        // pointer jumping in registers: the chain dies
 // the scan's halo: the next tile's first bytes, enough for the two-byte test at

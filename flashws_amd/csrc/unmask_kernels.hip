@@ -379,13 +379,8 @@ __global__ __launch_bounds__(kBlock) void k_unmask_stream(uint8_t *base, uint64_
                                                           const fws_frame_info *__restrict__ fr, uint32_t cap,
                                                           const uint32_t *__restrict__ n_dev,
                                                           const uint32_t *__restrict__ unit_first, uint64_t n_units,
-                                                          uint8_t *__restrict__ ok, const uint32_t *fgate,
-                                                          const uint64_t *fdone, uint32_t fepoch,
+                                                          uint8_t *__restrict__ ok,
                                                           uint32_t *__restrict__ seam) {
-    // k_stream ran: nothing to do if it finished the stream; else skip the 32 KiB
-    // super tiles it unmasked (done granules tagged with its epoch, stream_kernels.hip)
-    const bool fran = fgate != nullptr && fgate[kDecodeFModeCounter] != 0u;
-    if (fran && fgate[kDecodeFFailCounter] == 0u) return;
     uint32_t n = *n_dev;
     if (n > cap) n = cap;
     if (n == 0) return;
@@ -398,7 +393,6 @@ __global__ __launch_bounds__(kBlock) void k_unmask_stream(uint8_t *base, uint64_
         // decode's scan read last -- those lines are still in the 256 MB
         // Infinity Cache (MALL) when this pass re-reads them
         const uint64_t u = kRev ? n_units - 1u - ui : ui;
-        if (fran && (uint32_t)(fdone[u / (kFusedStBytes / 4096u)] >> 40) == fepoch) continue;
         const uint64_t c0 = u * 4096u + uint64_t(lane) * 16u;
         // kUtf8 (VALU-heavier per unit): the unit's loads are issued before the frame
         // lookup, whose dependent round trips then overlap them
@@ -1351,8 +1345,7 @@ int fws_launch_unmask_sorted_utf8(uint8_t *base, const fws_frame_desc *d, uint32
 
 int fws_launch_unmask_stream(uint8_t *base, uint64_t N, const fws_frame_info *frames, uint32_t cap,
                              const uint32_t *n_dev, const uint32_t *unit_first, uint8_t *utf8_ok,
-                             const uint32_t *fgate, const uint64_t *fdone, uint32_t fepoch, uint32_t *seam,
-                             hipStream_t s) {
+                             uint32_t *seam, hipStream_t s) {
     const uint64_t units = (N + 4095) / 4096;
     if (units == 0 || cap == 0) return 0;
     const dim3 grid(grid_for_units(units)), blk(kBlock);
@@ -1360,23 +1353,23 @@ int fws_launch_unmask_stream(uint8_t *base, uint64_t N, const fws_frame_info *fr
     if (utf8_ok == nullptr) {
         if (v == 0)
             hipLaunchKernelGGL((k_unmask_stream<true, false, false>), grid, blk, 0, s, (uint8_t *)base, N, frames, cap,
-                               n_dev, unit_first, units, nullptr, fgate, fdone, fepoch, nullptr);
+                               n_dev, unit_first, units, nullptr, nullptr);
         else if (v == 1)
             hipLaunchKernelGGL((k_unmask_stream<true, false, true>), grid, blk, 0, s, (uint8_t *)base, N, frames, cap,
-                               n_dev, unit_first, units, nullptr, fgate, fdone, fepoch, nullptr);
+                               n_dev, unit_first, units, nullptr, nullptr);
         else if (v == 2)
             hipLaunchKernelGGL((k_unmask_stream<false, false, false>), grid, blk, 0, s, (uint8_t *)base, N, frames,
-                               cap, n_dev, unit_first, units, nullptr, fgate, fdone, fepoch, nullptr);
+                               cap, n_dev, unit_first, units, nullptr, nullptr);
         else
             hipLaunchKernelGGL((k_unmask_stream<false, false, true>), grid, blk, 0, s, (uint8_t *)base, N, frames,
-                               cap, n_dev, unit_first, units, nullptr, fgate, fdone, fepoch, nullptr);
+                               cap, n_dev, unit_first, units, nullptr, nullptr);
     } else {
         if (v == 1 || v == 3)
             hipLaunchKernelGGL((k_unmask_stream<true, true, true>), grid, blk, 0, s, (uint8_t *)base, N, frames, cap,
-                               n_dev, unit_first, units, utf8_ok, nullptr, nullptr, 0u, seam);
+                               n_dev, unit_first, units, utf8_ok, seam);
         else
             hipLaunchKernelGGL((k_unmask_stream<true, true, false>), grid, blk, 0, s, (uint8_t *)base, N, frames, cap,
-                               n_dev, unit_first, units, utf8_ok, nullptr, nullptr, 0u, seam);
+                               n_dev, unit_first, units, utf8_ok, seam);
         hipLaunchKernelGGL(k_utf8_seam, dim3((unsigned)((units + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
                            (const uint8_t *)base, N, frames, cap, n_dev, unit_first, units, utf8_ok, seam);
     }

@@ -96,15 +96,3 @@ def test_generator_streams_decode_to_their_descriptors(cfg):
             assert v == good
         assert 0 < ok.sum() < len(ok)
 
-
-def test_one_launch_decode_is_the_default():
-    """The one-launch stream decode (k_stream, stream_kernels.hip) is the default
-    for streams of 1 MiB and more (mode 1); fws_internal_set_fused(-1) only reads
-    the mode. A fresh process, so no other test's setting leaks in."""
-    import subprocess
-    import sys
-    code = "from flashws_amd import _lib; print(_lib.lib().fws_internal_set_fused(-1))"
-    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120,
-                         cwd=str(__import__("pathlib").Path(__file__).resolve().parents[1]))
-    assert out.returncode == 0, out.stderr
-    assert out.stdout.strip().splitlines()[-1] in ("0", "1"), out

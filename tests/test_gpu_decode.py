@@ -16,31 +16,24 @@ from wsframes import frame
 
 pytestmark = pytest.mark.gpu
 
-# mode -> (fws_internal_set_resolve_mode, fws_internal_set_fused)
-RESOLVE_MODES = {"super_tile": (0, 0), "big_st": (1, 0), "small_read": (2, 0), "fused": (0, 2)}
+# mode -> fws_internal_set_resolve_mode
+RESOLVE_MODES = {"super_tile": 0, "big_st": 1, "small_read": 2}
 CNT_FAILED = 9              # decode_common.h Counter::kCntFallback (the resolve failed)
 CNT_BIG = 12                # decode_common.h Counter::kCntBig (super tiles on the big-ST path)
-CNT_FMODE, CNT_FFAIL, CNT_FTIMEOUT = 13, 14, 17   # kCntFMode, kCntFFail, kCntFTimeout (k_stream)
 
 
 @pytest.fixture(params=list(RESOLVE_MODES), autouse=True)
 def resolve_mode(request):
     """Every decode test runs on every decode path: the multi-launch path with
     the super-tile resolve in LDS (merge_kernels.hip) and with the big-ST path
-    forced for every super tile; the RX session's one-launch small-read kernel
-    (small_kernels.hip; streams <= 128 KiB with <= 256 headers, the rest fall
-    back to the super-tile path as the session does); and the one-pass decode
-    (stream_kernels.hip, the default for streams of 1 MiB and more) forced for
-    every stream, with the multi-launch path as its fallback where it declines
-    (dense tiles, protocol errors: the super tiles it finished are skipped)."""
+    forced for every super tile; and the RX session's one-launch small-read
+    kernel (small_kernels.hip; streams <= 128 KiB with <= 256 headers, the rest
+    fall back to the super-tile path as the session does)."""
     from flashws_amd import _lib
     L = _lib.lib()
-    rm, fm = RESOLVE_MODES[request.param]
-    old = L.fws_internal_set_resolve_mode(rm)
-    oldf = L.fws_internal_set_fused(fm)
+    old = L.fws_internal_set_resolve_mode(RESOLVE_MODES[request.param])
     yield request.param
     L.fws_internal_set_resolve_mode(old)
-    L.fws_internal_set_fused(oldf)
 
 
 def counters(ctx):
@@ -49,12 +42,6 @@ def counters(ctx):
     out = (C.c_uint32 * 32)()
     assert _lib.lib().fws_internal_decode_counters(ctx.h, out, 32) == 0
     return list(out)
-
-
-def fused_finished(ctx):
-    """True if the last decode ran k_stream and it finished the whole stream."""
-    c = counters(ctx)
-    return c[CNT_FMODE] == 1 and c[CNT_FFAIL] == 0 and c[CNT_FTIMEOUT] == 0
 
 
 def fell_back(ctx):
@@ -234,8 +221,6 @@ def test_c3_mixed_parity(ctx, cuda, resolve_mode):
     assert int(r["n_frames"]) == len(descs)
     if resolve_mode == "super_tile":
         assert not fell_back(ctx), "C3 must resolve on the super-tile path with LDS tables"
-    if resolve_mode == "fused":
-        assert fused_finished(ctx), "C3 must decode in one k_stream pass"
 
 
 def test_c2_full_parity(ctx, cuda, resolve_mode):
@@ -244,8 +229,6 @@ def test_c2_full_parity(ctx, cuda, resolve_mode):
     assert int(r["n_frames"]) == 65536
     if resolve_mode == "super_tile":
         assert not fell_back(ctx), "C2 must resolve on the super-tile path with LDS tables"
-    if resolve_mode == "fused":
-        assert fused_finished(ctx), "C2 must decode in one k_stream pass"
 
 
 @pytest.mark.parametrize("n_frames,payload", [(200_000, 64), (200_000, 120), (600_000, 16)])

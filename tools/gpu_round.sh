@@ -17,7 +17,6 @@
 #   sq_decode    SQ counters of the C3 decode kernels
 #   trace        phase clocks of k_scan and per-workgroup timelines of the resolve kernels
 #                (FWS_SCAN_PROF build: make -C flashws_amd/csrc prof, built beforehand)
-#   strace       per-super-tile clocks of k_stream (same prof build)
 set -o pipefail
 ROUND=${ROUND:-r03}
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
@@ -73,12 +72,8 @@ for step in "$@"; do
         timeout -k 10 300 python tools/prof_scan.py > "$O/prof_scan.json" 2> "$O/prof_scan.err" || fail trace $? "$O/prof_scan.err"
         timeout -k 10 300 python tools/prof_merge_trace.py > "$O/prof_merge_trace.json" 2> "$O/prof_merge_trace.err" \
             || fail trace $? "$O/prof_merge_trace.err" ;;
-    strace)
-        timeout -k 10 300 python tools/prof_stream.py all 4 > "$O/prof_stream.json" 2> "$O/prof_stream.err" \
-            || fail strace $? "$O/prof_stream.err"
-        cat "$O/prof_stream.json" | head -80 ;;
     dectests)
-        timeout -k 10 900 python -u -m pytest tests/test_gpu_decode.py tests/test_gpu_fused.py tests/test_gpu_configs.py -x -v --timeout 120 --timeout-method thread \
+        timeout -k 10 900 python -u -m pytest tests/test_gpu_decode.py tests/test_gpu_configs.py -x -v --timeout 120 --timeout-method thread \
             > "$O/dec_tests.log" 2>&1 || fail dectests $? "$O/dec_tests.log"
         tail -1 "$O/dec_tests.log" ;;
     tdec)

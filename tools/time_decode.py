@@ -1,8 +1,7 @@
 #!/usr/bin/env python3
 """Stream-decode timing of C2-stream, C3 and the dense 64 B workload (HIP events
-over back-to-back calls, >= 1 GiB of rotating device batches), for each decode
-path: the one-launch k_stream (fws_internal_set_fused 1, the default) and the
-multi-launch path (0). Prints one JSON object; checks frame counts.
+over back-to-back calls, >= 1 GiB of rotating device batches). Prints one JSON
+object; checks frame counts.
 
 usage: python tools/time_decode.py [reps]"""
 import json
@@ -15,9 +14,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from flashws_amd import _lib, gpu  # noqa: E402
 
 
-def time_cfg(name, wire, n, reps, mode):
+def time_cfg(name, wire, n, reps):
     L = _lib.lib()
-    old = L.fws_internal_set_fused(mode)
     dev = torch.device("cuda:0")
     nbuf = max(4, -(-(1 << 30) // len(wire)))
     bufs = [torch.from_numpy(wire).to(dev) for _ in range(nbuf)]
@@ -37,17 +35,12 @@ def time_cfg(name, wire, n, reps, mode):
     t = e0.elapsed_time(e1) / 1e3 / reps
     r = gpu.read_result(res)
     c = gpu.decode_counters(ctx)
-    import ctypes as C
-    raw = (C.c_uint32 * 32)()
-    L.fws_internal_decode_counters(ctx.h, raw, 32)
+
     payload = int(gpu.read_frames(frames, n)["payload_len"].sum())
     alg = len(wire) + payload
     ctx.close()
-    L.fws_internal_set_fused(old)
     return {"ms": round(t * 1e3, 4), "frac": round(alg / t / 8e12, 4), "status": int(r["status"]),
-            "frames_ok": int(r["n_frames"]) == n, "fmode": raw[13],
-            "first_failed_st": ((~raw[14]) & 0xFFFFFFFF) if raw[14] else None, "timeouts": raw[17],
-            "survivors": c["survivors"]}
+            "frames_ok": int(r["n_frames"]) == n, "survivors": c["survivors"], "big": c["big_super_tiles"]}
 
 
 def main():
@@ -56,9 +49,8 @@ def main():
     cfgs = [("C2", gpu.config_c2()), ("C3", gpu.config_c3()),
             ("dense64", gpu.config_c2(n_frames=200_000, payload=64))]
     for name, (wire, descs, _) in cfgs:
-        for mode in (1, 0):
-            out[f"{name}_{'k_stream' if mode else 'multi'}"] = time_cfg(name, wire, len(descs), reps, mode)
-            print(name, mode, out[f"{name}_{'k_stream' if mode else 'multi'}"], flush=True, file=sys.stderr)
+        out[name] = time_cfg(name, wire, len(descs), reps)
+        print(name, out[name], flush=True, file=sys.stderr)
     print(json.dumps(out))
 
 

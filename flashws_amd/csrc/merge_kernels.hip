@@ -545,10 +545,7 @@ __global__ __launch_bounds__(kMThreads) void k_merge(MergeParams P) {
     }
     uint32_t n;
     const uint32_t b = block_excl<uint32_t>(c, L.red32, &n);
-    if (tid == 0) {
-        atomicAdd(&C[kCntSurv], n);
-        P.st_n[s] = n;
-    }
+    if (tid == 0) P.st_n[s] = n;        // (the survivor total: summed by the path resolve, no hot atomic)
     if (tid < kStTiles) {
         L.tcnt[tid] = c;
         L.tsp[tid] = sp;
@@ -585,10 +582,12 @@ __global__ __launch_bounds__(kMThreads) void k_merge(MergeParams P) {
             // (i < n: past the last survivor every later tile has tbase n, and a
             // partial last super tile has up to 255 of them to walk)
             while (i < n && tl + 1 < kStTiles && L.tbase[tl + 1] <= i) ++tl;
-            nid[j] = i < n ? P.sid(t0 + tl, L.tsp[tl], i - L.tbase[tl]) : 0u;
+            // past n: a slot of this ST's first tile (a global slot 0 for every
+            // thread past n of every super tile was one line all of them queued on)
+            nid[j] = i < n ? P.sid(t0 + tl, L.tsp[tl], i - L.tbase[tl]) : t0 * kSlots + (j & (kSlots - 1u));
         }
 #pragma unroll
-        for (uint32_t j = 0; j < kPer; ++j) r[j] = *P.rec(nid[j]);   // unconditional: slot 0 past n
+        for (uint32_t j = 0; j < kPer; ++j) r[j] = *P.rec(nid[j]);   // unconditional (a local dummy past n)
 #pragma unroll
         for (uint32_t j = 0; j < kPer; ++j) {
             const uint32_t i = i0 + j;
@@ -936,16 +935,24 @@ __device__ void resolve_path(const MergeParams &P, PathLds &G) {
 
     // exclusive prefix of the per-ST frame counts, in ST order
     constexpr uint32_t kSper = 8;
-    uint32_t nf_path = 0;
+    uint32_t nf_path = 0, nsurv = 0;
     for (uint32_t s0 = 0; s0 < n_st; s0 += kSper * kMThreads) {
         const uint32_t lo = s0 + tid * kSper;
-        uint32_t fc[kSper];
-        uint32_t fs = 0;
+        uint32_t fc[kSper], sn[kSper];
+        uint32_t fs = 0, ss = 0;
 #pragma unroll
-        for (uint32_t j = 0; j < kSper; ++j) fc[j] = lo + j < n_st ? P.st_fbase[lo + j] : 0u;
+        for (uint32_t j = 0; j < kSper; ++j) {
+            fc[j] = lo + j < n_st ? P.st_fbase[lo + j] : 0u;
+            sn[j] = lo + j < n_st ? P.st_n[lo + j] : 0u;
+        }
 #pragma unroll
-        for (uint32_t j = 0; j < kSper; ++j) fs += fc[j];
-        uint32_t ft;
+        for (uint32_t j = 0; j < kSper; ++j) {
+            fs += fc[j];
+            ss += sn[j];
+        }
+        uint32_t ft, st;
+        (void)block_excl<uint32_t>(ss, G.red32, &st);
+        nsurv += st;
         uint32_t fpre = nf_path + block_excl<uint32_t>(fs, G.red32, &ft);
 #pragma unroll
         for (uint32_t j = 0; j < kSper; ++j) {
@@ -957,6 +964,7 @@ __device__ void resolve_path(const MergeParams &P, PathLds &G) {
     MP_MARK(15);
     MP_ADD(16, mc);
     if (tid != 0) return;
+    C[kCntSurv] = nsurv;
     if (root != kNone && !G.end_set) {               // no terminal on the path: cannot happen
         atomicOr(&C[kCntFallback], 1u);
         fws_decode_result r{};
@@ -968,7 +976,7 @@ __device__ void resolve_path(const MergeParams &P, PathLds &G) {
     // terminal: the path's last header, then ParseFrameHdr from its exit on error
     fws_decode_result r{};
     r.status = FWS_OK;
-    r.n_survivors = ld_acq(&C[kCntSurv]);
+    r.n_survivors = nsurv;
     uint64_t pos = 0;
     bool walk = N > 0 && root == kNone;              // no chain from offset 0 survived
     if (root != kNone) {
@@ -1389,7 +1397,7 @@ __global__ __launch_bounds__(kMThreads) void k_emit(MergeParams P) {
     // their stream-space plan units
     fws_frame_info rc[kPer];                         // unconditional (slot 0 for the unused ones):
 #pragma unroll                                        // conditional loads each waited for their data
-    for (uint32_t j = 0; j < kPer; ++j) rc[j] = *P.rec(fr[j] ? nd[j].sid : 0u);
+    for (uint32_t j = 0; j < kPer; ++j) rc[j] = *P.rec(fr[j] ? nd[j].sid : s * P.st_tiles * kSlots + j);
     uint32_t f = fbase + fpre;
 #pragma unroll
     for (uint32_t j = 0; j < kPer; ++j) {

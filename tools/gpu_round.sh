@@ -80,6 +80,11 @@ for step in "$@"; do
         timeout -k 10 300 python tools/time_decode.py 20 > "$O/time_decode.json" 2> "$O/time_decode.err" \
             || fail tdec $? "$O/time_decode.err"
         cat "$O/time_decode.err" | grep -v amdgpu.ids ;;
+    kdec)
+        for c in c3 dense; do
+            prof "kdec_$c" 300 --kernel-trace --stats -f csv -d "$O/kdec_$c" -o run -- python3 "$R/tools/run_decode.py" $c 20
+        done
+        for c in c3 dense; do cut -d, -f1-5 "$O/kdec_$c/run_kernel_stats.csv" | head -12; done ;;
     *) echo "unknown step $step"; exit 2 ;;
     esac
 done

@@ -405,13 +405,13 @@ int fws_decode_ensure(fws_gpu_ctx *ctx, uint64_t N, uint32_t cap) {
     al(&d.stage_info, nt * kSlots * sizeof(fws_frame_info));
     al(&d.spill_info, ns * sizeof(fws_frame_info)); al(&d.tile_spill, nt * 4);
     // super-tile resolve: results per slot id, EXIT tails, per-ST bases, big-ST scratch
-    rel(d.nres); rel(d.tails); rel(d.gnx); rel(d.tmark); rel(d.comp); rel(d.st_nodes); rel(d.st_n); rel(d.st_entry);
+    rel(d.nres); rel(d.tails); rel(d.gnx); rel(d.tpk); rel(d.tmark); rel(d.comp); rel(d.st_nodes); rel(d.st_n); rel(d.st_entry);
     rel(d.st_fbase); rel(d.bg_nx); rel(d.bg_wt); rel(d.bg_lref); rel(d.bg_ptr); rel(d.bg_sc); rel(d.bg_mark);
     const uint64_t nst = fws_merge_super_tiles_cap(nt);
     const uint32_t tcap = fws_merge_tail_cap(nt);
     const uint64_t nn = nt * kSlots + ns;
     al(&d.nres, nn * sizeof(fws_node_res));
-    al(&d.tails, (uint64_t)tcap * sizeof(fws_tail_rec)); al(&d.gnx, (uint64_t)tcap * 4); al(&d.tmark, ((uint64_t)tcap / 32 + 1) * 4);
+    al(&d.tails, (uint64_t)tcap * sizeof(fws_tail_rec)); al(&d.gnx, (uint64_t)tcap * 4); al(&d.tpk, (uint64_t)tcap * 16); al(&d.tmark, ((uint64_t)tcap / 32 + 1) * 4);
     al(&d.comp, (uint64_t)fws_merge_comp_cap() * 4);
     al(&d.st_nodes, fws_merge_st_nodes(nt) * sizeof(fws_st_node)); al(&d.st_n, nst * 4);
     al(&d.st_entry, nst * 4); al(&d.st_fbase, nst * 4);

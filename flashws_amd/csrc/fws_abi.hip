@@ -127,6 +127,7 @@ void fws_gpu_ctx_destroy(fws_gpu_ctx *ctx) {
     dev_free(d.nres);
     dev_free(d.tails);
     dev_free(d.gnx);
+    dev_free(d.tpk);
     dev_free(d.tmark);
     dev_free(d.comp);
     dev_free(d.st_nodes);

@@ -114,6 +114,8 @@ struct fws_decode_ws {
     fws_node_res *nres = nullptr;          // [max_nodes]
     fws_tail_rec *tails = nullptr;         // [tail_cap]
     uint32_t *gnx = nullptr;               // [tail_cap] next tail / terminal
+    uint64_t *tpk = nullptr;               // [2 * tail_cap] per tail: the landing entry, its frame
+                                           //   count, end record, ST (k_link -> its last workgroup)
     uint32_t *tmark = nullptr;             // [tail_cap / 32 + 1] tails that are some tail's next
     uint32_t *comp = nullptr;              // [fws_merge_comp_cap()] marked tails, compacted
     fws_st_node *st_nodes = nullptr;       // [max_st * kStCap] survivors per super tile (8 B each)

@@ -150,6 +150,7 @@ struct MergeParams {
     fws_node_res *nres;
     fws_tail_rec *tails;
     uint32_t *gnx;
+    uint64_t *tpk;                                   // [2 * tail_cap] tail_pack (k_link -> its last workgroup)
     uint32_t *tmark;                                 // tail-target bitmap (tail_cap / 32 + 1 words)
     uint32_t *comp;                                  // [kCompCap] compact index -> tail index
     fws_st_node *st_nodes;                           // [n_st][kStCap]
@@ -162,15 +163,19 @@ struct MergeParams {
     uint8_t *utf8_ok;                                // optional: preset per frame (TEXT, FIN, complete)
     uint32_t *unit_first;                            // unmask plan (fws_plan_ws), stream space
     uint64_t n_units;                                // ceil(N / kUnit), clamped to the plan's capacity
-    uint32_t force_big;                              // test hook: every ST on the big-ST path
+    uint32_t force_big;                              // test hook: every ST on the big-ST path, and the
+                                                     //   path resolve on its global-table branches
     uint32_t *zero_next;                             // the next call's counter set (k_emit zeroes it)
     uint32_t *bg_nx, *bg_wt, *bg_lref, *bg_ptr, *bg_sc, *bg_mark;   // big-ST scratch [max_nodes]
     uint64_t max_nodes;
 
     __device__ __forceinline__ bool big(uint32_t n) const { return force_big || n > kStCap; }
     // the record of a chain's tail survivor in ST s (fws_node_res::tail of a non-EXIT kind)
+    __device__ __forceinline__ uint32_t tail_sid(uint32_t s, const fws_node_res &r) const {
+        return (r.kind & kBigBit) ? r.tail : st_nodes[(uint64_t)s * kStCap + r.tail].sid;
+    }
     __device__ __forceinline__ const fws_frame_info *tail_rec(uint32_t s, const fws_node_res &r) const {
-        return (r.kind & kBigBit) ? rec(r.tail) : rec(st_nodes[(uint64_t)s * kStCap + r.tail].sid);
+        return rec(tail_sid(s, r));
     }
 
     // slot id of survivor r of tile t (stage slots, or the tile's spill run)
@@ -218,6 +223,12 @@ struct MergeParams {
 
 __device__ __forceinline__ uint32_t ld_acq(const uint32_t *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t ld_acq64(const uint64_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void gst64(uint64_t *p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <typename T>
@@ -714,15 +725,25 @@ __global__ __launch_bounds__(kMThreads) void k_merge(MergeParams P) {
 }
 
 // ------------------------------------------------------------- k_link + path
+constexpr uint32_t kStLds = 2048;                   // ST entries / bases in LDS up to this many STs (1 GiB)
+constexpr uint32_t kRegComp = 4u * kMThreads;       // marked tails whose tail_pack stays in registers
+
+// tail_pack of EXIT tail x (k_link's thread for x -> the last workgroup, sc1):
+// tpk[2x] = landing survivor as its ST's entry | frames of its chain in that ST << 32,
+// tpk[2x+1] = record of the path's last header if next(x) ends the path | (ST |
+// end kind << 30) << 32. A tail whose exit is no survivor: entry kNone, kind DEAD,
+// the last header is the tail's own record.
 struct PathLds {
     uint32_t words[kTailCapMax / 32];                // tail-target bitmap (+ the root's tail)
-    uint32_t wpre[kTailCapMax / 32];                 // marked tails before each word
-    uint16_t cnx[kCompCap];                          // compact next, or kCTerm (comp: P.comp)
-    uint32_t kb[2][kCompCap / 32];                   // kept bitmaps
+    uint16_t wpre[kTailCapMax / 32];                 // marked tails before each word (<= kCompCap)
+    uint16_t cnx[kCompCap];                          // compact next, or kCTerm
+    uint32_t kb[2][kCompCap / 32];                   // kept bitmaps (first: the compact list, mc <= kRegComp)
+    uint32_t sent[kStLds];                           // per ST: entry, frame count -> base (n_st <= kStLds)
+    uint32_t sfb[kStLds];
     uint32_t red32[kMWaves];
-    uint32_t root, rt, crt, root_ent, root_cnt, end_kind, end_set;
-    const fws_frame_info *end_rec;                   // the path's last header
+    uint32_t root, rt, crt, root_ent, root_cnt, end_kind, end_set, end_sid;
 };
+static_assert(sizeof(PathLds) <= 160u * 1024u, "k_link LDS");
 
 // Batched loop over c = tid + k * kMThreads < n: the loads of up to 4
 // iterations are issued before any of their uses.
@@ -762,23 +783,32 @@ __device__ void fail_capacity(const MergeParams &P) {
 }
 
 // The path from offset 0 over the target tails: ST entries and frame bases,
-// terminal, result. Runs in the last k_link workgroup.
+// terminal, result. Runs in the last k_link workgroup. Latency-bound: every
+// global load of a phase is issued before its first use, the per-tail data
+// arrives packed (tail_pack, one round of loads), and up to kStLds super tiles
+// keep their entries and bases in LDS until the final stores.
 __device__ void resolve_path(const MergeParams &P, PathLds &G) {
     uint32_t *const C = P.counters;
     const uint32_t tid = threadIdx.x;
     MP_INIT();
-    // k_merge's record of the root (an earlier launch), loaded beside the flags below
+    const uint32_t n_st = P.n_st;
+    const uint64_t N = P.N;
+    const bool lds_st = n_st <= kStLds && !P.force_big;
+    // the phase's loads, all issued up front: the flags and counts this launch
+    // handed off (sc1), k_merge's record of the root, the survivors per ST
+    const uint32_t fbk = ld_acq(&C[kCntFallback]), ovf = ld_acq(&C[kCntOverflow]), M = ld_acq(&C[kCntTails]);
     const uint32_t root_state = tid == 0 ? C[kCntRoot] : 0u;
     const uint32_t root_sid = tid == 0 ? C[kCntRootSid] : 0u;
     const uint32_t root_tail = tid == 0 ? C[kCntRootTail] : 0u;
     const uint32_t root_cnt = tid == 0 ? C[kCntRootCnt] : 0u;
-    if (ld_acq(&C[kCntFallback]) || (ld_acq(&C[kCntOverflow]) & 1u)) {
+    constexpr uint32_t kSper = 8;                    // STs per thread in a prefix pass
+    uint32_t sn0[kSper];
+#pragma unroll
+    for (uint32_t j = 0; j < kSper; ++j) sn0[j] = tid * kSper + j < n_st ? P.st_n[tid * kSper + j] : 0u;
+    if (fbk || (ovf & 1u)) {
         fail_capacity(P);                            // k_scan's spill or the tail list overflowed
         return;
     }
-    const uint32_t M = ld_acq(&C[kCntTails]);
-    const uint32_t n_st = P.n_st;
-    const uint64_t N = P.N;
     if (tid == 0) {
         uint32_t root = kNone, rt = kNone;
         fws_node_res rr{0, 0, 0, 0};
@@ -794,7 +824,7 @@ __device__ void resolve_path(const MergeParams &P, PathLds &G) {
             if (root_state == 0u) rr = P.nres[root];
             if (res_kind(rr) == kKindExit) rt = rr.tail;
             else {                                   // the root's chain ends in ST 0
-                G.end_rec = P.tail_rec(0, rr);
+                G.end_sid = P.tail_sid(0, rr);
                 G.end_kind = res_kind(rr);
                 G.end_set = 1;
             }
@@ -804,14 +834,25 @@ __device__ void resolve_path(const MergeParams &P, PathLds &G) {
         G.root_ent = rr.ent;
         G.root_cnt = rr.cnt;
     }
-    // ST bases start from zero counts
-    for (uint32_t s = tid; s < n_st; s += kMThreads) {
-        P.st_entry[s] = kNone;
-        P.st_fbase[s] = 0;
+    // ST entries and frame counts start empty
+    if (lds_st) {
+        for (uint32_t s = tid; s < n_st; s += kMThreads) {
+            G.sent[s] = kNone;
+            G.sfb[s] = 0;
+        }
+    } else {
+        for (uint32_t s = tid; s < n_st; s += kMThreads) {
+            P.st_entry[s] = kNone;
+            P.st_fbase[s] = 0;
+        }
     }
     __syncthreads();
     MP_MARK(10);
     const uint32_t root = G.root, rt = G.rt;
+    auto set_entry = [&](uint32_t s, uint32_t ent, uint32_t cnt) {
+        if (lds_st) { G.sent[s] = ent; G.sfb[s] = cnt; }
+        else { P.st_entry[s] = ent; P.st_fbase[s] = cnt; }
+    };
 
     // compact the marked tails (every next() target, plus the root's tail), in tail order
     const uint32_t words = (M + 31u) / 32u;
@@ -832,13 +873,17 @@ __device__ void resolve_path(const MergeParams &P, PathLds &G) {
         fail_capacity(P);
         return;
     }
+    // mc <= kRegComp: the compact list in LDS (kb, unused until the fixpoint) and
+    // each thread's tail_packs in registers from here to the entries
+    const bool reg = mc <= kRegComp && !P.force_big;
+    uint32_t *const comp = reg ? &G.kb[0][0] : P.comp;
     for (uint32_t w = w0; w < w1; ++w) {
-        G.wpre[w] = pre;
+        G.wpre[w] = (uint16_t)pre;
         uint32_t v = G.words[w];
         while (v) {
             const uint32_t b = (uint32_t)__ffs(v) - 1u;
             v &= v - 1u;
-            P.comp[pre++] = w * 32u + b;
+            comp[pre++] = w * 32u + b;
         }
     }
     __syncthreads();
@@ -846,8 +891,26 @@ __device__ void resolve_path(const MergeParams &P, PathLds &G) {
     auto rank = [&](uint32_t x) -> uint32_t {
         return G.wpre[x >> 5] + (uint32_t)__popc(G.words[x >> 5] & ((1u << (x & 31u)) - 1u));
     };
-    batched4(mc, [&](uint32_t c) { return ld_acq(&P.gnx[P.comp[c]]); },
-             [&](uint32_t c, uint32_t g) { G.cnx[c] = g >= kGTerm ? kCTerm : (uint16_t)rank(g); });
+    uint64_t pa[4] = {0, 0, 0, 0}, pb[4] = {0, 0, 0, 0};
+    if (reg) {
+        uint32_t g[4];
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) {
+            const uint32_t c = tid + j * kMThreads;
+            const uint32_t x = c < mc ? comp[c] : 0u;  // x = 0 past mc: unused loads of tail 0
+            g[j] = ld_acq(&P.gnx[x]);
+            pa[j] = ld_acq64(&P.tpk[2u * x]);
+            pb[j] = ld_acq64(&P.tpk[2u * x + 1u]);
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) {
+            const uint32_t c = tid + j * kMThreads;
+            if (c < mc) G.cnx[c] = g[j] >= kGTerm ? kCTerm : (uint16_t)rank(g[j]);
+        }
+    } else {
+        batched4(mc, [&](uint32_t c) { return ld_acq(&P.gnx[P.comp[c]]); },
+                 [&](uint32_t c, uint32_t g) { G.cnx[c] = g >= kGTerm ? kCTerm : (uint16_t)rank(g); });
+    }
     if (tid == 0) G.crt = rt == kNone ? kNone : rank(rt);
     __syncthreads();
     MP_MARK(12);
@@ -894,56 +957,46 @@ __device__ void resolve_path(const MergeParams &P, PathLds &G) {
     }
 
     // entries: the root, and every kept tail's landing survivor, with their chain counts
-    if (tid == 0 && root != kNone) {
-        P.st_entry[0] = G.root_ent;
-        P.st_fbase[0] = G.root_cnt;
-    }
-    for (uint32_t base = tid; base < mc; base += 4u * kMThreads) {
-        fws_tail_rec tr[4];
-        fws_node_res nr[4];
-        bool kept[4];
+    if (tid == 0 && root != kNone) set_entry(0, G.root_ent, G.root_cnt);
+    auto entry = [&](uint32_t c, uint64_t a, uint64_t b) {
+        if (!((ka[c >> 5] >> (c & 31u)) & 1u)) return;
+        const uint32_t ent = (uint32_t)a, hi = (uint32_t)(b >> 32);
+        if (ent != kNone) set_entry(hi & 0x3FFFFFFFu, ent, (uint32_t)(a >> 32));
+        if (G.cnx[c] == kCTerm) {                    // exactly one kept tail ends the path
+            G.end_sid = (uint32_t)b;
+            G.end_kind = hi >> 30;
+            G.end_set = 1;
+        }
+    };
+    if (reg) {
 #pragma unroll
         for (uint32_t j = 0; j < 4; ++j) {
-            const uint32_t c = base + j * kMThreads;
-            kept[j] = c < mc && ((ka[c >> 5] >> (c & 31u)) & 1u);
-            const uint32_t x = P.comp[kept[j] ? c : base];    // unconditional loads (base < mc)
-            tr[j] = P.tails[x];
-            tr[j].w = ld_acq(&P.tails[x].w);                  // handed off in this launch
+            const uint32_t c = tid + j * kMThreads;
+            if (c < mc) entry(c, pa[j], pb[j]);
         }
-#pragma unroll
-        for (uint32_t j = 0; j < 4; ++j) nr[j] = P.nres[kept[j] && tr[j].w != kTermDead ? tr[j].w : 0u];
-#pragma unroll
-        for (uint32_t j = 0; j < 4; ++j) {
-            if (!kept[j]) continue;
-            const uint32_t c = base + j * kMThreads;
-            const bool ends = G.cnx[c] == kCTerm;    // exactly one kept tail ends the path
-            if (tr[j].w == kTermDead) {
-                if (ends) { G.end_rec = P.rec(tr[j].id); G.end_kind = kKindDead; G.end_set = 1; }
-                continue;
-            }
-            P.st_entry[tr[j].wst] = nr[j].ent;
-            P.st_fbase[tr[j].wst] = nr[j].cnt;
-            if (ends) {
-                G.end_rec = P.tail_rec(tr[j].wst, nr[j]);
-                G.end_kind = res_kind(nr[j]);
-                G.end_set = 1;
-            }
-        }
+    } else {
+        batched4(mc, [&](uint32_t c) {
+                     const uint32_t x = P.comp[c];
+                     return ulonglong2{ld_acq64(&P.tpk[2u * x]), ld_acq64(&P.tpk[2u * x + 1u])};
+                 },
+                 [&](uint32_t c, ulonglong2 v) { entry(c, v.x, v.y); });
     }
     __syncthreads();
     MP_MARK(14);
 
-    // exclusive prefix of the per-ST frame counts, in ST order
-    constexpr uint32_t kSper = 8;
+    // exclusive prefix of the per-ST frame counts, in ST order; every ST's entry
+    // and base stored for k_emit
     uint32_t nf_path = 0, nsurv = 0;
     for (uint32_t s0 = 0; s0 < n_st; s0 += kSper * kMThreads) {
         const uint32_t lo = s0 + tid * kSper;
-        uint32_t fc[kSper], sn[kSper];
+        uint32_t fc[kSper], sn[kSper], en[kSper];
         uint32_t fs = 0, ss = 0;
 #pragma unroll
         for (uint32_t j = 0; j < kSper; ++j) {
-            fc[j] = lo + j < n_st ? P.st_fbase[lo + j] : 0u;
-            sn[j] = lo + j < n_st ? P.st_n[lo + j] : 0u;
+            const bool in = lo + j < n_st;
+            fc[j] = !in ? 0u : lds_st ? G.sfb[lo + j] : P.st_fbase[lo + j];
+            en[j] = !in ? kNone : lds_st ? G.sent[lo + j] : 0u;
+            sn[j] = s0 == 0 ? sn0[j] : in ? P.st_n[lo + j] : 0u;
         }
 #pragma unroll
         for (uint32_t j = 0; j < kSper; ++j) {
@@ -956,7 +1009,10 @@ __device__ void resolve_path(const MergeParams &P, PathLds &G) {
         uint32_t fpre = nf_path + block_excl<uint32_t>(fs, G.red32, &ft);
 #pragma unroll
         for (uint32_t j = 0; j < kSper; ++j) {
-            if (lo + j < n_st) P.st_fbase[lo + j] = fpre;
+            if (lo + j < n_st) {
+                P.st_fbase[lo + j] = fpre;
+                if (lds_st) P.st_entry[lo + j] = en[j];
+            }
             fpre += fc[j];
         }
         nf_path += ft;
@@ -980,7 +1036,7 @@ __device__ void resolve_path(const MergeParams &P, PathLds &G) {
     uint64_t pos = 0;
     bool walk = N > 0 && root == kNone;              // no chain from offset 0 survived
     if (root != kNone) {
-        const fws_frame_info fi = *G.end_rec;
+        const fws_frame_info fi = *P.rec(G.end_sid);
         pos = G.end_kind == kKindInc ? fi.hdr_off : exit_of(fi);
         walk = G.end_kind == kKindDead;
     }
@@ -1029,8 +1085,9 @@ __device__ void resolve_path(const MergeParams &P, PathLds &G) {
     MP_MARK(17);
 }
 
-// One thread per EXIT tail: the survivor its exit lands on, next(tail) and
-// the target bitmap. The last workgroup (atomic ticket) resolves the path.
+// One thread per EXIT tail: the survivor its exit lands on, next(tail), the
+// tail's tail_pack and the target bitmap. The last workgroup (atomic ticket)
+// resolves the path.
 // Hand-off inside the launch without release / acquire fences
 // (cdna_hip_programming.md Guideline 16, MI355X_MICROARCH.md "Valid forms",
 // first row): every handed-off word is stored sc1 (relaxed agent atomic
@@ -1047,18 +1104,24 @@ __global__ __launch_bounds__(kMThreads) void k_link(MergeParams P) {
     MP_T0();
     MP_INIT();
     const uint32_t x = blockIdx.x * kMThreads + tid;
-    const uint64_t tx = P.tails[x < P.tail_cap ? x : 0u].exit;   // with the counters (read past M: unused)
+    const fws_tail_rec &trx = P.tails[x < P.tail_cap ? x : 0u];   // with the counters (read past M: unused)
+    const uint64_t tx = trx.exit;
+    const uint32_t tid_rec = trx.id;
     const uint32_t M = C[kCntTails];
     if (x < M && !C[kCntFallback]) {
-        fws_tail_rec &tr = P.tails[x];
         const uint32_t w = P.find_node(tx);
-        uint32_t g = kGTerm | kKindDead;
+        const uint32_t wst = (uint32_t)(tx >> P.st_shift);
+        uint32_t g = kGTerm | kKindDead, ent = kNone, cnt = 0, esid = tid_rec;
         if (w != kTermDead) {
-            __hip_atomic_store(&tr.w, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             const fws_node_res r = P.nres[w];
             g = res_kind(r) == kKindExit ? r.tail : (kGTerm | res_kind(r));
+            ent = r.ent;
+            cnt = r.cnt;
+            if (g >= kGTerm) esid = P.tail_sid(wst, r);   // the path's last header if it ends here
         }
-        __hip_atomic_store(&P.gnx[x], g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        gst64(&P.tpk[2u * x], (uint64_t)ent | ((uint64_t)cnt << 32));
+        gst64(&P.tpk[2u * x + 1u], (uint64_t)esid | ((uint64_t)(wst | ((g >= kGTerm ? g & 3u : 0u) << 30)) << 32));
+        gst(&P.gnx[x], g);
         if (g < kGTerm) atomicOr(&P.tmark[g >> 5], 1u << (g & 31u));
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains
@@ -1488,6 +1551,7 @@ int fws_launch_merge(fws_gpu_ctx *ctx, const uint8_t *wire, uint64_t N, uint32_t
     P.nres = d.nres;
     P.tails = d.tails;
     P.gnx = d.gnx;
+    P.tpk = d.tpk;
     P.tmark = d.tmark;
     P.comp = d.comp;
     P.st_nodes = d.st_nodes;

@@ -3,7 +3,7 @@
 over back-to-back calls, >= 1 GiB of rotating device batches). Prints one JSON
 object; checks frame counts.
 
-usage: python tools/time_decode.py [reps]"""
+usage: python tools/time_decode.py [reps] [--lib PATH]   (--lib: an A/B build, e.g. libfws_gpu_exp.so)"""
 import json
 import os
 import sys
@@ -11,7 +11,10 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from flashws_amd import _lib, gpu  # noqa: E402
+from flashws_amd import _lib  # noqa: E402
+if "--lib" in sys.argv:
+    _lib.LIB_PATH = os.path.abspath(sys.argv[sys.argv.index("--lib") + 1])
+from flashws_amd import gpu  # noqa: E402
 
 
 def time_cfg(name, wire, n, reps):
@@ -44,7 +47,7 @@ def time_cfg(name, wire, n, reps):
 
 
 def main():
-    reps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+    reps = int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].isdigit() else 20
     out = {}
     cfgs = [("C2", gpu.config_c2()), ("C3", gpu.config_c3()),
             ("dense64", gpu.config_c2(n_frames=200_000, payload=64))]

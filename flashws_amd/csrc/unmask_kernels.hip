@@ -974,7 +974,18 @@ __device__ __forceinline__ void unmask_sorted_body(uint8_t *base, const fws_fram
                 v[j] = gload16<kNT>(c < E1 ? c : safe);
             }
         }
-        if (slow) {
+        if constexpr (kUtf8) {
+            // unmask in place (the masks die here: fewer live registers in the UTF-8 pass)
+#pragma unroll
+            for (int j = 0; j < kUnmaskU; ++j) {
+                const bool t = (m[j].x | m[j].y | m[j].z | m[j].w) != 0u;
+                v[j] = v[j] ^ m[j];
+                const uint64_t c = c0 + uint64_t(j) * 1024u;
+                if (!t || (slow && c >= E1)) continue;
+                if (!slow || (c >= E0 && c + 16u <= E1)) gstore16<kNT>(c, v[j]);
+                else store_bytes(c, v[j], E0, E1);
+            }
+        } else if (slow) {
             slow_unit_store<kNT>(c0, E0, E1, v, m);
         } else {
 #pragma unroll
@@ -989,7 +1000,7 @@ __device__ __forceinline__ void unmask_sorted_body(uint8_t *base, const fws_fram
                 uint32_t carry = 0;
 #pragma unroll
                 for (int j = 0; j < kUnmaskU; ++j) {
-                    const u32x4 x = v[j] ^ m[j];
+                    const u32x4 x = v[j];
                     uint32_t prev = __shfl_up(x.w, 1, 64);
                     if (lane == 0) prev = carry;
                     carry = __shfl(x.w, 63, 64);
@@ -1010,7 +1021,7 @@ __device__ __forceinline__ void unmask_sorted_body(uint8_t *base, const fws_fram
             asm volatile("" : "+v"(r0));             // opaque per unit: no hoisted per-dword offsets
 #pragma unroll
             for (int j = 0; j < kUnmaskU; ++j) {
-                const u32x4 x = v[j] ^ m[j];
+                const u32x4 x = v[j];
                 uint32_t prev = __shfl_up(x.w, 1, 64);
                 if (lane == 0) prev = carry;
                 carry = __shfl(x.w, 63, 64);
@@ -1215,8 +1226,11 @@ __device__ __forceinline__ void unmask_sorted_utf8_pipe(uint8_t *base, const fws
 }
 
 // unmask + per-region UTF-8 flags (C5 in descriptor mode); ok preset to 1
+#ifndef FWS_UTF8_WPE
+#define FWS_UTF8_WPE 1
+#endif
 template <bool kNT, bool kPipe>
-__global__ __launch_bounds__(kBlock) void k_unmask_sorted_utf8(uint8_t *base, const fws_frame_desc *__restrict__ d,
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FWS_UTF8_WPE))) void k_unmask_sorted_utf8(uint8_t *base, const fws_frame_desc *__restrict__ d,
                                                                uint32_t n, uint8_t *__restrict__ ok,
                                                                uint32_t *__restrict__ seam, uint64_t seam_units) {
     if (kPipe) unmask_sorted_utf8_pipe<kNT>(base, d, n, ok);
@@ -1228,10 +1242,18 @@ __global__ __launch_bounds__(kBlock) void k_unmask_sorted_utf8(uint8_t *base, co
 // ---------------------------------------------------------------- launchers
 using namespace fwsk;
 
-static int g_grid_cap = 16384;  // tuning hook: max workgroups of the streaming kernels
+// Workgroups of the streaming kernels: a grid-stride loop over 4 KiB units per
+// wavefront, capped per kernel family (measured on MI355X, tools/tune_c5.py):
+// the sorted unmask runs one unit per wavefront (1.39 vs 1.54 ms on C5's 4 GiB
+// at 16384 workgroups: its owner lookup and loads are not pipelined across a
+// wave's units), the UTF-8 form 16 (65536 workgroups: 1.61 vs 1.76 / 1.69 ms
+// at 16384 / 262144); the stream unmask 2 (3.04 vs 3.26 ms for the C5 stream
+// decode at 16384; C2 / C3 batches have <= 65536 units, one per wavefront either way).
+constexpr int kCapStream = 16384, kCapSorted = 1 << 20, kCapSortedUtf8 = 65536, kCapStreamUnmask = 131072;
+static int g_grid_cap = 0;  // tuning hook: max workgroups of every streaming kernel (0: the defaults above)
 extern "C" __attribute__((visibility("default"))) int fws_internal_set_grid_cap(int blocks) {
     const int old = g_grid_cap;
-    if (blocks > 0) g_grid_cap = blocks;
+    if (blocks >= 0) g_grid_cap = blocks;
     return old;
 }
 
@@ -1258,10 +1280,11 @@ extern "C" __attribute__((visibility("default"))) int fws_internal_set_stream_va
     return old;
 }
 
-static int grid_for_units(uint64_t units) {
-    // memory-bound: cap near 256 CUs x 8 blocks and grid-stride the rest
+static int grid_for_units(uint64_t units, int cap = kCapStream) {
+    // memory-bound: one wavefront per unit up to the cap, grid-stride past it
+    if (g_grid_cap > 0) cap = g_grid_cap;
     uint64_t blocks = (units + (kBlock / kWave) - 1) / (kBlock / kWave);
-    if (blocks > (uint64_t)g_grid_cap) blocks = (uint64_t)g_grid_cap;
+    if (blocks > (uint64_t)cap) blocks = (uint64_t)cap;
     if (blocks < 1) blocks = 1;
     return (int)blocks;
 }
@@ -1318,9 +1341,9 @@ int fws_launch_unmask_sorted(uint8_t *base, const fws_frame_desc *d, uint32_t n,
     if (n == 0) return 0;
     const uint64_t units = max_span / 4096u + 2u;
     if (g_sorted_early)
-        hipLaunchKernelGGL(k_unmask_sorted_early<true>, dim3(grid_for_units(units)), dim3(kBlock), 0, s, base, d, n);
+        hipLaunchKernelGGL(k_unmask_sorted_early<true>, dim3(grid_for_units(units, kCapSorted)), dim3(kBlock), 0, s, base, d, n);
     else
-        hipLaunchKernelGGL(k_unmask_sorted<true>, dim3(grid_for_units(units)), dim3(kBlock), 0, s, base, d, n);
+        hipLaunchKernelGGL(k_unmask_sorted<true>, dim3(grid_for_units(units, kCapSorted)), dim3(kBlock), 0, s, base, d, n);
     return fws_hip_status(hipGetLastError());
 }
 
@@ -1332,10 +1355,10 @@ int fws_launch_unmask_sorted_utf8(uint8_t *base, const fws_frame_desc *d, uint32
     if (r) return r;
     const uint64_t units = max_span / 4096u + 2u;
     if (g_sorted_utf8_pipe)
-        hipLaunchKernelGGL((k_unmask_sorted_utf8<true, true>), dim3(grid_for_units(units)), dim3(kBlock), 0, s, base, d,
+        hipLaunchKernelGGL((k_unmask_sorted_utf8<true, true>), dim3(grid_for_units(units, kCapSortedUtf8)), dim3(kBlock), 0, s, base, d,
                            n, ok, nullptr, 0ull);
     else
-        hipLaunchKernelGGL((k_unmask_sorted_utf8<true, false>), dim3(grid_for_units(units)), dim3(kBlock), 0, s, base,
+        hipLaunchKernelGGL((k_unmask_sorted_utf8<true, false>), dim3(grid_for_units(units, kCapSortedUtf8)), dim3(kBlock), 0, s, base,
                            d, n, ok, seam, seam_units);
     const uint64_t seam_blocks = (units + kBlock - 1) / kBlock;   // grid-stride: any span is covered
     hipLaunchKernelGGL(k_utf8_seam_sorted, dim3((unsigned)(seam_blocks < 4096u ? seam_blocks : 4096u)), dim3(kBlock), 0, s,
@@ -1348,7 +1371,7 @@ int fws_launch_unmask_stream(uint8_t *base, uint64_t N, const fws_frame_info *fr
                              uint32_t *seam, hipStream_t s) {
     const uint64_t units = (N + 4095) / 4096;
     if (units == 0 || cap == 0) return 0;
-    const dim3 grid(grid_for_units(units)), blk(kBlock);
+    const dim3 grid(grid_for_units(units, kCapStreamUnmask)), blk(kBlock);
     const int v = g_stream_variant;
     if (utf8_ok == nullptr) {
         if (v == 0)

@@ -37,7 +37,7 @@ def main():
             ts.append(e0.elapsed_time(e1) / 200 * 1e3)
         out[f"early{early}_grid{cap}"] = round(min(ts), 2)
         print(early, cap, out[f"early{early}_grid{cap}"], flush=True)
-    lib().fws_internal_set_grid_cap(16384)
+    lib().fws_internal_set_grid_cap(0)
     lib().fws_internal_set_sorted_early(0)
     print(json.dumps(out))
     ctx.close()

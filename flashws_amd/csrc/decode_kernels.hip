@@ -33,7 +33,17 @@
 
 namespace fwsk {
 
-constexpr uint32_t kScanBlocksPerCu = 8;     // resident k_scan workgroups per CU
+#ifndef FWS_SCAN_SETS
+#define FWS_SCAN_SETS 2
+#endif
+constexpr uint32_t kSets = FWS_SCAN_SETS;    // tiles in flight per wavefront (register sets)
+#ifndef FWS_SCAN_WAVES_EU
+#define FWS_SCAN_WAVES_EU 8
+#endif
+#ifndef FWS_SCAN_BPC
+#define FWS_SCAN_BPC 8
+#endif
+constexpr uint32_t kScanBlocksPerCu = FWS_SCAN_BPC;   // resident k_scan workgroups per CU
 
 #ifdef FWS_SCAN_PROF
 // phase clocks of k_scan summed over wavefronts (tools/prof_scan.py; build: make prof)
@@ -75,7 +85,7 @@ static_assert(sizeof(ScanLds) % 16 == 0, "16-B aligned per-wave areas");
 // survivors reserves its spill run with an atomic (and waits for it).
 // kPipe = false (streams shorter than one tile + halo): no prefetch.
 template <bool kPipe>
-__global__ __launch_bounds__(kScanThreads) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_scan(const uint8_t *__restrict__ wire, uint64_t N,
+__global__ __launch_bounds__(kScanThreads) __attribute__((amdgpu_waves_per_eu(FWS_SCAN_WAVES_EU, FWS_SCAN_WAVES_EU))) void k_scan(const uint8_t *__restrict__ wire, uint64_t N,
                                                        uint32_t n_tiles,
                                                        fws_frame_info *__restrict__ stage_info,
                                                        fws_frame_info *__restrict__ spill_info,
@@ -316,23 +326,36 @@ __global__ __launch_bounds__(kScanThreads) __attribute__((amdgpu_waves_per_eu(8,
             *reinterpret_cast<uint64_t *>(di32 + 4) = *reinterpret_cast<const uint64_t *>(f32 + 4);
             *dc = cv;
         }
-        prefetch(t + 2u * GW, pf, halo);
+        prefetch(t + kSets * GW, pf, halo);
     };
 
-    u32x4 pa[2], pah, pb[2], pbh;
-    prefetch(gw, pa, pah);
-    if (kPipe) {        // same younger-op count for set A on entry as on the loop back edge
-        asm volatile("" ::: "memory");             // keep the four stores between the two prefetches
+    auto dummy_stores = [&]() {   // same younger-op count for a set on entry as on the loop back edge
+        if (!kPipe) return;
+        asm volatile("" ::: "memory");             // keep the four stores between two prefetches
         *reinterpret_cast<u32x4 *>(dummy_info) = u32x4{0, 0, 0, 0};
         *(reinterpret_cast<uint64_t *>(dummy_info) + 2) = 0;
         *dummy_cnt = 0;
         asm volatile("" ::: "memory");
-    }
+    };
+    u32x4 pa[2], pah, pb[2], pbh;
+    prefetch(gw, pa, pah);
+    dummy_stores();
     prefetch(gw + GW, pb, pbh);
+#if FWS_SCAN_SETS == 3
+    u32x4 pc[2], pch;
+    dummy_stores();
+    prefetch(gw + 2u * GW, pc, pch);
+    for (uint32_t t = gw; t < n_tiles; t += 3u * GW) {
+        tile(t, pa, pah);
+        tile(t + GW, pb, pbh);
+        tile(t + 2u * GW, pc, pch);
+    }
+#else
     for (uint32_t t = gw; t < n_tiles; t += 2u * GW) {
         tile(t, pa, pah);
         tile(t + GW, pb, pbh);
     }
+#endif
 #ifdef FWS_SCAN_PROF
     if (lane == 0) {
         for (int i = 0; i < 8; ++i) atomicAdd(&g_scan_prof[i], (unsigned long long)prof_acc[i]);
@@ -405,7 +428,7 @@ int fws_decode_ensure(fws_gpu_ctx *ctx, uint64_t N, uint32_t cap) {
     al(&d.stage_info, nt * kSlots * sizeof(fws_frame_info));
     al(&d.spill_info, ns * sizeof(fws_frame_info)); al(&d.tile_spill, nt * 4);
     // super-tile resolve: results per slot id, EXIT tails, per-ST bases, big-ST scratch
-    rel(d.nres); rel(d.tails); rel(d.gnx); rel(d.tpk); rel(d.tmark); rel(d.comp); rel(d.st_nodes); rel(d.st_n); rel(d.st_entry);
+    rel(d.nres); rel(d.tails); rel(d.gnx); rel(d.tpk); rel(d.tmark); rel(d.comp); rel(d.st_nodes); rel(d.st_n); rel(d.st_nt); rel(d.st_entry);
     rel(d.st_fbase); rel(d.bg_nx); rel(d.bg_wt); rel(d.bg_lref); rel(d.bg_ptr); rel(d.bg_sc); rel(d.bg_mark);
     const uint64_t nst = fws_merge_super_tiles_cap(nt);
     const uint32_t tcap = fws_merge_tail_cap(nt);
@@ -413,7 +436,7 @@ int fws_decode_ensure(fws_gpu_ctx *ctx, uint64_t N, uint32_t cap) {
     al(&d.nres, nn * sizeof(fws_node_res));
     al(&d.tails, (uint64_t)tcap * sizeof(fws_tail_rec)); al(&d.gnx, (uint64_t)tcap * 4); al(&d.tpk, (uint64_t)tcap * 16); al(&d.tmark, ((uint64_t)tcap / 32 + 1) * 4);
     al(&d.comp, (uint64_t)fws_merge_comp_cap() * 4);
-    al(&d.st_nodes, fws_merge_st_nodes(nt) * sizeof(fws_st_node)); al(&d.st_n, nst * 4);
+    al(&d.st_nodes, fws_merge_st_nodes(nt) * sizeof(fws_st_node)); al(&d.st_n, nst * 4); al(&d.st_nt, nst * 4);
     al(&d.st_entry, nst * 4); al(&d.st_fbase, nst * 4);
     al(&d.bg_nx, nn * 4); al(&d.bg_wt, nn * 4); al(&d.bg_lref, nn * 4); al(&d.bg_ptr, 2 * nn * 4);
     al(&d.bg_sc, 2 * nn * 4); al(&d.bg_mark, nn * 4);

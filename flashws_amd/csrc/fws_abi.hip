@@ -132,6 +132,7 @@ void fws_gpu_ctx_destroy(fws_gpu_ctx *ctx) {
     dev_free(d.comp);
     dev_free(d.st_nodes);
     dev_free(d.st_n);
+    dev_free(d.st_nt);
     dev_free(d.st_entry);
     dev_free(d.st_fbase);
     dev_free(d.bg_nx);

@@ -120,6 +120,7 @@ struct fws_decode_ws {
     uint32_t *comp = nullptr;              // [fws_merge_comp_cap()] marked tails, compacted
     fws_st_node *st_nodes = nullptr;       // [max_st * kStCap] survivors per super tile (8 B each)
     uint32_t *st_n = nullptr;              // [max_st] survivors per super tile
+    uint32_t *st_nt = nullptr;             // [max_st] EXIT tails in the super tile's own run (0: overflow area)
     uint32_t *st_entry = nullptr;          // [max_st] the path's first header in the ST (local index / slot id)
     uint32_t *st_fbase = nullptr;          // [max_st] frames before the ST
     // big-ST path: super tiles with more survivors than LDS holds (dense small

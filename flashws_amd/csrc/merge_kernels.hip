@@ -63,6 +63,8 @@ constexpr uint32_t kStCap = 2048;                   // survivors of one ST in LD
 constexpr int kMThreads = 512;
 constexpr int kMWaves = kMThreads / 64;
 constexpr uint32_t kPer = kStCap / kMThreads;       // survivors per thread: i = kPer * tid + j
+constexpr uint32_t kWaveJump = 512;
+constexpr uint32_t kTailRun = 16;                   // EXIT tails of one super tile in its own tail-list run                 // k_merge: one wavefront pointer-jumps up to this many
 constexpr uint32_t kTailCapMax = 1u << 18;          // LDS bitmap of the path pruning
 constexpr uint32_t kCompCap = 32768;                // tails that are some tail's next (+ the root's)
 constexpr uint32_t kMaxPruneRounds = 64;
@@ -155,6 +157,7 @@ struct MergeParams {
     uint32_t *comp;                                  // [kCompCap] compact index -> tail index
     fws_st_node *st_nodes;                           // [n_st][kStCap]
     uint32_t *st_n;
+    uint32_t *st_nt;                                 // EXIT tails in the ST's own run (0: overflow area)
     uint32_t *st_entry;                              // local index of the ST's entry, or kNone
     uint32_t *st_fbase;
     fws_frame_info *frames;
@@ -190,6 +193,7 @@ struct MergeParams {
     __device__ uint32_t find_node(uint64_t x) const {
         const uint32_t t = (uint32_t)(x / kTile);
         const uint32_t n = tile_count[t], sp = tile_spill[t];
+        // (loading the 8 slots with the count, unconditionally, measured slower in k_link)
         if (sp == kNone) {
             uint64_t o[kSlots];
 #pragma unroll
@@ -253,6 +257,28 @@ __device__ __forceinline__ T block_excl(T v, T *sred, T *total) {
     return off + inc - v;
 }
 
+// The tail list: super tile s writes its k EXIT tails to its own run
+// [s * kTailRun, s * kTailRun + k) when k <= kTailRun (every C2 / C3 / C5
+// super tile), else to a run of the overflow area past n_st * kTailRun, taken
+// with one atomic. (One atomic per super tile on one counter word queued 513
+// workgroups behind each other: k_merge 18 -> see DESIGN 4.3.) Returns the
+// run's first tail index, or kNone when the overflow area is full (the decode
+// ends with FWS_ERR_CAPACITY).
+__device__ uint32_t reserve_tails(const MergeParams &P, uint32_t s, uint32_t k) {
+    if (k <= kTailRun) {
+        P.st_nt[s] = k;
+        return s * kTailRun;
+    }
+    P.st_nt[s] = 0;
+    const uint32_t fixed = P.n_st * kTailRun, room = P.tail_cap - fixed;
+    const uint32_t off = atomicAdd(&P.counters[kCntTails], k);
+    if (off > room || room - off < k) {
+        atomicOr(&P.counters[kCntFallback], 1u);
+        return kNone;
+    }
+    return fixed + off;
+}
+
 // ------------------------------------------------------------------ k_merge
 constexpr uint32_t kDenseWaves = 4;                 // k_merge wavefronts running dense_tile()
 constexpr uint32_t kMidCap = 8192;                  // big super tiles merged / emitted in LDS (else global scratch)
@@ -297,7 +323,6 @@ __device__ __forceinline__ uint32_t st_sid(const MergeParams &P, const MergeLds 
 __device__ void merge_big(const MergeParams &P, MergeLds &L, uint32_t s, uint32_t n) {
     const uint32_t tid = threadIdx.x, t0 = s * P.st_tiles;
     const uint64_t st_end = (uint64_t(s) + 1u) << P.st_shift;
-    uint32_t *const C = P.counters;
     uint32_t *const p0 = P.bg_ptr, *const p1 = P.bg_ptr + P.max_nodes;
     uint32_t *const c0 = P.bg_sc, *const c1 = P.bg_sc + P.max_nodes;
     // in-ST next of every survivor: the survivor at its exit (search in the exit's tile)
@@ -322,15 +347,7 @@ __device__ void merge_big(const MergeParams &P, MergeLds &L, uint32_t s, uint32_
         if (v == kBgExit) gst(P.bg_lref + id, atomicAdd(&L.n_tail, 1u));
     }
     __syncthreads();
-    if (tid == 0) {                                  // the ST's run of the tail list
-        const uint32_t k = L.n_tail;
-        uint32_t base = k ? atomicAdd(&C[kCntTails], k) : 0u;
-        if (k && (base > P.tail_cap || P.tail_cap - base < k)) {
-            atomicOr(&C[kCntFallback], 1u);
-            base = kNone;
-        }
-        L.tail_base = base;
-    }
+    if (tid == 0) L.tail_base = reserve_tails(P, s, L.n_tail);   // the ST's run of the tail list
     // pointer jumping over slot ids: every survivor -> its chain's tail, frame counts
     uint32_t *pc = p0, *pn = p1, *sc = c0, *sn = c1;
     for (;;) {
@@ -379,7 +396,6 @@ constexpr uint32_t kMidB = 4;
 __device__ void merge_mid(const MergeParams &P, MergeLds &L, uint32_t s, uint32_t n) {
     const uint32_t tid = threadIdx.x, t0 = s * P.st_tiles;
     const uint64_t st0 = uint64_t(s) << P.st_shift, st_end = st0 + (1ull << P.st_shift);
-    uint32_t *const C = P.counters;
     MP_INIT();
     // pass 1: tile-local offsets
     for (uint32_t base = tid; base < n; base += kMidB * kMThreads) {
@@ -445,15 +461,7 @@ __device__ void merge_mid(const MergeParams &P, MergeLds &L, uint32_t s, uint32_
     }
     __syncthreads();
     MP_MARK(19);
-    if (tid == 0) {                                  // the ST's run of the tail list
-        const uint32_t k = L.n_tail;
-        uint32_t base = k ? atomicAdd(&C[kCntTails], k) : 0u;
-        if (k && (base > P.tail_cap || P.tail_cap - base < k)) {
-            atomicOr(&C[kCntFallback], 1u);
-            base = kNone;
-        }
-        L.tail_base = base;
-    }
+    if (tid == 0) L.tail_base = reserve_tails(P, s, L.n_tail);   // the ST's run of the tail list
     // pointer jumping in place: ptr and frame count move together in one word
     for (;;) {
         int changed = 0;
@@ -624,12 +632,16 @@ __global__ __launch_bounds__(kMThreads) void k_merge(MergeParams P) {
         sl[j] = inside ? L.tcnt[tl] : 0u;
     }
     for (;;) {
+        // the kPer searches' reads of a step issue together (unconditional, in bounds)
+        uint32_t ov[kPer];
+#pragma unroll
+        for (uint32_t j = 0; j < kPer; ++j) ov[j] = L.off[(sb[j] + (sl[j] >> 1) - (sl[j] > 1 ? 1u : 0u)) & (kStCap - 1u)];
         bool more = false;
 #pragma unroll
         for (uint32_t j = 0; j < kPer; ++j) {
             if (sl[j] > 1) {
                 const uint32_t half = sl[j] >> 1;
-                if (L.off[sb[j] + half - 1] < xr[j]) sb[j] += half;
+                if (ov[j] < xr[j]) sb[j] += half;
                 sl[j] -= half;
                 more |= sl[j] > 1;
             }
@@ -659,31 +671,55 @@ __global__ __launch_bounds__(kMThreads) void k_merge(MergeParams P) {
         if (i0 + j < n && vv[j] == kNxExit) L.lref[i0 + j] = atomicAdd(&L.n_tail, 1u);
     __syncthreads();
     MP_MARK(2);
-    // reserve the ST's run of the tail list
-    if (tid == 0) {
-        const uint32_t k = L.n_tail;
-        uint32_t base = k ? atomicAdd(&C[kCntTails], k) : 0u;
-        if (k && (base > P.tail_cap || P.tail_cap - base < k)) {
-            atomicOr(&C[kCntFallback], 1u);
-            base = kNone;
-        }
-        L.tail_base = base;
-    }
+    // reserve the ST's run of the tail list (a wave that takes no part in the
+    // jumping below, so the atomic's round trip overlaps it)
+    if (tid == kMThreads - 64) L.tail_base = reserve_tails(P, s, L.n_tail);
     // pointer jumping in place: every survivor -> its chain's tail, with frame
     // counts (pointer and count move together in one word, so a read of a word
-    // another thread is rewriting sees either pair, both consistent)
-    for (;;) {
-        int changed = 0;
-        for (uint32_t i = tid; i < n; i += kMThreads) {
-            const uint32_t w = L.pw[i];
-            const uint32_t p = w & 0xFFFFu;
-            const uint32_t wp = L.pw[p];
-            if ((wp & 0xFFFFu) != p) {
-                L.pw[i] = (wp & 0xFFFFu) | (((w >> 16) + (wp >> 16)) << 16);
-                changed = 1;
+    // another lane is rewriting sees either pair, both consistent). Up to
+    // kWaveJump survivors (every C2 / C3 super tile) one wavefront does it with
+    // no workgroup barrier per round (a wave's LDS operations are ordered);
+    // more take the whole workgroup.
+    if (n <= kWaveJump) {
+        if (tid < 64) {
+            constexpr uint32_t J = kWaveJump / 64;
+            for (;;) {
+                // one synchronous round: every read of the round before any write; the
+                // reads are unconditional (in-bounds words past n, unused) so the J
+                // reads issue back to back under one wait, twice per round
+                uint32_t w[J], wp[J];
+#pragma unroll
+                for (uint32_t j = 0; j < J; ++j) w[j] = L.pw[tid + 64u * j];
+#pragma unroll
+                for (uint32_t j = 0; j < J; ++j) wp[j] = L.pw[w[j] & (kStCap - 1u)];
+                bool ch = false;
+#pragma unroll
+                for (uint32_t j = 0; j < J; ++j) {
+                    const uint32_t i = tid + 64u * j;
+                    if (i < n && (wp[j] & 0xFFFFu) != (w[j] & 0xFFFFu)) {
+                        L.pw[i] = (wp[j] & 0xFFFFu) | (((w[j] >> 16) + (wp[j] >> 16)) << 16);
+                        ch = true;
+                    }
+                }
+                wave_sync();
+                if (!__any(ch)) break;
             }
         }
-        if (!__syncthreads_or(changed)) break;
+        __syncthreads();
+    } else {
+        for (;;) {
+            int changed = 0;
+            for (uint32_t i = tid; i < n; i += kMThreads) {
+                const uint32_t w = L.pw[i];
+                const uint32_t p = w & 0xFFFFu;
+                const uint32_t wp = L.pw[p];
+                if ((wp & 0xFFFFu) != p) {
+                    L.pw[i] = (wp & 0xFFFFu) | (((w >> 16) + (wp >> 16)) << 16);
+                    changed = 1;
+                }
+            }
+            if (!__syncthreads_or(changed)) break;
+        }
     }
     MP_MARK(3);
     const uint32_t tb = L.tail_base;
@@ -796,7 +832,8 @@ __device__ void resolve_path(const MergeParams &P, PathLds &G) {
     const bool lds_st = n_st <= kStLds && !P.force_big;
     // the phase's loads, all issued up front: the flags and counts this launch
     // handed off (sc1), k_merge's record of the root, the survivors per ST
-    const uint32_t fbk = ld_acq(&C[kCntFallback]), ovf = ld_acq(&C[kCntOverflow]), M = ld_acq(&C[kCntTails]);
+    const uint32_t fbk = ld_acq(&C[kCntFallback]), ovf = ld_acq(&C[kCntOverflow]);
+    const uint32_t M = n_st * kTailRun + ld_acq(&C[kCntTails]);   // tail index space: the runs + overflow
     const uint32_t root_state = tid == 0 ? C[kCntRoot] : 0u;
     const uint32_t root_sid = tid == 0 ? C[kCntRootSid] : 0u;
     const uint32_t root_tail = tid == 0 ? C[kCntRootTail] : 0u;
@@ -1103,26 +1140,38 @@ __global__ __launch_bounds__(kMThreads) void k_link(MergeParams P) {
     MP_START(29);
     MP_T0();
     MP_INIT();
-    const uint32_t x = blockIdx.x * kMThreads + tid;
-    const fws_tail_rec &trx = P.tails[x < P.tail_cap ? x : 0u];   // with the counters (read past M: unused)
-    const uint64_t tx = trx.exit;
-    const uint32_t tid_rec = trx.id;
-    const uint32_t M = C[kCntTails];
-    if (x < M && !C[kCntFallback]) {
-        const uint32_t w = P.find_node(tx);
-        const uint32_t wst = (uint32_t)(tx >> P.st_shift);
-        uint32_t g = kGTerm | kKindDead, ent = kNone, cnt = 0, esid = tid_rec;
-        if (w != kTermDead) {
-            const fws_node_res r = P.nres[w];
-            g = res_kind(r) == kKindExit ? r.tail : (kGTerm | res_kind(r));
-            ent = r.ent;
-            cnt = r.cnt;
-            if (g >= kGTerm) esid = P.tail_sid(wst, r);   // the path's last header if it ends here
+    // tail index space: the super tiles' runs [0, fixed), then the overflow area
+    // (k_merge's reserve_tails); one thread per run slot, a grid-stride loop past it
+    const uint32_t fixed = P.n_st * kTailRun, stride = gridDim.x * kMThreads;
+    uint32_t x = blockIdx.x * kMThreads + tid;
+    // the first tail's loads beside the counters (read past the valid ones: unused)
+    fws_tail_rec tr = P.tails[x < P.tail_cap ? x : 0u];
+    uint32_t nt = x < fixed ? P.st_nt[x / kTailRun] : 0u;
+    const uint32_t total = fixed + C[kCntTails];
+    if (!C[kCntFallback]) {
+        while (x < total) {
+            if (x >= fixed || x % kTailRun < nt) {
+                const uint64_t tx = tr.exit;
+                const uint32_t w = P.find_node(tx);
+                const uint32_t wst = (uint32_t)(tx >> P.st_shift);
+                uint32_t g = kGTerm | kKindDead, ent = kNone, cnt = 0, esid = tr.id;
+                if (w != kTermDead) {
+                    const fws_node_res r = P.nres[w];
+                    g = res_kind(r) == kKindExit ? r.tail : (kGTerm | res_kind(r));
+                    ent = r.ent;
+                    cnt = r.cnt;
+                    if (g >= kGTerm) esid = P.tail_sid(wst, r);   // the path's last header if it ends here
+                }
+                gst64(&P.tpk[2u * x], (uint64_t)ent | ((uint64_t)cnt << 32));
+                gst64(&P.tpk[2u * x + 1u], (uint64_t)esid | ((uint64_t)(wst | ((g >= kGTerm ? g & 3u : 0u) << 30)) << 32));
+                gst(&P.gnx[x], g);
+                if (g < kGTerm) atomicOr(&P.tmark[g >> 5], 1u << (g & 31u));
+            }
+            x += stride;
+            if (x >= total) break;
+            tr = P.tails[x];
+            nt = x < fixed ? P.st_nt[x / kTailRun] : 0u;
         }
-        gst64(&P.tpk[2u * x], (uint64_t)ent | ((uint64_t)cnt << 32));
-        gst64(&P.tpk[2u * x + 1u], (uint64_t)esid | ((uint64_t)(wst | ((g >= kGTerm ? g & 3u : 0u) << 30)) << 32));
-        gst(&P.gnx[x], g);
-        if (g < kGTerm) atomicOr(&P.tmark[g >> 5], 1u << (g & 31u));
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains
     __syncthreads();
@@ -1360,7 +1409,8 @@ __global__ __launch_bounds__(kMThreads) void k_emit(MergeParams P) {
         return;
     }
     // (loading all kStCap rows with the words above, before n is known, measured
-    // 9.4 -> 13.6 us on C3: 16 MB of rows instead of ~1 MB)
+    // 9.4 -> 13.6 us on C3: 16 MB of rows instead of ~1 MB; the first 512 rows
+    // that way, with the entry's row from its thread through LDS, 9.1 -> ~15 us)
     const fws_st_node *const tab = P.st_nodes + (uint64_t)s * kStCap;
     const uint32_t i0 = kPer * tid;
     fws_st_node nd[kPer];
@@ -1539,6 +1589,7 @@ int fws_launch_merge(fws_gpu_ctx *ctx, const uint8_t *wire, uint64_t N, uint32_t
     P.st_shift = (uint32_t)__builtin_ctz(P.st_tiles) + (uint32_t)__builtin_ctz(kTile);
     P.n_st = (uint32_t)fws_merge_super_tiles(n_tiles);
     if (P.n_st > d.max_st) return FWS_ERR_INTERNAL;   // fws_decode_ensure sized the tables
+    if ((uint64_t)P.n_st * kTailRun > d.tail_cap) return FWS_ERR_CAPACITY;   // > 8 GiB streams
     P.stage_info = d.stage_info;
     P.spill_info = d.spill_info;
     P.spill_w = d.spill_info;
@@ -1556,6 +1607,7 @@ int fws_launch_merge(fws_gpu_ctx *ctx, const uint8_t *wire, uint64_t N, uint32_t
     P.comp = d.comp;
     P.st_nodes = d.st_nodes;
     P.st_n = d.st_n;
+    P.st_nt = d.st_nt;
     P.st_entry = d.st_entry;
     P.st_fbase = d.st_fbase;
     P.frames = frames;
@@ -1576,7 +1628,8 @@ int fws_launch_merge(fws_gpu_ctx *ctx, const uint8_t *wire, uint64_t N, uint32_t
     P.max_nodes = d.max_nodes;
     const dim3 grid(P.n_st ? P.n_st : 1u), blk(kMThreads);
     hipLaunchKernelGGL(k_merge, grid, blk, 0, s, P);
-    hipLaunchKernelGGL(k_link, dim3((P.tail_cap + kMThreads - 1) / kMThreads), blk, 0, s, P);
+    const uint32_t fixed = P.n_st * kTailRun;         // k_link: one thread per run slot (+ a loop past them)
+    hipLaunchKernelGGL(k_link, dim3(fixed ? (fixed + kMThreads - 1) / kMThreads : 1u), blk, 0, s, P);
     hipLaunchKernelGGL(k_emit, grid, blk, 0, s, P);
     return fws_hip_status(hipGetLastError());
 }

@@ -186,6 +186,34 @@ def test_false_chains_join_the_path(ctx, cuda, seed):
     check(ctx, cuda, b"".join(bytes(f) for f in frames))
 
 
+@pytest.mark.parametrize("stride", [256, 1000, 2900, 4500])
+def test_many_exit_tails_per_super_tile(ctx, cuda, stride):
+    """Planted 126-form headers of 65,000 B inside long payloads, one every
+    `stride` bytes: each survives its tile and leaves its super tile, so every
+    64 KiB super tile of this 2.4 MB stream has ~250, ~65, ~22 or ~14 EXIT
+    tails -- past, past and just past k_merge's per-super-tile run of 16 (the
+    overflow area, taken with an atomic, and k_link's loop over it), and
+    within it. Bit-exact with the oracle; at ~250 per super tile the tail list
+    (64 per super tile + 4096) is full and the decode ends with
+    FWS_ERR_CAPACITY, nothing listed or unmasked."""
+    rng = np.random.default_rng(stride)
+    frames = []
+    for i in range(40):
+        f = bytearray(frame(2, rng.integers(0, 256, 60000, dtype=np.uint8).tobytes(),
+                            key=int(rng.integers(0, 2**32))))
+        for q in range(8 + 64, len(f) - 16, stride):
+            f[q:q + 8] = bytes([0x82, 0xFE]) + (65000).to_bytes(2, "big") + int(rng.integers(0, 2**32)).to_bytes(4, "little")
+        frames.append(bytes(f))
+    wire = np.frombuffer(b"".join(frames), dtype=np.uint8)
+    if stride > 256:
+        check(ctx, cuda, wire)
+        return
+    got, _, r = decode(ctx, wire, cuda)
+    from flashws_amd import _lib
+    assert int(r["status"]) == _lib.FWS_ERR_CAPACITY and int(r["n_frames"]) == 0
+    assert np.array_equal(got, wire)
+
+
 @pytest.mark.parametrize("seed", range(3))
 def test_tiny_frames_dense_tiles(ctx, cuda, seed):
     """Frames of 0..24 B payload (~100 headers per 2 KiB tile): k_scan leaves

@@ -33,17 +33,18 @@
 
 namespace fwsk {
 
-#ifndef FWS_SCAN_SETS
-#define FWS_SCAN_SETS 2
+// FWS_ABL / FWS_ABL_NOHALO / FWS_ABL_NOSTORE: ablation builds for timing only
+// (make exp; tools/scan_ablation.py), never the product library
+#ifndef FWS_ABL
+#define FWS_ABL 0
 #endif
-constexpr uint32_t kSets = FWS_SCAN_SETS;    // tiles in flight per wavefront (register sets)
-#ifndef FWS_SCAN_WAVES_EU
-#define FWS_SCAN_WAVES_EU 8
+#ifndef FWS_SCAN_NT
+#define FWS_SCAN_NT 0
 #endif
-#ifndef FWS_SCAN_BPC
-#define FWS_SCAN_BPC 8
-#endif
-constexpr uint32_t kScanBlocksPerCu = FWS_SCAN_BPC;   // resident k_scan workgroups per CU
+constexpr bool kScanNT = FWS_SCAN_NT != 0;   // nontemporal stream loads
+constexpr uint32_t kSets = 2;                // tiles in flight per wavefront (register sets; 3 sets
+                                             //   at 6 waves per SIMD measured slower)
+constexpr uint32_t kScanBlocksPerCu = 8;     // resident k_scan workgroups per CU
 
 #ifdef FWS_SCAN_PROF
 // phase clocks of k_scan summed over wavefronts (tools/prof_scan.py; build: make prof)
@@ -85,7 +86,7 @@ static_assert(sizeof(ScanLds) % 16 == 0, "16-B aligned per-wave areas");
 // survivors reserves its spill run with an atomic (and waits for it).
 // kPipe = false (streams shorter than one tile + halo): no prefetch.
 template <bool kPipe>
-__global__ __launch_bounds__(kScanThreads) __attribute__((amdgpu_waves_per_eu(FWS_SCAN_WAVES_EU, FWS_SCAN_WAVES_EU))) void k_scan(const uint8_t *__restrict__ wire, uint64_t N,
+__global__ __launch_bounds__(kScanThreads) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_scan(const uint8_t *__restrict__ wire, uint64_t N,
                                                        uint32_t n_tiles,
                                                        fws_frame_info *__restrict__ stage_info,
                                                        fws_frame_info *__restrict__ spill_info,
@@ -116,9 +117,13 @@ __global__ __launch_bounds__(kScanThreads) __attribute__((amdgpu_waves_per_eu(FW
         if (!kPipe) return;
         const uint64_t o = uint64_t(tt < last_inner ? tt : last_inner) * kTile;
         // coalesced: each load instruction reads 1 KiB contiguous (lane L: 16 B at 16L)
-        pf[0] = gload16(reinterpret_cast<uintptr_t>(wire + o + L16));
-        pf[1] = gload16(reinterpret_cast<uintptr_t>(wire + o + 1024u + L16));
-        halo = gload16(reinterpret_cast<uintptr_t>(wire + o + kTile + (L16 < kHaloX ? L16 : 0u)));
+        pf[0] = gload16<kScanNT>(reinterpret_cast<uintptr_t>(wire + o + L16));
+        pf[1] = gload16<kScanNT>(reinterpret_cast<uintptr_t>(wire + o + 1024u + L16));
+#if FWS_ABL_NOHALO
+        halo = pf[0];
+#else
+        halo = gload16<kScanNT>(reinterpret_cast<uintptr_t>(wire + o + kTile + (L16 < kHaloX ? L16 : 0u)));
+#endif
     };
 
     auto tile = [&](const uint32_t t, u32x4 (&pf)[2], u32x4 &halo) {
@@ -149,7 +154,12 @@ __global__ __launch_bounds__(kScanThreads) __attribute__((amdgpu_waves_per_eu(FW
             }
             wave_sync();
             SCAN_MARK(0);
-
+#if FWS_ABL == 1      // ablation (exp builds, timing only): stage the tile, nothing else
+            {
+                const uint32_t v = *reinterpret_cast<const uint32_t *>(B + L32);
+                ns = (uint32_t)__popcll(__ballot(v == 0x12345678u));
+            }
+#else
             // candidate bits of this lane's 32 offsets, candidate numbering by a wave scan
             uint32_t cm;
             {
@@ -171,7 +181,13 @@ __global__ __launch_bounds__(kScanThreads) __attribute__((amdgpu_waves_per_eu(FW
             bool dense = nc > kCandCap;                        // wave-uniform
             SCAN_MARK(1);
             SCAN_COUNT(5, nc);
+#if FWS_ABL == 2      // ablation: candidate bits and their scan only
+            ns = nc;
+            dense = false;
+            if (false) {
+#else
             if (!dense) {
+#endif
                 {
                     uint32_t bits = cm, k = cp;
                     while (bits) {
@@ -309,9 +325,13 @@ __global__ __launch_bounds__(kScanThreads) __attribute__((amdgpu_waves_per_eu(FW
                 ns = kDenseTile;
                 rec = false;
             }
+#endif
             SCAN_MARK(3);
         }
         // the tile's three stores, every lane active (idle lanes -> the dummy line)
+#if FWS_ABL_NOSTORE
+        if (ns == 0x7FFFFFFFu)
+#endif
         {
             fws_frame_info *di = !rec ? dummy_info
                                       : spill == kNone ? stage_info + (uint64_t)t * kSlots + srank
@@ -341,21 +361,10 @@ __global__ __launch_bounds__(kScanThreads) __attribute__((amdgpu_waves_per_eu(FW
     prefetch(gw, pa, pah);
     dummy_stores();
     prefetch(gw + GW, pb, pbh);
-#if FWS_SCAN_SETS == 3
-    u32x4 pc[2], pch;
-    dummy_stores();
-    prefetch(gw + 2u * GW, pc, pch);
-    for (uint32_t t = gw; t < n_tiles; t += 3u * GW) {
-        tile(t, pa, pah);
-        tile(t + GW, pb, pbh);
-        tile(t + 2u * GW, pc, pch);
-    }
-#else
     for (uint32_t t = gw; t < n_tiles; t += 2u * GW) {
         tile(t, pa, pah);
         tile(t + GW, pb, pbh);
     }
-#endif
 #ifdef FWS_SCAN_PROF
     if (lane == 0) {
         for (int i = 0; i < 8; ++i) atomicAdd(&g_scan_prof[i], (unsigned long long)prof_acc[i]);
@@ -396,6 +405,21 @@ static uint32_t g_scan_blocks_per_cu = 0;   // tuning override (tools/), 0 = def
 extern "C" int fws_internal_set_scan_blocks_per_cu(int v) {
     g_scan_blocks_per_cu = v > 0 ? (uint32_t)v : 0u;
     return 0;
+}
+
+// timing hook (tools/scan_ablation.py): k_scan alone over a device stream
+extern "C" __attribute__((visibility("default"))) int fws_internal_scan_only(fws_gpu_ctx *ctx, const uint8_t *wire,
+                                                                         uint64_t N, hipStream_t s) {
+    fws_decode_ws &d = ctx->dec;
+    const int r = fws_decode_ensure(ctx, N, 16);
+    if (r) return r;
+    const uint32_t n_tiles = (uint32_t)((N + kTile - 1) / kTile);
+    if (!n_tiles || N < kTile + kHaloX) return FWS_ERR_INVALID;
+    const uint32_t need = (n_tiles + kScanWaves - 1) / kScanWaves;
+    const uint32_t sg = need < d.scan_grid ? need : d.scan_grid;
+    hipLaunchKernelGGL(k_scan<true>, dim3(sg), dim3(kScanThreads), 0, s, wire, N, n_tiles, d.stage_info, d.spill_info,
+                       d.tile_spill, d.tile_count, d.cnt_base, (uint32_t)d.max_surv, d.scan_dummy);
+    return fws_hip_status(hipGetLastError());
 }
 
 int fws_decode_ensure(fws_gpu_ctx *ctx, uint64_t N, uint32_t cap) {

@@ -34,7 +34,9 @@ enum Counter {
     kCntTicket = 10,     // k_link workgroups finished (the last one resolves the path)
     kCntTails = 11,      // super-tile exit tails appended by k_merge
     kCntBig = 12,        // super tiles that took k_merge's big-ST path (diagnostic)
-    // 13..17: unused
+    kCntScanDense = 13,  // tiles k_scan marked kDenseTile (k_merge rewrites their counts: its early
+                         //   landing lookups need a stream with none)
+    // 14..17: unused
     kCntRootCnt = 18,    //   ::cnt (ent is 0) -- resolve_path skips four dependent loads
     kCntCount = 19
 };

@@ -324,6 +324,7 @@ __global__ __launch_bounds__(kScanThreads) __attribute__((amdgpu_waves_per_eu(8,
                 // left to dense_tile() in k_merge (frames under ~32 B)
                 ns = kDenseTile;
                 rec = false;
+                if (lane == 0) atomicAdd(&counters[kCntScanDense], 1u);
             }
 #endif
             SCAN_MARK(3);

@@ -64,7 +64,8 @@ constexpr int kMThreads = 512;
 constexpr int kMWaves = kMThreads / 64;
 constexpr uint32_t kPer = kStCap / kMThreads;       // survivors per thread: i = kPer * tid + j
 constexpr uint32_t kWaveJump = 512;
-constexpr uint32_t kTailRun = 16;                   // EXIT tails of one super tile in its own tail-list run                 // k_merge: one wavefront pointer-jumps up to this many
+constexpr uint32_t kTailRun = 16;
+constexpr uint32_t kLandCap = 256;                  // k_merge: EXIT tails whose landing survivor it looks up                   // EXIT tails of one super tile in its own tail-list run                 // k_merge: one wavefront pointer-jumps up to this many
 constexpr uint32_t kTailCapMax = 1u << 18;          // LDS bitmap of the path pruning
 constexpr uint32_t kCompCap = 32768;                // tails that are some tail's next (+ the root's)
 constexpr uint32_t kMaxPruneRounds = 64;
@@ -286,7 +287,13 @@ struct MergeLds {
     uint32_t tcnt[kStTiles];
     uint32_t tsp[kStTiles];
     uint32_t tbase[kStTiles];
-    uint16_t boff[kMidCap];                          // mid path: tile-local offset of survivor i
+    union {
+        uint16_t boff[kMidCap];                      // mid path: tile-local offset of survivor i
+        struct {                                     // LDS path: EXIT tail lref -> its exit (the
+            uint64_t texit[kLandCap];                //   landing lookups) -> slot id of the survivor
+            uint32_t tland[kLandCap];                //   there, kTermDead, or kNone
+        };
+    };
     union {
         struct {
             union {
@@ -304,6 +311,7 @@ struct MergeLds {
     uint32_t red32[kMWaves];
     uint32_t n_tail, tail_base;
 };
+static_assert(sizeof(MergeLds) <= 160u * 1024u / 3u, "three k_merge workgroups per CU (513 super tiles of C2 / C3)");
 
 // Slot id of survivor i of ST s (tile by a search of the ST's tile prefix in LDS).
 __device__ __forceinline__ uint32_t st_sid(const MergeParams &P, const MergeLds &L, uint32_t t0, uint32_t i) {
@@ -380,7 +388,7 @@ __device__ void merge_big(const MergeParams &P, MergeLds &L, uint32_t s, uint32_
         P.nres[id] = fws_node_res{ref, cnt, id, kind | kBigBit};
         if (gld(P.bg_nx + id) == kBgExit) {
             const uint64_t x = exit_of(*P.rec(id));
-            P.tails[tb + gld(P.bg_lref + id)] = fws_tail_rec{x, id, kTermDead, (uint32_t)(x >> P.st_shift), 0u};
+            P.tails[tb + gld(P.bg_lref + id)] = fws_tail_rec{x, id, kNone, (uint32_t)(x >> P.st_shift), 0u};
         }
     }
 }
@@ -504,11 +512,40 @@ __device__ void merge_mid(const MergeParams &P, MergeLds &L, uint32_t s, uint32_
             const uint32_t ref = kind == kKindExit ? tb + lr[b] : tid_[b];
             P.nres[id[b]] = fws_node_res{ref, cnt, id[b], kind | kBigBit};
             if (t == i && kind == kKindExit)
-                P.tails[tb + own[b]] = fws_tail_rec{x[b], id[b], kTermDead, (uint32_t)(x[b] >> P.st_shift), 0u};
+                P.tails[tb + own[b]] = fws_tail_rec{x[b], id[b], kNone, (uint32_t)(x[b] >> P.st_shift), 0u};
         }
     }
     __syncthreads();
     MP_MARK(21);
+}
+
+// Pointer jumping in place by one wavefront over pw[0, n), n <= 64 J: every
+// survivor -> its chain's tail, with frame counts (pointer and count move
+// together in one word). One synchronous round = every read of the round
+// before any write; the reads are unconditional (in-bounds words past n,
+// unused) so the J reads issue back to back under one wait, twice per round;
+// a wave's LDS operations are ordered, so no barrier per round.
+template <uint32_t J>
+__device__ __forceinline__ void wave_jump(uint32_t *pw, uint32_t n) {
+    const uint32_t lane = threadIdx.x & 63;
+    for (;;) {
+        uint32_t w[J], wp[J];
+#pragma unroll
+        for (uint32_t j = 0; j < J; ++j) w[j] = pw[lane + 64u * j];
+#pragma unroll
+        for (uint32_t j = 0; j < J; ++j) wp[j] = pw[w[j] & (kStCap - 1u)];
+        bool ch = false;
+#pragma unroll
+        for (uint32_t j = 0; j < J; ++j) {
+            const uint32_t i = lane + 64u * j;
+            if (i < n && (wp[j] & 0xFFFFu) != (w[j] & 0xFFFFu)) {
+                pw[i] = (wp[j] & 0xFFFFu) | (((w[j] >> 16) + (wp[j] >> 16)) << 16);
+                ch = true;
+            }
+        }
+        wave_sync();
+        if (!__any(ch)) break;
+    }
 }
 
 __global__ __launch_bounds__(kMThreads) void k_merge(MergeParams P) {
@@ -571,6 +608,7 @@ __global__ __launch_bounds__(kMThreads) void k_merge(MergeParams P) {
         L.tbase[tid] = b;
     }
     if (tid == 0) L.n_tail = 0;
+    const bool no_land = C[kCntScanDense] != 0;      // (k_scan's, read here: visible to this launch)
     __syncthreads();
     MP_MARK(0);
     MP_VAL(22, n);
@@ -668,12 +706,39 @@ __global__ __launch_bounds__(kMThreads) void k_merge(MergeParams P) {
     __syncthreads();                                 // off[] dead: lref[] reuses it
 #pragma unroll
     for (uint32_t j = 0; j < kPer; ++j)
-        if (i0 + j < n && vv[j] == kNxExit) L.lref[i0 + j] = atomicAdd(&L.n_tail, 1u);
+        if (i0 + j < n && vv[j] == kNxExit) {
+            const uint32_t k = atomicAdd(&L.n_tail, 1u);
+            L.lref[i0 + j] = k;
+            if (k < kLandCap) L.texit[k] = exit_of(r[j]);
+        }
     __syncthreads();
     MP_MARK(2);
     // reserve the ST's run of the tail list (a wave that takes no part in the
     // jumping below, so the atomic's round trip overlaps it)
     if (tid == kMThreads - 64) L.tail_base = reserve_tails(P, s, L.n_tail);
+    // the landing survivor of each EXIT tail (k_link's lookup, done here by the
+    // waves the jumping below leaves idle, so its two load rounds overlap it):
+    // the exit's tile count and its 8 stage slots in one round; a spilled tile
+    // is left to k_link (kNone), and so is every tail of a stream with dense
+    // tiles (another k_merge workgroup may be rewriting a tile's count and
+    // spill offset while this one reads them)
+    if (tid >= 64 && tid - 64 < L.n_tail && tid - 64 < kLandCap) {
+        const uint32_t k = tid - 64;
+        uint32_t w = kNone;                          // every looked-up slot is written (kNone: k_link's)
+        if (!no_land) {
+            const uint64_t x = L.texit[k];
+            const uint32_t t = (uint32_t)(x / kTile);
+            uint64_t o[kSlots];
+#pragma unroll
+            for (uint32_t q = 0; q < kSlots; ++q) o[q] = P.stage_info[t * kSlots + q].hdr_off;
+            const uint32_t tc = P.tile_count[t], tsp = P.tile_spill[t];
+            uint32_t hit = kTermDead;
+#pragma unroll
+            for (uint32_t q = 0; q < kSlots; ++q) hit = (q < tc && o[q] == x) ? t * kSlots + q : hit;
+            if (tsp == kNone && tc <= kSlots) w = hit;
+        }
+        L.tland[k] = w;
+    }
     // pointer jumping in place: every survivor -> its chain's tail, with frame
     // counts (pointer and count move together in one word, so a read of a word
     // another lane is rewriting sees either pair, both consistent). Up to
@@ -682,28 +747,8 @@ __global__ __launch_bounds__(kMThreads) void k_merge(MergeParams P) {
     // more take the whole workgroup.
     if (n <= kWaveJump) {
         if (tid < 64) {
-            constexpr uint32_t J = kWaveJump / 64;
-            for (;;) {
-                // one synchronous round: every read of the round before any write; the
-                // reads are unconditional (in-bounds words past n, unused) so the J
-                // reads issue back to back under one wait, twice per round
-                uint32_t w[J], wp[J];
-#pragma unroll
-                for (uint32_t j = 0; j < J; ++j) w[j] = L.pw[tid + 64u * j];
-#pragma unroll
-                for (uint32_t j = 0; j < J; ++j) wp[j] = L.pw[w[j] & (kStCap - 1u)];
-                bool ch = false;
-#pragma unroll
-                for (uint32_t j = 0; j < J; ++j) {
-                    const uint32_t i = tid + 64u * j;
-                    if (i < n && (wp[j] & 0xFFFFu) != (w[j] & 0xFFFFu)) {
-                        L.pw[i] = (wp[j] & 0xFFFFu) | (((w[j] >> 16) + (wp[j] >> 16)) << 16);
-                        ch = true;
-                    }
-                }
-                wave_sync();
-                if (!__any(ch)) break;
-            }
+            if (n <= kWaveJump / 2) wave_jump<kWaveJump / 128>(L.pw, n);
+            else wave_jump<kWaveJump / 64>(L.pw, n);
         }
         __syncthreads();
     } else {
@@ -744,7 +789,8 @@ __global__ __launch_bounds__(kMThreads) void k_merge(MergeParams P) {
         tab[i] = nd;
         if (vv[j] == kNxExit) {
             const uint64_t x = exit_of(r[j]);
-            P.tails[tb + L.lref[i]] = fws_tail_rec{x, nid[j], kTermDead, (uint32_t)(x >> P.st_shift), 0u};
+            const uint32_t k = L.lref[i];
+            P.tails[tb + k] = fws_tail_rec{x, nid[j], k < kLandCap ? L.tland[k] : kNone, (uint32_t)(x >> P.st_shift), 0u};
         }
         if (s == 0 && i == 0 && r[j].hdr_off == 0) {  // the root's chain, for resolve_path
             C[kCntRootSid] = nid[j];
@@ -1152,7 +1198,7 @@ __global__ __launch_bounds__(kMThreads) void k_link(MergeParams P) {
         while (x < total) {
             if (x >= fixed || x % kTailRun < nt) {
                 const uint64_t tx = tr.exit;
-                const uint32_t w = P.find_node(tx);
+                const uint32_t w = tr.w != kNone ? tr.w : P.find_node(tx);   // k_merge looked most up
                 const uint32_t wst = (uint32_t)(tx >> P.st_shift);
                 uint32_t g = kGTerm | kKindDead, ent = kNone, cnt = 0, esid = tr.id;
                 if (w != kTermDead) {

@@ -42,6 +42,10 @@ METRIC = "GiB/s masked WS payload unmasked, device-resident frame batch; % HBM r
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 GIB = float(1 << 30)
 DENSE_FRAMES, DENSE_PAYLOAD = 200000, 64   # SURVEY §6 dense small-frame workload
+# untimed calls before an extra config's timed ones: the 4 GiB C5 descriptor pass
+# measured 1.76 ms over its first 10 calls after one warm-up call and 1.58 ms over
+# the next 10 (tools/c5_warmup_probe.py, profiles/r03/c5_warmup.txt)
+EXTRA_WARMUP = 10
 
 
 def parse():
@@ -591,9 +595,10 @@ def c1_echo_extra(device=0):
     return out
 
 
-def _time(fn, steps, stream):
+def _time(fn, steps, stream, warmup=1):
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    fn(0)
+    for i in range(warmup):
+        fn(i)
     torch.cuda.synchronize()
     ev0.record(stream)
     for i in range(steps):
@@ -607,9 +612,9 @@ def batch_extra(ctx, bufs, dd, n, payload_bytes, args, stream):
     """fws_gpu_unmask_batch (k_plan + k_unmask_desc: any descriptor order) on
     the same C2 batches: the step, and the unmask kernel alone."""
     steps = max(20, args.steps // 2)
-    t = _time(lambda i: gpu.unmask_batch(ctx, bufs[i % args.nbuf], dd, n), steps, stream)
+    t = _time(lambda i: gpu.unmask_batch(ctx, bufs[i % args.nbuf], dd, n), steps, stream, warmup=EXTRA_WARMUP)
     gpu.unmask_plan(ctx, bufs[0], dd, n)
-    tk = _time(lambda i: gpu.unmask_run(ctx, bufs[i % args.nbuf], dd, n), steps, stream)
+    tk = _time(lambda i: gpu.unmask_run(ctx, bufs[i % args.nbuf], dd, n), steps, stream, warmup=EXTRA_WARMUP)
     return {"GiB_per_s": round(payload_bytes / t / GIB, 1), "ms_per_step": round(t * 1e3, 4),
             "k_unmask_desc_us": round(tk * 1e6, 2),
             "path": "fws_gpu_unmask_batch: k_plan + k_unmask_desc (descriptors in any order)"}
@@ -637,7 +642,7 @@ def stream_decode_extra(ctx, wire_c2, dev, args):
         def step(i):
             rc, _, _, _ = gpu.decode_stream(c, bufs[i % nbuf], cap, frames=frames, result=res, utf8_ok=ok)
             assert rc == 0, rc
-        t = _time(step, steps, stream)
+        t = _time(step, steps, stream, warmup=EXTRA_WARMUP)
         r = gpu.read_result(res)
         assert int(r["status"]) == 0 and int(r["n_frames"]) == n_frames, (name, r)
         payload = int(gpu.read_frames(frames, n_frames)["payload_len"].sum())
@@ -712,7 +717,7 @@ def stream_decode_extra(ctx, wire_c2, dev, args):
     total = int(d4["payload_len"].sum())
     dsts = [torch.empty(total + 64, dtype=torch.uint8, device=dev) for _ in range(4)]
     dd4 = gpu.descs_to_device(d4, dev)
-    t = _time(lambda i: gpu.unmask_gather(c, dsts[i % 4], src, dd4, len(d4)), steps, stream)
+    t = _time(lambda i: gpu.unmask_gather(c, dsts[i % 4], src, dd4, len(d4)), steps, stream, warmup=EXTRA_WARMUP)
     out["C4_fragmented_reassemble"] = {"GiB_per_s": round(total / t / GIB, 1), "ms_per_step": round(t * 1e3, 4),
                                        "fragments": len(d4), "alg_GB_per_s": round((len(w4) + total) / t / 1e9, 1)}
     c.close()
@@ -736,7 +741,7 @@ def stream_decode_extra(ctx, wire_c2, dev, args):
     c = gpu.Ctx(dev.index or 0, max_frames=n, max_stream_bytes=tx_total)
     touts = [torch.empty(tx_total, dtype=torch.uint8, device=dev) for _ in range(4)]
     olen = torch.empty(1, dtype=torch.int64, device=dev)
-    t = _time(lambda i: gpu.encode_frames(c, touts[i % 4], tsrc, tdd, n, out_len=olen), steps, stream)
+    t = _time(lambda i: gpu.encode_frames(c, touts[i % 4], tsrc, tdd, n, out_len=olen), steps, stream, warmup=EXTRA_WARMUP)
     assert int(olen.item()) == tx_total
     out["C2_tx_encode"] = {"GiB_per_s": round(n * pl / t / GIB, 1), "ms_per_step": round(t * 1e3, 4),
                            "frames": n, "alg_GB_per_s": round((n * pl + tx_total) / t / 1e9, 1),
@@ -758,7 +763,7 @@ def stream_decode_extra(ctx, wire_c2, dev, args):
         gpu.unmask_sorted_utf8(c, wd, dd5, len(d5), ok)
         torch.cuda.synchronize()
         flags_ok = bool(np.array_equal(ok.cpu().numpy(), np.asarray(ok5, dtype=np.uint8)[:len(d5)]))
-        t = _time(lambda i: gpu.unmask_sorted_utf8(c, wd, dd5, len(d5), ok), 10, stream)
+        t = _time(lambda i: gpu.unmask_sorted_utf8(c, wd, dd5, len(d5), ok), 10, stream, warmup=EXTRA_WARMUP)
         pl5 = int(d5["payload_len"].sum())
         out["C5_utf8_descriptor"] = {"GiB_per_s": round(pl5 / t / GIB, 1), "ms_per_step": round(t * 1e3, 4),
                                      "frames": len(d5), "alg_GB_per_s": round((len(w5) + pl5) / t / 1e9, 1),

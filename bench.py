@@ -595,6 +595,13 @@ def c1_echo_extra(device=0):
     return out
 
 
+def _step_roofline(alg_bytes, t, basis):
+    """roofline block of a whole extra step (every launch) against HBM peak"""
+    a = alg_bytes / t / 1e9
+    return {"bound": "hbm", "achieved": round(a, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(a / HBM_PEAK_GBS, 4), "basis": basis, "alg_bytes_per_step": int(alg_bytes)}
+
+
 def _time(fn, steps, stream, warmup=1):
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for i in range(warmup):
@@ -719,7 +726,8 @@ def stream_decode_extra(ctx, wire_c2, dev, args):
     dd4 = gpu.descs_to_device(d4, dev)
     t = _time(lambda i: gpu.unmask_gather(c, dsts[i % 4], src, dd4, len(d4)), steps, stream, warmup=EXTRA_WARMUP)
     out["C4_fragmented_reassemble"] = {"GiB_per_s": round(total / t / GIB, 1), "ms_per_step": round(t * 1e3, 4),
-                                       "fragments": len(d4), "alg_GB_per_s": round((len(w4) + total) / t / 1e9, 1)}
+                                       "fragments": len(d4), "alg_GB_per_s": round((len(w4) + total) / t / 1e9, 1),
+                                       "roofline": _step_roofline(len(w4) + total, t, "whole fws_gpu_unmask_gather step: wire read + payload written out of place")}
     c.close()
     del src, dsts, w4
     # TX: the C2 shape sent by a client -- 65 536 x 4 KiB payloads (back to
@@ -745,7 +753,8 @@ def stream_decode_extra(ctx, wire_c2, dev, args):
     assert int(olen.item()) == tx_total
     out["C2_tx_encode"] = {"GiB_per_s": round(n * pl / t / GIB, 1), "ms_per_step": round(t * 1e3, 4),
                            "frames": n, "alg_GB_per_s": round((n * pl + tx_total) / t / 1e9, 1),
-                           "path": "fws_gpu_encode_frames: client frames (header + key + masked payload)"}
+                           "path": "fws_gpu_encode_frames: client frames (header + key + masked payload)",
+                           "roofline": _step_roofline(n * pl + tx_total, t, "whole fws_gpu_encode_frames step: payload read + frames written")}
     c.close()
     del touts, tsrc
     # C5 per-GPU share: 262 144 x 16 KiB TEXT frames (4 GiB), decode + fused-launch UTF-8 flags
@@ -768,7 +777,8 @@ def stream_decode_extra(ctx, wire_c2, dev, args):
         out["C5_utf8_descriptor"] = {"GiB_per_s": round(pl5 / t / GIB, 1), "ms_per_step": round(t * 1e3, 4),
                                      "frames": len(d5), "alg_GB_per_s": round((len(w5) + pl5) / t / 1e9, 1),
                                      "flags_match_generator": flags_ok,
-                                     "path": "fws_gpu_unmask_sorted_utf8: k_unmask_sorted_utf8 + k_utf8_seam_sorted"}
+                                     "path": "fws_gpu_unmask_sorted_utf8: k_unmask_sorted_utf8 + k_utf8_seam_sorted",
+                                     "roofline": _step_roofline(len(w5) + pl5, t, "whole fws_gpu_unmask_sorted_utf8 step: wire read + payload written")}
         c.close()
         del w5, wd
     # end-to-end: pinned host -> HBM -> unmask -> host (PCIe-inclusive), C2

@@ -194,8 +194,8 @@ def test_many_exit_tails_per_super_tile(ctx, cuda, stride):
     tails -- past, past and just past k_merge's per-super-tile run of 16 (the
     overflow area, taken with an atomic, and k_link's loop over it), and
     within it. Bit-exact with the oracle; at ~250 per super tile the tail list
-    (64 per super tile + 4096) is full and the decode ends with
-    FWS_ERR_CAPACITY, nothing listed or unmasked."""
+    of a workspace sized for this stream (64 per super tile + 4096) is full and
+    the decode ends with FWS_ERR_CAPACITY, nothing listed or unmasked."""
     rng = np.random.default_rng(stride)
     frames = []
     for i in range(40):
@@ -205,13 +205,19 @@ def test_many_exit_tails_per_super_tile(ctx, cuda, stride):
             f[q:q + 8] = bytes([0x82, 0xFE]) + (65000).to_bytes(2, "big") + int(rng.integers(0, 2**32)).to_bytes(4, "little")
         frames.append(bytes(f))
     wire = np.frombuffer(b"".join(frames), dtype=np.uint8)
-    if stride > 256:
-        check(ctx, cuda, wire)
-        return
-    got, _, r = decode(ctx, wire, cuda)
-    from flashws_amd import _lib
-    assert int(r["status"]) == _lib.FWS_ERR_CAPACITY and int(r["n_frames"]) == 0
-    assert np.array_equal(got, wire)
+    # a fresh context: its decode workspace (tail list included) is sized by this
+    # stream, not by the larger streams earlier tests decoded
+    small = gpu.Ctx(0, max_frames=len(wire) // 6 + 16, max_stream_bytes=len(wire))
+    try:
+        if stride > 256:
+            check(small, cuda, wire)
+            return
+        got, _, r = decode(small, wire, cuda)
+        from flashws_amd import _lib
+        assert int(r["status"]) == _lib.FWS_ERR_CAPACITY and int(r["n_frames"]) == 0
+        assert np.array_equal(got, wire)
+    finally:
+        small.close()
 
 
 @pytest.mark.parametrize("seed", range(3))

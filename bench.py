@@ -796,6 +796,16 @@ def stream_decode_extra(ctx, wire_c2, dev, args):
     out["C2_end_to_end_pcie"] = {"GiB_per_s": round(int(descs["payload_len"].sum()) / t / GIB, 1),
                                  "ms_per_step": round(t * 1e3, 3),
                                  "path": "pinned H2D + fws_gpu_unmask_batch + D2H, one stream"}
+    # zero copy: the same batch unmasked by fws_gpu_unmask_sorted on the pinned host
+    # buffer itself -- the kernel's loads and stores cross PCIe in both directions at
+    # once, no copy engine and no device staging (tools/zc_probe.py)
+    zc = torch.from_numpy(wire_c2.copy()).pin_memory()
+    t = _time(lambda i: gpu.unmask_sorted(ctx, zc, dd, n), 10, stream, warmup=2)
+    zc_ok = bool(np.array_equal(zc.numpy(), wire_c2))      # 12 in-place passes: masked again
+    out["C2_end_to_end_zero_copy"] = {"GiB_per_s": round(int(descs["payload_len"].sum()) / t / GIB, 1),
+                                      "ms_per_step": round(t * 1e3, 3), "bytes_restored": zc_ok,
+                                      "path": "fws_gpu_unmask_sorted on the pinned host batch (zero copy over PCIe)"}
+    del zc
     # end to end, pipelined: C2 wire batches from pinned host memory through fws_rx_pipe
     # (H2D -> parse + unmask -> D2H of bytes, frames, result; depth 3 streams)
     del dbuf

@@ -408,6 +408,61 @@ __global__ __launch_bounds__(kBlock) void k_unmask_stream(uint8_t *base, uint64_
         }
         const uint32_t flo = unit_first[u];
         const uint32_t fhi = (u + 1 < n_units) ? unit_first[u + 1] : n - 1;
+        if (!kUtf8 && fhi - flo >= 2u && fhi - flo < 64u) {
+            // 3..64 frames meet the unit (frames under ~2 KiB): lane i holds frame
+            // flo + i in registers, as unit-relative offsets, and each chunk finds its
+            // frames by a binary search over the lanes (ds_bpermute), so the unit costs
+            // two dependent global round trips (unit_first, the records) instead of a
+            // search through global records per chunk
+            const uint32_t nf = fhi - flo + 1u;
+            const uint64_t U = u * 4096u;
+            u32x4 v[kUnmaskU];
+#pragma unroll
+            for (int j = 0; j < kUnmaskU; ++j) {      // the unit's data, overlapping the record loads
+                const uint64_t c = c0 + uint64_t(j) * 1024u;
+                v[j] = gload16<kNT>(b0 + (c < N ? c : U));
+            }
+            const fws_frame_info fi = fr[flo + (lane < (int)nf ? (uint32_t)lane : nf - 1u)];
+            const StreamFrame sf = stream_frame(fi, N);
+            auto rel = [&](uint64_t x) -> int32_t {   // unit-relative, clamped to [-16, 4096 + 16]
+                return x + 16u <= U ? -16 : (x >= U + 4112u ? 4112 : (int32_t)(x - U));
+            };
+            const int32_t fh = rel(fi.hdr_off), fp = rel(sf.po), fe = rel(sf.pe);
+            const uint32_t fk = rotr32(sf.key, 8u * ((uint32_t)(U - sf.po) & 3u));   // key phase at 4-aligned bytes
+            u32x4 m[kUnmaskU];
+#pragma unroll
+            for (int j = 0; j < kUnmaskU; ++j) {
+                const int32_t rc = j * 1024 + lane * 16;
+                uint32_t lo = 0;                      // last frame with hdr_off <= chunk start
+#pragma unroll
+                for (uint32_t s = 32; s; s >>= 1) {
+                    const int32_t h = (int32_t)__shfl((int)fh, (int)(lo + s), 64);
+                    if (lo + s < nf && h <= rc) lo += s;
+                }
+                m[j] = u32x4{0u, 0u, 0u, 0u};
+                bool go = true;
+                for (uint32_t k = lo;; ++k) {         // the frames from there that start before the chunk end
+                    const uint32_t kk = k < 64u ? k : 63u;
+                    const int32_t h = (int32_t)__shfl((int)fh, (int)(kk), 64);
+                    const int32_t p = (int32_t)__shfl((int)fp, (int)(kk), 64), e = (int32_t)__shfl((int)fe, (int)(kk), 64);
+                    const uint32_t key = (uint32_t)__shfl((int)fk, (int)kk, 64);
+                    go = go && k < nf && h < rc + 16;
+                    if (go) {
+                        m[j].x |= key & sel_bytes32(rc, p, e);
+                        m[j].y |= key & sel_bytes32(rc + 4, p, e);
+                        m[j].z |= key & sel_bytes32(rc + 8, p, e);
+                        m[j].w |= key & sel_bytes32(rc + 12, p, e);
+                    }
+                    if (!__any(go)) break;
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < kUnmaskU; ++j) {
+                const uint64_t c = c0 + uint64_t(j) * 1024u;
+                if (c < N && (m[j].x | m[j].y | m[j].z | m[j].w)) gstore16<kNT>(b0 + c, v[j] ^ m[j]);
+            }
+            continue;
+        }
         if (fhi - flo >= 2u) {                       // small frames: per-chunk search
             uint32_t carry = 0;                      // lane 63's last unmasked dword of step j - 1
 #pragma unroll 1

@@ -374,6 +374,11 @@ __device__ __forceinline__ uint32_t utf8_chunk_err32(const u32x4 &u, uint32_t pr
     return e0 | utf8_err(x.y, x.x) | utf8_err(x.z, x.y) | utf8_err(x.w, x.z);
 }
 
+#ifndef FWS_UNMASK_PRE
+#define FWS_UNMASK_PRE 1
+#endif
+constexpr bool kUnmaskPre = FWS_UNMASK_PRE != 0;   // A/B: every unit's loads before its frame lookup
+
 template <bool kNT, bool kUtf8, bool kRev>
 __global__ __launch_bounds__(kBlock) void k_unmask_stream(uint8_t *base, uint64_t N,
                                                           const fws_frame_info *__restrict__ fr, uint32_t cap,
@@ -397,7 +402,7 @@ __global__ __launch_bounds__(kBlock) void k_unmask_stream(uint8_t *base, uint64_
         // kUtf8 (VALU-heavier per unit): the unit's loads are issued before the frame
         // lookup, whose dependent round trips then overlap them
         u32x4 pre[kUnmaskU];
-        if constexpr (kUtf8) {
+        if constexpr (kUtf8 || kUnmaskPre) {
             const uint64_t last = (N - 1u) & ~uint64_t(15);
 #pragma unroll
             for (int j = 0; j < kUnmaskU; ++j) {
@@ -420,7 +425,8 @@ __global__ __launch_bounds__(kBlock) void k_unmask_stream(uint8_t *base, uint64_
 #pragma unroll
             for (int j = 0; j < kUnmaskU; ++j) {      // the unit's data, overlapping the record loads
                 const uint64_t c = c0 + uint64_t(j) * 1024u;
-                v[j] = gload16<kNT>(b0 + (c < N ? c : U));
+                if constexpr (kUnmaskPre) v[j] = pre[j];
+                else v[j] = gload16<kNT>(b0 + (c < N ? c : U));
             }
             const fws_frame_info fi = fr[flo + (lane < (int)nf ? (uint32_t)lane : nf - 1u)];
             const StreamFrame sf = stream_frame(fi, N);
@@ -557,7 +563,7 @@ __global__ __launch_bounds__(kBlock) void k_unmask_stream(uint8_t *base, uint64_
         u32x4 v[kUnmaskU];
 #pragma unroll
         for (int j = 0; j < kUnmaskU; ++j) {
-            if constexpr (kUtf8) v[j] = pre[j];    // (a dead chunk's bytes are never stored)
+            if constexpr (kUtf8 || kUnmaskPre) v[j] = pre[j];    // (a dead chunk's bytes are never stored)
             else v[j] = gload16<kNT>(live[j] ? ca[j] : safe);
         }
 #pragma unroll

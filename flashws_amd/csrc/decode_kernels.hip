@@ -98,7 +98,9 @@ __global__ __launch_bounds__(kScanThreads) __attribute__((amdgpu_waves_per_eu(8,
     const uint32_t lane = threadIdx.x & 63;
     ScanLds &W = lds_w[threadIdx.x >> 6];
     uint8_t *const B = W.bytes;
-    const uint32_t gw = blockIdx.x * kScanWaves + (threadIdx.x >> 6);
+    // wave-uniform: readfirstlane keeps the tile index and every tile-level
+    // address in SGPRs (threadIdx.x >> 6 alone is a VGPR to the compiler)
+    const uint32_t gw = __builtin_amdgcn_readfirstlane(blockIdx.x * kScanWaves + (threadIdx.x >> 6));
     const uint32_t GW = gridDim.x * kScanWaves;
     const uint32_t L32 = lane * 32u;
     const uint32_t L16 = lane * 16u;

@@ -30,7 +30,7 @@ __global__ __launch_bounds__(kBlock) void k_utf8(const uint8_t *__restrict__ bas
     if (n_dev && *n_dev < n) n = *n_dev;
     const int lane = threadIdx.x & 63;
     const uint32_t nw = gridDim.x * (kBlock / 64);
-    for (uint32_t f = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6); f < n; f += nw) {
+    for (uint32_t f = blockIdx.x * (kBlock / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); f < n; f += nw) {
         uint64_t off, len;
         bool eligible = true;
         if (kFrames) {

@@ -215,7 +215,7 @@ __global__ __launch_bounds__(kBlock) void k_mask_single(uint8_t *base, fws_frame
     const uintptr_t safe = a0 & ~uintptr_t(15);
     const int lane = threadIdx.x & (kWave - 1);
     const uint64_t nwaves = uint64_t(gridDim.x) * (kBlock / kWave);
-    for (uint64_t u = uint64_t(blockIdx.x) * (kBlock / kWave) + threadIdx.x / kWave; u < n_units;
+    for (uint64_t u = uint64_t(blockIdx.x) * (kBlock / kWave) + __builtin_amdgcn_readfirstlane(threadIdx.x / kWave); u < n_units;
          u += nwaves) {
         uintptr_t ca[kUnmaskU];
         bool live[kUnmaskU], full[kUnmaskU];

@@ -265,14 +265,14 @@ def test_c2_full_parity(ctx, cuda, resolve_mode):
         assert not fell_back(ctx), "C2 must resolve on the super-tile path with LDS tables"
 
 
-@pytest.mark.parametrize("n_frames,payload", [(200_000, 64), (200_000, 120), (600_000, 16)])
+@pytest.mark.parametrize("n_frames,payload", [(200_000, 64), (200_000, 120), (1_600_000, 16)])
 def test_dense_64b_frames(ctx, cuda, resolve_mode, n_frames, payload):
-    """200 000 x 64 B frames, 120 B, and 600 000 x 16 B. These
-    streams (4-26 MiB) are short, so the resolve uses 64 KiB super tiles
-    (st_tiles_for, merge_kernels.hip): 64 B and 120 B frames then fit the LDS
-    tables; 16 B frames (~3 000 per super tile) take the big-ST path, merged
-    and emitted in LDS (merge_mid / emit_mid), or over global scratch when
-    forced -- bit-exact either way."""
+    """200 000 x 64 B frames, 120 B, and 1 600 000 x 16 B. These
+    streams (14-35 MiB) are short, so the resolve uses 32 or 64 KiB super
+    tiles (st_tiles_for, merge_kernels.hip): 64 B and 120 B frames then fit
+    the LDS tables; 16 B frames in the 35 MiB stream (~3 000 per 64 KiB super
+    tile) take the big-ST path, merged and emitted in LDS (merge_mid /
+    emit_mid), or over global scratch when forced -- bit-exact either way."""
     wire, descs, _ = gpu.config_c2(seed=65, n_frames=n_frames, payload=payload)
     r = check(ctx, cuda, wire)
     assert int(r["n_frames"]) == n_frames

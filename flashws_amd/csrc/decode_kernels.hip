@@ -131,6 +131,10 @@ __global__ __launch_bounds__(kScanThreads) __attribute__((amdgpu_waves_per_eu(8,
     auto tile = [&](const uint32_t t, u32x4 (&pf)[2], u32x4 &halo) {
         const bool valid = t < n_tiles;                    // wave-uniform
         const uint64_t t0 = uint64_t(t) * kTile;
+        // stream bytes from the tile start, saturated at 1 MiB (scalar): every
+        // per-node bound below is then 32-bit (exits past the tile + halo are
+        // leaves whatever their exact offset)
+        const uint32_t rem = valid ? (N - t0 > (1u << 20) ? (1u << 20) : (uint32_t)(N - t0)) : 0u;
         uint32_t ns = 0, srank = 0, spill = kNone;
         bool rec = false;
         fws_frame_info fi;
@@ -217,9 +221,9 @@ __global__ __launch_bounds__(kScanThreads) __attribute__((amdgpu_waves_per_eu(8,
                             p = W.pos[k];
                             live = true;
                             const uint32_t len7 = B[p + 1u] & 127u;
-                            if (len7 < 126u && t0 + p + 6u <= N) {
+                            if (len7 < 126u && p + 6u <= rem) {
                                 const uint32_t nx = p + 6u + len7;
-                                if (nx < kTile && t0 + nx < N) live = (W.cm[nx >> 5] >> cand_pbit(nx & 31u)) & 1u;
+                                if (nx < kTile && nx < rem) live = (W.cm[nx >> 5] >> cand_pbit(nx & 31u)) & 1u;
                             }
                         }
                         if (live) atomicOr(&W.lm[p >> 5], 1u << (p & 31u));
@@ -254,22 +258,23 @@ __global__ __launch_bounds__(kScanThreads) __attribute__((amdgpu_waves_per_eu(8,
                     window16(wl, wh, p & 15u, d);
                     uint64_t plen = 0;
                     uint32_t key = 0;
-                    const int r = act ? lean_parse(d, N - (t0 + p), plen, key) : -1;
+                    const int r = act ? lean_parse(d, rem - p, plen, key) : -1;   // (p < rem)
                     uint32_t ptr = kDeadLane;
                     if (r == 0) {
                         ptr = lane;                            // incomplete header at the stream end
                     } else if (r > 0) {
-                        const uint64_t nxo = t0 + p + (uint64_t)r + plen;
-                        if (nxo >= t0 + kTile || nxo >= N) {
+                        // the exit, tile-relative, with the length saturated at 64 KiB
+                        const uint32_t hx = p + (uint32_t)r + (plen > 0xFFFFu ? 0x10000u : (uint32_t)plen);
+                        if (hx >= kTile || hx >= rem) {
                             ptr = lane;                        // leaves the tile / the stream
-                            const uint64_t hx = nxo - t0;      // unless its exit, in the halo, is no header
-                            if (nxo + 2u <= N && hx + 1u < kTile + kHaloX) {
+                            // unless its exit, in the halo, is no header
+                            if (hx + 2u <= rem && hx + 1u < kTile + kHaloX) {
                                 const uint32_t e0 = B[hx], e1 = B[hx + 1u];
                                 if ((e0 & 0x77u) > 2u || !(e1 & 0x80u)) ptr = kDeadLane;
                             }
                         } else {
                             // the node at the exit: a candidate (direct) or live bit, ranked
-                            const uint32_t nx = (uint32_t)(nxo - t0);
+                            const uint32_t nx = hx;
                             const uint32_t m = direct ? W.cm[nx >> 5] : W.lm[nx >> 5];
                             const uint32_t bit = direct ? cand_pbit(nx & 31u) : nx & 31u;
                             if ((m >> bit) & 1u) ptr = W.lpre[nx >> 5] + (uint32_t)__popc(m & ((1u << bit) - 1u));
@@ -318,7 +323,7 @@ __global__ __launch_bounds__(kScanThreads) __attribute__((amdgpu_waves_per_eu(8,
                         fi.opcode = (uint8_t)(b0 & 15u);
                         fi.fin = (uint8_t)(b0 >> 7);
                         fi.hdr_len = (uint8_t)r;
-                        fi.flags = (t0 + p + (uint64_t)r + plen > N) ? (uint8_t)FWS_FRAME_TRUNCATED : (uint8_t)0;
+                        fi.flags = (p + (uint64_t)r + plen > N - t0) ? (uint8_t)FWS_FRAME_TRUNCATED : (uint8_t)0;
                     }
                 }
             }

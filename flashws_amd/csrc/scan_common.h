@@ -128,7 +128,10 @@ __device__ __forceinline__ int parse_window(const u32x4 &lo, const u32x4 &hi, ui
 // that passed the two-byte test (so RSV, opcode and MASK are valid): header
 // length (> 0), 0 = incomplete (the same avail checks in the same order), or
 // FWS_ERR_TOO_LARGE; payload length and key. Window d = bytes p..p+15.
-__device__ __forceinline__ int lean_parse(const uint32_t d[4], uint64_t avail, uint64_t &plen, uint32_t &key) {
+// (avail: bytes from the header to the stream end, any width -- only its
+// comparisons with 2..14 matter, so k_scan passes a saturated 32-bit count)
+template <typename Avail>
+__device__ __forceinline__ int lean_parse(const uint32_t d[4], Avail avail, uint64_t &plen, uint32_t &key) {
     if (avail < 2) return 0;                                       // :443-445
     const uint32_t len7 = (d[0] >> 8) & 127u;
     if (len7 < 126u) {

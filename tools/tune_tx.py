@@ -1,6 +1,8 @@
 #!/usr/bin/env python3
 """A/B of k_tx_encode (compiler's allocation, 4 waves/SIMD) vs k_tx_encode_w5
-(5 waves/SIMD) on the C2 TX shape, HIP events; outputs checked equal."""
+(5 waves/SIMD) on the C2 TX shape, HIP events; outputs checked equal.
+
+usage: python tools/tune_tx.py [--lib PATH]   (--lib: an A/B build; the output's sha256 is printed)"""
 import json
 import os
 import sys
@@ -8,6 +10,9 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from flashws_amd import _lib  # noqa: E402
+if "--lib" in sys.argv:
+    _lib.LIB_PATH = os.path.abspath(sys.argv[sys.argv.index("--lib") + 1])
 from flashws_amd import gpu, lib  # noqa: E402
 import run_tx  # noqa: E402
 
@@ -31,7 +36,9 @@ def main(steps=100):
         torch.cuda.synchronize()
         res.setdefault(f"w5={w5}", []).append(round(e0.elapsed_time(e1) / steps * 1e3, 2))
     lib().fws_internal_set_tx_w5(0)
-    print(json.dumps({"tx_step_us": res}))
+    import hashlib
+    sha = hashlib.sha256(ref.cpu().numpy().tobytes()).hexdigest()[:16]
+    print(json.dumps({"lib": os.path.basename(_lib.LIB_PATH), "tx_step_us": res, "out_sha16": sha}))
     ctx.close()
 
 

@@ -282,8 +282,10 @@ __device__ __forceinline__ void tx_encode_body(uint8_t *__restrict__ out, const 
     }
 }
 
-// 4 waves per SIMD (107 VGPRs) as the compiler allocates it, or 5 with two
-// spilled registers (the rare second-seam loop); tuning hook below.
+// 4 waves per SIMD (107 VGPRs) as the compiler allocates it, or 5 (96 VGPRs,
+// no spill with ROCm 7.2): 5 is the default (C2 TX step 96 -> 90 us, order-
+// swapped A/B, profiles/r03/session3/tx_w5_ab.jsonl; 6 waves spill 18 VGPRs);
+// tuning hook below.
 __global__ __launch_bounds__(kBlock) void k_tx_encode(uint8_t *__restrict__ out, const uint8_t *__restrict__ src,
                                                       const fws_tx_desc *__restrict__ d, uint32_t n,
                                                       const uint64_t *__restrict__ obase,
@@ -300,7 +302,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
 
 }  // namespace fwsk
 
-static int g_tx_w5 = 0;  // tuning hook: 1 = k_tx_encode_w5
+static int g_tx_w5 = 1;  // tuning hook: 1 = k_tx_encode_w5 (default), 0 = the compiler's 4 waves
 extern "C" __attribute__((visibility("default"))) int fws_internal_set_tx_w5(int on) {
     const int old = g_tx_w5;
     g_tx_w5 = on != 0;

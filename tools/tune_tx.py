@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""A/B of k_tx_encode (compiler's allocation, 4 waves/SIMD) vs k_tx_encode_w5
+"""A/B of k_tx_encode (compiler's allocation, 4 waves/SIMD) vs k_tx_encode_w5 (the default)
 (5 waves/SIMD) on the C2 TX shape, HIP events; outputs checked equal.
 
 usage: python tools/tune_tx.py [--lib PATH]   (--lib: an A/B build; the output's sha256 is printed)"""
@@ -20,7 +20,7 @@ import run_tx  # noqa: E402
 def main(steps=100):
     ctx, outs, src, dd, n, total = run_tx.setup()
     res, ref = {}, None
-    for w5 in (0, 1, 0, 1):
+    for w5 in ((1, 0, 1, 0, 1, 0) if "--rev" in sys.argv else (0, 1, 0, 1)):
         lib().fws_internal_set_tx_w5(w5)
         for i in range(10):
             gpu.encode_frames(ctx, outs[i % 4], src, dd, n)
@@ -35,7 +35,7 @@ def main(steps=100):
         e1.record()
         torch.cuda.synchronize()
         res.setdefault(f"w5={w5}", []).append(round(e0.elapsed_time(e1) / steps * 1e3, 2))
-    lib().fws_internal_set_tx_w5(0)
+    lib().fws_internal_set_tx_w5(1)
     import hashlib
     sha = hashlib.sha256(ref.cpu().numpy().tobytes()).hexdigest()[:16]
     print(json.dumps({"lib": os.path.basename(_lib.LIB_PATH), "tx_step_us": res, "out_sha16": sha}))

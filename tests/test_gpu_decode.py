@@ -109,6 +109,24 @@ def test_truncated_payload(ctx, cuda):
     assert int(r["carry_unread"]) == 777
 
 
+@pytest.mark.parametrize("cut", [1, 3, 7, 40, 97, 3001])
+def test_dense_units_cut_anywhere(ctx, cuda, cut):
+    """Units that meet 3-64 frames (k_unmask_stream's register-held frames,
+    unit-relative offsets clamped to the unit) with the stream ending inside a
+    payload, inside a header, or on a unit edge: frames of 0-180 B with random
+    keys, bit-exact with the oracle including the carry-out."""
+    rng = np.random.default_rng(5000 + cut)
+    parts, total = [], 0
+    while total < 3 * 4096 + cut + 500:
+        n = int(rng.integers(0, 180))
+        parts.append(frame(int(rng.choice([1, 2, 0])), rng.integers(0, 256, n, dtype=np.uint8).tobytes(),
+                           fin=int(rng.random() < 0.8), key=int(rng.integers(0, 2**32))))
+        total += len(parts[-1])
+    wire = b"".join(parts)
+    check(ctx, cuda, wire[:3 * 4096 + cut])
+    check(ctx, cuda, wire[:len(wire) - cut])
+
+
 @pytest.mark.parametrize("bad,code", [(bytes([0xC2, 0x80]), -1), (bytes([0x83, 0x80]), -9),
                                       (bytes([0x82, 0x05]), -3),
                                       (bytes([0x82, 0xFF]) + (2**32 + 1).to_bytes(8, "big"), -2)])

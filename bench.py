@@ -534,7 +534,9 @@ def c1_echo_extra(device=0):
     reference's own unchanged echo client (tests/new-ws-echo/test_ws_client.cpp,
     oracle/_ref/ws_ref_client_1, 40,000 messages, its HashArr check every
     16,384th) against the hooked and the plain server. Host-memory path: every
-    read crosses PCIe twice when hooked."""
+    read crosses PCIe twice when hooked. `gpu_hook_batched`:
+    GpuRxHook::EnableBatched, the reads of all connections of one loop step in
+    one GPU round trip."""
     import subprocess
     import tempfile
     dropin = os.path.join(ROOT, "oracle", "_ref", "ws_dropin")
@@ -542,10 +544,10 @@ def c1_echo_extra(device=0):
     if not os.path.exists(dropin):
         return {"status": "absent: oracle/_ref/ws_dropin not built"}
 
-    def server(gpu, conns, port=0):
+    def server(mode, conns, port=0):
         args = [dropin, "server", "--port", str(port), "--conns", str(conns), "--max-seconds", "60"]
-        if gpu:
-            args += ["--gpu", "--device", str(device)]
+        if mode != "reference":
+            args += ["--gpu-batch" if mode == "gpu_hook_batched" else "--gpu", "--device", str(device)]
         p = subprocess.Popen(args, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
         line = p.stdout.readline()
         if not line.startswith("listening"):
@@ -561,21 +563,23 @@ def c1_echo_extra(device=0):
 
     out = {"workload": "C1: loopback echo, 4 KiB masked BIN frames, window 1, plain ws:// on 127.0.0.1",
            "server": "reference FLoop + WSServerSocket<false> (ws_dropin); hooked = + fws_amd::GpuRxHook::Enable"}
-    for clients, msgs in ((1, 20000), (8, 4000)):
-        for hooked in (False, True):
-            p, port = server(hooked, clients)
+    for clients, msgs in ((1, 20000), (8, 4000), (64, 500)):
+        for mode in ("reference", "gpu_hook", "gpu_hook_batched"):
+            if clients == 1 and mode == "gpu_hook_batched":
+                continue                     # one read per loop step: the per-read path's round trip
+            p, port = server(mode, clients)
             r = subprocess.run([dropin, "client", "--port", str(port), "--clients", str(clients), "--msgs", str(msgs),
                                 "--warmup", "200", "--msg-len", "4096", "--max-seconds", "60"],
                                capture_output=True, text=True, timeout=120)
             st = finish(p)
             rec = json.loads(r.stdout.strip().splitlines()[-1]) if r.stdout.strip() else {}
-            out[f"{clients}_client{'s' if clients > 1 else ''}_{'gpu_hook' if hooked else 'reference'}"] = {
+            out[f"{clients}_client{'s' if clients > 1 else ''}_{mode}"] = {
                 "goodput_rx_tx_mbps": rec.get("goodput_rx_tx_mbps"), "rtt_us": rec.get("rtt_us"),
                 "msgs_per_s": rec.get("msgs_per_s"), "verified": bool(rec.get("verified")) and r.returncode == 0,
-                "gpu_reads": st.get("gpu_reads")}
+                "gpu_reads": st.get("gpu_reads"), "gpu_batches": st.get("gpu_batches")}
     if os.path.exists(refcli):
         for hooked in (False, True):
-            p, port = server(hooked, 1, port=58600)   # the port compiled into the reference client
+            p, port = server("gpu_hook" if hooked else "reference", 1, port=58600)   # the reference client's port
             with tempfile.TemporaryDirectory() as td:
                 r = subprocess.run([refcli], capture_output=True, text=True, timeout=120, cwd=td)
             st = finish(p)

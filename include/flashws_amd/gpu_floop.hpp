@@ -35,6 +35,21 @@
 // access struct and pointers to members (no reference file is edited). The
 // wrapped on_close retires the connection's decoder (freed at the next read).
 //
+// Batched (plain ws://): EnableBatched(listen, loop) makes
+// every OPEN connection's read of one FLoop::OneStep wait in a pending list
+// (the reference decodes it inside the read loop, floop.h:661-703); at the end
+// of the step -- the loop's on_event callback, floop.h:743, which the hook
+// wraps and chains to the application's -- the reads of all connections go to
+// the GPU in one fws_rx_mux_feed (one H2D, one launch, one D2H) and their
+// events are dispatched in read order. A connection with a second read in the
+// same step (a full read buffer, floop.h:670-672), or whose peer closes in the
+// step (on_eof), has the pending batch decoded first, so each connection sees
+// its events in order and before its EOF. Per connection the callbacks are the
+// per-read path's; only their timing moves to the end of the step. A
+// protocol error closes the connection as the reference does and removes it
+// from the loop (DeleteFd, as floop.h:672-674 does after a read). More
+// connections than mux slots fall back to the per-read decoder.
+//
 // wss:// (SURVEY §8f rank 4): the under-socket is the reference's TLSSocket,
 // whose readable callback (tls_on_readable_, tls_socket.h:206-209) receives
 // the reads OpenSSL has already decrypted on the CPU (SSL_read loop,
@@ -44,7 +59,9 @@
 
 #include <cstdio>
 #include <cstring>
+#include <functional>
 #include <memory>
+#include <stdexcept>
 #include <string_view>
 #include <unordered_map>
 #include <utility>
@@ -61,6 +78,17 @@ struct TcpAccess : fws::TCPSocket {
 
 struct TlsAccess : fws::TLSSocket {
     using fws::TLSSocket::tls_on_readable_;
+};
+
+struct TcpEofAccess : fws::TCPSocket {
+    using fws::TCPSocket::on_eof_;
+};
+
+// the loop's end-of-OneStep callback (floop.h:743) and DeleteFd (floop.h:348)
+template <class Loop>
+struct LoopAccess : Loop {
+    using Loop::on_event_;
+    using Loop::DeleteFd;
 };
 
 // the under-socket's readable callback member (the one InitUnderOnReadImp sets)
@@ -129,13 +157,47 @@ public:
         });
     }
 
+    // Batched decode of each loop step's reads (plain ws://; see the header).
+    // Call after Enable's prerequisites and after any SetOnEventFunc of the
+    // application (the hook chains to it).
+    template <class Loop>
+    void EnableBatched(Sock &listen, Loop &loop, uint32_t max_conns = 1024) {
+        static_assert(!kTls, "batched decode is for plain ws:// (TLS reads come from SSL_read one by one)");
+        Enable(listen);
+        if (fws_rx_mux_create(ctx_.get(), max_conns, &mux_) != 0) throw std::runtime_error("fws_rx_mux_create failed");
+        for (uint32_t i = max_conns; i-- > 0;) free_slots_.push_back(i);
+        using LA = detail::LoopAccess<Loop>;
+        auto app_event = loop.*(&LA::on_event_);      // the application's (or the loop's no-op)
+        Loop *lp = &loop;
+        app_on_event_ = [app_event, lp]() mutable { app_event(*lp); };
+        delete_fd_ = [lp](void *p) { (lp->*(&LA::DeleteFd))(p, false); };
+        GpuRxHookT *self = this;
+        loop.SetOnEventFunc([self](Loop &) {
+            self->Flush();
+            self->app_on_event_();
+        });
+    }
+
+    ~GpuRxHookT() {
+        if (mux_) fws_rx_mux_destroy(mux_);
+    }
+
     size_t connections() const { return conns_.size(); }
     uint64_t gpu_reads() const { return gpu_reads_; }
+    uint64_t gpu_batches() const { return gpu_batches_; }
 
 private:
+    static constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
     struct Conn {
         Sock *ws;
-        std::unique_ptr<GpuRxDecoder<fws::IOBuffer>> dec;
+        std::unique_ptr<GpuRxDecoder<fws::IOBuffer>> dec;   // per-read path (no mux slot)
+        uint32_t slot = kNoSlot;                           // batched path: fws_rx_mux slot
+        bool pending = false;                              // a read of this step waits in pending_
+        fws::TCPSocket::OnEofFunc ref_eof;                 // the under-socket's own on_eof
+    };
+    struct Pending {
+        USock *u;
+        fws::IOBuffer buf;
     };
 
     // Maps decoded events onto the reference's own members (see the header).
@@ -175,18 +237,106 @@ private:
     void Attach(Sock &w) {
         auto &c = conns_[&w.under_socket()];
         c.ws = &w;
-        c.dec = std::make_unique<GpuRxDecoder<fws::IOBuffer>>(ctx_);
+        if (c.slot != kNoSlot) free_slots_.push_back(c.slot);   // a stale entry at a reused address
+        c.slot = kNoSlot;
+        c.dec.reset();
+        c.pending = false;
+        if (mux_ && !free_slots_.empty() && fws_rx_mux_reset(mux_, free_slots_.back()) == 0) {
+            c.slot = free_slots_.back();
+            free_slots_.pop_back();
+        } else {
+            c.dec = std::make_unique<GpuRxDecoder<fws::IOBuffer>>(ctx_);
+        }
         GpuRxHookT *self = this;
         w.under_socket().SetOnReadable([self](USock &u, fws::IOBuffer &&buf, void *ud) {
             self->OnReadable(u, std::move(buf), ud);
         });
+        if constexpr (!kTls) {
+            if (c.slot != kNoSlot) {
+                auto &eof = static_cast<fws::TCPSocket &>(w.under_socket()).*(&detail::TcpEofAccess::on_eof_);
+                c.ref_eof = eof;
+                eof = [self](fws::TCPSocket &t, void *ud) { self->OnEof(t, ud); };
+            }
+        }
     }
 
     void Retire(Sock &w) {
         auto it = conns_.find(&w.under_socket());
         if (it == conns_.end()) return;
-        retired_.push_back(std::move(it->second.dec));   // may be mid-dispatch: freed at the next read
+        if (it->second.dec) retired_.push_back(std::move(it->second.dec));   // may be mid-dispatch: freed at the next read
+        if (it->second.slot != kNoSlot) free_slots_.push_back(it->second.slot);
         conns_.erase(it);
+    }
+
+    // The peer closed (floop.h:678-690): this connection's pending read is
+    // decoded first, then the under-socket's own on_eof runs.
+    void OnEof(fws::TCPSocket &t, void *ud) {
+        auto it = conns_.find(static_cast<USock *>(&t));
+        if (it == conns_.end()) return;              // retired: its socket is being torn down
+        fws::TCPSocket::OnEofFunc ref = it->second.ref_eof;
+        if (it->second.pending) Flush();
+        if (ref) ref(t, ud);
+    }
+
+    // The step's pending reads: one fws_rx_mux_feed, then each read's events
+    // in read order (ws_server_socket.h:172-196 per read).
+    void Flush() {
+        if (pending_.empty()) return;
+        std::vector<Pending> batch;
+        batch.swap(pending_);
+        std::vector<fws_rx_read> reads;
+        std::vector<uint32_t> idx;                   // reads[k] -> batch index
+        reads.reserve(batch.size());
+        for (uint32_t i = 0; i < batch.size(); ++i) {
+            auto it = conns_.find(batch[i].u);
+            if (it == conns_.end()) continue;
+            it->second.pending = false;
+            fws::IOBuffer &b = batch[i].buf;
+            reads.push_back(fws_rx_read{it->second.slot, 0u, b.data + b.start_pos, (uint64_t)b.size,
+                                        (uint64_t)(b.capacity - b.start_pos)});
+            idx.push_back(i);
+        }
+        std::vector<fws_rx_read_result> res(reads.size());
+        const int rc = reads.empty() ? 0 : fws_rx_mux_feed(mux_, reads.data(), (uint32_t)reads.size(), res.data());
+        if (!reads.empty()) ++gpu_batches_;
+        for (size_t k = 0; k < reads.size(); ++k) {
+            Pending &p = batch[idx[k]];
+            auto it = conns_.find(p.u);               // an earlier read's callbacks may have closed it
+            if (it == conns_.end()) continue;
+            Sock &sock = *it->second.ws;
+            if ((sock.*(&A::server_status_)) != A::kOpen) continue;
+            ++gpu_reads_;
+            const uint32_t slot = it->second.slot;
+            int ret = rc;
+            if (rc == 0) {
+                ret = res[k].ret;
+                Sink sink{sock};
+                GpuRxDecoder<fws::IOBuffer>::DispatchEvents(p.buf, res[k].events, res[k].n_events, res[k].ctl, sink);
+            }
+            Finish(sock, *p.u, ret, [&]() {
+                uint32_t op = 0;
+                (void)fws_rx_mux_error(mux_, slot, &op);
+                return op;
+            }, true);
+        }
+    }
+
+    // After a read's events: a protocol error closes the connection with the
+    // reference's reason; a closed or failed socket's TCP socket is closed
+    // (ws_server_socket.h:176-194) and, on the batched path, removed from the
+    // loop as the read loop does after a read (floop.h:672-674).
+    template <class ErrOp>
+    void Finish(Sock &sock, USock &u, int ret, ErrOp &&err_opcode, bool batched) {
+        if (ret < 0) {
+            SetErrorText(ret, err_opcode());
+            const std::string_view e = fws::GetErrorStrV();
+            const size_t max_len = fws::constants::WS_MAX_CONTROL_FRAME_SIZE - A::kCtlHdr - 2U;
+            sock.Close(fws::WS_ABNORMAL_CLOSE, std::string_view{e.data(), std::min(e.size(), max_len)});
+        }
+        if (ret < 0 || ((sock.*(&A::server_status_)) == A::kClosed && !(sock.*(&A::in_shutting_down_)))) {
+            sock.under_socket().Close();
+            if (batched && delete_fd_) delete_fd_(static_cast<void *>(&u));
+        }
     }
 
     // ws_server_socket.h:172-196 with OnRecvData on the GPU.
@@ -197,18 +347,21 @@ private:
             ref_readable_(u, std::move(buf), ud);
             return;
         }
+        if (it->second.slot != kNoSlot) {            // batched: decoded at the end of the step
+            if (it->second.pending) {                // a second read this step: the batch goes first
+                Flush();
+                it = conns_.find(&u);
+                if (it == conns_.end() || (it->second.ws->*(&A::server_status_)) != A::kOpen) return;
+            }
+            it->second.pending = true;
+            pending_.push_back(Pending{&u, std::move(buf)});
+            return;
+        }
         Sock &sock = *it->second.ws;
         GpuRxDecoder<fws::IOBuffer> *dec = it->second.dec.get();   // `it` may be erased by on_close
         ++gpu_reads_;
         const int ret = dec->OnRecvData(buf, Sink{sock});
-        if (ret < 0) {
-            SetErrorText(ret, dec->error_opcode());
-            const std::string_view e = fws::GetErrorStrV();
-            const size_t max_len = fws::constants::WS_MAX_CONTROL_FRAME_SIZE - A::kCtlHdr - 2U;
-            sock.Close(fws::WS_ABNORMAL_CLOSE, std::string_view{e.data(), std::min(e.size(), max_len)});
-        }
-        if (ret < 0 || ((sock.*(&A::server_status_)) == A::kClosed && !(sock.*(&A::in_shutting_down_))))
-            sock.under_socket().Close();
+        Finish(sock, u, ret, [&]() { return dec->error_opcode(); }, false);
     }
 
     // The error texts ParseFrameHdr sets (w_socket.h:452, 468, 494-496); -3 sets none.
@@ -234,7 +387,13 @@ private:
     typename U::Func ref_readable_;
     std::unordered_map<USock *, Conn> conns_;
     std::vector<std::unique_ptr<GpuRxDecoder<fws::IOBuffer>>> retired_;
-    uint64_t gpu_reads_ = 0;
+    uint64_t gpu_reads_ = 0, gpu_batches_ = 0;
+    // batched path
+    fws_rx_mux *mux_ = nullptr;
+    std::vector<uint32_t> free_slots_;
+    std::vector<Pending> pending_;
+    std::function<void()> app_on_event_;
+    std::function<void(void *)> delete_fd_;
 };
 
 using GpuRxHook = GpuRxHookT<false>;      // ws://

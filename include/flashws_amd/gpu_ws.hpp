@@ -76,6 +76,15 @@ public:
         uint64_t n_ev = 0, ctl_used = 0;
         // the session's own event / control sinks: sized by what the read holds
         const int ret = fws_rx_session_feed_view(s_, data, size, cap, &ev, &n_ev, &ctl, &ctl_used);
+        DispatchEvents(io_buf, ev, n_ev, ctl, sink);
+        return ret;
+    }
+
+    // One read's decoded events onto the sink, in order (OnRecvData's callbacks,
+    // w_socket.h:629-747); also used for the reads of a batched feed (fws_rx_mux).
+    template <class Sink>
+    static void DispatchEvents(IOBuffer &io_buf, const fws_rx_event *ev, uint64_t n_ev, const uint8_t *ctl,
+                               Sink &sink) {
         for (uint64_t i = 0; i < n_ev; ++i) {
             const fws_rx_event &e = ev[i];
             const std::string_view payload((const char *)ctl + e.ctl_off, e.kind == 0 && !e.is_ctl ? 0 : e.size);
@@ -98,7 +107,6 @@ public:
                 sink.on_read(e.opcode, std::move(b), e.frame_end != 0, e.msg_end != 0, true);
             }
         }
-        return ret;
     }
 
     // The opcode of the frame the last failing read stopped at (for the

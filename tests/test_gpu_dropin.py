@@ -12,6 +12,10 @@ is moved to the MI355X by ONE added call, fws_amd::GpuRxHook::Enable
   reference's error text) and the server's on_close log must be identical;
 * load: the reference's WSClientSocket with many connections, every echoed
   byte checked, PINGs answered, clean CLOSE handshakes, through the GPU hook;
+* batched: the same scripted parity, load runs and the
+  reference's echo client with GpuRxHook::EnableBatched, which decodes the
+  reads of all connections of one FLoop step in one GPU round trip
+  (fws_rx_mux) at the end of the step;
 * wss:// (SURVEY §8f rank 4): the same scripted parity and a load run over
   the reference's TLSSocket (WSServerSocket<true> + fws_amd::GpuRxHookTls):
   OpenSSL decrypts on the CPU, the GPU decodes the plaintext reads. The
@@ -36,13 +40,13 @@ TLS_ARGS = ["--tls", "--cert", os.path.join(ROOT, "tests", "tls", "server.crt"),
 
 
 class Server:
-    def __init__(self, gpu, conns, max_seconds=90, tls=False):
+    def __init__(self, gpu, conns, max_seconds=90, tls=False, batch=False):
         if not os.path.exists(DROPIN):
             pytest.fail("oracle/_ref/ws_dropin not built (make -C oracle ref in the build container; "
                         "__graft_entry__.build() produces it)", pytrace=False)
         args = [DROPIN, "server", "--conns", str(conns), "--max-seconds", str(max_seconds)]
         if gpu:
-            args.append("--gpu")
+            args.append("--gpu-batch" if batch else "--gpu")
         if tls:
             args += TLS_ARGS
         self.p = subprocess.Popen(args, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
@@ -128,8 +132,8 @@ def _scripts():
 SCRIPTS = _scripts()
 
 
-def _run_all(gpu, tls=False):
-    srv = Server(gpu, conns=len(SCRIPTS), tls=tls)
+def _run_all(gpu, tls=False, batch=False):
+    srv = Server(gpu, conns=len(SCRIPTS), tls=tls, batch=batch)
     got = {}
     for name, (stream, chunks) in SCRIPTS.items():
         head, data = wsraw.run_script(srv.port, stream, chunks, tls=tls)
@@ -137,11 +141,16 @@ def _run_all(gpu, tls=False):
     return got, srv.finish()
 
 
-@pytest.mark.parametrize("tls", [False, True], ids=["ws", "wss"])
-def test_dropin_scripted_parity_with_reference_server(cuda, tls):
+@pytest.mark.parametrize("tls,batch", [(False, False), (True, False), (False, True)], ids=["ws", "wss", "ws_batched"])
+def test_dropin_scripted_parity_with_reference_server(cuda, tls, batch):
+    """Scripted sessions (split reads, PING, fragmented messages, protocol
+    errors, CLOSE) against the reference server and the hooked one, per read
+    and batched per loop step (GpuRxHook::EnableBatched): handshake replies,
+    every echoed / control / close frame byte and the close log are equal."""
     ref, ref_srv = _run_all(gpu=False, tls=tls)
-    gpu, gpu_srv = _run_all(gpu=True, tls=tls)
+    gpu, gpu_srv = _run_all(gpu=True, tls=tls, batch=batch)
     assert gpu_srv["gpu_reads"] > 0 and ref_srv["gpu_reads"] == 0
+    assert (gpu_srv["gpu_batches"] > 0) == batch
     for name in SCRIPTS:
         assert gpu[name][0] == ref[name][0], name                     # handshake reply
         assert gpu[name][1] == ref[name][1], (name, wsraw.parse_server_frames(ref[name][1])[-2:],
@@ -159,10 +168,13 @@ def test_dropin_scripted_parity_with_reference_server(cuda, tls):
     assert sum(1 for f in fr if f[1] == 10) > 0                       # PONGs
 
 
-@pytest.mark.parametrize("clients,msg_len,tls", [(1, 4096, False), (8, 4096, False), (4, 70000, False),
-                                                 (16, 512, False), (8, 4096, True), (2, 70000, True)])
-def test_dropin_reference_client_load(cuda, clients, msg_len, tls):
-    srv = Server(True, conns=clients, tls=tls)
+@pytest.mark.parametrize("clients,msg_len,tls,batch", [(1, 4096, False, False), (8, 4096, False, False),
+                                                       (4, 70000, False, False), (16, 512, False, False),
+                                                       (8, 4096, True, False), (2, 70000, True, False),
+                                                       (8, 4096, False, True), (4, 70000, False, True),
+                                                       (16, 512, False, True)])
+def test_dropin_reference_client_load(cuda, clients, msg_len, tls, batch):
+    srv = Server(True, conns=clients, tls=tls, batch=batch)
     r = subprocess.run([DROPIN, "client", "--port", str(srv.port), "--clients", str(clients), "--msgs", "600",
                         "--warmup", "20", "--msg-len", str(msg_len), "--ping-every", "50", "--max-seconds", "60"]
                        + (["--tls"] if tls else []), capture_output=True, text=True, timeout=90)
@@ -172,13 +184,15 @@ def test_dropin_reference_client_load(cuda, clients, msg_len, tls):
     assert cli["verified"] is True and cli["pongs"] == clients * (620 // 50)
     assert st["gpu_reads"] > 0 and st["msgs"] == clients * 620
     assert all(c == [1000, b"bye".hex()] for c in st["close_log_hex"][:clients])
+    if batch:                       # the step's reads went to the GPU together
+        assert 0 < st["gpu_batches"] <= st["gpu_reads"]
 
 
 REF_CLIENTS = {n: os.path.join(ROOT, "oracle", "_ref", f"ws_ref_client_{n}") for n in (1, 8)}
 REF_CLIENT_PORT = 58600        # oracle/refclient/test_def.h (compile-time in the reference client)
 
 
-def run_reference_client(n_clients, gpu, tmp_path):
+def run_reference_client(n_clients, gpu, tmp_path, batch=False):
     """The reference's unchanged tests/new-ws-echo/test_ws_client.cpp (built by
     oracle/Makefile `refclient` with our loopback test_def.h: 4 KiB BIN
     messages, 40,000 in total) against the drop-in server. Returns the client's
@@ -188,7 +202,7 @@ def run_reference_client(n_clients, gpu, tmp_path):
         pytest.fail(f"{exe} not built (make -C oracle refclient in the build container)", pytrace=False)
     args = [DROPIN, "server", "--port", str(REF_CLIENT_PORT), "--conns", str(n_clients), "--max-seconds", "90"]
     if gpu:
-        args.append("--gpu")
+        args.append("--gpu-batch" if batch else "--gpu")
     p = subprocess.Popen(args, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
     line = p.stdout.readline()
     assert line.startswith("listening"), (line, p.stderr.read()[-2000:] if p.poll() is not None else "")
@@ -198,14 +212,14 @@ def run_reference_client(n_clients, gpu, tmp_path):
     return r, json.loads(out.strip().splitlines()[-1])
 
 
-@pytest.mark.parametrize("n_clients", [1, 8])
-def test_reference_echo_client_through_gpu_hook(cuda, n_clients, tmp_path):
+@pytest.mark.parametrize("n_clients,batch", [(1, False), (8, False), (8, True)], ids=["1", "8", "8_batched"])
+def test_reference_echo_client_through_gpu_hook(cuda, n_clients, batch, tmp_path):
     """C1 through the reference's own echo client: every message the client gets
     back was unmasked by the MI355X (GpuRxHook), its FWS_ASSERT(size ==
     MAX_DATA_LEN) holds for each one (test_ws_client.cpp:217) and its HashArr
     of the echoed payload equals the hash of what it sent at every 16,384th
     message (test_ws_client.cpp:260-277; a mismatch aborts the client)."""
-    r, st = run_reference_client(n_clients, True, tmp_path)
+    r, st = run_reference_client(n_clients, True, tmp_path, batch=batch)
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-2000:])
     data_hash = [ln.split(":")[1].strip() for ln in r.stdout.splitlines() if ln.startswith("data hash:")]
     checks = [ln.rsplit("hash value:", 1)[1].split(",")[0].strip() for ln in r.stdout.splitlines()

@@ -53,6 +53,7 @@ struct Opts {
     std::string cert, key;
     int port = 0;
     bool gpu = false;
+    bool gpu_batch = false;             // --gpu-batch: GpuRxHook::EnableBatched
     int device = 0;
     int conns = 1;
     int clients = 1;
@@ -141,7 +142,14 @@ int RunServer(const Opts &o) {
     if (o.gpu) {
         gpu = std::make_unique<fws_amd::GpuContext>(o.device);
         hook = std::make_unique<fws_amd::GpuRxHookT<kTls>>(*gpu);
-        hook->Enable(ws);                      // the one added line
+        bool batched = false;
+        if constexpr (!kTls) {
+            if (o.gpu_batch) {                 // (or: every read of a loop step in one GPU batch)
+                hook->EnableBatched(ws, srv.loop);
+                batched = true;
+            }
+        }
+        if (!batched) hook->Enable(ws);        // the one added line
     }
 
     if (ws.StartListen("127.0.0.1", uint16_t(o.port), 128, fws::TCPSocket::REUSE_ADDR_MODE) < 0) die("listen");
@@ -168,9 +176,10 @@ int RunServer(const Opts &o) {
     }
     log += "]";
     std::printf("{\"mode\": \"server\", \"tls\": %s, \"gpu\": %s, \"msgs\": %llu, \"bytes\": %llu, \"closes\": %d, "
-                "\"close_log_hex\": %s, \"gpu_reads\": %llu}\n",
+                "\"close_log_hex\": %s, \"gpu_reads\": %llu, \"gpu_batches\": %llu}\n",
                 kTls ? "true" : "false", o.gpu ? "true" : "false", (unsigned long long)srv.msgs, (unsigned long long)srv.bytes, srv.closes,
-                log.c_str(), (unsigned long long)(hook ? hook->gpu_reads() : 0));
+                log.c_str(), (unsigned long long)(hook ? hook->gpu_reads() : 0),
+                (unsigned long long)(hook ? hook->gpu_batches() : 0));
     std::fflush(stdout);
     if constexpr (kTls) std::_Exit(0);        // see RunClient: no static TLS teardown
     return 0;
@@ -312,6 +321,7 @@ int main(int argc, char **argv) {
         else if (a == "--cert") o.cert = next();
         else if (a == "--key") o.key = next();
         else if (a == "--gpu") o.gpu = true;
+        else if (a == "--gpu-batch") o.gpu = o.gpu_batch = true;
         else if (a == "--device") o.device = std::atoi(next().c_str());
         else if (a == "--conns") o.conns = std::atoi(next().c_str());
         else if (a == "--clients") o.clients = std::atoi(next().c_str());

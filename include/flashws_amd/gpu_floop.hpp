@@ -35,7 +35,7 @@
 // access struct and pointers to members (no reference file is edited). The
 // wrapped on_close retires the connection's decoder (freed at the next read).
 //
-// Batched (plain ws://): EnableBatched(listen, loop) makes
+// Batched (ws:// and wss://): EnableBatched(listen, loop) makes
 // every OPEN connection's read of one FLoop::OneStep wait in a pending list
 // (the reference decodes it inside the read loop, floop.h:661-703); at the end
 // of the step -- the loop's on_event callback, floop.h:743, which the hook
@@ -78,6 +78,7 @@ struct TcpAccess : fws::TCPSocket {
 
 struct TlsAccess : fws::TLSSocket {
     using fws::TLSSocket::tls_on_readable_;
+    using fws::TLSSocket::tls_on_eof_;
 };
 
 struct TcpEofAccess : fws::TCPSocket {
@@ -96,12 +97,16 @@ template <bool kTls> struct UnderAccess;
 template <> struct UnderAccess<false> {
     using Sock = fws::TCPSocket;
     using Func = fws::TCPSocket::OnReadableFunc;
+    using EofFunc = fws::TCPSocket::OnEofFunc;
     static constexpr auto member = &TcpAccess::on_readable_;
+    static constexpr auto eof_member = &TcpEofAccess::on_eof_;
 };
 template <> struct UnderAccess<true> {
     using Sock = fws::TLSSocket;
     using Func = fws::TLSSocket::TLSOnReadbleFunc;
+    using EofFunc = fws::TLSSocket::TLSOnEofFunc;   // (called from the base's on_eof, tls_socket.h:468)
     static constexpr auto member = &TlsAccess::tls_on_readable_;
+    static constexpr auto eof_member = &TlsAccess::tls_on_eof_;
 };
 
 template <bool kTls>
@@ -157,12 +162,11 @@ public:
         });
     }
 
-    // Batched decode of each loop step's reads (plain ws://; see the header).
-    // Call after Enable's prerequisites and after any SetOnEventFunc of the
-    // application (the hook chains to it).
+    // Batched decode of each loop step's reads (ws:// and wss://; see the
+    // header). Call after any SetOnEventFunc of the application (the hook
+    // chains to it).
     template <class Loop>
     void EnableBatched(Sock &listen, Loop &loop, uint32_t max_conns = 1024) {
-        static_assert(!kTls, "batched decode is for plain ws:// (TLS reads come from SSL_read one by one)");
         Enable(listen);
         if (fws_rx_mux_create(ctx_.get(), max_conns, &mux_) != 0) throw std::runtime_error("fws_rx_mux_create failed");
         for (uint32_t i = max_conns; i-- > 0;) free_slots_.push_back(i);
@@ -193,7 +197,7 @@ private:
         std::unique_ptr<GpuRxDecoder<fws::IOBuffer>> dec;   // per-read path (no mux slot)
         uint32_t slot = kNoSlot;                           // batched path: fws_rx_mux slot
         bool pending = false;                              // a read of this step waits in pending_
-        fws::TCPSocket::OnEofFunc ref_eof;                 // the under-socket's own on_eof
+        typename U::EofFunc ref_eof;                       // the under-socket's own on_eof
     };
     struct Pending {
         USock *u;
@@ -251,12 +255,10 @@ private:
         w.under_socket().SetOnReadable([self](USock &u, fws::IOBuffer &&buf, void *ud) {
             self->OnReadable(u, std::move(buf), ud);
         });
-        if constexpr (!kTls) {
-            if (c.slot != kNoSlot) {
-                auto &eof = static_cast<fws::TCPSocket &>(w.under_socket()).*(&detail::TcpEofAccess::on_eof_);
-                c.ref_eof = eof;
-                eof = [self](fws::TCPSocket &t, void *ud) { self->OnEof(t, ud); };
-            }
+        if (c.slot != kNoSlot) {
+            auto &eof = static_cast<USock &>(w.under_socket()).*(U::eof_member);
+            c.ref_eof = eof;
+            eof = [self](USock &t, void *ud) { self->OnEof(t, ud); };
         }
     }
 
@@ -270,10 +272,10 @@ private:
 
     // The peer closed (floop.h:678-690): this connection's pending read is
     // decoded first, then the under-socket's own on_eof runs.
-    void OnEof(fws::TCPSocket &t, void *ud) {
-        auto it = conns_.find(static_cast<USock *>(&t));
+    void OnEof(USock &t, void *ud) {
+        auto it = conns_.find(&t);
         if (it == conns_.end()) return;              // retired: its socket is being torn down
-        fws::TCPSocket::OnEofFunc ref = it->second.ref_eof;
+        typename U::EofFunc ref = it->second.ref_eof;
         if (it->second.pending) Flush();
         if (ref) ref(t, ud);
     }

@@ -12,7 +12,7 @@ is moved to the MI355X by ONE added call, fws_amd::GpuRxHook::Enable
   reference's error text) and the server's on_close log must be identical;
 * load: the reference's WSClientSocket with many connections, every echoed
   byte checked, PINGs answered, clean CLOSE handshakes, through the GPU hook;
-* batched: the same scripted parity, load runs and the
+* batched (SURVEY §8f rank 1, ws:// and wss://): the same scripted parity, load runs and the
   reference's echo client with GpuRxHook::EnableBatched, which decodes the
   reads of all connections of one FLoop step in one GPU round trip
   (fws_rx_mux) at the end of the step;
@@ -141,7 +141,8 @@ def _run_all(gpu, tls=False, batch=False):
     return got, srv.finish()
 
 
-@pytest.mark.parametrize("tls,batch", [(False, False), (True, False), (False, True)], ids=["ws", "wss", "ws_batched"])
+@pytest.mark.parametrize("tls,batch", [(False, False), (True, False), (False, True), (True, True)],
+                         ids=["ws", "wss", "ws_batched", "wss_batched"])
 def test_dropin_scripted_parity_with_reference_server(cuda, tls, batch):
     """Scripted sessions (split reads, PING, fragmented messages, protocol
     errors, CLOSE) against the reference server and the hooked one, per read
@@ -172,7 +173,7 @@ def test_dropin_scripted_parity_with_reference_server(cuda, tls, batch):
                                                        (4, 70000, False, False), (16, 512, False, False),
                                                        (8, 4096, True, False), (2, 70000, True, False),
                                                        (8, 4096, False, True), (4, 70000, False, True),
-                                                       (16, 512, False, True)])
+                                                       (16, 512, False, True), (8, 4096, True, True)])
 def test_dropin_reference_client_load(cuda, clients, msg_len, tls, batch):
     srv = Server(True, conns=clients, tls=tls, batch=batch)
     r = subprocess.run([DROPIN, "client", "--port", str(srv.port), "--clients", str(clients), "--msgs", "600",

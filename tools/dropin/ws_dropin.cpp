@@ -142,14 +142,8 @@ int RunServer(const Opts &o) {
     if (o.gpu) {
         gpu = std::make_unique<fws_amd::GpuContext>(o.device);
         hook = std::make_unique<fws_amd::GpuRxHookT<kTls>>(*gpu);
-        bool batched = false;
-        if constexpr (!kTls) {
-            if (o.gpu_batch) {                 // (or: every read of a loop step in one GPU batch)
-                hook->EnableBatched(ws, srv.loop);
-                batched = true;
-            }
-        }
-        if (!batched) hook->Enable(ws);        // the one added line
+        if (o.gpu_batch) hook->EnableBatched(ws, srv.loop);   // (or: every read of a loop step in one GPU batch)
+        else hook->Enable(ws);                 // the one added line
     }
 
     if (ws.StartListen("127.0.0.1", uint16_t(o.port), 128, fws::TCPSocket::REUSE_ADDR_MODE) < 0) die("listen");

@@ -306,6 +306,10 @@ private:
             auto it = conns_.find(p.u);               // an earlier read's callbacks may have closed it
             if (it == conns_.end()) continue;
             Sock &sock = *it->second.ws;
+            // closed by an earlier read's callbacks in this step (an application
+            // closing another connection): its read is dropped -- the per-read path
+            // would hand it to the reference's closing-state callback, but the mux
+            // has already unmasked it in place
             if ((sock.*(&A::server_status_)) != A::kOpen) continue;
             ++gpu_reads_;
             const uint32_t slot = it->second.slot;

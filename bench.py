@@ -599,6 +599,23 @@ def c1_echo_extra(device=0):
     return out
 
 
+def check_c5_stream(rec):
+    """Fail the bench when the C5 stream record's correctness fields disagree:
+    the per-frame UTF-8 flags of the call on the masked batch must equal the
+    generator's (count and frame by frame), and that call must decode every frame."""
+    bad = []
+    if rec.get("utf8_invalid_frames") != rec.get("utf8_invalid_frames_expected"):
+        bad.append(f"utf8_invalid_frames {rec.get('utf8_invalid_frames')} != expected "
+                   f"{rec.get('utf8_invalid_frames_expected')}")
+    if rec.get("flags_match_generator") is not True:
+        bad.append("per-frame UTF-8 flags differ from the generator's")
+    if rec.get("first_call_status") != 0 or rec.get("first_call_frames") != rec.get("frames"):
+        bad.append(f"first call status {rec.get('first_call_status')} frames {rec.get('first_call_frames')}")
+    if bad:
+        raise RuntimeError("C5 stream decode record failed its checks: " + "; ".join(bad))
+    return rec
+
+
 def _step_roofline(alg_bytes, t, basis):
     """roofline block of a whole extra step (every launch) against HBM peak"""
     a = alg_bytes / t / 1e9
@@ -638,7 +655,7 @@ def stream_decode_extra(ctx, wire_c2, dev, args):
     steps = max(4, min(args.steps, 50)) // 2 * 2         # even: in-place XOR restores the input
     out = {}
 
-    def decode_cfg(name, wire, n_frames, utf8=False, nbuf=None, pipelined=True):
+    def decode_cfg(name, wire, n_frames, utf8=False, nbuf=None, pipelined=True, expect_ok=None):
         if nbuf is None:
             # rotate >= 1 GiB of distinct batches so the 256 MB Infinity Cache cannot
             # serve a step from the one before: 4 for C2 / C3, 77 of the
@@ -653,6 +670,25 @@ def stream_decode_extra(ctx, wire_c2, dev, args):
         def step(i):
             rc, _, _, _ = gpu.decode_stream(c, bufs[i % nbuf], cap, frames=frames, result=res, utf8_ok=ok)
             assert rc == 0, rc
+        checks = {}
+        if utf8:
+            # the flags are only meaningful on masked input: take them from the first
+            # call on the fresh (masked) batch, before the timed loop, then XOR the
+            # batch back (in-place unmask is an involution). In the timed loop below
+            # every call unmasks the previous call's output in place, so with one
+            # buffer the calls alternate between masked text and the re-masked result
+            # (whose flags say "invalid"); the flags read after it are not reported.
+            step(0)
+            torch.cuda.synchronize()
+            r0 = gpu.read_result(res)
+            checks["utf8_invalid_frames"] = int((ok[:n_frames] == 0).sum().item())
+            if expect_ok is not None:
+                checks["flags_match_generator"] = bool(np.array_equal(
+                    ok[:n_frames].cpu().numpy(), np.asarray(expect_ok, dtype=np.uint8)[:n_frames]))
+            checks["first_call_status"] = int(r0["status"])
+            checks["first_call_frames"] = int(r0["n_frames"])
+            step(1)
+            torch.cuda.synchronize()
         t = _time(step, steps, stream, warmup=EXTRA_WARMUP)
         r = gpu.read_result(res)
         assert int(r["status"]) == 0 and int(r["n_frames"]) == n_frames, (name, r)
@@ -667,7 +703,10 @@ def stream_decode_extra(ctx, wire_c2, dev, args):
                             "frac": round(alg / HBM_PEAK_GBS, 4), "basis": "whole fws_gpu_decode_stream step",
                             "alg_bytes_per_step": len(wire) + payload}}
         if utf8:
-            rec["utf8_invalid_frames"] = int((ok[:n_frames] == 0).sum().item())
+            rec.update(checks)
+            rec["timed_input"] = (f"{nbuf} in-place buffer(s): the timed calls alternate between masked text and "
+                                  "its unmasked output (XOR involution); utf8_invalid_frames is from the call on "
+                                  "the masked batch before timing")
         if pipelined and nbuf >= 4:
             # two batches in flight (two connections' reads): a context, a frame list and a
             # stream each, so one batch's latency-bound resolve overlaps the other's streaming
@@ -764,8 +803,9 @@ def stream_decode_extra(ctx, wire_c2, dev, args):
     # C5 per-GPU share: 262 144 x 16 KiB TEXT frames (4 GiB), decode + fused-launch UTF-8 flags
     if args.c5:
         w5, d5, ok5 = gpu.config_c5()
-        rec = decode_cfg("C5", w5, len(d5), utf8=True, nbuf=1)
+        rec = decode_cfg("C5", w5, len(d5), utf8=True, nbuf=1, expect_ok=ok5)
         rec["utf8_invalid_frames_expected"] = int((ok5 == 0).sum())
+        check_c5_stream(rec)
         out["C5_utf8_text_decode"] = rec
         # the same batch in descriptor mode (a batch split at frame boundaries knows its
         # frames): one pass of unmask + UTF-8 flags, fws_gpu_unmask_sorted_utf8
@@ -776,6 +816,9 @@ def stream_decode_extra(ctx, wire_c2, dev, args):
         gpu.unmask_sorted_utf8(c, wd, dd5, len(d5), ok)
         torch.cuda.synchronize()
         flags_ok = bool(np.array_equal(ok.cpu().numpy(), np.asarray(ok5, dtype=np.uint8)[:len(d5)]))
+        if not flags_ok:
+            raise RuntimeError("C5 descriptor mode: UTF-8 flags differ from the generator's")
+        gpu.unmask_sorted_utf8(c, wd, dd5, len(d5), ok)       # masked again (XOR involution)
         t = _time(lambda i: gpu.unmask_sorted_utf8(c, wd, dd5, len(d5), ok), 10, stream, warmup=EXTRA_WARMUP)
         pl5 = int(d5["payload_len"].sum())
         out["C5_utf8_descriptor"] = {"GiB_per_s": round(pl5 / t / GIB, 1), "ms_per_step": round(t * 1e3, 4),

@@ -425,6 +425,11 @@ extern "C" __attribute__((visibility("default"))) int fws_internal_scan_only(fws
     if (!n_tiles || N < kTile + kHaloX) return FWS_ERR_INVALID;
     const uint32_t need = (n_tiles + kScanWaves - 1) / kScanWaves;
     const uint32_t sg = need < d.scan_grid ? need : d.scan_grid;
+    // its own zeroed counter set (set 0) every call, so the spill offsets and
+    // kCntScanDense start clean; the next decode zeroes the set it uses
+    hipError_t e = hipMemsetAsync(d.cnt_base, 0, kCntStride * 4, s);
+    if (e != hipSuccess) return fws_hip_status(e);
+    d.cnt_dirty = true;
     hipLaunchKernelGGL(k_scan<true>, dim3(sg), dim3(kScanThreads), 0, s, wire, N, n_tiles, d.stage_info, d.spill_info,
                        d.tile_spill, d.tile_count, d.cnt_base, (uint32_t)d.max_surv, d.scan_dummy);
     return fws_hip_status(hipGetLastError());

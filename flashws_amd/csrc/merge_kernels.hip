@@ -66,9 +66,9 @@ constexpr uint32_t kStCap = 2048;                   // survivors of one ST in LD
 constexpr int kMThreads = 512;
 constexpr int kMWaves = kMThreads / 64;
 constexpr uint32_t kPer = kStCap / kMThreads;       // survivors per thread: i = kPer * tid + j
-constexpr uint32_t kWaveJump = 512;
-constexpr uint32_t kTailRun = 16;
-constexpr uint32_t kLandCap = 256;                  // k_merge: EXIT tails whose landing survivor it looks up                   // EXIT tails of one super tile in its own tail-list run                 // k_merge: one wavefront pointer-jumps up to this many
+constexpr uint32_t kWaveJump = 512;                 // k_merge: one wavefront pointer-jumps up to this many
+constexpr uint32_t kTailRun = 16;                   // EXIT tails of one super tile in its own tail-list run
+constexpr uint32_t kLandCap = 256;                  // k_merge: EXIT tails whose landing survivor it looks up
 constexpr uint32_t kTailCapMax = 1u << 18;          // LDS bitmap of the path pruning
 constexpr uint32_t kCompCap = 32768;                // tails that are some tail's next (+ the root's)
 constexpr uint32_t kMaxPruneRounds = 64;

@@ -42,13 +42,16 @@
 // wraps and chains to the application's -- the reads of all connections go to
 // the GPU in one fws_rx_mux_feed (one H2D, one launch, one D2H) and their
 // events are dispatched in read order. A connection with a second read in the
-// same step (a full read buffer, floop.h:670-672), or whose peer closes in the
-// step (on_eof), has the pending batch decoded first, so each connection sees
-// its events in order and before its EOF. Per connection the callbacks are the
-// per-read path's; only their timing moves to the end of the step. A
-// protocol error closes the connection as the reference does and removes it
-// from the loop (DeleteFd, as floop.h:672-674 does after a read). More
-// connections than mux slots fall back to the per-read decoder.
+// same step (a full read buffer, floop.h:670-672), whose peer closes in the
+// step (on_eof), or which the loop closes in the step (the EOF / error branch,
+// floop.h:715-730 -> on_close) has the pending batch decoded first, so each
+// connection sees its events in order and before its EOF / on_close. Per
+// connection the callbacks are the per-read path's; only their timing moves to
+// the end of the step. A read of a connection that an earlier read's callbacks
+// closed in the same step goes to the reference's own readable callback, as on
+// the per-read path. A protocol error closes the connection as the reference
+// does and removes it from the loop (DeleteFd, as floop.h:672-674 does after a
+// read). More connections than mux slots fall back to the per-read decoder.
 //
 // wss:// (SURVEY §8f rank 4): the under-socket is the reference's TLSSocket,
 // whose readable callback (tls_on_readable_, tls_socket.h:206-209) receives
@@ -178,6 +181,7 @@ public:
         GpuRxHookT *self = this;
         loop.SetOnEventFunc([self](Loop &) {
             self->Flush();
+            self->DeleteDeferred();
             self->app_on_event_();
         });
     }
@@ -202,6 +206,7 @@ private:
     struct Pending {
         USock *u;
         fws::IOBuffer buf;
+        void *ud;
     };
 
     // Maps decoded events onto the reference's own members (see the header).
@@ -262,9 +267,25 @@ private:
         }
     }
 
+    // The wrapped on_close. A read of this connection still pending in the step
+    // is decoded and dispatched first: the reference has already delivered it
+    // inside the read loop (floop.h:661-703) when the same step's EOF / error
+    // branch closes the socket (floop.h:715-730: DeleteFd(true) -> Close ->
+    // on_close), so on_read comes before on_close as there. That flush runs
+    // inside the loop's DeleteFd: it neither closes this socket again nor
+    // removes any socket from the loop then (DeleteDeferred does, at the end of
+    // the step; a DeleteFd nested in DeleteFd could move the map entry the outer
+    // call still holds).
     void Retire(Sock &w) {
         auto it = conns_.find(&w.under_socket());
         if (it == conns_.end()) return;
+        if (it->second.pending && retiring_ == nullptr) {
+            retiring_ = static_cast<USock *>(&w.under_socket());
+            Flush();
+            retiring_ = nullptr;
+            it = conns_.find(&w.under_socket());
+            if (it == conns_.end()) return;
+        }
         if (it->second.dec) retired_.push_back(std::move(it->second.dec));   // may be mid-dispatch: freed at the next read
         if (it->second.slot != kNoSlot) free_slots_.push_back(it->second.slot);
         conns_.erase(it);
@@ -307,10 +328,16 @@ private:
             if (it == conns_.end()) continue;
             Sock &sock = *it->second.ws;
             // closed by an earlier read's callbacks in this step (an application
-            // closing another connection): its read is dropped -- the per-read path
-            // would hand it to the reference's closing-state callback, but the mux
-            // has already unmasked it in place
-            if ((sock.*(&A::server_status_)) != A::kOpen) continue;
+            // closing another connection): the read goes to the reference's own
+            // callback, as on the per-read path -- in a closing state it does not
+            // decode the bytes (the mux has unmasked them in place), it closes the
+            // TCP socket (ws_server_socket.h:187-194)
+            if ((sock.*(&A::server_status_)) != A::kOpen) {
+                if (p.u == retiring_) continue;      // inside its own Close already
+                ref_readable_(*p.u, std::move(p.buf), p.ud);
+                if (!p.u->is_open()) DeleteFd(p.u);
+                continue;
+            }
             ++gpu_reads_;
             const uint32_t slot = it->second.slot;
             int ret = rc;
@@ -339,10 +366,24 @@ private:
             const size_t max_len = fws::constants::WS_MAX_CONTROL_FRAME_SIZE - A::kCtlHdr - 2U;
             sock.Close(fws::WS_ABNORMAL_CLOSE, std::string_view{e.data(), std::min(e.size(), max_len)});
         }
+        if (&u == retiring_) return;                  // closing already (Retire)
         if (ret < 0 || ((sock.*(&A::server_status_)) == A::kClosed && !(sock.*(&A::in_shutting_down_)))) {
             sock.under_socket().Close();
-            if (batched && delete_fd_) delete_fd_(static_cast<void *>(&u));
+            if (batched) DeleteFd(&u);
         }
+    }
+
+    // Remove a closed socket from the loop as the read loop does after a read
+    // (floop.h:672-674); inside Retire's flush, at the end of the step instead.
+    void DeleteFd(USock *u) {
+        if (!delete_fd_ || u == retiring_) return;
+        if (retiring_) deferred_.push_back(u);
+        else delete_fd_(static_cast<void *>(u));
+    }
+    void DeleteDeferred() {
+        std::vector<USock *> d;
+        d.swap(deferred_);
+        for (USock *u : d) delete_fd_(static_cast<void *>(u));   // FLoop::DeleteFd: a no-op if gone
     }
 
     // ws_server_socket.h:172-196 with OnRecvData on the GPU.
@@ -357,10 +398,13 @@ private:
             if (it->second.pending) {                // a second read this step: the batch goes first
                 Flush();
                 it = conns_.find(&u);
-                if (it == conns_.end() || (it->second.ws->*(&A::server_status_)) != A::kOpen) return;
+                if (it == conns_.end() || (it->second.ws->*(&A::server_status_)) != A::kOpen) {
+                    ref_readable_(u, std::move(buf), ud);    // as the top of this function does
+                    return;
+                }
             }
             it->second.pending = true;
-            pending_.push_back(Pending{&u, std::move(buf)});
+            pending_.push_back(Pending{&u, std::move(buf), ud});
             return;
         }
         Sock &sock = *it->second.ws;
@@ -400,6 +444,8 @@ private:
     std::vector<Pending> pending_;
     std::function<void()> app_on_event_;
     std::function<void(void *)> delete_fd_;
+    USock *retiring_ = nullptr;                        // Retire's flush in progress for this socket
+    std::vector<USock *> deferred_;                    // DeleteFd at the end of the step
 };
 
 using GpuRxHook = GpuRxHookT<false>;      // ws://

@@ -6,6 +6,7 @@ import os
 import socket
 
 import numpy as np
+import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
@@ -103,3 +104,17 @@ def test_kfd_gpu_count(tmp_path):
     assert bench.kfd_gpu_count(str(tmp_path), env={"ROCR_VISIBLE_DEVICES": "0,1"}) == 2
     assert bench.kfd_gpu_count(str(tmp_path), env={"HIP_VISIBLE_DEVICES": ""}) == 0
     assert bench.kfd_gpu_count(str(tmp_path / "absent"), env={}) is None
+
+
+def test_c5_stream_record_check_fails_loudly():
+    """bench.py's C5 stream record: its UTF-8 flags come from the call on the
+    masked batch and a mismatch with the generator makes the bench raise
+    (a record once showed 262144 invalid frames against 2692)."""
+    import bench
+    good = {"frames": 262144, "utf8_invalid_frames": 2692, "utf8_invalid_frames_expected": 2692,
+            "flags_match_generator": True, "first_call_status": 0, "first_call_frames": 262144}
+    assert bench.check_c5_stream(dict(good)) == good
+    for bad in ({"utf8_invalid_frames": 262144}, {"utf8_invalid_frames_expected": 2693},
+                {"flags_match_generator": False}, {"first_call_status": -1}, {"first_call_frames": 5}):
+        with pytest.raises(RuntimeError):
+            bench.check_c5_stream({**good, **bad})

@@ -229,3 +229,29 @@ def test_reference_echo_client_through_gpu_hook(cuda, n_clients, batch, tmp_path
     assert all(c == data_hash[0] for c in checks)
     assert "avg (rx+tx) goodput" in r.stdout
     assert st["gpu"] is True and st["gpu_reads"] > 0 and st["msgs"] == 40000
+
+
+@pytest.mark.parametrize("scenario", ["close_peers", "eof_with_data"])
+@pytest.mark.parametrize("mode", ["gpu", "gpu_batch"])
+def test_dropin_same_step_reads_match_reference(cuda, scenario, mode):
+    """Two reads in one FLoop step (tests/dropin_steps.py): (close_peers) A's
+    on_read closes connection B while B's read of the same step is still to be
+    handled -- the batched hook hands it to the reference's closing-state
+    callback as the per-read path does, so B's TCP socket is closed at once;
+    (eof_with_data) B's last data and its EOF arrive in one event -- the batched
+    hook decodes B's pending read before on_close (floop.h:715-730), so the
+    message is counted as in the reference. Everything both clients receive and
+    the server's message count and close log equal the reference server's."""
+    import dropin_steps
+    ref = dropin_steps.run_scenario(DROPIN, "reference", scenario)
+    got = dropin_steps.run_scenario(DROPIN, mode, scenario)
+    assert got["server"]["gpu_reads"] > 0
+    if mode == "gpu_batch":
+        assert got["server"]["gpu_batches"] > 0
+    for k in ("msgs", "bytes", "close_log_hex"):
+        assert got["server"][k] == ref["server"][k], (k, got["server"], ref["server"])
+    assert got["a_frames"] == ref["a_frames"] and got["b_frames"] == ref["b_frames"], (got, ref)
+    if scenario == "close_peers":
+        assert ref["b_frames"] == [(1, 8, (1000).to_bytes(2, "big") + b"peer")]
+    else:
+        assert ref["server"]["msgs"] == 3          # sleep, shutwr and B's last data frame

@@ -11,6 +11,12 @@
 //   (WriteFrame, ws_server_socket.h:131-141); PONG parts are ignored. Prints
 //   "listening <port>", then one JSON line when --conns connections closed:
 //   messages echoed, the on_close (code, reason) log, GPU reads.
+//   --commands (tests only): a message whose payload starts with "cmd:" is a
+//   command -- "cmd:sleep:<ms>" (echoed; the loop's end-of-step callback then
+//   sleeps, so the next step collects every read sent meanwhile),
+//   "cmd:close-peers" (echoed; Close(1000, "peer") on every other connection),
+//   "cmd:shutwr" (not echoed; shutdown(SHUT_WR) of this connection's TCP socket),
+//   "cmd:noecho..." (counted, not echoed).
 // --tls (both modes): wss:// -- WSServerSocket<true> / WSClientSocket<true> over
 //   the reference's TLSSocket and SSLManager (server: --cert / --key files, no
 //   peer verification); the server's hook is then fws_amd::GpuRxHookTls, which
@@ -62,6 +68,7 @@ struct Opts {
     size_t warmup = 50;
     size_t ping_every = 0;
     int max_seconds = 60;
+    bool commands = false;
 };
 
 [[noreturn]] void die(const char *what) {
@@ -84,6 +91,8 @@ struct Server {
     int closes = 0;
     std::vector<std::pair<uint32_t, std::string>> close_log;
     std::unordered_set<void *> live;   // user data constructed by on_new_connection
+    std::vector<void *> socks;         // open WS sockets (--commands: close-peers)
+    int sleep_ms = 0;                  // --commands: sleep at the end of this step
 
     static fws::IOBuffer NewMsg(size_t cap) {
         fws::IOBuffer b = fws::RequestBuf(kHead + cap);
@@ -105,10 +114,11 @@ int RunServer(const Opts &o) {
     WS ws{};
     if (ws.Init() < 0) die("WSServerSocket::Init");
     Server *S = &srv;
-    ws.SetOnNewConnection([S](WS &, std::string_view, std::string_view, std::string_view, std::string_view,
+    ws.SetOnNewConnection([S](WS &w, std::string_view, std::string_view, std::string_view, std::string_view,
                               std::string_view, std::string_view &, std::string_view &, void *ud) {
         new (ud) ConnCtx{Server::NewMsg(1u << 16), 2u};
         S->live.insert(ud);
+        S->socks.push_back(&w);
         return 0;
     });
     ws.SetOnRead([S](WS &s, uint32_t opcode, fws::IOBuffer &&part, bool, bool is_msg_end, bool is_ctl, void *ud) {
@@ -127,16 +137,39 @@ int RunServer(const Opts &o) {
         if (is_msg_end) {
             ++S->msgs;
             S->bytes += uint64_t(c.msg.size);
-            if (s.WriteFrame(std::move(c.msg), fws::WSTxFrameType(c.opcode), true) < 0) die("WriteFrame");
+            const std::string_view m{reinterpret_cast<const char *>(c.msg.data + c.msg.start_pos), size_t(c.msg.size)};
+            const bool cmd = S->o.commands && m.substr(0, 4) == "cmd:";
+            bool echo = true;
+            std::vector<WS *> peers;
+            if (cmd && m.substr(4, 6) == "sleep:") S->sleep_ms = std::atoi(std::string(m.substr(10)).c_str());
+            if (cmd && m.substr(4) == "close-peers")
+                for (void *p : S->socks) if (p != &s) peers.push_back(static_cast<WS *>(p));
+            if (cmd && m.substr(4) == "shutwr") {
+                if constexpr (!kTls) s.under_socket().Shutdown(fws::TCPSocket::SHUT_WR_MODE);   // ws:// only
+                echo = false;
+            }
+            if (cmd && m.substr(4, 6) == "noecho") echo = false;
+            if (echo && s.WriteFrame(std::move(c.msg), fws::WSTxFrameType(c.opcode), true) < 0) die("WriteFrame");
             c.msg = Server::NewMsg(1u << 16);
+            for (WS *p : peers) p->Close(fws::WS_NORMAL_CLOSE, "peer");
         }
     });
-    ws.SetOnClose([S](WS &, uint32_t code, std::string_view reason, void *ud) {
+    ws.SetOnClose([S](WS &w, uint32_t code, std::string_view reason, void *ud) {
+        S->socks.erase(std::remove(S->socks.begin(), S->socks.end(), static_cast<void *>(&w)), S->socks.end());
         S->close_log.emplace_back(code, std::string(reason));
         if (S->live.erase(ud)) std::destroy_at(static_cast<ConnCtx *>(ud));
         if (++S->closes >= S->o.conns) S->loop.StopRun();
     });
 
+    if (o.commands) {
+        // the application's end-of-step callback (the batched hook chains to it)
+        srv.loop.SetOnEventFunc([S](Loop &) {
+            if (S->sleep_ms > 0) {
+                ::usleep(useconds_t(S->sleep_ms) * 1000u);
+                S->sleep_ms = 0;
+            }
+        });
+    }
     std::unique_ptr<fws_amd::GpuContext> gpu;
     std::unique_ptr<fws_amd::GpuRxHookT<kTls>> hook;
     if (o.gpu) {
@@ -324,6 +357,7 @@ int main(int argc, char **argv) {
         else if (a == "--warmup") o.warmup = std::strtoull(next().c_str(), nullptr, 10);
         else if (a == "--ping-every") o.ping_every = std::strtoull(next().c_str(), nullptr, 10);
         else if (a == "--max-seconds") o.max_seconds = std::atoi(next().c_str());
+        else if (a == "--commands") o.commands = true;
         else die(("unknown option " + a).c_str());
     }
     if (o.mode == "server") return o.tls ? RunServer<true>(o) : RunServer<false>(o);

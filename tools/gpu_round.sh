@@ -18,7 +18,7 @@
 #   trace        phase clocks of k_scan and per-workgroup timelines of the resolve kernels
 #                (FWS_SCAN_PROF build: make -C flashws_amd/csrc prof, built beforehand)
 set -o pipefail
-ROUND=${ROUND:-r03}
+ROUND=${ROUND:-r04}
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 O=$R/gpurun_out/$ROUND
 mkdir -p "$O"

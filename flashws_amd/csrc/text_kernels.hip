@@ -190,9 +190,149 @@ __global__ __launch_bounds__(kBlock) void k_gather_fast(uint8_t *__restrict__ ds
     }
 }
 
+// ------------------------------------------------------------- one launch
+// k_gather_one: the same gather with no plan launch, for batches of at most
+// kGatherLdsMax regions (C4: 1427 fragments). Every workgroup of a persistent
+// grid builds the whole dst prefix (dbase) in LDS from the descriptors -- one
+// round of coalesced loads (L2-resident after the first workgroups) and a
+// block scan, about the latency of one dependent round trip -- and then walks
+// its units as k_gather_fast does; the unit's regions come from two rounds of
+// 64 lane probes into that LDS prefix instead of the plan's unit map. The plan
+// launch (k_out_plan, 6.9 us on C4) and its launch boundary are gone.
+constexpr uint32_t kGatherLdsMax = 2048;
+constexpr uint32_t kGatherPer = kGatherLdsMax / kBlock;   // regions per thread in the block scan
+
+// The last f < n with base[f] <= pos (base[0] = 0 <= pos; base in LDS): lane
+// probes at a stride, then inside the bracketed stride. Wave-uniform result.
+__device__ __forceinline__ uint32_t lds_owner(const uint64_t *base, uint32_t n, uint64_t pos, int lane) {
+    const uint32_t stride = (n + 63u) / 64u;                // <= kGatherLdsMax / 64
+    const uint32_t i1 = (uint32_t)lane * stride;
+    const uint64_t m1 = __ballot(i1 < n && base[i1] <= pos);
+    const uint32_t j = 63u - (uint32_t)__builtin_clzll(m1);
+    const uint32_t i2 = j * stride + (uint32_t)lane;
+    const uint64_t m2 = __ballot((uint32_t)lane < stride && i2 < n && base[i2] <= pos);
+    return __builtin_amdgcn_readfirstlane(j * stride + (63u - (uint32_t)__builtin_clzll(m2)));
+}
+
+// Requires dst 16-B aligned and 1 <= n <= kGatherLdsMax.
+__global__ __launch_bounds__(kBlock) void k_gather_one(uint8_t *__restrict__ dst, const uint8_t *__restrict__ src,
+                                                       const fws_frame_desc *__restrict__ d, uint32_t n) {
+    __shared__ uint64_t s_base[kGatherLdsMax + 1];
+    __shared__ uint64_t s_wsum[kBlock / 64];
+    const int lane = threadIdx.x & 63;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // dbase in LDS: lengths (all loads in flight together), then each thread's
+    // contiguous run of kGatherPer regions, a block scan of the run sums
+    {
+        uint64_t l[kGatherPer];
+#pragma unroll
+        for (uint32_t i = 0; i < kGatherPer; ++i) {
+            const uint32_t f = threadIdx.x + i * kBlock;
+            l[i] = f < n ? d[f].payload_len : 0;
+        }
+#pragma unroll
+        for (uint32_t i = 0; i < kGatherPer; ++i) {
+            const uint32_t f = threadIdx.x + i * kBlock;
+            if (f < n) s_base[f] = l[i];
+        }
+        __syncthreads();
+        const uint32_t f0 = threadIdx.x * kGatherPer;
+        uint64_t sum = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < kGatherPer; ++i) {
+            l[i] = f0 + i < n ? s_base[f0 + i] : 0;
+            sum += l[i];
+        }
+        const uint64_t inc = wave_incl_scan64(sum, lane);
+        if (lane == 63) s_wsum[wave] = inc;
+        __syncthreads();                              // every run read before it is overwritten
+        uint64_t run = inc - sum;
+        for (uint32_t i = 0; i < wave; ++i) run += s_wsum[i];
+#pragma unroll
+        for (uint32_t i = 0; i < kGatherPer; ++i) {
+            if (f0 + i < n) s_base[f0 + i] = run;
+            run += l[i];
+        }
+        if (f0 < n && f0 + kGatherPer >= n) s_base[n] = run;
+        __syncthreads();
+    }
+    const uint64_t total = s_base[n];
+    const uint64_t n_units = (total + kGatherUnit - 1) / kGatherUnit;
+    const uint64_t nw = (uint64_t)gridDim.x * (kBlock / 64);
+    for (uint64_t u = (uint64_t)blockIdx.x * (kBlock / 64) + wave; u < n_units; u += nw) {
+        const uint32_t flo = lds_owner(s_base, n, u * kGatherUnit, lane);
+        const uint32_t fhi = u + 1 < n_units ? lds_owner(s_base, n, (u + 1) * kGatherUnit, lane) : n - 1;
+        const uint64_t a0 = u * kGatherUnit + (uint64_t)lane * 16u;
+        if (fhi - flo >= 2u) {                         // many small regions: per-chunk search
+            for (int j = 0; j < 4; ++j) {
+                const uint64_t a = a0 + (uint64_t)j * 1024u;
+                if (a >= total) break;
+                const uint32_t f = find_frame(s_base, flo, fhi, a);
+                const uint64_t fb = s_base[f], fe = s_base[f + 1];
+                if (a + 16 <= fe) {
+                    const fws_frame_desc fd = d[f];
+                    const uintptr_t sa = (uintptr_t)(src + fd.payload_off + (a - fb));
+                    const uintptr_t sb = sa & ~uintptr_t(15);
+                    const uint32_t sh = (uint32_t)(sa & 15u);
+                    const u32x4 v0 = gload16(sb), v1 = gload16(sh ? sb + 16u : sb);
+                    const uint32_t rk = rotr32(fd.key, 8u * ((uint32_t)(a - fb + fd.phase) & 3u));
+                    gstore16<true>((uintptr_t)(dst + a), shr_bytes(v0, v1, sh) ^ rk);
+                } else {
+                    gather_bytes(dst, src, d, s_base, f, a, total);
+                }
+            }
+            continue;
+        }
+        // at most two regions: uniform metadata (k_gather_fast's body)
+        const uint64_t B0 = s_base[flo], B1 = s_base[flo + 1];
+        const uint64_t B2 = fhi > flo ? s_base[flo + 2] : B1;
+        const fws_frame_desc d0 = d[flo], d1 = d[fhi];
+        const uintptr_t S0 = (uintptr_t)(src + d0.payload_off) - (uintptr_t)B0;
+        const uintptr_t S1 = (uintptr_t)(src + d1.payload_off) - (uintptr_t)B1;
+        uintptr_t sb[4];
+        uint32_t sh[4], rk[4];
+        bool full[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint64_t a = a0 + (uint64_t)j * 1024u;
+            const bool in0 = a >= B0 && a + 16 <= B1;
+            const bool in1 = fhi > flo && a >= B1 && a + 16 <= B2;
+            full[j] = (in0 || in1) && a + 16 <= total;
+            const uintptr_t sa = (in1 ? S1 : S0) + (uintptr_t)a;
+            sb[j] = full[j] ? (sa & ~uintptr_t(15)) : ((uintptr_t)(src + d0.payload_off) & ~uintptr_t(15));
+            sh[j] = (uint32_t)(sa & 15u);
+            const uint32_t ph = in1 ? (uint32_t)(a - B1) + d1.phase : (uint32_t)(a - B0) + d0.phase;
+            rk[j] = rotr32(in1 ? d1.key : d0.key, 8u * (ph & 3u));
+        }
+        u32x4 v0[4], v1[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            uintptr_t s1 = full[j] && sh[j] ? sb[j] + 16u : sb[j];
+            asm volatile("" : "+v"(s1));
+            v0[j] = gload16(sb[j]);
+            v1[j] = gload16(s1);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint64_t a = a0 + (uint64_t)j * 1024u;
+            if (full[j]) gstore16<true>((uintptr_t)(dst + a), shr_bytes(v0[j], v1[j], sh[j]) ^ rk[j]);
+            else if (a < total) gather_bytes(dst, src, d, s_base, flo, a, total);
+        }
+    }
+}
+
 }  // namespace fwsk
 
 using namespace fwsk;
+
+// tuning / test hook: 1 = k_gather_one for batches of <= kGatherLdsMax regions
+// (default), 0 = always the plan launch + k_gather_fast
+static int g_gather_one = 1;
+extern "C" __attribute__((visibility("default"))) int fws_internal_set_gather_one(int on) {
+    const int old = g_gather_one;
+    g_gather_one = on != 0;
+    return old;
+}
 
 int fws_launch_utf8_descs(const uint8_t *base, const fws_frame_desc *descs, uint32_t n, uint8_t *ok,
                           hipStream_t s) {
@@ -206,6 +346,26 @@ int fws_launch_utf8_descs(const uint8_t *base, const fws_frame_desc *descs, uint
 int fws_launch_gather(uint8_t *dst, const uint8_t *src, const fws_frame_desc *d, uint32_t n, fws_plan_ws &ws,
                       uint64_t max_bytes, hipStream_t s) {
     if (n == 0) return 0;
+    if (g_gather_one && n <= kGatherLdsMax) {
+        // persistent: as many workgroups as are resident at once (each builds the
+        // prefix once; a grid-stride loop over units), fewer for a small batch
+        static int resident[64] = {};
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return FWS_ERR_INVALID;
+        if (!resident[dev]) {
+            int cus = 0, per = 0;
+            if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+                hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_gather_one, kBlock, 0) != hipSuccess)
+                return FWS_ERR_NO_DEVICE;
+            resident[dev] = cus * (per > 0 ? per : 1);
+        }
+        uint64_t blocks = (max_bytes / kGatherUnit + 4) / 4;
+        const uint64_t cap = (uint64_t)resident[dev];
+        if (blocks > cap) blocks = cap;
+        if (blocks < 1) blocks = 1;
+        hipLaunchKernelGGL(k_gather_one, dim3((unsigned)blocks), dim3(kBlock), 0, s, dst, src, d, n);
+        return fws_hip_status(hipGetLastError());
+    }
     int r = fws_launch_gather_plan(d, n, ws, s);
     if (r) return r;
     uint64_t units = max_bytes / kGatherUnit + 1;

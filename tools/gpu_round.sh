@@ -76,6 +76,10 @@ for step in "$@"; do
         timeout -k 10 900 python -u -m pytest tests/test_gpu_decode.py tests/test_gpu_configs.py -x -v --timeout 120 --timeout-method thread \
             > "$O/dec_tests.log" 2>&1 || fail dectests $? "$O/dec_tests.log"
         tail -1 "$O/dec_tests.log" ;;
+    dropin)
+        timeout -k 10 600 python -u -m pytest tests/test_gpu_dropin.py -x -v --timeout 120 --timeout-method thread \
+            > "$O/dropin_tests.log" 2>&1 || fail dropin $? "$O/dropin_tests.log"
+        tail -1 "$O/dropin_tests.log" ;;
     tdec)
         timeout -k 10 300 python tools/time_decode.py 20 > "$O/time_decode.json" 2> "$O/time_decode.err" \
             || fail tdec $? "$O/time_decode.err"

@@ -36,6 +36,14 @@ struct fws_seg_desc {
 };
 int fws_launch_decode_segments(uint8_t *batch, const fws_seg_desc *segs, uint32_t n, fws_frame_info *frames,
                                fws_decode_result *res, hipStream_t s);
+// registered host memory (fws_gpu_host_register, rx_pipe.cpp): the device
+// address of [p, p + n) when it lies inside one registered range, else null
+uint8_t *fws_host_alias(const void *p, uint64_t n);
+void fws_host_registry_add(const uint8_t *host, uint64_t bytes, uint8_t *dev);
+void fws_host_registry_remove(const uint8_t *host);
+// one segment, its descriptor by value (the RX session's staged read)
+int fws_launch_decode_one(uint8_t *batch, const fws_seg_desc &d, fws_frame_info *frames, fws_decode_result *res,
+                          hipStream_t s);
 
 // Device workspace for the chunk plan of one descriptor batch.
 // Descriptor batches are planned two ways in one launch (k_plan): chunk space

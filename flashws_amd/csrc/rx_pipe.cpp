@@ -19,6 +19,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
+#include <mutex>
 #include <vector>
 
 #include "fws_internal.h"
@@ -64,15 +66,64 @@ static void free_slot(fws_rx_pipe_slot &s) {
     s = fws_rx_pipe_slot{};
 }
 
+// Host ranges registered through fws_gpu_host_register (caller memory the GPU
+// may read and write in place, e.g. the reference's MemPool read buffers), for
+// the RX session and mux: a read that lies inside one is decoded where it is,
+// without the pinned staging copies (fws_host_alias).
+namespace {
+struct HostRange {
+    const uint8_t *host;
+    uint64_t bytes;
+    uint8_t *dev;
+};
+std::mutex g_reg_mu;
+std::vector<HostRange> g_reg;          // sorted by host, disjoint
+}  // namespace
+
+void fws_host_registry_add(const uint8_t *host, uint64_t bytes, uint8_t *dev) {
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    const HostRange r{host, bytes, dev};
+    g_reg.insert(std::upper_bound(g_reg.begin(), g_reg.end(), r,
+                                  [](const HostRange &a, const HostRange &b) { return a.host < b.host; }),
+                 r);
+}
+
+void fws_host_registry_remove(const uint8_t *host) {
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    g_reg.erase(std::remove_if(g_reg.begin(), g_reg.end(), [&](const HostRange &r) { return r.host == host; }),
+                g_reg.end());
+}
+
+uint8_t *fws_host_alias(const void *p, uint64_t n) {
+    const uint8_t *q = (const uint8_t *)p;
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    auto it = std::upper_bound(g_reg.begin(), g_reg.end(), q,
+                               [](const uint8_t *x, const HostRange &r) { return x < r.host; });
+    if (it == g_reg.begin()) return nullptr;
+    --it;
+    const uint64_t off = (uint64_t)(q - it->host);
+    if (q < it->host || off > it->bytes || n > it->bytes - off) return nullptr;
+    return it->dev + off;
+}
+
 extern "C" {
 
 int fws_gpu_host_register(void *host_ptr, uint64_t bytes) {
     if (!host_ptr || !bytes) return FWS_ERR_INVALID;
-    return fws_hip_status(hipHostRegister(host_ptr, bytes, hipHostRegisterDefault));
+    hipError_t e = hipHostRegister(host_ptr, bytes, hipHostRegisterMapped);
+    if (e != hipSuccess) return fws_hip_status(e);
+    void *dev = nullptr;
+    if ((e = hipHostGetDevicePointer(&dev, host_ptr, 0)) != hipSuccess || !dev) {
+        (void)hipHostUnregister(host_ptr);
+        return fws_hip_status(e != hipSuccess ? e : hipErrorInvalidValue);
+    }
+    fws_host_registry_add((const uint8_t *)host_ptr, bytes, (uint8_t *)dev);
+    return 0;
 }
 
 int fws_gpu_host_unregister(void *host_ptr) {
     if (!host_ptr) return FWS_ERR_INVALID;
+    fws_host_registry_remove((const uint8_t *)host_ptr);
     return fws_hip_status(hipHostUnregister(host_ptr));
 }
 

@@ -2,10 +2,12 @@
 // for host read buffers, with the byte work on the GPU.
 //
 // Per read: the continuation of a frame in progress is unmasked with the
-// carried (rotated) key (fws_gpu_mask), the rest of the read -- prefixed with
-// any header bytes staged from the previous read -- goes through
-// fws_gpu_decode_stream (parallel header parse + unmask), the unmasked bytes
-// come back into the caller's buffer, and the host replays the reference's
+// carried (rotated) key, the rest of the read -- prefixed with any header
+// bytes staged from the previous read -- is parsed and unmasked (one launch of
+// k_decode_one for reads whose header stream fits the small-read kernel, else
+// fws_gpu_decode_stream), the unmasked bytes end up in the caller's buffer --
+// in place when it lies in registered host memory (fws_gpu_host_register),
+// else through pinned staging or device copies -- and the host replays the reference's
 // per-part bookkeeping over the decoded frame list (no byte parsing, no XOR on
 // the host) to produce the exact on_read() / PONG / CLOSE event sequence and
 // carried RX state (w_socket.h:223-245). Host code only; server side only
@@ -20,6 +22,9 @@
 namespace {
 
 constexpr int kWaitHead = 0, kWaitPayload = 1;   // w_socket.h:225-228
+// reads in registered host memory up to this size are decoded in place (one
+// workgroup streams them over PCIe); larger ones take the device path
+constexpr uint64_t kInPlaceMax = 256u << 10;
 
 inline uint32_t rotr(uint32_t v, uint32_t b) {     // base/constexpr_math.h:67-82
     b &= 31u;
@@ -355,25 +360,64 @@ static int feed_impl(fws_rx_session *s, uint8_t *buf, uint64_t size, uint64_t bu
                                              hipMemcpyDeviceToHost, st));
     };
     const bool small = L <= kSmallMax;
-    if (size <= fws_rx_session::kZcMax) {
-        // tiny read: the host stages [continuation | 16-B pad | header stream]
-        // in pinned memory and the kernels work on it there (no copy-engine
-        // transfers of the bytes)
-        uint8_t *cont = s->hstage;
-        uint8_t *hs = s->hstage + ((u + 15) & ~15ull);
-        if (u) {
-            memcpy(cont, buf, u);
-            if ((r = fws_gpu_mask(cont, u, s->key, st))) return r;
+    bool frames_here = false;                    // every frame record already in hframes
+    // a read in registered host memory (fws_gpu_host_register: e.g. the MemPool
+    // read buffers the drop-in hook registers) is decoded where it lies, when the
+    // header stream needs no staged bytes in front and both parts start 16-B
+    // aligned (the kernels' chunk grid)
+    uint8_t *const dev = (part0 == 0 && size <= kInPlaceMax && small) ? fws_host_alias(buf, size) : nullptr;
+    const bool in_place = dev && ((uintptr_t)dev & 15u) == 0 && (rest == 0 || ((uintptr_t)(dev + u) & 15u) == 0);
+    if (in_place) {
+        const uint32_t segcap = (uint32_t)(L / 6 + 2 < kSmallFrames ? L / 6 + 2 : kSmallFrames);
+        if ((r = s->host_room(segcap > fws_rx_session::kSpec ? segcap : fws_rx_session::kSpec))) return r;
+        fws_seg_desc d{};
+        d.cont_off = 0;
+        d.hs_off = u;
+        d.u = (uint32_t)u;
+        d.key = s->key;
+        d.L = (uint32_t)(rest ? L : 0);
+        d.fcap = segcap;
+        if ((r = fws_launch_decode_one(dev, d, s->hframes, s->hres, st))) return r;
+        if ((e = hipStreamSynchronize(st)) != hipSuccess) return fws_hip_status(e);
+        frames_here = true;
+        if (rest && s->hres->status == FWS_SMALL_DECLINED) {
+            if ((r = launch(dev + u, false))) return r;       // the parallel decode, in place
+            if ((e = hipStreamSynchronize(st)) != hipSuccess) return fws_hip_status(e);
+            frames_here = false;
         }
+    } else if (size <= fws_rx_session::kZcMax) {
+        // tiny read: the host stages [continuation | 16-B pad | header stream]
+        // in pinned memory; one launch (k_decode_one: the continuation unmask,
+        // then the small-read decode) works on it there and writes the result
+        // and the frame records straight into the pinned landing block -- no
+        // copy-engine transfer and no second launch on the round trip
+        uint8_t *cont = s->hstage;
+        const uint64_t hs_off = (u + 15) & ~15ull;
+        uint8_t *hs = s->hstage + hs_off;
+        if (u) memcpy(cont, buf, u);
         if (rest) {
             if (part0) memcpy(hs, s->hdr, part0);
             memcpy(hs + part0, buf + u, rest);
-            if ((r = launch(hs, small))) return r;
         }
+        const uint32_t segcap = (uint32_t)(L / 6 + 2 < kSmallFrames ? L / 6 + 2 : kSmallFrames);
+        if ((r = s->host_room(segcap > fws_rx_session::kSpec ? segcap : fws_rx_session::kSpec))) return r;
+        fws_seg_desc d{};
+        d.cont_off = 0;
+        d.hs_off = hs_off;
+        d.u = (uint32_t)u;
+        d.key = s->key;
+        d.L = (uint32_t)(rest ? L : 0);
+        d.fcap = segcap;
+        d.fbase = 0;
+        if ((r = fws_launch_decode_one(s->hstage, d, s->hframes, s->hres, st))) return r;
         if ((e = hipStreamSynchronize(st)) != hipSuccess) return fws_hip_status(e);
+        frames_here = true;
         if (rest && s->hres->status == FWS_SMALL_DECLINED) {
+            // more than kSmallFrames headers: the parallel decode on the same bytes
+            // (the continuation is unmasked already; the header stream untouched)
             if ((r = launch(hs, false))) return r;
             if ((e = hipStreamSynchronize(st)) != hipSuccess) return fws_hip_status(e);
+            frames_here = false;
         }
         if (u) memcpy(buf, cont, u);
         if (rest) memcpy(buf + u, hs + part0, rest);
@@ -403,7 +447,7 @@ static int feed_impl(fws_rx_session *s, uint8_t *buf, uint64_t size, uint64_t bu
     }
     if (rest) res = *s->hres;
     if (res.status == FWS_ERR_CAPACITY) return FWS_ERR_CAPACITY;
-    if (res.n_frames > spec) {
+    if (res.n_frames > spec && !frames_here) {
         if ((r = s->host_room((uint32_t)res.n_frames))) return r;
         if ((e = hipMemcpy(s->hframes, s->dframes, (uint64_t)res.n_frames * sizeof(fws_frame_info),
                            hipMemcpyDeviceToHost)) != hipSuccess)
@@ -602,6 +646,7 @@ int fws_rx_mux_feed(fws_rx_mux *m, const fws_rx_read *reads, uint32_t n, fws_rx_
     struct Plan {
         uint64_t u, rest, L, cont_off, hs_off;
         uint32_t part0, seg;                     // seg: index in the launch, or kNone (session path)
+        uint8_t *dev;                            // decoded in place (registered host memory), or null
     };
     std::vector<Plan> plan(n);
     uint64_t bytes = 0, frames = 0;
@@ -615,32 +660,49 @@ int fws_rx_mux_feed(fws_rx_mux *m, const fws_rx_read *reads, uint32_t n, fws_rx_
         p.rest = size - p.u;
         p.L = p.rest ? p.part0 + p.rest : 0;
         p.seg = kNone;
+        p.dev = nullptr;
         if (size == 0 || size > kMuxMaxRead || p.L > kSmallMax) continue;
-        p.cont_off = bytes;
-        p.hs_off = al16(bytes + p.u);
-        bytes = al16(p.hs_off + p.L) + 16;       // + 16: the small decode reads one chunk past L
+        // in place when the read lies in registered host memory, needs no staged
+        // header bytes, starts on the kernels' 16-B chunk grid and is either all
+        // continuation or all header stream (a declined header stream is decoded
+        // again by the session path, which must see the continuation still masked)
+        uint8_t *dv = p.part0 == 0 && (p.u == 0 || p.rest == 0) ? fws_host_alias(reads[i].buf, size) : nullptr;
+        if (dv && ((uintptr_t)dv & 15u) == 0) {
+            p.dev = dv;
+        } else {
+            p.cont_off = bytes;
+            p.hs_off = al16(bytes + p.u);
+            bytes = al16(p.hs_off + p.L) + 16;   // + 16: the small decode reads one chunk past L
+        }
         p.seg = nseg++;
         frames += p.L / 6 + 2 < kSmallFrames ? p.L / 6 + 2 : kSmallFrames;
     }
     const uint64_t desc_bytes = al16((uint64_t)nseg * sizeof(fws_seg_desc));
     const uint64_t res_bytes = al16((uint64_t)nseg * sizeof(fws_decode_result));
     if (nseg) {
-        if ((r = m->ensure(bytes, desc_bytes + res_bytes + frames * sizeof(fws_frame_info)))) return r;
+        if ((r = m->ensure(bytes ? bytes : 16, desc_bytes + res_bytes + frames * sizeof(fws_frame_info)))) return r;
         fws_seg_desc *hd = (fws_seg_desc *)m->hmeta;
+        // the kernel's base: the pinned staging (zero-copy round) or its device copy
+        const uintptr_t kbase = (uintptr_t)(bytes <= m->zc_max ? m->hbuf : m->dbuf);
         uint32_t fbase = 0;
         for (uint32_t i = 0; i < n; ++i) {
             const Plan &p = plan[i];
             if (p.seg == kNone) continue;
             fws_rx_session *s = m->conns[reads[i].conn];
             const uint8_t *buf = reads[i].buf;
-            if (p.u) memcpy(m->hbuf + p.cont_off, buf, p.u);
-            if (p.rest) {
-                if (p.part0) memcpy(m->hbuf + p.hs_off, s->hdr, p.part0);
-                memcpy(m->hbuf + p.hs_off + p.part0, buf + p.u, p.rest);
-            }
             fws_seg_desc &d = hd[p.seg];
-            d.cont_off = p.cont_off;
-            d.hs_off = p.hs_off;
+            if (p.dev) {                         // offsets from the base, modulo 2^64
+                d.cont_off = (uint64_t)((uintptr_t)p.dev - kbase);
+                d.hs_off = (uint64_t)((uintptr_t)(p.dev + p.u) - kbase);
+            } else {
+                if (p.u) memcpy(m->hbuf + p.cont_off, buf, p.u);
+                if (p.rest) {
+                    if (p.part0) memcpy(m->hbuf + p.hs_off, s->hdr, p.part0);
+                    memcpy(m->hbuf + p.hs_off + p.part0, buf + p.u, p.rest);
+                }
+                d.cont_off = p.cont_off;
+                d.hs_off = p.hs_off;
+            }
             d.u = (uint32_t)p.u;
             d.key = s->key;
             d.L = (uint32_t)p.L;
@@ -692,8 +754,10 @@ int fws_rx_mux_feed(fws_rx_mux *m, const fws_rx_read *reads, uint32_t n, fws_rx_
         if (p.seg == kNone || (p.rest && (res.status == FWS_SMALL_DECLINED || res.status == FWS_ERR_CAPACITY))) {
             ret = feed_impl(s, rd.buf, rd.size, rd.capacity);          // the session path, on the original bytes
         } else {
-            if (p.u) memcpy(rd.buf, m->hbuf + p.cont_off, p.u);
-            if (p.rest) memcpy(rd.buf + p.u, m->hbuf + p.hs_off + p.part0, p.rest);
+            if (!p.dev) {                                                // staged: the bytes back
+                if (p.u) memcpy(rd.buf, m->hbuf + p.cont_off, p.u);
+                if (p.rest) memcpy(rd.buf + p.u, m->hbuf + p.hs_off + p.part0, p.rest);
+            }
             ret = replay(s, rd.buf, rd.size, rd.capacity, p.u, p.part0, p.rest, p.L, res, hfr + hd[p.seg].fbase);
         }
         if (ret < 0) s->err_code = ret;

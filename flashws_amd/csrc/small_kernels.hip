@@ -161,14 +161,14 @@ __global__ __launch_bounds__(kSThreads) void k_decode_small(uint8_t *__restrict_
 // connection's frame in progress (unmasked with its carried, rotated key,
 // w_socket.h:607-617) followed by its header stream (staged header bytes +
 // the rest of the read), decoded as above.
-__global__ __launch_bounds__(kSThreads) void k_decode_segments(uint8_t *__restrict__ batch,
-                                                               const fws_seg_desc *__restrict__ segs,
-                                                               fws_frame_info *__restrict__ frames,
-                                                               fws_decode_result *__restrict__ res) {
-    const fws_seg_desc d = segs[blockIdx.x];
+__device__ __forceinline__ void decode_segment(uint8_t *__restrict__ batch, const fws_seg_desc &d,
+                                               fws_frame_info *__restrict__ frames,
+                                               fws_decode_result *__restrict__ res) {
     const uint32_t tid = threadIdx.x;
-    // continuation: 16-B aligned start, so every 4-byte group uses the key as is
-    uint8_t *const cont = batch + d.cont_off;
+    // continuation: 16-B aligned start, so every 4-byte group uses the key as is.
+    // Offsets are taken modulo 2^64: a read decoded in place (registered host
+    // memory, rx_session.cpp) is addressed relative to the batch base too.
+    uint8_t *const cont = reinterpret_cast<uint8_t *>(reinterpret_cast<uintptr_t>(batch) + d.cont_off);
     for (uint32_t c = tid; 16u * c < d.u; c += kSThreads) {
         const uint32_t lo = 16u * c;
         if (lo + 16u <= d.u) {
@@ -179,7 +179,25 @@ __global__ __launch_bounds__(kSThreads) void k_decode_segments(uint8_t *__restri
             for (uint32_t j = lo; j < d.u; ++j) cont[j] ^= (uint8_t)(d.key >> (8u * (j & 3u)));
         }
     }
-    if (d.L) decode_small_wg(batch + d.hs_off, d.L, frames + d.fbase, d.fcap, res + blockIdx.x);
+    if (d.L)
+        decode_small_wg(reinterpret_cast<uint8_t *>(reinterpret_cast<uintptr_t>(batch) + d.hs_off), d.L,
+                        frames + d.fbase, d.fcap, res);
+}
+
+__global__ __launch_bounds__(kSThreads) void k_decode_segments(uint8_t *__restrict__ batch,
+                                                               const fws_seg_desc *__restrict__ segs,
+                                                               fws_frame_info *__restrict__ frames,
+                                                               fws_decode_result *__restrict__ res) {
+    decode_segment(batch, segs[blockIdx.x], frames, res + blockIdx.x);
+}
+
+// One read of one connection (fws_rx_session's staged path): the segment
+// descriptor travels as a kernel argument, so the launch needs no metadata
+// copy; frames and result go straight to the session's pinned landing block.
+__global__ __launch_bounds__(kSThreads) void k_decode_one(uint8_t *__restrict__ batch, fws_seg_desc d,
+                                                          fws_frame_info *__restrict__ frames,
+                                                          fws_decode_result *__restrict__ res) {
+    decode_segment(batch, d, frames, res);
 }
 
 }  // namespace fwsk
@@ -188,6 +206,13 @@ int fws_launch_decode_segments(uint8_t *batch, const fws_seg_desc *segs, uint32_
                                fws_decode_result *res, hipStream_t s) {
     if (!n) return 0;
     hipLaunchKernelGGL(fwsk::k_decode_segments, dim3(n), dim3(fwsk::kSThreads), 0, s, batch, segs, frames, res);
+    return fws_hip_status(hipGetLastError());
+}
+
+int fws_launch_decode_one(uint8_t *batch, const fws_seg_desc &d, fws_frame_info *frames, fws_decode_result *res,
+                          hipStream_t s) {
+    if (d.L > kSmallMax || !res || (d.fcap && !frames)) return FWS_ERR_INVALID;
+    hipLaunchKernelGGL(fwsk::k_decode_one, dim3(1), dim3(fwsk::kSThreads), 0, s, batch, d, frames, res);
     return fws_hip_status(hipGetLastError());
 }
 

@@ -209,6 +209,36 @@ def config_c5(seed=42, n_frames=262144, payload=16384, invalid_permille=10):
 
 
 # ------------------------------------------------------------ RX session
+class HostArena:
+    """Page-aligned host memory registered with fws_gpu_host_register: reads
+    placed in it are decoded in place by RxSession / RxMux (the drop-in hook
+    registers the reference's MemPool read buffers the same way)."""
+
+    def __init__(self, nbytes):
+        self.raw = np.zeros(nbytes + 8192, dtype=np.uint8)
+        off = (-self.raw.ctypes.data) % 4096
+        self.mem = self.raw[off:off + nbytes]
+        check("fws_gpu_host_register", lib().fws_gpu_host_register(self.mem.ctypes.data, nbytes))
+        self.pos = 0
+
+    def place(self, data, align_off=0):
+        """A view of the arena holding `data`, starting align_off bytes past a
+        64-B boundary (the arena is reused round-robin)."""
+        n = len(data)
+        start = ((self.pos + 63) // 64) * 64 + align_off
+        if start + n + 64 > len(self.mem):
+            start = align_off
+        v = self.mem[start:start + n]
+        v[:] = np.frombuffer(bytes(data), dtype=np.uint8)
+        self.pos = start + n
+        return v
+
+    def close(self):
+        if self.mem is not None:
+            lib().fws_gpu_host_unregister(self.mem.ctypes.data)
+            self.mem = None
+
+
 class RxSession:
     """fws_rx_session: OnRecvData (w_socket.h:543-769) over the GPU for host reads."""
 
@@ -217,15 +247,17 @@ class RxSession:
         check("fws_rx_session_create", lib().fws_rx_session_create(ctx.h, 1 if is_server else 0, C.byref(h)))
         self.h = h
 
-    def feed(self, data, extra_cap=0, ev_cap=1 << 16, ctl_cap=1 << 20):
-        buf = np.frombuffer(bytes(data), dtype=np.uint8).copy()
+    def feed(self, data, extra_cap=0, ev_cap=1 << 16, ctl_cap=1 << 20, arena=None, align_off=0):
+        """arena: a HostArena to place the read in (decoded in place), else a fresh host copy."""
+        buf = (arena.place(data, align_off) if arena is not None
+               else np.frombuffer(bytes(data), dtype=np.uint8).copy())
         ev = np.zeros(ev_cap, dtype=RX_EVENT)
         ctl = np.zeros(ctl_cap, dtype=np.uint8)
         n_ev, ctl_used = C.c_uint64(0), C.c_uint64(0)
         ret = lib().fws_rx_session_feed(self.h, buf.ctypes.data if len(buf) else None, len(buf),
                                         len(buf) + extra_cap, ev.ctypes.data, ev_cap, C.byref(n_ev),
                                         ctl.ctypes.data, ctl_cap, C.byref(ctl_used))
-        return ret, buf, ev[:n_ev.value].copy(), ctl[:ctl_used.value].copy()
+        return ret, (buf.copy() if arena is not None else buf), ev[:n_ev.value].copy(), ctl[:ctl_used.value].copy()
 
     def state(self):
         st = _lib.RxState()
@@ -265,9 +297,12 @@ class RxMux:
         self.h = h
         self.n = n_conns
 
-    def feed(self, reads, extra_cap=0):
-        """reads: [(conn, bytes)]. Returns [(ret, unmasked bytes, events, ctl bytes)]."""
-        bufs = [np.frombuffer(bytes(d), dtype=np.uint8).copy() for _, d in reads]
+    def feed(self, reads, extra_cap=0, arena=None, align_off=None):
+        """reads: [(conn, bytes)]. Returns [(ret, unmasked bytes, events, ctl bytes)].
+        arena: a HostArena the reads are placed in (align_off(i) -> offset past a
+        64-B boundary for read i), else fresh host copies."""
+        bufs = [arena.place(d, align_off(i) if align_off else 0) if arena is not None
+                else np.frombuffer(bytes(d), dtype=np.uint8).copy() for i, (_, d) in enumerate(reads)]
         rr = np.zeros(len(reads), dtype=_lib.RX_READ)
         for i, ((conn, _), b) in enumerate(zip(reads, bufs)):
             rr[i] = (conn, 0, b.ctypes.data if len(b) else 0, len(b), len(b) + extra_cap)
@@ -284,7 +319,7 @@ class RxMux:
             ctl = np.zeros(n_ctl, dtype=np.uint8)
             if n_ctl:
                 C.memmove(ctl.ctypes.data, int(o["ctl"]), n_ctl)
-            res.append((int(o["ret"]), b, ev, ctl))
+            res.append((int(o["ret"]), b.copy() if arena is not None else b, ev, ctl))
         return res
 
     def reset(self, conn):

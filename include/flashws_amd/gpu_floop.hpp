@@ -53,6 +53,14 @@
 // does and removes it from the loop (DeleteFd, as floop.h:672-674 does after a
 // read). More connections than mux slots fall back to the per-read decoder.
 //
+// Zero copy (default on): each read buffer the loop hands over is a MemPool
+// slot (RequestBuf, buffer_manager.h:90-95 -> MemPool::allocate, flash_alloc.h:
+// 137-244: a power-of-two slot inside a block the pool never frees); the hook
+// registers every slot it sees once (fws_gpu_host_register), and the GPU then
+// decodes the read where it lies -- no copy into pinned staging and back
+// (rx_session.cpp: reads whose parts start on the 16-B chunk grid and need no
+// staged header bytes). SetZeroCopy(false) keeps every read staged.
+//
 // wss:// (SURVEY §8f rank 4): the under-socket is the reference's TLSSocket,
 // whose readable callback (tls_on_readable_, tls_socket.h:206-209) receives
 // the reads OpenSSL has already decrypted on the CPU (SSL_read loop,
@@ -67,6 +75,7 @@
 #include <stdexcept>
 #include <string_view>
 #include <unordered_map>
+#include <unordered_set>
 #include <utility>
 #include <vector>
 
@@ -188,7 +197,11 @@ public:
 
     ~GpuRxHookT() {
         if (mux_) fws_rx_mux_destroy(mux_);
+        for (uint8_t *p : registered_) (void)fws_gpu_host_unregister(p);
     }
+
+    // Register the read buffers for in-place decode (default), or not.
+    void SetZeroCopy(bool on) { zero_copy_ = on; }
 
     size_t connections() const { return conns_.size(); }
     uint64_t gpu_reads() const { return gpu_reads_; }
@@ -386,6 +399,17 @@ private:
         for (USock *u : d) delete_fd_(static_cast<void *>(u));   // FLoop::DeleteFd: a no-op if gone
     }
 
+    // A read buffer's MemPool slot, registered once (the pool never frees its
+    // blocks, so the registration stays valid; flash_alloc.h:137-244).
+    void EnsureRegistered(const fws::IOBuffer &b) {
+        if (!zero_copy_ || !b.data || b.capacity < 4096) return;
+        if (registered_.count(b.data) || unregistrable_.count(b.data)) return;
+        size_t slot = 4096;
+        while (slot < b.capacity) slot <<= 1;              // RoundUpPow2 of the request (MemPool::allocate)
+        if (fws_gpu_host_register(b.data, slot) == 0) registered_.insert(b.data);
+        else unregistrable_.insert(b.data);              // staged from then on
+    }
+
     // ws_server_socket.h:172-196 with OnRecvData on the GPU.
     void OnReadable(USock &u, fws::IOBuffer &&buf, void *ud) {
         retired_.clear();
@@ -394,6 +418,7 @@ private:
             ref_readable_(u, std::move(buf), ud);
             return;
         }
+        EnsureRegistered(buf);
         if (it->second.slot != kNoSlot) {            // batched: decoded at the end of the step
             if (it->second.pending) {                // a second read this step: the batch goes first
                 Flush();
@@ -445,6 +470,9 @@ private:
     std::function<void()> app_on_event_;
     std::function<void(void *)> delete_fd_;
     USock *retiring_ = nullptr;                        // Retire's flush in progress for this socket
+    // zero copy: MemPool slots registered for in-place decode
+    bool zero_copy_ = true;
+    std::unordered_set<uint8_t *> registered_, unregistrable_;
     std::vector<USock *> deferred_;                    // DeleteFd at the end of the step
 };
 

@@ -13,4 +13,5 @@ step ab && for i in 1 2; do
   timeout -k 10 120 python tools/time_decode.py 20 --lib flashws_amd/lib/libfws_gpu_nolean.so >> $O/dec_ab.jsonl 2>/dev/null &&
   timeout -k 10 120 python tools/time_decode.py 20 --lib flashws_amd/lib/libfws_gpu.so >> $O/dec_ab.jsonl 2>/dev/null || exit 1
 done && cat $O/scan_ab.jsonl $O/dec_ab.jsonl && \
+step emit_ab && timeout -k 10 200 python tools/ab_emit_path.py 20 > $O/emit_path_ab.jsonl 2>&1 && cat $O/emit_path_ab.jsonl && \
 ROUND=r04 bash tools/gpu_round.sh dropin bench

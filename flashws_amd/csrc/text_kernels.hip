@@ -371,7 +371,9 @@ int fws_launch_gather(uint8_t *dst, const uint8_t *src, const fws_frame_desc *d,
     uint64_t units = max_bytes / kGatherUnit + 1;
     if (units > ws.unit_cap) units = ws.unit_cap;
     uint64_t blocks = (units + 3) / 4;
-    if (blocks > 16384) blocks = 16384;
+    // one wave per unit in one pass (a cap at 16 384 workgroups left a C2-shaped
+    // TX batch's last 129 units to a second round of a few waves)
+    if (blocks > (1u << 30)) blocks = 1u << 30;
     if (blocks < 1) blocks = 1;
     hipLaunchKernelGGL(k_gather_fast, dim3((unsigned)blocks), dim3(kBlock), 0, s, dst, src, d, n, ws.cbase,
                        ws.unit_first, ws.unit_cap, ws.total);

@@ -340,7 +340,9 @@ int fws_gpu_encode_frames(fws_gpu_ctx *ctx, void *dev_out, uint64_t out_cap, con
     if ((r = fws_launch_tx_plan(dev_descs, n, ws, out_cap, dev_out_len, s))) return r;
     uint64_t u = units < ws.unit_cap ? units : ws.unit_cap;
     uint64_t blocks = (u + 3) / 4;
-    if (blocks > 16384) blocks = 16384;
+    // one wave per unit in one pass (a cap at 16 384 workgroups left a C2-shaped
+    // TX batch's last 129 units to a second round of a few waves)
+    if (blocks > (1u << 30)) blocks = 1u << 30;
     if (g_tx_w5)
         hipLaunchKernelGGL(k_tx_encode_w5, dim3((unsigned)blocks), dim3(kBlock), 0, s, (uint8_t *)dev_out,
                            (const uint8_t *)dev_src, dev_descs, n, ws.cbase, ws.unit_first, ws.unit_cap, ws.total);

@@ -41,12 +41,6 @@ namespace fwsk {
 #ifndef FWS_SCAN_NT
 #define FWS_SCAN_NT 0
 #endif
-// FWS_SCAN_LEAN: nodes read the 3 (rarely 9) header bytes the chain needs from
-// LDS instead of parsing a 16-B register window; b0 and the key are read for
-// survivors only
-#ifndef FWS_SCAN_LEAN
-#define FWS_SCAN_LEAN 1
-#endif
 constexpr bool kScanNT = FWS_SCAN_NT != 0;   // nontemporal stream loads
 constexpr uint32_t kSets = 2;                // tiles in flight per wavefront (register sets; 3 sets
                                              //   at 6 waves per SIMD measured slower)
@@ -257,58 +251,6 @@ __global__ __launch_bounds__(kScanThreads) __attribute__((amdgpu_waves_per_eu(8,
                     // node `lane`: full parse, next node (lane index), leaf or dead
                     const bool act = lane < M;
                     const uint32_t p = act ? (direct ? W.pos[lane] : W.lpos[lane]) : 0u;
-#if FWS_SCAN_LEAN
-                    // the chain needs the header length and the payload length only:
-                    // bytes p+1..p+3 (and p+4..p+9 for the 64-bit form, below); the key,
-                    // b0 and the exact 64-bit length wait for the survivor records
-                    const uint32_t b1 = B[p + 1u], b2 = B[p + 2u], b3 = B[p + 3u];
-                    const uint32_t len7 = b1 & 127u;
-                    const uint32_t avail = rem - p;            // >= 1 for an active node
-                    uint32_t hl = len7 < 126u ? 6u : 8u;
-                    uint32_t pl = len7 < 126u ? len7 : ((b2 << 8) | b3);   // saturated at 64 KiB below
-                    uint32_t hi32 = 0, lo32 = 0;
-                    bool too_large = false;
-                    if (__any(act && len7 == 127u)) {          // ~1 candidate in 64
-                        if (len7 == 127u) {
-                            const uint32_t b4 = B[p + 4u], b5 = B[p + 5u], b6 = B[p + 6u];
-                            const uint32_t b7 = B[p + 7u], b8 = B[p + 8u], b9 = B[p + 9u];
-                            hi32 = (b2 << 24) | (b3 << 16) | (b4 << 8) | b5;
-                            lo32 = (b6 << 24) | (b7 << 16) | (b8 << 8) | b9;
-                            too_large = hi32 > 1u || (hi32 == 1u && lo32 != 0u);   // > 2^32, :493-498
-                            hl = 14u;
-                            pl = hi32 ? 0x10000u : (lo32 > 0x10000u ? 0x10000u : lo32);
-                        }
-                    }
-                    // ParseFrameHdr's returns in its order of checks (:443-445, 476-516)
-                    const uint32_t need = len7 < 126u ? 6u : (len7 == 126u ? 8u : 10u);
-                    const int r = !act ? -1
-                                       : avail < 2u || avail < need ? 0
-                                       : too_large ? FWS_ERR_TOO_LARGE
-                                       : (len7 == 127u && avail < 14u) ? 0 : (int)hl;
-                    const uint64_t plen = len7 == 127u ? (((uint64_t)hi32 << 32) | lo32) : (uint64_t)pl;
-                    // the exit, tile-relative, with the length saturated at 64 KiB; the
-                    // four lookups it may need are loaded together, clamped in bounds
-                    const uint32_t hx = p + hl + pl;
-                    const uint32_t hxc = hx < kTile + kHaloX - 2u ? hx : kTile + kHaloX - 2u;
-                    const uint32_t e0 = B[hxc], e1 = B[hxc + 1u];
-                    const uint32_t wi = (hx < kTile ? hx : kTile - 1u) >> 5;
-                    const uint32_t m = direct ? W.cm[wi] : W.lm[wi];
-                    const uint32_t pre = W.lpre[wi];
-                    uint32_t ptr = kDeadLane;
-                    if (r == 0) {
-                        ptr = lane;                            // incomplete header at the stream end
-                    } else if (r > 0) {
-                        if (hx >= kTile || hx >= rem) {
-                            ptr = lane;                        // leaves the tile / the stream
-                            // unless its exit, in the halo, is no header
-                            if (hx + 2u <= rem && hx + 1u < kTile + kHaloX && ((e0 & 0x77u) > 2u || !(e1 & 0x80u)))
-                                ptr = kDeadLane;
-                        } else {
-                            const uint32_t bit = direct ? cand_pbit(hx & 31u) : hx & 31u;
-                            if ((m >> bit) & 1u) ptr = pre + (uint32_t)__popc(m & ((1u << bit) - 1u));
-                        }
-                    }
-#else
                     const uint32_t a = p & ~15u;
                     const u32x4 wl = *reinterpret_cast<const u32x4 *>(B + a);
                     const u32x4 wh = *reinterpret_cast<const u32x4 *>(B + a + 16u);
@@ -338,7 +280,6 @@ __global__ __launch_bounds__(kScanThreads) __attribute__((amdgpu_waves_per_eu(8,
                             if ((m >> bit) & 1u) ptr = W.lpre[nx >> 5] + (uint32_t)__popc(m & ((1u << bit) - 1u));
                         }
                     }
-#endif
                     // pointer jumping in registers: every chain ends at its leaf (a
                     // lane pointing at itself) or dies
                     for (;;) {
@@ -375,15 +316,8 @@ __global__ __launch_bounds__(kScanThreads) __attribute__((amdgpu_waves_per_eu(8,
                     }
                     rec = surv && ns != 0;
                     fi.hdr_off = t0 + p;
-#if FWS_SCAN_LEAN
-                    if (r > 0 && __any(rec)) {                 // b0 and the key: survivors only
-                        const uint32_t b0 = B[p];
-                        const uint32_t kq = p + (uint32_t)r - 4u;
-                        const uint32_t key = B[kq] | (B[kq + 1u] << 8) | (B[kq + 2u] << 16) | (B[kq + 3u] << 24);
-#else
                     if (r > 0) {
                         const uint32_t b0 = d[0] & 0xFFu;
-#endif
                         fi.payload_len = plen;
                         fi.key = key;
                         fi.opcode = (uint8_t)(b0 & 15u);

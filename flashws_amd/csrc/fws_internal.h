@@ -34,8 +34,12 @@ struct fws_seg_desc {
     uint32_t fbase;
     uint32_t pad;
 };
+// flag (optional, host memory): `seq` is stored there once every segment's
+// results are visible to the host; ctr (with flag): a monotonic device counter,
+// target = its value once this launch's n workgroups have counted
 int fws_launch_decode_segments(uint8_t *batch, const fws_seg_desc *segs, uint32_t n, fws_frame_info *frames,
-                               fws_decode_result *res, hipStream_t s);
+                               fws_decode_result *res, hipStream_t s, uint32_t *ctr = nullptr, uint32_t target = 0,
+                               uint32_t *flag = nullptr, uint32_t seq = 0);
 // registered host memory (fws_gpu_host_register, rx_pipe.cpp): the device
 // address of [p, p + n) when it lies inside one registered range, else null
 uint8_t *fws_host_alias(const void *p, uint64_t n);
@@ -43,7 +47,10 @@ void fws_host_registry_add(const uint8_t *host, uint64_t bytes, uint8_t *dev);
 void fws_host_registry_remove(const uint8_t *host);
 // one segment, its descriptor by value (the RX session's staged read)
 int fws_launch_decode_one(uint8_t *batch, const fws_seg_desc &d, fws_frame_info *frames, fws_decode_result *res,
-                          hipStream_t s);
+                          hipStream_t s, uint32_t *flag = nullptr, uint32_t seq = 0);
+// wait for a host_done flag (small_kernels.hip): spin briefly, then
+// synchronize the stream (which also reports a failed launch)
+int fws_wait_flag(const volatile uint32_t *flag, uint32_t seq, hipStream_t s);
 
 // Device workspace for the chunk plan of one descriptor batch.
 // Descriptor batches are planned two ways in one launch (k_plan): chunk space

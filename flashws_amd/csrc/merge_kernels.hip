@@ -173,7 +173,6 @@ struct MergeParams {
     uint32_t force_big;                              // test hook: every ST on the big-ST path, and the
                                                      //   path resolve on its global-table branches
     uint32_t *zero_next;                             // the next call's counter set (k_emit zeroes it)
-    uint32_t emit_serial;                            // test hook: k_emit_path walks the path serially
     uint32_t *bg_nx, *bg_wt, *bg_lref, *bg_ptr, *bg_sc, *bg_mark;   // big-ST scratch [max_nodes]
     uint64_t max_nodes;
 
@@ -1260,8 +1259,7 @@ constexpr uint32_t kDepthRounds = 16;                // then pointer doubling
 // The big-ST path of k_emit (k_merge's merge_big): the same marking of the
 // entry's chain by pointer doubling, over slot ids in global scratch; the
 // frames in offset order are the ST's survivors in tile order.
-__device__ void emit_big(const MergeParams &P, uint32_t s, uint32_t n, uint32_t e, uint32_t fbase, uint32_t lim,
-                         uint32_t last) {
+__device__ void emit_big(const MergeParams &P, uint32_t s, uint32_t n, uint32_t e, uint32_t fbase, uint32_t lim) {
     __shared__ uint32_t s_tb[kStTiles], s_tsp[kStTiles], s_red[kMWaves];
     const uint32_t tid = threadIdx.x, t0 = s * P.st_tiles;
     uint32_t c = 0, sp = kNone;
@@ -1323,7 +1321,7 @@ __device__ void emit_big(const MergeParams &P, uint32_t s, uint32_t n, uint32_t 
         if (fr && o < lim) {
             const fws_frame_info fi = *P.rec(id);
             P.put_frame(o, fi);
-            P.plan_units(o, fi.hdr_off, exit_of(fi), o == last);
+            P.plan_units(o, fi.hdr_off, exit_of(fi), o == lim - 1);
         }
         f += rt;
     }
@@ -1337,7 +1335,7 @@ constexpr uint32_t kMidPer = kMidCap / kMThreads;
 constexpr uint32_t kMidBatch = 4;
 static_assert(kMidPer * kMThreads == kMidCap && kMidPer % kMidBatch == 0, "mid survivors per thread");
 __device__ void emit_mid(const MergeParams &P, EmitLds &L, uint32_t s, uint32_t n, uint32_t e, uint32_t fbase,
-                         uint32_t lim, uint32_t last) {
+                         uint32_t lim) {
     const uint32_t tid = threadIdx.x, t0 = s * P.st_tiles;
     uint32_t c = 0, sp = kNone;
     if (tid < P.st_tiles && t0 + tid < P.n_tiles) {
@@ -1434,24 +1432,31 @@ __device__ void emit_mid(const MergeParams &P, EmitLds &L, uint32_t s, uint32_t 
             if (!((fm >> (j0 + j)) & 1u)) continue;
             if (f < lim) {
                 P.put_frame(f, rc[j]);
-                P.plan_units(f, rc[j].hdr_off, exit_of(rc[j]), f == last);
+                P.plan_units(f, rc[j].hdr_off, exit_of(rc[j]), f == lim - 1);
             }
             ++f;
         }
     }
 }
 
-// ST s's frames on the path: entry e (its chain marked), frames [fbase, ...)
-// below lim written in offset order with their plan units; frame `last` spans
-// to the end of the stream in the plan.
-__device__ __forceinline__ void emit_st(const MergeParams &P, EmitLds &L, uint32_t s, uint32_t n, uint32_t e, uint32_t fbase,
-                        uint32_t lim, uint32_t last) {
-    const uint32_t tid = threadIdx.x;
+// 6 waves per SIMD (80 VGPRs, no spill; the compiler's own choice, 91, held two
+// workgroups per CU: C2 / C3's 513 super tiles then need a second round of one)
+__global__ __launch_bounds__(kMThreads) __attribute__((amdgpu_waves_per_eu(6))) void k_emit(MergeParams P) {
+    __shared__ EmitLds L;
+    const uint32_t s = blockIdx.x, tid = threadIdx.x;
     uint32_t *const C = P.counters;
+    MP_START(28);
+    MP_T0();
     MP_INIT();
+    if (s == 0)                                      // the next call's counter set
+        for (uint32_t w = tid; w < kCntStride; w += kMThreads) P.zero_next[w] = 0u;
+    if (s >= P.n_st) return;
+    const uint32_t fb = C[kCntFallback], e = P.st_entry[s], fbase = P.st_fbase[s], n = P.st_n[s];
+    const uint32_t lim = C[kCntFrames];
+    if (fb || e == kNone || fbase >= lim) return;
     if (P.big(n)) {
-        if (n <= kMidCap && !P.force_big) emit_mid(P, L, s, n, e, fbase, lim, last);
-        else emit_big(P, s, n, e, fbase, lim, last);
+        if (n <= kMidCap && !P.force_big) emit_mid(P, L, s, n, e, fbase, lim);
+        else emit_big(P, s, n, e, fbase, lim);
         return;
     }
     // (loading all kStCap rows with the words above, before n is known, measured
@@ -1563,368 +1568,12 @@ __device__ __forceinline__ void emit_st(const MergeParams &P, EmitLds &L, uint32
         if (!fr[j]) continue;
         if (f < lim) {
             P.put_frame(f, rc[j]);
-            P.plan_units(f, rc[j].hdr_off, exit_of(rc[j]), f == last);
+            P.plan_units(f, rc[j].hdr_off, exit_of(rc[j]), f == lim - 1);
         }
         ++f;
     }
     __syncthreads();
     MP_MARK(26);
-}
-
-__global__ __launch_bounds__(kMThreads) __attribute__((amdgpu_waves_per_eu(6))) void k_emit(MergeParams P) {
-    __shared__ EmitLds L;
-    const uint32_t s = blockIdx.x, tid = threadIdx.x;
-    uint32_t *const C = P.counters;
-    MP_START(28);
-    MP_T0();
-    if (s == 0)                                      // the next call's counter set
-        for (uint32_t w = tid; w < kCntStride; w += kMThreads) P.zero_next[w] = 0u;
-    if (s >= P.n_st) return;
-    const uint32_t fb = C[kCntFallback], e = P.st_entry[s], fbase = P.st_fbase[s], n = P.st_n[s];
-    const uint32_t lim = C[kCntFrames];
-    if (fb || e == kNone || fbase >= lim) return;
-    emit_st(P, L, s, n, e, fbase, lim, lim - 1u);
-    MP_ADD(27, 1);
-    MP_SPAN(28, 29);
-}
-
-// ------------------------------------------------------------- k_emit_path
-// k_link + k_emit in one launch for streams of up to kFusedStMax super tiles
-// (C2, C3 and the dense 64 B workload): every k_emit workgroup resolves the
-// path itself -- the EXIT tails' next() (one round of tail records, one of
-// their landing survivors' chain results), the path's tails marked by pointer
-// doubling from the root's tail in LDS, the per-ST entries and frame bases by
-// one block scan -- and then emits its own super tile as k_emit does. The
-// redundant work is ~1 tail per super tile per workgroup (L2-resident), and it
-// replaces a launch boundary plus k_link's per-tail phase, ticket and
-// single-workgroup resolve. Workgroup 0 also finishes the terminal (error
-// walk, carry-out), the result, the frame count and the survivor total.
-// More than kFusedTailMax EXIT tails (adversarial streams): each workgroup
-// walks the path serially from the root over global memory instead.
-constexpr uint32_t kFusedStMax = 1024;
-constexpr uint32_t kFusedTailMax = 4096;
-constexpr uint16_t kFTerm = 0xFFFF;
-
-struct FusedLds {
-    uint16_t jmp[2][kFusedTailMax];                  // compact next tail (doubling), kFTerm past the end
-    uint8_t mark[kFusedTailMax];                     // on the path
-    uint32_t runb[kFusedStMax + 1];                  // compact index of ST s's first run tail
-    uint32_t sfc[kFusedStMax];                       // frames of ST s on the path -> exclusive prefix
-    uint32_t sent[kFusedStMax];                      // entry of ST s, or kNone
-    uint32_t red32[kMWaves];
-    uint32_t root, rt, root_ent, root_cnt, end_sid, end_kind, end_set, nf_path, nsurv;
-};
-static_assert(kFusedTailMax < kFTerm, "FusedLds field widths");
-
-union EmitPathLds {                                  // the path phase, then the ST's emit
-    FusedLds f;
-    EmitLds e;
-};
-
-// next() of EXIT tail x (a tail-list slot index): the landing survivor w and its
-// chain result; g = the next tail's slot index, or kGTerm | kind at the path's end
-struct TailNext {
-    uint32_t g, ent, cnt, esid, wst;
-};
-__device__ __forceinline__ TailNext tail_next(const MergeParams &P, const fws_tail_rec &tr) {
-    const uint64_t tx = tr.exit;
-    const uint32_t w = tr.w != kNone ? tr.w : P.find_node(tx);   // k_merge looked most up
-    TailNext o{kGTerm | kKindDead, kNone, 0u, tr.id, (uint32_t)(tx >> P.st_shift)};
-    if (w != kTermDead) {
-        const fws_node_res r = P.nres[w];
-        o.g = res_kind(r) == kKindExit ? r.tail : (kGTerm | res_kind(r));
-        o.ent = r.ent;
-        o.cnt = r.cnt;
-        if (o.g >= kGTerm) o.esid = P.tail_sid(o.wst, r);   // the path's last header if it ends here
-    }
-    return o;
-}
-
-// A tail on the path: its landing survivor is that ST's entry; the one whose
-// next() ends the path gives the terminal.
-__device__ __forceinline__ void path_tail(const MergeParams &P, FusedLds &G, const TailNext &o) {
-    if (o.ent != kNone && o.wst < P.n_st) {
-        G.sent[o.wst] = o.ent;
-        G.sfc[o.wst] = o.cnt;
-    }
-    if (o.g >= kGTerm) {                             // exactly one tail on the path ends it
-        G.end_sid = o.esid;
-        G.end_kind = o.g & 3u;
-        G.end_set = 1;
-    }
-}
-
-// More tails than the LDS tables hold: the path itself, tail by tail from the
-// root's (offsets increase along next(): at most one tail per ST). One thread.
-__device__ __forceinline__ void serial_path(const MergeParams &P, FusedLds &G, uint32_t rt) {
-    uint32_t x = rt;
-    for (uint32_t step = 0; step <= P.n_st; ++step) {
-        const TailNext o = tail_next(P, P.tails[x]);
-        path_tail(P, G, o);
-        if (o.g >= kGTerm) break;
-        x = o.g;
-    }
-}
-
-// The path in this workgroup: G.sent / G.sfc (entry and frame base of every ST),
-// G.end_*, G.nf_path. Returns false when a workspace limit was hit (the decode
-// fails with FWS_ERR_CAPACITY; workgroup 0 writes the result).
-__device__ __forceinline__ bool path_in_wg(const MergeParams &P, FusedLds &G) {
-    uint32_t *const C = P.counters;
-    const uint32_t tid = threadIdx.x;
-    const uint32_t n_st = P.n_st, fixed = n_st * kTailRun;
-    constexpr uint32_t kSt = kFusedStMax / kMThreads;          // STs per thread
-    // one round: the flags, the overflow tail count, the root record, every ST's
-    // run length and its first run tail (almost every ST has at most one)
-    const uint32_t fbk = C[kCntFallback], ovf = C[kCntOverflow], n_ovf = C[kCntTails];
-    const uint32_t root_state = C[kCntRoot];
-    uint32_t nt[kSt], sn = 0;
-    fws_tail_rec t0[kSt];
-    const bool wg0 = blockIdx.x == 0;                // (workgroup 0 also sums the survivors)
-#pragma unroll
-    for (uint32_t j = 0; j < kSt; ++j) {
-        const uint32_t st = tid * kSt + j;
-        nt[j] = st < n_st ? P.st_nt[st] : 0u;
-        t0[j] = P.tails[st < n_st ? st * kTailRun : 0u];
-        sn += (wg0 && st < n_st) ? P.st_n[st] : 0u;
-    }
-    if (fbk || (ovf & 1u)) return false;
-    if (tid == 0) {
-        uint32_t root = kNone, rt = kNone;
-        fws_node_res rr{0, 0, 0, 0};
-        if (root_state >= 2u) {
-            root = C[kCntRootSid];
-            rr = fws_node_res{C[kCntRootTail], C[kCntRootCnt], 0u, root_state - 2u};
-        } else if (root_state == 0u && P.n_tiles && P.tile_count[0]) {
-            const uint32_t id0 = P.sid(0, P.tile_spill[0], 0);
-            if (P.rec(id0)->hdr_off == 0) {
-                root = id0;
-                rr = P.nres[root];
-            }
-        }
-        G.end_set = 0;
-        if (root != kNone) {
-            if (res_kind(rr) == kKindExit) rt = rr.tail;
-            else {                                   // the root's chain ends in ST 0
-                G.end_sid = P.tail_sid(0, rr);
-                G.end_kind = res_kind(rr);
-                G.end_set = 1;
-            }
-        }
-        G.root = root;
-        G.rt = rt;
-        G.root_ent = rr.ent;
-        G.root_cnt = rr.cnt;
-    }
-    // compact tail numbering: the STs' runs in ST order, then the overflow area
-    uint32_t ntt = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < kSt; ++j) ntt += nt[j];
-    uint32_t m_run, nsurv;
-    uint32_t pre = block_excl<uint32_t>(ntt, G.red32, &m_run);
-    (void)block_excl<uint32_t>(sn, G.red32, &nsurv);
-    if (tid == 0) G.nsurv = nsurv;
-#pragma unroll
-    for (uint32_t j = 0; j < kSt; ++j) {
-        const uint32_t st = tid * kSt + j;
-        if (st < n_st) {
-            G.runb[st] = pre;
-            G.sent[st] = kNone;
-            G.sfc[st] = 0;
-        }
-        pre += nt[j];
-    }
-    const uint32_t M = m_run + n_ovf;
-    const bool serial = M > kFusedTailMax || P.emit_serial;   // (uniform)
-    __syncthreads();
-    const uint32_t root = G.root, rt = G.rt;
-    if (tid == 0 && root != kNone) {
-        G.sent[0] = G.root_ent;
-        G.sfc[0] = G.root_cnt;
-    }
-    auto comp = [&](uint32_t x) -> uint32_t {        // slot index -> compact index
-        return x < fixed ? G.runb[x / kTailRun] + x % kTailRun : m_run + (x - fixed);
-    };
-    if (!serial) {
-        // next() of every tail into LDS: the run tails by their ST's thread (the
-        // first one's result kept in registers for the entries below), the
-        // overflow tails round-robin
-        TailNext tn[kSt];
-#pragma unroll
-        for (uint32_t j = 0; j < kSt; ++j) {
-            const uint32_t st = tid * kSt + j;
-            tn[j] = TailNext{kGTerm, kNone, 0u, 0u, 0u};
-            if (st >= n_st || nt[j] == 0) continue;
-            tn[j] = tail_next(P, t0[j]);
-            G.jmp[0][G.runb[st]] = tn[j].g >= kGTerm ? kFTerm : (uint16_t)comp(tn[j].g);
-            for (uint32_t k = 1; k < nt[j]; ++k) {
-                const TailNext o = tail_next(P, P.tails[st * kTailRun + k]);
-                G.jmp[0][G.runb[st] + k] = o.g >= kGTerm ? kFTerm : (uint16_t)comp(o.g);
-            }
-        }
-        for (uint32_t k = tid; k < n_ovf; k += kMThreads) {
-            const TailNext o = tail_next(P, P.tails[fixed + k]);
-            G.jmp[0][m_run + k] = o.g >= kGTerm ? kFTerm : (uint16_t)comp(o.g);
-        }
-        for (uint32_t c = tid; c < M; c += kMThreads) G.mark[c] = 0;
-        __syncthreads();
-        if (tid == 0 && rt != kNone) G.mark[comp(rt)] = 1;
-        __syncthreads();
-        // the path's tails: marks double along next() from the root's tail (two
-        // pointer buffers, one barrier a round: after round k every tail within
-        // 2^(k+1) steps of the root is marked)
-        for (uint32_t round = 0;; ++round) {
-            const uint16_t *const ja = G.jmp[round & 1u];
-            uint16_t *const jb = G.jmp[(round & 1u) ^ 1u];
-            int changed = 0;
-            for (uint32_t c = tid; c < M; c += kMThreads) {
-                const uint16_t p = ja[c];
-                if (p != kFTerm && G.mark[c] && !G.mark[p]) {
-                    G.mark[p] = 1;
-                    changed = 1;
-                }
-                jb[c] = p == kFTerm ? kFTerm : ja[p];
-            }
-            if (!__syncthreads_or(changed)) break;
-        }
-        // entries: every marked tail's landing survivor (results recomputed for
-        // the rare tails past an ST's first)
-#pragma unroll
-        for (uint32_t j = 0; j < kSt; ++j) {
-            const uint32_t st = tid * kSt + j;
-            if (st >= n_st) continue;
-            if (nt[j] && G.mark[G.runb[st]]) path_tail(P, G, tn[j]);
-            for (uint32_t k = 1; k < nt[j]; ++k)
-                if (G.mark[G.runb[st] + k]) path_tail(P, G, tail_next(P, P.tails[st * kTailRun + k]));
-        }
-        for (uint32_t k = tid; k < n_ovf; k += kMThreads)
-            if (G.mark[m_run + k]) path_tail(P, G, tail_next(P, P.tails[fixed + k]));
-    } else if (tid == 0 && rt != kNone) {
-        serial_path(P, G, rt);
-    }
-    __syncthreads();
-    // frame bases: exclusive prefix of the per-ST frame counts in ST order
-    uint32_t fc[kSt], fs = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < kSt; ++j) {
-        const uint32_t st = tid * kSt + j;
-        fc[j] = st < n_st ? G.sfc[st] : 0u;
-        fs += fc[j];
-    }
-    uint32_t nf;
-    uint32_t fpre = block_excl<uint32_t>(fs, G.red32, &nf);
-#pragma unroll
-    for (uint32_t j = 0; j < kSt; ++j) {
-        const uint32_t st = tid * kSt + j;
-        if (st < n_st) G.sfc[st] = fpre;
-        fpre += fc[j];
-    }
-    if (tid == 0) G.nf_path = nf;
-    __syncthreads();
-    return true;
-}
-
-// Workgroup 0: the terminal (ParseFrameHdr's walk from the path's exit on an
-// error, carry-out), the result, the frame count and the survivor total; the
-// walk frames and their plan units; the plan's tail when the path's last frame
-// turns out to be the last one. As resolve_path's terminal.
-__device__ __forceinline__ void finish_path(const MergeParams &P, const FusedLds &G) {
-    uint32_t *const C = P.counters;
-    const uint64_t N = P.N;
-    const uint32_t nsurv = G.nsurv;
-    C[kCntSurv] = nsurv;
-    const uint32_t root = G.root, nf_path = G.nf_path;
-    if (root != kNone && !G.end_set) {               // no terminal on the path: cannot happen
-        atomicOr(&C[kCntFallback], 1u);
-        fws_decode_result r{};
-        r.status = FWS_ERR_INTERNAL;
-        C[kCntFrames] = 0;
-        *P.res = r;
-        return;
-    }
-    fws_decode_result r{};
-    r.status = FWS_OK;
-    r.n_survivors = nsurv;
-    uint64_t pos = 0;
-    bool walk = N > 0 && root == kNone;              // no chain from offset 0 survived
-    if (root != kNone) {
-        const fws_frame_info fi = *P.rec(G.end_sid);
-        pos = G.end_kind == kKindInc ? fi.hdr_off : exit_of(fi);
-        walk = G.end_kind == kKindDead;
-    }
-    uint32_t nf = nf_path;
-    const uint32_t cap = P.cap;
-    if (walk) {
-        for (;;) {
-            if (pos >= N) break;
-            Hdr h;
-            const uint64_t q = pos;
-            const int rc = parse_hdr([&](int i) -> uint32_t { return P.wire[q + i]; }, N - q, true, h);
-            if (rc < 0) { r.status = rc; r.err_off = q; break; }
-            if (rc == 0) break;                      // incomplete trailing header
-            const uint64_t po = q + rc;
-            if (nf < cap) {
-                fws_frame_info fi;
-                fi.hdr_off = q; fi.payload_len = h.plen; fi.key = h.key; fi.opcode = (uint8_t)h.opcode;
-                fi.fin = (uint8_t)h.fin; fi.hdr_len = (uint8_t)rc;
-                fi.flags = (po + h.plen > N) ? (uint8_t)FWS_FRAME_TRUNCATED : (uint8_t)0;
-                P.put_frame(nf, fi);
-            }
-            ++nf;
-            pos = po + h.plen;
-        }
-    }
-    if (r.status == FWS_OK) {
-        if (pos > N) { r.carry_unread = pos - N; r.consumed = N; }
-        else if (pos < N) { r.carry_hdr_len = (uint32_t)(N - pos); r.consumed = pos; }
-        else r.consumed = N;
-    } else {
-        r.consumed = r.err_off;
-    }
-    if (nf > cap && r.status == FWS_OK) r.status = FWS_ERR_CAPACITY;
-    r.n_frames = nf;
-    const uint32_t lim = nf < cap ? nf : cap;
-    C[kCntFrames] = lim;
-    if (lim > nf_path) {
-        // walk frames (within one tile; the workgroups span the path frames): each
-        // walk frame's span, the last one's to the end of the stream
-        for (uint32_t f = nf_path; f < lim; ++f) {
-            const uint64_t h = P.frames[f].hdr_off;
-            P.plan_units(f, h, f + 1 < lim ? P.frames[f + 1].hdr_off : 0, f + 1 == lim);
-        }
-    } else if (walk && lim == nf_path && nf_path > 0 && nf_path < cap) {
-        // the path's last frame is the last one after all: its span reaches the
-        // stream end (its workgroup planned it up to its exit)
-        const uint64_t e = exit_of(*P.rec(G.end_sid));
-        for (uint64_t u = (e + kUnit - 1) / kUnit; u < P.n_units; ++u) P.unit_first[u] = nf_path - 1;
-    }
-    *P.res = r;
-}
-
-__global__ __launch_bounds__(kMThreads) __attribute__((amdgpu_waves_per_eu(6))) void k_emit_path(MergeParams P) {
-    __shared__ EmitPathLds U;
-    FusedLds &G = U.f;
-    const uint32_t s = blockIdx.x, tid = threadIdx.x;
-    uint32_t *const C = P.counters;
-    MP_START(28);
-    MP_T0();
-    if (s == 0)                                      // the next call's counter set
-        for (uint32_t w = tid; w < kCntStride; w += kMThreads) P.zero_next[w] = 0u;
-    if (!path_in_wg(P, G)) {
-        if (s == 0) fail_capacity(P);                // k_scan's spill or the tail list overflowed
-        return;
-    }
-    // frames of the path below the capacity; the path's last frame spans to the
-    // stream end unless an error walk may follow it (then workgroup 0 decides)
-    const uint32_t nf_path = G.nf_path, cap = P.cap;
-    const uint32_t lim = nf_path < cap ? nf_path : cap;
-    const bool may_walk = G.root == kNone || (G.end_set && G.end_kind == kKindDead);
-    const uint32_t last = (may_walk && nf_path < cap) ? kNone : lim - 1u;
-    const uint32_t e = s < P.n_st ? G.sent[s] : kNone, fbase = s < P.n_st ? G.sfc[s] : 0u;
-    if (s == 0 && tid == 0) finish_path(P, G);
-    __syncthreads();                                 // FusedLds dead: EmitLds reuses it
-    if (s >= P.n_st || e == kNone || fbase >= lim) return;
-    emit_st(P, U.e, s, P.st_n[s], e, fbase, lim, last);
     MP_ADD(27, 1);
     MP_SPAN(28, 29);
 }
@@ -1949,16 +1598,6 @@ extern "C" int fws_internal_merge_prof(unsigned long long *out, int reset) {
 
 // ------------------------------------------------------------------ host side
 using namespace fwsk;
-
-// tuning / test hook: 1 = k_emit_path (the path resolved in every k_emit
-// workgroup) for streams of <= kFusedStMax super tiles (default), 2 = the same
-// with its serial path walk forced, 0 = k_link + k_emit always
-static int g_emit_path = 1;
-extern "C" __attribute__((visibility("default"))) int fws_internal_set_emit_path(int on) {
-    const int old = g_emit_path;
-    g_emit_path = on >= 0 && on <= 2 ? on : 1;
-    return old;
-}
 
 // super tiles of kStTiles tiles, halved while that gives fewer than kStTarget
 // (a short stream's resolve then spreads over more CUs), down to kStTilesMin
@@ -2031,7 +1670,6 @@ int fws_launch_merge(fws_gpu_ctx *ctx, const uint8_t *wire, uint64_t N, uint32_t
     P.n_units = units < ctx->plan.unit_cap ? units : ctx->plan.unit_cap;
     P.force_big = force_big ? 1u : 0u;
     P.zero_next = zero_next;
-    P.emit_serial = g_emit_path == 2 ? 1u : 0u;
     P.bg_nx = d.bg_nx;
     P.bg_wt = d.bg_wt;
     P.bg_lref = d.bg_lref;
@@ -2041,11 +1679,6 @@ int fws_launch_merge(fws_gpu_ctx *ctx, const uint8_t *wire, uint64_t N, uint32_t
     P.max_nodes = d.max_nodes;
     const dim3 grid(P.n_st ? P.n_st : 1u), blk(kMThreads);
     hipLaunchKernelGGL(k_merge, grid, blk, 0, s, P);
-    if (g_emit_path && P.n_st <= kFusedStMax && !force_big) {
-        // each k_emit workgroup resolves the path itself (k_link folded in)
-        hipLaunchKernelGGL(k_emit_path, grid, blk, 0, s, P);
-        return fws_hip_status(hipGetLastError());
-    }
     const uint32_t fixed = P.n_st * kTailRun;         // k_link: one thread per run slot (+ a loop past them)
     hipLaunchKernelGGL(k_link, dim3(fixed ? (fixed + kMThreads - 1) / kMThreads : 1u), blk, 0, s, P);
     hipLaunchKernelGGL(k_emit, grid, blk, 0, s, P);

@@ -15,6 +15,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <chrono>
 #include <vector>
 
 #include "fws_internal.h"
@@ -65,6 +66,8 @@ struct fws_rx_session {
     // result block back)
     static constexpr uint64_t kZcMax = 16u << 10;
     uint8_t *hstage = nullptr;
+    uint32_t *hflag = nullptr;         // host_done flag of the one-launch paths (coherent pinned word)
+    uint32_t seq = 0;
     fws_decode_result *hres = nullptr;
     fws_frame_info *hframes = nullptr;
     uint32_t hfcap = 0;
@@ -219,6 +222,11 @@ struct fws_rx_session {
         }
         if (stage && !hstage && (e = hipHostMalloc((void **)&hstage, 2 * kZcMax + 64)) != hipSuccess)
             return fws_hip_status(e);
+        if (!hflag) {
+            if ((e = hipHostMalloc((void **)&hflag, 64, hipHostMallocCoherent)) != hipSuccess) return fws_hip_status(e);
+            *hflag = 0;
+            seq = 0;
+        }
         return host_room(kSpec);
     }
 
@@ -236,6 +244,20 @@ struct fws_rx_session {
         return 0;
     }
 };
+
+int fws_wait_flag(const volatile uint32_t *flag, uint32_t seq, hipStream_t s) {
+    const uint32_t *f = (const uint32_t *)flag;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t i = 0;; ++i) {
+        if (__atomic_load_n(f, __ATOMIC_ACQUIRE) == seq) return 0;
+        if ((i & 255u) == 255u && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(200)) break;
+        __builtin_ia32_pause();
+    }
+    // a long decode (or a failed launch): block on the stream instead of spinning
+    const hipError_t e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return fws_hip_status(e);
+    return __atomic_load_n(f, __ATOMIC_ACQUIRE) == seq ? 0 : FWS_ERR_INTERNAL;
+}
 
 extern "C" {
 
@@ -263,6 +285,7 @@ void fws_rx_session_destroy(fws_rx_session *s) {
     if (s->dres) (void)hipFree(s->dres);
     if (s->hres) (void)hipHostFree(s->hres);
     if (s->hstage) (void)hipHostFree(s->hstage);
+    if (s->hflag) (void)hipHostFree(s->hflag);
     if (s->stream && !s->borrowed_stream) (void)hipStreamDestroy(s->stream);
     delete s;
 }
@@ -377,8 +400,9 @@ static int feed_impl(fws_rx_session *s, uint8_t *buf, uint64_t size, uint64_t bu
         d.key = s->key;
         d.L = (uint32_t)(rest ? L : 0);
         d.fcap = segcap;
-        if ((r = fws_launch_decode_one(dev, d, s->hframes, s->hres, st))) return r;
-        if ((e = hipStreamSynchronize(st)) != hipSuccess) return fws_hip_status(e);
+        const uint32_t seq = ++s->seq;
+        if ((r = fws_launch_decode_one(dev, d, s->hframes, s->hres, st, s->hflag, seq))) return r;
+        if ((r = fws_wait_flag(s->hflag, seq, st))) return r;
         frames_here = true;
         if (rest && s->hres->status == FWS_SMALL_DECLINED) {
             if ((r = launch(dev + u, false))) return r;       // the parallel decode, in place
@@ -409,8 +433,9 @@ static int feed_impl(fws_rx_session *s, uint8_t *buf, uint64_t size, uint64_t bu
         d.L = (uint32_t)(rest ? L : 0);
         d.fcap = segcap;
         d.fbase = 0;
-        if ((r = fws_launch_decode_one(s->hstage, d, s->hframes, s->hres, st))) return r;
-        if ((e = hipStreamSynchronize(st)) != hipSuccess) return fws_hip_status(e);
+        const uint32_t seq = ++s->seq;
+        if ((r = fws_launch_decode_one(s->hstage, d, s->hframes, s->hres, st, s->hflag, seq))) return r;
+        if ((r = fws_wait_flag(s->hflag, seq, st))) return r;
         frames_here = true;
         if (rest && s->hres->status == FWS_SMALL_DECLINED) {
             // more than kSmallFrames headers: the parallel decode on the same bytes
@@ -539,6 +564,10 @@ struct fws_rx_mux {
     uint64_t mcap = 0;
     std::vector<uint8_t> seen;        // per connection: fed in this call
     uint64_t zc_max = 0;              // batches up to this many bytes: kernels on the pinned buffers
+    uint32_t *dctr = nullptr;         // host_done counter of the zero-copy launch (monotonic)
+    uint32_t ctr_total = 0;
+    uint32_t *hflag = nullptr;        // and its flag (coherent pinned word)
+    uint32_t seq = 0;
 
     int ensure(uint64_t bytes, uint64_t meta) {
         hipError_t e;
@@ -587,6 +616,13 @@ int fws_rx_mux_create(fws_gpu_ctx *ctx, uint32_t n_conns, fws_rx_mux **out) {
     }
     m->conns.resize(n_conns, nullptr);
     m->seen.resize(n_conns, 0);
+    if ((r = fws_hip_status(hipMalloc((void **)&m->dctr, 64))) ||
+        (r = fws_hip_status(hipMemset(m->dctr, 0, 64))) ||
+        (r = fws_hip_status(hipHostMalloc((void **)&m->hflag, 64, hipHostMallocCoherent)))) {
+        fws_rx_mux_destroy(m);
+        return r;
+    }
+    *m->hflag = 0;
     const char *zc = getenv("FWS_MUX_ZC_MAX");
     m->zc_max = zc ? strtoull(zc, nullptr, 10) : kMuxZcMax;
     for (uint32_t i = 0; i < n_conns; ++i) {
@@ -608,6 +644,8 @@ void fws_rx_mux_destroy(fws_rx_mux *m) {
     if (m->dbuf) (void)hipFree(m->dbuf);
     if (m->hmeta) (void)hipHostFree(m->hmeta);
     if (m->dmeta) (void)hipFree(m->dmeta);
+    if (m->dctr) (void)hipFree(m->dctr);
+    if (m->hflag) (void)hipHostFree(m->hflag);
     if (m->stream) (void)hipStreamDestroy(m->stream);
     delete m;
 }
@@ -718,8 +756,12 @@ int fws_rx_mux_feed(fws_rx_mux *m, const fws_rx_read *reads, uint32_t n, fws_rx_
         if (bytes <= m->zc_max) {
             fws_decode_result *hr = (fws_decode_result *)(m->hmeta + desc_bytes);
             fws_frame_info *hf = (fws_frame_info *)(m->hmeta + desc_bytes + res_bytes);
-            if ((r = fws_launch_decode_segments(m->hbuf, (const fws_seg_desc *)m->hmeta, nseg, hf, hr, st))) return r;
-            if ((e = hipStreamSynchronize(st)) != hipSuccess) return fws_hip_status(e);
+            const uint32_t target = m->ctr_total + nseg, seq = ++m->seq;
+            if ((r = fws_launch_decode_segments(m->hbuf, (const fws_seg_desc *)m->hmeta, nseg, hf, hr, st, m->dctr,
+                                                target, m->hflag, seq)))
+                return r;
+            m->ctr_total = target;
+            if ((r = fws_wait_flag(m->hflag, seq, st))) return r;
         } else {
             fws_decode_result *dres = (fws_decode_result *)(m->dmeta + desc_bytes);
             fws_frame_info *dfr = (fws_frame_info *)(m->dmeta + desc_bytes + res_bytes);

@@ -184,11 +184,35 @@ __device__ __forceinline__ void decode_segment(uint8_t *__restrict__ batch, cons
                         frames + d.fbase, d.fcap, res);
 }
 
+// Completion for a host that polls instead of synchronizing the stream (the
+// launch + hipStreamSynchronize round trip is ~3.5 us longer than a kernel
+// storing a flag the host spins on; tools/rtt_probe.hip): every wave drains its
+// stores, the workgroup meets, and one lane releases at system scope and
+// stores `seq` to the flag in host memory. With a counter (several
+// workgroups), each workgroup releases and counts; the one completing the
+// count stores the flag. The counter is monotonic across launches (the host
+// passes the value this launch completes).
+__device__ __forceinline__ void host_done(uint32_t *ctr, uint32_t target, uint32_t *flag, uint32_t seq) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x != 0 || !flag) return;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");                  // system scope
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (ctr) {
+        const uint32_t v = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) + 1u;
+        if (v != target) return;
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "");
+    }
+    __hip_atomic_store(flag, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 __global__ __launch_bounds__(kSThreads) void k_decode_segments(uint8_t *__restrict__ batch,
                                                                const fws_seg_desc *__restrict__ segs,
                                                                fws_frame_info *__restrict__ frames,
-                                                               fws_decode_result *__restrict__ res) {
+                                                               fws_decode_result *__restrict__ res, uint32_t *ctr,
+                                                               uint32_t target, uint32_t *flag, uint32_t seq) {
     decode_segment(batch, segs[blockIdx.x], frames, res + blockIdx.x);
+    host_done(ctr, target, flag, seq);
 }
 
 // One read of one connection (fws_rx_session's staged path): the segment
@@ -196,23 +220,27 @@ __global__ __launch_bounds__(kSThreads) void k_decode_segments(uint8_t *__restri
 // copy; frames and result go straight to the session's pinned landing block.
 __global__ __launch_bounds__(kSThreads) void k_decode_one(uint8_t *__restrict__ batch, fws_seg_desc d,
                                                           fws_frame_info *__restrict__ frames,
-                                                          fws_decode_result *__restrict__ res) {
+                                                          fws_decode_result *__restrict__ res, uint32_t *flag,
+                                                          uint32_t seq) {
     decode_segment(batch, d, frames, res);
+    host_done(nullptr, 0u, flag, seq);
 }
 
 }  // namespace fwsk
 
 int fws_launch_decode_segments(uint8_t *batch, const fws_seg_desc *segs, uint32_t n, fws_frame_info *frames,
-                               fws_decode_result *res, hipStream_t s) {
+                               fws_decode_result *res, hipStream_t s, uint32_t *ctr, uint32_t target, uint32_t *flag,
+                               uint32_t seq) {
     if (!n) return 0;
-    hipLaunchKernelGGL(fwsk::k_decode_segments, dim3(n), dim3(fwsk::kSThreads), 0, s, batch, segs, frames, res);
+    hipLaunchKernelGGL(fwsk::k_decode_segments, dim3(n), dim3(fwsk::kSThreads), 0, s, batch, segs, frames, res, ctr,
+                       target, flag, seq);
     return fws_hip_status(hipGetLastError());
 }
 
 int fws_launch_decode_one(uint8_t *batch, const fws_seg_desc &d, fws_frame_info *frames, fws_decode_result *res,
-                          hipStream_t s) {
+                          hipStream_t s, uint32_t *flag, uint32_t seq) {
     if (d.L > kSmallMax || !res || (d.fcap && !frames)) return FWS_ERR_INVALID;
-    hipLaunchKernelGGL(fwsk::k_decode_one, dim3(1), dim3(fwsk::kSThreads), 0, s, batch, d, frames, res);
+    hipLaunchKernelGGL(fwsk::k_decode_one, dim3(1), dim3(fwsk::kSThreads), 0, s, batch, d, frames, res, flag, seq);
     return fws_hip_status(hipGetLastError());
 }
 

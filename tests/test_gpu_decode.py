@@ -16,9 +16,8 @@ from wsframes import frame
 
 pytestmark = pytest.mark.gpu
 
-# mode -> (fws_internal_set_resolve_mode, fws_internal_set_emit_path)
-RESOLVE_MODES = {"super_tile": (0, 1), "super_tile_serial": (0, 2), "super_tile_link": (0, 0), "big_st": (1, 1),
-                 "small_read": (2, 1)}
+# mode -> fws_internal_set_resolve_mode
+RESOLVE_MODES = {"super_tile": 0, "big_st": 1, "small_read": 2}
 CNT_FAILED = 9              # decode_common.h Counter::kCntFallback (the resolve failed)
 CNT_BIG = 12                # decode_common.h Counter::kCntBig (super tiles on the big-ST path)
 
@@ -26,22 +25,15 @@ CNT_BIG = 12                # decode_common.h Counter::kCntBig (super tiles on t
 @pytest.fixture(params=list(RESOLVE_MODES), autouse=True)
 def resolve_mode(request):
     """Every decode test runs on every decode path: the multi-launch path with
-    the super-tile resolve in LDS (merge_kernels.hip) -- the path resolved in
-    every k_emit_path workgroup (default up to 1024 super tiles; also with its
-    serial walk forced, the form for streams with more EXIT tails than its LDS
-    tables hold), or by k_link's last workgroup then k_emit -- and with the
-    big-ST path forced for every
-    super tile; and the RX session's one-launch small-read kernel
-    (small_kernels.hip; streams <= 128 KiB with <= 256 headers, the rest fall
-    back to the super-tile path as the session does)."""
+    the super-tile resolve in LDS (merge_kernels.hip) and with the big-ST path
+    forced for every super tile; and the RX session's one-launch small-read
+    kernel (small_kernels.hip; streams <= 128 KiB with <= 256 headers, the rest
+    fall back to the super-tile path as the session does)."""
     from flashws_amd import _lib
     L = _lib.lib()
-    rm, ep = RESOLVE_MODES[request.param]
-    old = L.fws_internal_set_resolve_mode(rm)
-    old_ep = L.fws_internal_set_emit_path(ep)
+    old = L.fws_internal_set_resolve_mode(RESOLVE_MODES[request.param])
     yield request.param
     L.fws_internal_set_resolve_mode(old)
-    L.fws_internal_set_emit_path(old_ep)
 
 
 def counters(ctx):
@@ -279,7 +271,7 @@ def test_c3_mixed_parity(ctx, cuda, resolve_mode):
     wire, descs, _ = gpu.config_c3(seed=9, target=64 << 20)
     r = check(ctx, cuda, wire)
     assert int(r["n_frames"]) == len(descs)
-    if resolve_mode.startswith("super_tile"):
+    if resolve_mode == "super_tile":
         assert not fell_back(ctx), "C3 must resolve on the super-tile path with LDS tables"
 
 
@@ -287,7 +279,7 @@ def test_c2_full_parity(ctx, cuda, resolve_mode):
     wire, descs, _ = gpu.config_c2()
     r = check(ctx, cuda, wire)
     assert int(r["n_frames"]) == 65536
-    if resolve_mode.startswith("super_tile"):
+    if resolve_mode == "super_tile":
         assert not fell_back(ctx), "C2 must resolve on the super-tile path with LDS tables"
 
 

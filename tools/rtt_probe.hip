@@ -10,7 +10,8 @@
 //   session_feed     fws_rx_session_feed of one 4 KiB masked frame (the per-read
 //                    drop-in path), host buffer in pageable memory
 //   session_feed_reg the same on a hipHostRegister-ed buffer (fws_gpu_host_register)
-//   mux_feed_N       fws_rx_mux_feed of N connections' 4 KiB reads (N = 1, 8, 64)
+//   mux_feed_N       fws_rx_mux_feed of N connections' 4 KiB reads (N = 1, 8, 64),
+//                    in pageable memory (staged) and _reg: registered (in place)
 // argv[1] = "spin" sets hipDeviceScheduleSpin before the context, "yield"
 // hipDeviceScheduleYield, "block" hipDeviceScheduleBlockingSync, else the default.
 // Build: hipcc --offload-arch=gfx950 -O2 -I../include rtt_probe.hip -L../flashws_amd/lib -lfws_gpu
@@ -146,23 +147,30 @@ int main(int argc, char **argv) {
         std::free(reg);
         fws_rx_session_destroy(s);
     }
-    for (uint32_t n : {1u, 8u, 64u}) {
-        fws_rx_mux *m = nullptr;
-        fws_rx_mux_create(ctx, n, &m);
-        std::vector<std::vector<uint8_t>> bufs(n, std::vector<uint8_t>(cap));
-        std::vector<fws_rx_read> rd(n);
-        std::vector<fws_rx_read_result> res(n);
-        const std::string name = "mux_feed_" + std::to_string(n);
-        run(name.c_str(), reps / 4, [&] {
-            for (uint32_t i = 0; i < n; ++i) {
-                std::memcpy(bufs[i].data(), frame.data(), frame.size());
-                rd[i] = fws_rx_read{i, 0u, bufs[i].data(), frame.size(), cap};
-            }
-            if (fws_rx_mux_feed(m, rd.data(), n, res.data()) != 0) std::abort();
-            for (uint32_t i = 0; i < n; ++i)
-                if (res[i].ret != 0 || res[i].n_events != 1) std::abort();
-        });
-        fws_rx_mux_destroy(m);
+    for (int reg = 0; reg < 2; ++reg) {
+        for (uint32_t n : {1u, 8u, 64u}) {
+            fws_rx_mux *m = nullptr;
+            fws_rx_mux_create(ctx, n, &m);
+            // the reads in pageable memory (staged) or in registered memory (in place)
+            uint8_t *arena = (uint8_t *)aligned_alloc(4096, (size_t)n * cap);
+            if (reg) fws_gpu_host_register(arena, (uint64_t)n * cap);
+            std::vector<fws_rx_read> rd(n);
+            std::vector<fws_rx_read_result> res(n);
+            const std::string name = std::string("mux_feed_") + std::to_string(n) + (reg ? "_reg" : "");
+            run(name.c_str(), reps / 4, [&] {
+                for (uint32_t i = 0; i < n; ++i) {
+                    uint8_t *b = arena + (size_t)i * cap;
+                    std::memcpy(b, frame.data(), frame.size());
+                    rd[i] = fws_rx_read{i, 0u, b, frame.size(), cap};
+                }
+                if (fws_rx_mux_feed(m, rd.data(), n, res.data()) != 0) std::abort();
+                for (uint32_t i = 0; i < n; ++i)
+                    if (res[i].ret != 0 || res[i].n_events != 1) std::abort();
+            });
+            if (reg) fws_gpu_host_unregister(arena);
+            std::free(arena);
+            fws_rx_mux_destroy(m);
+        }
     }
     fws_gpu_ctx_destroy(ctx);
     return 0;

@@ -192,13 +192,15 @@ __global__ __launch_bounds__(kBlock) void k_gather_fast(uint8_t *__restrict__ ds
 
 // ------------------------------------------------------------- one launch
 // k_gather_one: the same gather with no plan launch, for batches of at most
-// kGatherLdsMax regions (C4: 1427 fragments). Every workgroup of a persistent
+// kGatherLdsMax regions (C4: 1427 fragments). Every workgroup of a grid-stride
 // grid builds the whole dst prefix (dbase) in LDS from the descriptors -- one
 // round of coalesced loads (L2-resident after the first workgroups) and a
 // block scan, about the latency of one dependent round trip -- and then walks
-// its units as k_gather_fast does; the unit's regions come from two rounds of
-// 64 lane probes into that LDS prefix instead of the plan's unit map. The plan
-// launch (k_out_plan, 6.9 us on C4) and its launch boundary are gone.
+// its units as k_gather_fast does. The regions of a wave's first 64 units are
+// found up front, one unit per lane (a binary search of that LDS prefix), and
+// read back per unit with readlane; later units use two rounds of 64 lane
+// probes. The plan launch (k_out_plan, 6.9 us on C4) and its launch boundary
+// are gone.
 constexpr uint32_t kGatherLdsMax = 2048;
 constexpr uint32_t kGatherPer = kGatherLdsMax / kBlock;   // regions per thread in the block scan
 
@@ -212,6 +214,17 @@ __device__ __forceinline__ uint32_t lds_owner(const uint64_t *base, uint32_t n, 
     const uint32_t i2 = j * stride + (uint32_t)lane;
     const uint64_t m2 = __ballot((uint32_t)lane < stride && i2 < n && base[i2] <= pos);
     return __builtin_amdgcn_readfirstlane(j * stride + (63u - (uint32_t)__builtin_clzll(m2)));
+}
+
+// The same search by one lane: binary search over base[0, n) (per-lane result).
+__device__ __forceinline__ uint32_t lds_search(const uint64_t *base, uint32_t n, uint64_t pos) {
+    uint32_t lo = 0, hi = n - 1;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1u) >> 1;
+        if (base[mid] <= pos) lo = mid;
+        else hi = mid - 1u;
+    }
+    return lo;
 }
 
 // Requires dst 16-B aligned and 1 <= n <= kGatherLdsMax.
@@ -259,9 +272,27 @@ __global__ __launch_bounds__(kBlock) void k_gather_one(uint8_t *__restrict__ dst
     const uint64_t total = s_base[n];
     const uint64_t n_units = (total + kGatherUnit - 1) / kGatherUnit;
     const uint64_t nw = (uint64_t)gridDim.x * (kBlock / 64);
-    for (uint64_t u = (uint64_t)blockIdx.x * (kBlock / 64) + wave; u < n_units; u += nw) {
-        const uint32_t flo = lds_owner(s_base, n, u * kGatherUnit, lane);
-        const uint32_t fhi = u + 1 < n_units ? lds_owner(s_base, n, (u + 1) * kGatherUnit, lane) : n - 1;
+    const uint64_t ufirst = (uint64_t)blockIdx.x * (kBlock / 64) + wave;
+    // the regions of the wave's first 64 units, one unit per lane, all lanes
+    // searching at once (one chain of LDS round trips per wave, not two per unit)
+    uint32_t my_lo = 0, my_hi = n - 1;
+    {
+        const uint64_t u = ufirst + (uint64_t)lane * nw;
+        if (u < n_units) {
+            my_lo = lds_search(s_base, n, u * kGatherUnit);
+            if (u + 1 < n_units) my_hi = lds_search(s_base, n, (u + 1) * kGatherUnit);
+        }
+    }
+    uint32_t k = 0;
+    for (uint64_t u = ufirst; u < n_units; u += nw, ++k) {
+        uint32_t flo, fhi;
+        if (k < 64u) {
+            flo = __builtin_amdgcn_readlane(my_lo, k);
+            fhi = __builtin_amdgcn_readlane(my_hi, k);
+        } else {
+            flo = lds_owner(s_base, n, u * kGatherUnit, lane);
+            fhi = u + 1 < n_units ? lds_owner(s_base, n, (u + 1) * kGatherUnit, lane) : n - 1;
+        }
         const uint64_t a0 = u * kGatherUnit + (uint64_t)lane * 16u;
         if (fhi - flo >= 2u) {                         // many small regions: per-chunk search
             for (int j = 0; j < 4; ++j) {
@@ -328,6 +359,12 @@ using namespace fwsk;
 // tuning / test hook: 1 = k_gather_one for batches of <= kGatherLdsMax regions
 // (default), 0 = always the plan launch + k_gather_fast
 static int g_gather_one = 1;
+static int g_gather_blocks = 0;        // tuning: k_gather_one grid cap (0 = 4 x resident workgroups)
+extern "C" __attribute__((visibility("default"))) int fws_internal_set_gather_blocks(int blocks) {
+    const int old = g_gather_blocks;
+    g_gather_blocks = blocks > 0 ? blocks : 0;
+    return old;
+}
 extern "C" __attribute__((visibility("default"))) int fws_internal_set_gather_one(int on) {
     const int old = g_gather_one;
     g_gather_one = on != 0;
@@ -343,26 +380,42 @@ int fws_launch_utf8_descs(const uint8_t *base, const fws_frame_desc *descs, uint
     return fws_hip_status(hipGetLastError());
 }
 
+// k_gather_one's grid: 4 x the resident workgroups (each builds the prefix
+// once; a grid-stride loop over units, 2-3 per wave on C4): fewer workgroups
+// leave a static tail (1 x resident: 0.095 ms on C4), more repeat the prefix
+// build (one unit per wave: 0.098 ms); 4 x: 0.0865 ms
+// (profiles/r04/ab_gather.jsonl). Fewer for a small reservation.
+static int gather_one_grid(uint64_t max_bytes, uint64_t *out) {
+    static int resident[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return FWS_ERR_INVALID;
+    if (!resident[dev]) {
+        int cus = 0, per = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_gather_one, kBlock, 0) != hipSuccess)
+            return FWS_ERR_NO_DEVICE;
+        resident[dev] = cus * (per > 0 ? per : 1);
+    }
+    uint64_t blocks = (max_bytes / kGatherUnit + 4) / 4;
+    const uint64_t cap = g_gather_blocks ? (uint64_t)g_gather_blocks : 4u * (uint64_t)resident[dev];
+    if (blocks > cap) blocks = cap;
+    *out = blocks < 1 ? 1 : blocks;
+    return 0;
+}
+
+// tuning hook: the grid k_gather_one gets for a context of max_bytes (0 on error)
+extern "C" __attribute__((visibility("default"))) uint64_t fws_internal_gather_one_grid(uint64_t max_bytes) {
+    uint64_t b = 0;
+    return gather_one_grid(max_bytes, &b) == 0 ? b : 0;
+}
+
 int fws_launch_gather(uint8_t *dst, const uint8_t *src, const fws_frame_desc *d, uint32_t n, fws_plan_ws &ws,
                       uint64_t max_bytes, hipStream_t s) {
     if (n == 0) return 0;
     if (g_gather_one && n <= kGatherLdsMax) {
-        // persistent: as many workgroups as are resident at once (each builds the
-        // prefix once; a grid-stride loop over units), fewer for a small batch
-        static int resident[64] = {};
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return FWS_ERR_INVALID;
-        if (!resident[dev]) {
-            int cus = 0, per = 0;
-            if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-                hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_gather_one, kBlock, 0) != hipSuccess)
-                return FWS_ERR_NO_DEVICE;
-            resident[dev] = cus * (per > 0 ? per : 1);
-        }
-        uint64_t blocks = (max_bytes / kGatherUnit + 4) / 4;
-        const uint64_t cap = (uint64_t)resident[dev];
-        if (blocks > cap) blocks = cap;
-        if (blocks < 1) blocks = 1;
+        uint64_t blocks = 0;
+        const int r = gather_one_grid(max_bytes, &blocks);
+        if (r != 0) return r;
         hipLaunchKernelGGL(k_gather_one, dim3((unsigned)blocks), dim3(kBlock), 0, s, dst, src, d, n);
         return fws_hip_status(hipGetLastError());
     }

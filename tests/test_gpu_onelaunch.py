@@ -73,7 +73,7 @@ def test_gather_one_launch(ctx, cuda, gather_mode, shape):
 
 
 def test_gather_one_small_context(cuda, gather_mode):
-    """A context reserved for 1 MiB gathering a 40 MiB message: the persistent
+    """A context reserved for 1 MiB gathering a 40 MiB message: the
     grid is sized from the reservation, its grid-stride loop still covers every
     unit."""
     wire, descs, _ = gpu.config_c4(seed=9, target=40 << 20)
@@ -91,3 +91,32 @@ def test_gather_one_small_context(cuda, gather_mode):
     assert np.array_equal(dst[:total].cpu().numpy(), exp)
     assert int(dst[total:].sum()) == 0
     c.close()
+
+
+@pytest.mark.parametrize("blocks", [1, 3, 0])
+@pytest.mark.parametrize("shape", ["c4_like", "small_2000", "exactly_2048"])
+def test_gather_one_grid_sizes(ctx, cuda, shape, blocks):
+    """The one-launch gather at a forced grid (fws_internal_set_gather_blocks):
+    1 and 3 workgroups leave hundreds of units per wave (past the 64 found up
+    front, one per lane: the per-unit probe path), 0 the default 4 x resident."""
+    L = _lib.lib()
+    old_one, old_blocks = L.fws_internal_set_gather_one(1), L.fws_internal_set_gather_blocks(blocks)
+    try:
+        rng = np.random.default_rng(7 + blocks)
+        host, regions = _regions(shape, rng)
+        descs = np.array(regions, dtype=gpu.FRAME_DESC)
+        total = int(descs["payload_len"].sum())
+        dst = torch.zeros(total + 48, dtype=torch.uint8, device=cuda)
+        gpu.unmask_gather(ctx, dst, torch.from_numpy(host).to(cuda), gpu.descs_to_device(descs, cuda), len(descs))
+        exp, w = np.zeros(total, dtype=np.uint8), 0
+        for o, n, k, ph in regions:
+            seg = host[o:o + n].copy()
+            orc.orc_mask("ws_mask_fast", seg, orc.orc().orc_rotr32(k, 8 * ph))
+            exp[w:w + n] = seg
+            w += n
+        got = dst[:total].cpu().numpy()
+        assert np.array_equal(got, exp), int(np.flatnonzero(got != exp)[0])
+        assert int(dst[total:].sum()) == 0
+    finally:
+        L.fws_internal_set_gather_one(old_one)
+        L.fws_internal_set_gather_blocks(old_blocks)

@@ -302,6 +302,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
 
 }  // namespace fwsk
 
+// tuning hook: k_tx_encode grid cap (0 = one wave per output unit, the default:
+// 2-8 x the resident workgroups with a grid-stride loop measured 0.091-0.104
+// against 0.0906 ms, profiles/r04/ab_tx.jsonl)
+static int g_tx_blocks = 0;
+extern "C" __attribute__((visibility("default"))) int fws_internal_set_tx_blocks(int blocks) {
+    const int old = g_tx_blocks;
+    g_tx_blocks = blocks > 0 ? blocks : 0;
+    return old;
+}
+
 static int g_tx_w5 = 1;  // tuning hook: 1 = k_tx_encode_w5 (default), 0 = the compiler's 4 waves
 extern "C" __attribute__((visibility("default"))) int fws_internal_set_tx_w5(int on) {
     const int old = g_tx_w5;
@@ -343,6 +353,7 @@ int fws_gpu_encode_frames(fws_gpu_ctx *ctx, void *dev_out, uint64_t out_cap, con
     // one wave per unit in one pass (a cap at 16 384 workgroups left a C2-shaped
     // TX batch's last 129 units to a second round of a few waves)
     if (blocks > (1u << 30)) blocks = 1u << 30;
+    if (g_tx_blocks && blocks > (uint64_t)g_tx_blocks) blocks = (uint64_t)g_tx_blocks;
     if (g_tx_w5)
         hipLaunchKernelGGL(k_tx_encode_w5, dim3((unsigned)blocks), dim3(kBlock), 0, s, (uint8_t *)dev_out,
                            (const uint8_t *)dev_src, dev_descs, n, ws.cbase, ws.unit_first, ws.unit_cap, ws.total);

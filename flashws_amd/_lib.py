@@ -52,6 +52,9 @@ RX_READ = np.dtype([("conn", "<u4"), ("flags", "<u4"), ("buf", "<u8"), ("size", 
 RX_READ_RESULT = np.dtype([("ret", "<i4"), ("pad", "<u4"), ("events", "<u8"), ("n_events", "<u8"),
                            ("ctl", "<u8"), ("ctl_used", "<u8")])
 assert RX_READ.itemsize == 32 and RX_READ_RESULT.itemsize == 40
+DECODE_JOB = np.dtype([("wire", "<u8"), ("len", "<u8"), ("frames", "<u8"), ("cap", "<u4"), ("reserved", "<u4"),
+                       ("result", "<u8"), ("utf8_ok", "<u8")])
+assert DECODE_JOB.itemsize == 48
 
 
 class RxState(C.Structure):
@@ -114,6 +117,9 @@ SIGNATURES = [
     ("fws_rx_pipe_destroy", None, [_P]),
     ("fws_rx_pipe_submit", _I, [_P, _P, _U64, _PU64]),
     ("fws_rx_pipe_wait", _I, [_P, _U64, C.POINTER(C.c_void_p), _PU64, _P, C.POINTER(C.c_void_p)]),
+    ("fws_decode_engine_create", _I, [_I, _U32, _U64, _U64, C.POINTER(C.c_void_p)]),
+    ("fws_decode_engine_destroy", None, [_P]),
+    ("fws_decode_engine_run", _I, [_P, _P, _U32, _P]),
 ]
 
 _lib = None

@@ -1,0 +1,173 @@
+// decode_engine.cpp -- fws_decode_engine: fws_gpu_decode_stream over many
+// independent streams, pipelined on one device.
+//
+// A stream decode is two passes over the wire with a latency-bound resolve
+// between them: k_scan (issue-bound: ~49 of its 66 us on C3 are VALU issue,
+// DESIGN.md §4.3b), then k_merge -> k_link -> k_emit (~39 us of dependent
+// round trips), then k_unmask_stream (HBM-bound). One call leaves the HBM idle
+// during the scan's issue-bound stretches and the resolve. The engine keeps
+// three decodes in flight on two HIP streams:
+//
+//   stream X (scan):     scan(j)   scan(j+1)   scan(j+2)   ...
+//   stream Y (rest):          resolve(j) unmask(j)  resolve(j+1) unmask(j+1) ...
+//
+// Job j uses workspace j % 3 (a private fws_gpu_ctx); Y waits for scan(j) before
+// resolve(j), and X waits for job j's unmask before scan(j + 3) reuses its
+// workspace. With scan_cus > 0, X is created with a CU mask of that many CUs
+// spread over the whole CU index range and Y with the complement, so the scan of
+// one job and the unmask of another share the GPU by partition instead of by
+// whichever queue the dispatcher serves first.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <new>
+
+#include "fws_internal.h"
+
+namespace {
+
+constexpr int kSlots = 3;                  // decodes in flight (workspaces)
+
+}  // namespace
+
+struct fws_decode_engine {
+    int device = 0;
+    fws_gpu_ctx *ctx[kSlots] = {};
+    bool used[kSlots] = {};
+    hipStream_t sx = nullptr, sy = nullptr;
+    hipEvent_t ev_in = nullptr, ev_out = nullptr;
+    hipEvent_t ev_scan[kSlots] = {}, ev_done[kSlots] = {};
+    uint64_t max_frames = 0, max_bytes = 0;
+    bool utf8_ready = false;
+    uint32_t next = 0;                     // the next job's workspace
+};
+
+static void engine_free(fws_decode_engine *e) {
+    if (!e) return;
+    (void)hipSetDevice(e->device);
+    if (e->sx) (void)hipStreamSynchronize(e->sx);
+    if (e->sy) (void)hipStreamSynchronize(e->sy);
+    for (int k = 0; k < kSlots; ++k) {
+        if (e->ev_scan[k]) (void)hipEventDestroy(e->ev_scan[k]);
+        if (e->ev_done[k]) (void)hipEventDestroy(e->ev_done[k]);
+        fws_gpu_ctx_destroy(e->ctx[k]);
+    }
+    if (e->ev_in) (void)hipEventDestroy(e->ev_in);
+    if (e->ev_out) (void)hipEventDestroy(e->ev_out);
+    if (e->sx) (void)hipStreamDestroy(e->sx);
+    if (e->sy) (void)hipStreamDestroy(e->sy);
+    delete e;
+}
+
+// Workspaces for jobs of up to `frames` frames / `bytes` bytes (and UTF-8
+// seams): a growth drains the engine first (the workspaces may be in use).
+static int engine_reserve(fws_decode_engine *e, uint64_t frames, uint64_t bytes, bool utf8) {
+    if (frames <= e->max_frames && bytes <= e->max_bytes && (!utf8 || e->utf8_ready)) return 0;
+    int r;
+    if ((r = fws_hip_status(hipStreamSynchronize(e->sx))) || (r = fws_hip_status(hipStreamSynchronize(e->sy))))
+        return r;
+    const uint64_t f = frames > e->max_frames ? frames : e->max_frames;
+    const uint64_t b = bytes > e->max_bytes ? bytes : e->max_bytes;
+    if (f > 0xFFFFFFFFull) return FWS_ERR_CAPACITY;
+    for (int k = 0; k < kSlots; ++k) {
+        if ((r = fws_gpu_ctx_reserve(e->ctx[k], f, b))) return r;
+        if ((r = fws_decode_prepare(e->ctx[k], b, (uint32_t)f, utf8 || e->utf8_ready))) return r;
+    }
+    e->max_frames = f;
+    e->max_bytes = b;
+    e->utf8_ready = e->utf8_ready || utf8;
+    return 0;
+}
+
+extern "C" {
+
+int fws_decode_engine_create(int device, uint32_t scan_cus, uint64_t max_frames, uint64_t max_stream_bytes,
+                             fws_decode_engine **out) {
+    if (!out) return FWS_ERR_INVALID;
+    *out = nullptr;
+    fws_decode_engine *e = new (std::nothrow) fws_decode_engine();
+    if (!e) return FWS_ERR_INTERNAL;
+    e->device = device;
+    int r = 0;
+    for (int k = 0; k < kSlots && !r; ++k) r = fws_gpu_ctx_create(device, &e->ctx[k]);
+    int cus = 0;
+    if (!r) r = fws_hip_status(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+    if (!r && scan_cus >= (uint32_t)cus) r = FWS_ERR_INVALID;
+    if (!r && scan_cus > 0) {
+        // CU i goes to the scan stream when floor((i + 1) s / C) > floor(i s / C):
+        // s CUs spread evenly over the index range, the rest to the other stream
+        uint32_t mx[64] = {}, my[64] = {};
+        const uint32_t words = ((uint32_t)cus + 31u) / 32u;
+        if (words > 64u) r = FWS_ERR_INVALID;
+        for (uint32_t i = 0; !r && i < (uint32_t)cus; ++i) {
+            const bool x = ((uint64_t)(i + 1) * scan_cus) / (uint32_t)cus > ((uint64_t)i * scan_cus) / (uint32_t)cus;
+            (x ? mx : my)[i / 32] |= 1u << (i % 32);
+        }
+        if (!r) r = fws_hip_status(hipExtStreamCreateWithCUMask(&e->sx, words, mx));
+        if (!r) r = fws_hip_status(hipExtStreamCreateWithCUMask(&e->sy, words, my));
+    } else if (!r) {
+        r = fws_hip_status(hipStreamCreateWithFlags(&e->sx, hipStreamNonBlocking));
+        if (!r) r = fws_hip_status(hipStreamCreateWithFlags(&e->sy, hipStreamNonBlocking));
+    }
+    const unsigned evf = hipEventDisableTiming;
+    if (!r) r = fws_hip_status(hipEventCreateWithFlags(&e->ev_in, evf));
+    if (!r) r = fws_hip_status(hipEventCreateWithFlags(&e->ev_out, evf));
+    for (int k = 0; k < kSlots && !r; ++k) {
+        r = fws_hip_status(hipEventCreateWithFlags(&e->ev_scan[k], evf));
+        if (!r) r = fws_hip_status(hipEventCreateWithFlags(&e->ev_done[k], evf));
+    }
+    if (!r && (max_frames || max_stream_bytes)) r = engine_reserve(e, max_frames, max_stream_bytes, false);
+    if (r) {
+        engine_free(e);
+        return r;
+    }
+    *out = e;
+    return 0;
+}
+
+void fws_decode_engine_destroy(fws_decode_engine *e) { engine_free(e); }
+
+int fws_decode_engine_run(fws_decode_engine *e, const fws_decode_job *jobs, uint32_t n, void *stream) {
+    if (!e || (n && !jobs)) return FWS_ERR_INVALID;
+    hipStream_t s = (hipStream_t)stream;
+    int r;
+    if ((r = fws_hip_status(hipSetDevice(e->device)))) return r;
+    // every argument checked (and the workspaces grown) before anything is queued
+    uint64_t mf = 0, mb = 0;
+    bool utf8 = false;
+    for (uint32_t j = 0; j < n; ++j) {
+        const fws_decode_job &q = jobs[j];
+        if (!q.dev_result || (q.len && !q.dev_wire) || (q.cap && !q.dev_frames) || q.reserved) return FWS_ERR_INVALID;
+        if (((uintptr_t)q.dev_wire & 15u) != 0) return FWS_ERR_INVALID;
+        if (q.cap > mf) mf = q.cap;
+        if (q.len > mb) mb = q.len;
+        utf8 = utf8 || q.dev_utf8_ok;
+    }
+    if (n == 0) return 0;
+    if ((r = engine_reserve(e, mf, mb, utf8))) return r;
+    if ((r = fws_hip_status(hipEventRecord(e->ev_in, s))) || (r = fws_hip_status(hipStreamWaitEvent(e->sx, e->ev_in, 0))) ||
+        (r = fws_hip_status(hipStreamWaitEvent(e->sy, e->ev_in, 0))))
+        return r;
+    for (uint32_t j = 0; j < n; ++j) {
+        const fws_decode_job &q = jobs[j];
+        const uint32_t k = e->next;
+        e->next = (k + 1) % kSlots;
+        fws_gpu_ctx *c = e->ctx[k];
+        uint8_t *w = (uint8_t *)q.dev_wire;
+        if ((r = fws_decode_prepare(c, q.len, q.cap, q.dev_utf8_ok != nullptr))) return r;   // sized: no allocation
+        if (e->used[k] && (r = fws_hip_status(hipStreamWaitEvent(e->sx, e->ev_done[k], 0)))) return r;
+        if ((r = fws_launch_decode_scan(c, w, q.len, e->sx))) return r;
+        if ((r = fws_hip_status(hipEventRecord(e->ev_scan[k], e->sx)))) return r;
+        if ((r = fws_hip_status(hipStreamWaitEvent(e->sy, e->ev_scan[k], 0)))) return r;
+        if ((r = fws_launch_decode_resolve(c, w, q.len, q.dev_frames, q.cap, q.dev_result, q.dev_utf8_ok, e->sy)))
+            return r;
+        if ((r = fws_decode_unmask(c, w, q.len, q.dev_frames, q.cap, q.dev_utf8_ok, e->sy))) return r;
+        if ((r = fws_hip_status(hipEventRecord(e->ev_done[k], e->sy)))) return r;
+        e->used[k] = true;
+    }
+    // every scan precedes its resolve on Y, so Y's end is the engine's end
+    if ((r = fws_hip_status(hipEventRecord(e->ev_out, e->sy)))) return r;
+    return fws_hip_status(hipStreamWaitEvent(s, e->ev_out, 0));
+}
+
+}  // extern "C"

@@ -483,15 +483,14 @@ int fws_decode_ensure(fws_gpu_ctx *ctx, uint64_t N, uint32_t cap) {
     return 0;
 }
 
-int fws_launch_decode(fws_gpu_ctx *ctx, uint8_t *wire, uint64_t N, fws_frame_info *frames, uint32_t cap,
-                      fws_decode_result *res, uint8_t *utf8_ok, hipStream_t s) {
+// The decode's first half: this call's counter set (zeroed by the previous
+// call's k_emit, or here when a call did not finish its launches) and k_scan.
+int fws_launch_decode_scan(fws_gpu_ctx *ctx, uint8_t *wire, uint64_t N, hipStream_t s) {
     fws_decode_ws &d = ctx->dec;
     const uint32_t n_tiles = (uint32_t)((N + kTile - 1) / kTile);
     hipError_t e;
-    // counters: this call's set was zeroed by the previous call's k_emit launch
     d.parity ^= 1u;
     d.counters = d.cnt_base + d.parity * kCntStride;
-    uint32_t *const next = d.cnt_base + (d.parity ^ 1u) * kCntStride;
     if (d.cnt_dirty) {
         if ((e = hipMemsetAsync(d.counters, 0, kCntStride * 4, s)) != hipSuccess) return fws_hip_status(e);
         d.cnt_dirty = false;
@@ -505,10 +504,26 @@ int fws_launch_decode(fws_gpu_ctx *ctx, uint8_t *wire, uint64_t N, fws_frame_inf
                            (uint32_t)d.max_surv, d.scan_dummy);
         if ((e = hipGetLastError()) != hipSuccess) return fws_hip_status(e);
     }
-    // super-tile resolve; g_resolve_mode 1 sends every super tile down the big-ST
-    // path (tests), mode 2 decodes as mode 0 here. Slot ids are 32-bit.
+    return 0;
+}
+
+// The second half, on the counter set the scan used (k_emit zeroes the other
+// set for the context's next call): the super-tile resolve. g_resolve_mode 1
+// sends every super tile down the big-ST path (tests), mode 2 decodes as mode 0
+// here. Slot ids are 32-bit.
+int fws_launch_decode_resolve(fws_gpu_ctx *ctx, uint8_t *wire, uint64_t N, fws_frame_info *frames, uint32_t cap,
+                              fws_decode_result *res, uint8_t *utf8_ok, hipStream_t s) {
+    fws_decode_ws &d = ctx->dec;
+    const uint32_t n_tiles = (uint32_t)((N + kTile - 1) / kTile);
+    uint32_t *const next = d.cnt_base + (d.parity ^ 1u) * kCntStride;
     if (N >= (1ull << 39)) return FWS_ERR_CAPACITY;
     const int r = fws_launch_merge(ctx, wire, N, n_tiles, frames, cap, res, utf8_ok, g_resolve_mode == 1, next, s);
     if (r == 0) d.cnt_dirty = false;
     return r;
+}
+
+int fws_launch_decode(fws_gpu_ctx *ctx, uint8_t *wire, uint64_t N, fws_frame_info *frames, uint32_t cap,
+                      fws_decode_result *res, uint8_t *utf8_ok, hipStream_t s) {
+    const int r = fws_launch_decode_scan(ctx, wire, N, s);
+    return r ? r : fws_launch_decode_resolve(ctx, wire, N, frames, cap, res, utf8_ok, s);
 }

@@ -281,19 +281,29 @@ int fws_gpu_decode_stream(fws_gpu_ctx *ctx, void *dev_wire, uint64_t len, fws_fr
         if ((r = fws_hip_status(hipStreamSynchronize(s)))) return r;
         if (st != FWS_SMALL_DECLINED) return 0;
     }
-    if ((r = fws_decode_ensure(ctx, len, cap))) return r;
-    const uint64_t units = (len / 16 + 2ull * cap) / 256 + 2;
-    if ((r = fws_ctx_ensure_plan(ctx, cap, units))) return r;
+    if ((r = fws_decode_prepare(ctx, len, cap, dev_utf8_ok != nullptr))) return r;
     if ((r = fws_launch_decode(ctx, (uint8_t *)dev_wire, len, dev_frames, cap, dev_result, dev_utf8_ok, s)))
         return r;
-    if (cap == 0 || len == 0) return 0;
-    // the resolve left the device frame count, the stream-space unmask plan of the
-    // decoded frames and (with dev_utf8_ok) each frame's TEXT/FIN/complete preset;
-    // the unmask checks UTF-8 while the payload is in registers
-    const uint32_t *n_dev = ctx->dec.counters + kDecodeFramesCounter;
-    if (dev_utf8_ok && (r = fws_ctx_ensure_seam(ctx, len))) return r;
-    return fws_launch_unmask_stream((uint8_t *)dev_wire, len, dev_frames, cap, n_dev, ctx->plan.unit_first,
-                                    dev_utf8_ok, ctx->seam, s);
+    return fws_decode_unmask(ctx, (uint8_t *)dev_wire, len, dev_frames, cap, dev_utf8_ok, s);
 }
 
 }  // extern "C"
+
+int fws_decode_prepare(fws_gpu_ctx *ctx, uint64_t len, uint32_t cap, bool utf8) {
+    int r;
+    if ((r = fws_decode_ensure(ctx, len, cap))) return r;
+    const uint64_t units = (len / 16 + 2ull * cap) / 256 + 2;
+    if ((r = fws_ctx_ensure_plan(ctx, cap, units))) return r;
+    return utf8 ? fws_ctx_ensure_seam(ctx, len) : 0;
+}
+
+int fws_decode_unmask(fws_gpu_ctx *ctx, uint8_t *wire, uint64_t len, fws_frame_info *frames, uint32_t cap,
+                      uint8_t *utf8_ok, hipStream_t s) {
+    if (cap == 0 || len == 0) return 0;
+    // the resolve left the device frame count, the stream-space unmask plan of the
+    // decoded frames and (with utf8_ok) each frame's TEXT/FIN/complete preset;
+    // the unmask checks UTF-8 while the payload is in registers
+    const uint32_t *n_dev = ctx->dec.counters + kDecodeFramesCounter;
+    return fws_launch_unmask_stream(wire, len, frames, cap, n_dev, ctx->plan.unit_first, utf8_ok, ctx->seam, s);
+}
+

@@ -207,6 +207,17 @@ int fws_decode_ensure(fws_gpu_ctx *ctx, uint64_t N, uint32_t cap);
 // utf8_ok (optional): per-frame UTF-8 flags, preset here, finished by fws_launch_unmask_stream
 int fws_launch_decode(fws_gpu_ctx *ctx, uint8_t *wire, uint64_t N, fws_frame_info *frames, uint32_t cap,
                       fws_decode_result *res, uint8_t *utf8_ok, hipStream_t s);
+// the same in two halves, which may run on two streams (fws_decode_engine): the
+// scan, then -- after it, with nothing else on this context in between -- the
+// resolve
+int fws_launch_decode_scan(fws_gpu_ctx *ctx, uint8_t *wire, uint64_t N, hipStream_t s);
+int fws_launch_decode_resolve(fws_gpu_ctx *ctx, uint8_t *wire, uint64_t N, fws_frame_info *frames, uint32_t cap,
+                              fws_decode_result *res, uint8_t *utf8_ok, hipStream_t s);
+// fws_gpu_decode_stream's workspace for a stream of len bytes / cap frames (may reallocate)
+int fws_decode_prepare(fws_gpu_ctx *ctx, uint64_t len, uint32_t cap, bool utf8);
+// its unmask launch (after the resolve, on the resolve's stream)
+int fws_decode_unmask(fws_gpu_ctx *ctx, uint8_t *wire, uint64_t len, fws_frame_info *frames, uint32_t cap,
+                      uint8_t *utf8_ok, hipStream_t s);
 // merge_kernels.hip: from k_scan's survivors to the frame list, the result and the
 // unmask plan (k_merge -> k_link + path -> k_emit); no grid barrier anywhere
 uint64_t fws_merge_super_tiles(uint64_t n_tiles);

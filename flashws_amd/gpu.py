@@ -9,7 +9,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._lib import FRAME_DESC, FRAME_INFO, DECODE_RESULT, RX_EVENT, TX_DESC, GenParams, check, lib
+from ._lib import DECODE_JOB, FRAME_DESC, FRAME_INFO, DECODE_RESULT, RX_EVENT, TX_DESC, GenParams, check, lib
 
 
 def _stream_handle(stream=None):
@@ -150,6 +150,41 @@ def decode_stream(ctx, wire, cap, frames=None, result=None, utf8_ok=None, stream
     rc = lib().fws_gpu_decode_stream(ctx.h, _ptr(wire), n, _ptr(frames), cap, _ptr(result), u,
                                      _stream_handle(stream))
     return rc, frames, result, utf8_ok
+
+
+class DecodeEngine:
+    """fws_decode_engine: fws_gpu_decode_stream over many independent streams,
+    the scan of one job pipelined with the resolve + unmask of another
+    (scan_cus > 0: the scans on that many CUs, the rest on the others)."""
+
+    def __init__(self, device=0, scan_cus=0, max_frames=0, max_stream_bytes=0):
+        h = C.c_void_p()
+        check("fws_decode_engine_create", lib().fws_decode_engine_create(device, scan_cus, max_frames,
+                                                                         max_stream_bytes, C.byref(h)))
+        self.h = h
+
+    def run(self, jobs, stream=None):
+        """jobs: (wire, cap, frames, result[, utf8_ok]) tuples of device tensors
+        (len = wire.numel()). Returns the status; nothing synchronised."""
+        a = np.zeros(len(jobs), dtype=DECODE_JOB)
+        for i, j in enumerate(jobs):
+            wire, cap, frames, result = j[:4]
+            u = j[4] if len(j) > 4 else None
+            a[i] = (wire.data_ptr(), wire.numel(), frames.data_ptr(), cap, 0, result.data_ptr(),
+                    u.data_ptr() if u is not None else 0)
+        self._jobs = a                                   # alive until the next run
+        return lib().fws_decode_engine_run(self.h, C.c_void_p(a.ctypes.data), len(jobs), _stream_handle(stream))
+
+    def close(self):
+        if self.h:
+            lib().fws_decode_engine_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def read_result(result):

@@ -47,7 +47,6 @@ DENSE_FRAMES, DENSE_PAYLOAD = 200000, 64   # SURVEY §6 dense small-frame worklo
 # the next 10 (tools/c5_warmup_probe.py, profiles/r03/c5_warmup.txt)
 EXTRA_WARMUP = 10
 ENGINE_JOBS = 16               # batches per fws_decode_engine run (distinct buffers)
-ENGINE_SCAN_CUS = 0            # CUs given to the engine's scan stream (0: no partition)
 
 
 def parse():
@@ -754,8 +753,7 @@ def stream_decode_extra(ctx, wire_c2, dev, args):
             ebufs = bufs + [torch.from_numpy(wire).to(dev) for _ in range(ENGINE_JOBS - nbuf)]
             efr = [torch.empty_like(frames) for _ in range(ENGINE_JOBS)]
             ers = [torch.zeros_like(res) for _ in range(ENGINE_JOBS)]
-            eng = gpu.DecodeEngine(dev.index or 0, scan_cus=ENGINE_SCAN_CUS, max_frames=cap,
-                                   max_stream_bytes=len(wire))
+            eng = gpu.DecodeEngine(dev.index or 0, max_frames=cap, max_stream_bytes=len(wire))
             jobs = [(ebufs[j], cap, efr[j], ers[j]) for j in range(ENGINE_JOBS)]
             def estep(i):
                 rc = eng.run(jobs, stream=stream)
@@ -766,10 +764,10 @@ def stream_decode_extra(ctx, wire_c2, dev, args):
                 assert int(rj["status"]) == 0 and int(rj["n_frames"]) == n_frames, (name, "engine", j, rj)
             rec["engine"] = {"GiB_per_s": round(payload / te / GIB, 1), "ms_per_batch": round(te * 1e3, 4),
                              "roofline_frac": round((len(wire) + payload) / te / 1e9 / HBM_PEAK_GBS, 4),
-                             "jobs_per_run": ENGINE_JOBS, "scan_cus": ENGINE_SCAN_CUS,
-                             "path": "fws_decode_engine_run: one run of distinct batches, scans on one HIP stream "
-                                     "(CU subset when scan_cus > 0), resolve + unmask on another, 3 in flight; "
-                                     "every job's status and frame count checked"}
+                             "jobs_per_run": ENGINE_JOBS,
+                             "path": "fws_decode_engine_run: one run of distinct batches, whole decodes alternating "
+                                     "over two HIP streams with a workspace each; every job's status and frame "
+                                     "count checked"}
             eng.close()
             del ebufs, efr, ers
         del bufs

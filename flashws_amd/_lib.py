@@ -117,7 +117,7 @@ SIGNATURES = [
     ("fws_rx_pipe_destroy", None, [_P]),
     ("fws_rx_pipe_submit", _I, [_P, _P, _U64, _PU64]),
     ("fws_rx_pipe_wait", _I, [_P, _U64, C.POINTER(C.c_void_p), _PU64, _P, C.POINTER(C.c_void_p)]),
-    ("fws_decode_engine_create", _I, [_I, _U32, _U64, _U64, C.POINTER(C.c_void_p)]),
+    ("fws_decode_engine_create", _I, [_I, _U64, _U64, C.POINTER(C.c_void_p)]),
     ("fws_decode_engine_destroy", None, [_P]),
     ("fws_decode_engine_run", _I, [_P, _P, _U32, _P]),
 ]

@@ -2,21 +2,27 @@
 // independent streams, pipelined on one device.
 //
 // A stream decode is two passes over the wire with a latency-bound resolve
-// between them: k_scan (issue-bound: ~49 of its 66 us on C3 are VALU issue,
-// DESIGN.md §4.3b), then k_merge -> k_link -> k_emit (~39 us of dependent
-// round trips), then k_unmask_stream (HBM-bound). One call leaves the HBM idle
-// during the scan's issue-bound stretches and the resolve. The engine keeps
-// three decodes in flight on two HIP streams:
+// between them: k_scan (66 us on C3, ~4 TB/s of reads, VALU issue ~49 us of
+// it), then k_merge -> k_link -> k_emit (~39 us of dependent round trips with
+// few waves), then k_unmask_stream (HBM-bound). One call leaves the HBM mostly
+// idle during the resolve. The engine keeps decodes in flight on two HIP
+// streams, each with its own workspaces (a private fws_gpu_ctx per job slot),
+// so one job's resolve overlaps another's streaming kernels.
 //
-//   stream X (scan):     scan(j)   scan(j+1)   scan(j+2)   ...
-//   stream Y (rest):          resolve(j) unmask(j)  resolve(j+1) unmask(j+1) ...
-//
-// Job j uses workspace j % 3 (a private fws_gpu_ctx); Y waits for scan(j) before
-// resolve(j), and X waits for job j's unmask before scan(j + 3) reuses its
-// workspace. With scan_cus > 0, X is created with a CU mask of that many CUs
-// spread over the whole CU index range and Y with the complement, so the scan of
-// one job and the unmask of another share the GPU by partition instead of by
-// whichever queue the dispatcher serves first.
+// Schedules (fws_internal_set_engine_mode, measured on MI355X C3 batches,
+// profiles/r04/engine/):
+//   0 (default)  job j's whole decode on stream j % 2: 0.165 ms per batch (C3,
+//                16 jobs per run; the bench's two contexts on two streams:
+//                0.158-0.161).
+//   1            split phases: every scan on stream X, every resolve + unmask
+//                on stream Y, three jobs in flight (Y waits for scan(j), X
+//                waits for job j's unmask before reusing its workspace for
+//                j + 3): 0.201 ms -- a scan running beside an unmask slows
+//                both (k_scan's own reads run at ~4 TB/s, so the two are not
+//                issue- and HBM-bound complements), and the scans ahead of
+//                the resolve take the CUs the unmask needs.
+//   1 + CU partition (fws_internal_set_engine_scan_cus: X on that many CUs
+//                spread over the index range, Y on the rest): 0.29-0.39 ms.
 #include <hip/hip_runtime.h>
 
 #include <cstring>
@@ -26,9 +32,23 @@
 
 namespace {
 
-constexpr int kSlots = 3;                  // decodes in flight (workspaces)
+constexpr int kSlots = 3;                  // workspaces (decodes in flight)
+
+int g_engine_mode = 0;                     // tuning hook: the schedule (header comment)
+uint32_t g_engine_scan_cus = 0;            // tuning hook: mode 1's CU partition (0: none)
 
 }  // namespace
+
+extern "C" __attribute__((visibility("default"))) int fws_internal_set_engine_mode(int m) {
+    const int old = g_engine_mode;
+    if (m == 0 || m == 1) g_engine_mode = m;
+    return old;
+}
+extern "C" __attribute__((visibility("default"))) int fws_internal_set_engine_scan_cus(int cus) {
+    const int old = (int)g_engine_scan_cus;
+    g_engine_scan_cus = cus > 0 ? (uint32_t)cus : 0u;
+    return old;
+}
 
 struct fws_decode_engine {
     int device = 0;
@@ -40,6 +60,7 @@ struct fws_decode_engine {
     uint64_t max_frames = 0, max_bytes = 0;
     bool utf8_ready = false;
     uint32_t next = 0;                     // the next job's workspace
+    int mode = 0;                          // the schedule this engine was created with
 };
 
 static void engine_free(fws_decode_engine *e) {
@@ -81,13 +102,14 @@ static int engine_reserve(fws_decode_engine *e, uint64_t frames, uint64_t bytes,
 
 extern "C" {
 
-int fws_decode_engine_create(int device, uint32_t scan_cus, uint64_t max_frames, uint64_t max_stream_bytes,
-                             fws_decode_engine **out) {
+int fws_decode_engine_create(int device, uint64_t max_frames, uint64_t max_stream_bytes, fws_decode_engine **out) {
     if (!out) return FWS_ERR_INVALID;
     *out = nullptr;
     fws_decode_engine *e = new (std::nothrow) fws_decode_engine();
     if (!e) return FWS_ERR_INTERNAL;
     e->device = device;
+    e->mode = g_engine_mode;
+    const uint32_t scan_cus = e->mode == 1 ? g_engine_scan_cus : 0u;
     int r = 0;
     for (int k = 0; k < kSlots && !r; ++k) r = fws_gpu_ctx_create(device, &e->ctx[k]);
     int cus = 0;
@@ -148,6 +170,30 @@ int fws_decode_engine_run(fws_decode_engine *e, const fws_decode_job *jobs, uint
     if ((r = fws_hip_status(hipEventRecord(e->ev_in, s))) || (r = fws_hip_status(hipStreamWaitEvent(e->sx, e->ev_in, 0))) ||
         (r = fws_hip_status(hipStreamWaitEvent(e->sy, e->ev_in, 0))))
         return r;
+    if (e->mode == 0) {
+        // job j's whole decode on stream j % 2, workspace j % 2 (stream order
+        // serialises the jobs that share a workspace). Left alone the two streams
+        // fall into step (both scan, both resolve, both unmask: a kernel trace,
+        // profiles/r04/engine/); making each scan wait for the previous job's scan,
+        // so that scans alternate, measured slower (0.170-0.177 against
+        // 0.165 ms, profiles/r04/engine/sweep_scan_order.jsonl)
+        for (uint32_t j = 0; j < n; ++j) {
+            const fws_decode_job &q = jobs[j];
+            const uint32_t k = e->next;
+            e->next = (k + 1) % 2;
+            fws_gpu_ctx *c = e->ctx[k];
+            hipStream_t st = k ? e->sy : e->sx;
+            uint8_t *w = (uint8_t *)q.dev_wire;
+            if ((r = fws_decode_prepare(c, q.len, q.cap, q.dev_utf8_ok != nullptr))) return r;
+            if ((r = fws_launch_decode(c, w, q.len, q.dev_frames, q.cap, q.dev_result, q.dev_utf8_ok, st))) return r;
+            if ((r = fws_decode_unmask(c, w, q.len, q.dev_frames, q.cap, q.dev_utf8_ok, st))) return r;
+        }
+        if ((r = fws_hip_status(hipEventRecord(e->ev_done[0], e->sx))) ||
+            (r = fws_hip_status(hipEventRecord(e->ev_done[1], e->sy))) ||
+            (r = fws_hip_status(hipStreamWaitEvent(s, e->ev_done[0], 0))))
+            return r;
+        return fws_hip_status(hipStreamWaitEvent(s, e->ev_done[1], 0));
+    }
     for (uint32_t j = 0; j < n; ++j) {
         const fws_decode_job &q = jobs[j];
         const uint32_t k = e->next;

@@ -154,13 +154,24 @@ def decode_stream(ctx, wire, cap, frames=None, result=None, utf8_ok=None, stream
 
 class DecodeEngine:
     """fws_decode_engine: fws_gpu_decode_stream over many independent streams,
-    the scan of one job pipelined with the resolve + unmask of another
-    (scan_cus > 0: the scans on that many CUs, the rest on the others)."""
+    decodes kept in flight on two HIP streams. mode / scan_cus select the
+    schedule through the library's tuning hooks (0: whole decodes alternating
+    over the two streams, the default; 1: scans on one stream, resolve + unmask
+    on the other, CU-partitioned when scan_cus > 0) -- for A/B runs only."""
 
-    def __init__(self, device=0, scan_cus=0, max_frames=0, max_stream_bytes=0):
-        h = C.c_void_p()
-        check("fws_decode_engine_create", lib().fws_decode_engine_create(device, scan_cus, max_frames,
-                                                                         max_stream_bytes, C.byref(h)))
+    def __init__(self, device=0, max_frames=0, max_stream_bytes=0, mode=None, scan_cus=0):
+        L = lib()
+        old = None
+        if mode is not None:
+            old = (L.fws_internal_set_engine_mode(mode), L.fws_internal_set_engine_scan_cus(scan_cus))
+        try:
+            h = C.c_void_p()
+            check("fws_decode_engine_create", L.fws_decode_engine_create(device, max_frames, max_stream_bytes,
+                                                                         C.byref(h)))
+        finally:
+            if old is not None:
+                L.fws_internal_set_engine_mode(old[0])
+                L.fws_internal_set_engine_scan_cus(old[1])
         self.h = h
 
     def run(self, jobs, stream=None):

@@ -180,18 +180,15 @@ int fws_gpu_decode_stream(fws_gpu_ctx *ctx, void *dev_wire, uint64_t len,
 /* ---- batched stream decode: many independent streams ----------------------
  * fws_gpu_decode_stream over a list of independent streams (the buffers of
  * many connections, or successive batches of one: FLoop's loop hands each
- * socket's bytes to its own OnRecvData, floop.h:661-703), pipelined on the
- * device: the header scan of job j + 1 runs while job j is resolved and
- * unmasked. The scan is issue-bound and the unmask HBM-bound,
- * so the engine runs them on two HIP streams, optionally on disjoint CU sets
- * (scan_cus > 0: that many CUs for the scans, the rest for resolve + unmask;
- * 0 = both streams on every CU). Each job's frames, result, UTF-8 flags and
- * unmasked bytes equal fws_gpu_decode_stream on that job alone. Jobs must not
- * share memory. The work is ordered after everything already on `stream`,
- * and `stream` waits for all of it (synchronise `stream` to read results).
- * An engine is used from one host thread at a time; it owns its workspaces
- * (3 stream decodes in flight), sized by max_frames / max_stream_bytes per job
- * (a larger job grows them after draining the engine). */
+ * socket's bytes to its own OnRecvData, floop.h:661-703), with decodes kept
+ * in flight on two HIP streams so one job's latency-bound resolve overlaps
+ * another's streaming kernels. Each job's frames, result,
+ * UTF-8 flags and unmasked bytes equal fws_gpu_decode_stream on that job
+ * alone. Jobs must not share memory. The work is ordered after everything
+ * already on `stream`, and `stream` waits for all of it (synchronise `stream`
+ * to read results). An engine is used from one host thread at a time; it owns
+ * its workspaces, sized by max_frames / max_stream_bytes per job (a larger job
+ * grows them after draining the engine). */
 typedef struct fws_decode_job {
     void *dev_wire;                 /* 16-B aligned, as fws_gpu_decode_stream */
     uint64_t len;
@@ -203,8 +200,7 @@ typedef struct fws_decode_job {
 } fws_decode_job;                   /* 48 bytes */
 
 typedef struct fws_decode_engine fws_decode_engine;
-int fws_decode_engine_create(int device, uint32_t scan_cus, uint64_t max_frames, uint64_t max_stream_bytes,
-                             fws_decode_engine **out);
+int fws_decode_engine_create(int device, uint64_t max_frames, uint64_t max_stream_bytes, fws_decode_engine **out);
 void fws_decode_engine_destroy(fws_decode_engine *e);
 int fws_decode_engine_run(fws_decode_engine *e, const fws_decode_job *jobs, uint32_t n, void *stream);
 

@@ -1,8 +1,9 @@
 """GPU: fws_decode_engine (batched stream decode, include/fws_gpu.h). Every
 job's unmasked bytes, frame list, result and UTF-8 flags must equal
 fws_gpu_decode_stream on that job alone -- the engine only reorders launches
-over its three workspaces and two streams (scan / resolve + unmask), with or
-without a CU partition. The single-stream decode is itself pinned to the
+over its workspaces and two streams, in each schedule: whole decodes
+alternating over the streams (the default) and the split-phase schedule (scans
+on one stream, resolve + unmask on the other), with or without a CU partition. The single-stream decode is itself pinned to the
 oracle and the reference's vectors (test_gpu_decode.py, test_gpu_configs.py);
 here the jobs mix random frame streams, protocol errors, incomplete tails,
 streams shorter than one tile, empty streams and generator batches, in runs
@@ -75,14 +76,18 @@ def _compare(got, exp, n_bytes):
         assert torch.equal(go[:m], eo[:m])
 
 
-@pytest.mark.parametrize("scan_cus", [0, 96])
+SCHEDULES = [(0, 0), (1, 0), (1, 96)]               # (mode, scan_cus): default, split phases, + CU partition
+
+
+@pytest.mark.parametrize("sched", SCHEDULES, ids=["alternate", "split", "split_cu96"])
 @pytest.mark.parametrize("utf8", [False, True], ids=["plain", "utf8"])
-def test_engine_matches_single_decodes(ctx, cuda, scan_cus, utf8):
-    rng = np.random.default_rng(4040 + scan_cus + utf8)
+def test_engine_matches_single_decodes(ctx, cuda, sched, utf8):
+    mode, scan_cus = sched
+    rng = np.random.default_rng(4040 + 7 * mode + scan_cus + utf8)
     streams = _streams(rng, 14)
     cap = 1 << 16
     exp = _run_reference(ctx, streams, cap, cuda, utf8)
-    eng = gpu.DecodeEngine(0, scan_cus=scan_cus, max_frames=cap, max_stream_bytes=8 << 20)
+    eng = gpu.DecodeEngine(0, max_frames=cap, max_stream_bytes=8 << 20, mode=mode, scan_cus=scan_cus)
     got, jobs = [], []
     for s in streams:
         w = _dev(s, cuda)
@@ -98,12 +103,13 @@ def test_engine_matches_single_decodes(ctx, cuda, scan_cus, utf8):
     eng.close()
 
 
-def test_engine_repeated_runs_and_growth(ctx, cuda):
+@pytest.mark.parametrize("sched", SCHEDULES, ids=["alternate", "split", "split_cu96"])
+def test_engine_repeated_runs_and_growth(ctx, cuda, sched):
     """Several runs on one engine (workspaces reused across runs), the second
     with jobs larger than the reservation (the engine drains and grows)."""
     rng = np.random.default_rng(77)
     cap = 1 << 15
-    eng = gpu.DecodeEngine(0, scan_cus=128, max_frames=1024, max_stream_bytes=1 << 20)
+    eng = gpu.DecodeEngine(0, max_frames=1024, max_stream_bytes=1 << 20, mode=sched[0], scan_cus=sched[1])
     for run in range(3):
         streams = _streams(rng, 7 + run)
         if run == 1:
@@ -122,11 +128,11 @@ def test_engine_repeated_runs_and_growth(ctx, cuda):
 
 def test_engine_c3_batches(ctx, cuda):
     """Eight C3 batches (256 MiB each would not fit the test budget: 32 MiB
-    slices of the C3 generator) through the CU-partitioned engine."""
+    slices of the C3 generator) through the default engine."""
     cap = 1 << 16
     streams = [gpu.config_c3(seed=60 + i, target=32 << 20)[0].tobytes() for i in range(8)]
     exp = _run_reference(ctx, streams, cap, cuda, False)
-    eng = gpu.DecodeEngine(0, scan_cus=112, max_frames=cap, max_stream_bytes=32 << 20)
+    eng = gpu.DecodeEngine(0, max_frames=cap, max_stream_bytes=32 << 20)
     got = [(_dev(s, cuda), torch.zeros(cap * gpu.FRAME_INFO.itemsize, dtype=torch.uint8, device=cuda),
             torch.zeros(gpu.DECODE_RESULT.itemsize, dtype=torch.uint8, device=cuda), None) for s in streams]
     assert eng.run([(g[0][:len(s)], cap, g[1], g[2]) for g, s in zip(got, streams)]) == 0
@@ -148,5 +154,5 @@ def test_engine_rejects_bad_jobs_before_queueing(cuda):
     torch.cuda.synchronize()
     assert int(rs.sum()) == 0                            # nothing ran, not even the good job
     with pytest.raises(_lib.FwsError):
-        gpu.DecodeEngine(0, scan_cus=100000)
+        gpu.DecodeEngine(0, mode=1, scan_cus=100000)      # more CUs than the device has
     eng.close()

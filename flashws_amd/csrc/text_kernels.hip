@@ -202,7 +202,6 @@ __global__ __launch_bounds__(kBlock) void k_gather_fast(uint8_t *__restrict__ ds
 // probes. The plan launch (k_out_plan, 6.9 us on C4) and its launch boundary
 // are gone.
 constexpr uint32_t kGatherLdsMax = 2048;
-constexpr uint32_t kGatherPer = kGatherLdsMax / kBlock;   // regions per thread in the block scan
 
 // The last f < n with base[f] <= pos (base[0] = 0 <= pos; base in LDS): lane
 // probes at a stride, then inside the bracketed stride. Wave-uniform result.
@@ -227,11 +226,18 @@ __device__ __forceinline__ uint32_t lds_search(const uint64_t *base, uint32_t n,
     return lo;
 }
 
-// Requires dst 16-B aligned and 1 <= n <= kGatherLdsMax.
-__global__ __launch_bounds__(kBlock) void k_gather_one(uint8_t *__restrict__ dst, const uint8_t *__restrict__ src,
-                                                       const fws_frame_desc *__restrict__ d, uint32_t n) {
+// Requires dst 16-B aligned and 1 <= n <= kGatherLdsMax. 7 waves per SIMD
+// (72 VGPRs; the 2 spilled ones live only on the probe path of units past the
+// 64th per wave); the compiler's own choice is 74 VGPRs, 6 waves.
+#ifndef FWS_GATHER_WPE
+#define FWS_GATHER_WPE 7
+#endif
+template <uint32_t kT>
+__global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(FWS_GATHER_WPE))) void k_gather_one(uint8_t *__restrict__ dst, const uint8_t *__restrict__ src,
+                                                   const fws_frame_desc *__restrict__ d, uint32_t n) {
+    constexpr uint32_t kGatherPer = kGatherLdsMax / kT;   // regions per thread in the block scan
     __shared__ uint64_t s_base[kGatherLdsMax + 1];
-    __shared__ uint64_t s_wsum[kBlock / 64];
+    __shared__ uint64_t s_wsum[kT / 64];
     const int lane = threadIdx.x & 63;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     // dbase in LDS: lengths (all loads in flight together), then each thread's
@@ -240,12 +246,12 @@ __global__ __launch_bounds__(kBlock) void k_gather_one(uint8_t *__restrict__ dst
         uint64_t l[kGatherPer];
 #pragma unroll
         for (uint32_t i = 0; i < kGatherPer; ++i) {
-            const uint32_t f = threadIdx.x + i * kBlock;
+            const uint32_t f = threadIdx.x + i * kT;
             l[i] = f < n ? d[f].payload_len : 0;
         }
 #pragma unroll
         for (uint32_t i = 0; i < kGatherPer; ++i) {
-            const uint32_t f = threadIdx.x + i * kBlock;
+            const uint32_t f = threadIdx.x + i * kT;
             if (f < n) s_base[f] = l[i];
         }
         __syncthreads();
@@ -271,24 +277,27 @@ __global__ __launch_bounds__(kBlock) void k_gather_one(uint8_t *__restrict__ dst
     }
     const uint64_t total = s_base[n];
     const uint64_t n_units = (total + kGatherUnit - 1) / kGatherUnit;
-    const uint64_t nw = (uint64_t)gridDim.x * (kBlock / 64);
-    const uint64_t ufirst = (uint64_t)blockIdx.x * (kBlock / 64) + wave;
+    const uint64_t nw = (uint64_t)gridDim.x * (kT / 64);
+    const uint64_t ufirst = (uint64_t)blockIdx.x * (kT / 64) + wave;
     // the regions of the wave's first 64 units, one unit per lane, all lanes
     // searching at once (one chain of LDS round trips per wave, not two per unit)
-    uint32_t my_lo = 0, my_hi = n - 1;
+    // (both region indices < kGatherLdsMax: packed in one register, lo | hi << 16)
+    uint32_t my_lh = (n - 1u) << 16;
     {
         const uint64_t u = ufirst + (uint64_t)lane * nw;
         if (u < n_units) {
-            my_lo = lds_search(s_base, n, u * kGatherUnit);
-            if (u + 1 < n_units) my_hi = lds_search(s_base, n, (u + 1) * kGatherUnit);
+            const uint32_t lo = lds_search(s_base, n, u * kGatherUnit);
+            const uint32_t hi = u + 1 < n_units ? lds_search(s_base, n, (u + 1) * kGatherUnit) : n - 1u;
+            my_lh = lo | (hi << 16);
         }
     }
     uint32_t k = 0;
     for (uint64_t u = ufirst; u < n_units; u += nw, ++k) {
         uint32_t flo, fhi;
         if (k < 64u) {
-            flo = __builtin_amdgcn_readlane(my_lo, k);
-            fhi = __builtin_amdgcn_readlane(my_hi, k);
+            const uint32_t lh = __builtin_amdgcn_readlane(my_lh, k);
+            flo = lh & 0xFFFFu;
+            fhi = lh >> 16;
         } else {
             flo = lds_owner(s_base, n, u * kGatherUnit, lane);
             fhi = u + 1 < n_units ? lds_owner(s_base, n, (u + 1) * kGatherUnit, lane) : n - 1;
@@ -385,19 +394,31 @@ int fws_launch_utf8_descs(const uint8_t *base, const fws_frame_desc *descs, uint
 // leave a static tail (1 x resident: 0.095 ms on C4), more repeat the prefix
 // build (one unit per wave: 0.098 ms); 4 x: 0.0865 ms
 // (profiles/r04/ab_gather.jsonl). Fewer for a small reservation.
+static int g_gather_threads = 256, g_gather_mult = 4;   // tuning hook: k_gather_one shape
+extern "C" __attribute__((visibility("default"))) int fws_internal_set_gather_shape(int threads, int mult) {
+    if (threads != 256 && threads != 512) return FWS_ERR_INVALID;
+    g_gather_threads = threads;
+    g_gather_mult = mult > 0 ? mult : 4;
+    return 0;
+}
+
 static int gather_one_grid(uint64_t max_bytes, uint64_t *out) {
-    static int resident[64] = {};
+    static int resident[2][64] = {};
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return FWS_ERR_INVALID;
-    if (!resident[dev]) {
+    const int v = g_gather_threads == 512 ? 1 : 0;
+    if (!resident[v][dev]) {
         int cus = 0, per = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_gather_one, kBlock, 0) != hipSuccess)
+            (v ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_gather_one<512>, 512, 0)
+               : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_gather_one<256>, 256, 0)) != hipSuccess)
             return FWS_ERR_NO_DEVICE;
-        resident[dev] = cus * (per > 0 ? per : 1);
+        resident[v][dev] = cus * (per > 0 ? per : 1);
     }
-    uint64_t blocks = (max_bytes / kGatherUnit + 4) / 4;
-    const uint64_t cap = g_gather_blocks ? (uint64_t)g_gather_blocks : 4u * (uint64_t)resident[dev];
+    const uint64_t wpb = (uint64_t)g_gather_threads / 64u;
+    uint64_t blocks = (max_bytes / kGatherUnit + wpb) / wpb;
+    const uint64_t cap = g_gather_blocks ? (uint64_t)g_gather_blocks
+                                         : (uint64_t)g_gather_mult * (uint64_t)resident[v][dev];
     if (blocks > cap) blocks = cap;
     *out = blocks < 1 ? 1 : blocks;
     return 0;
@@ -416,7 +437,10 @@ int fws_launch_gather(uint8_t *dst, const uint8_t *src, const fws_frame_desc *d,
         uint64_t blocks = 0;
         const int r = gather_one_grid(max_bytes, &blocks);
         if (r != 0) return r;
-        hipLaunchKernelGGL(k_gather_one, dim3((unsigned)blocks), dim3(kBlock), 0, s, dst, src, d, n);
+        if (g_gather_threads == 512)
+            hipLaunchKernelGGL(k_gather_one<512>, dim3((unsigned)blocks), dim3(512), 0, s, dst, src, d, n);
+        else
+            hipLaunchKernelGGL(k_gather_one<256>, dim3((unsigned)blocks), dim3(256), 0, s, dst, src, d, n);
         return fws_hip_status(hipGetLastError());
     }
     int r = fws_launch_gather_plan(d, n, ws, s);

@@ -7,7 +7,7 @@ destinations, modes alternated ABAB in one process; the one-launch form also
 at fixed grid sizes (fws_internal_set_gather_blocks; 0 = the resident count). One JSON line per
 (config, mode, rep).
 
-usage: python tools/ab_gather.py [reps]"""
+usage: python tools/ab_gather.py [reps] [--lib PATH]"""
 import ctypes
 import json
 import os
@@ -17,6 +17,11 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from flashws_amd import _lib, gpu  # noqa: E402
+
+if "--lib" in sys.argv:                      # an A/B build (make exp), e.g. libfws_gpu_w6.so
+    _lib.LIB_PATH = os.path.abspath(sys.argv[sys.argv.index("--lib") + 1])
+    del sys.argv[sys.argv.index("--lib"):sys.argv.index("--lib") + 2]
+LIB = os.path.basename(_lib.LIB_PATH)
 
 
 def main():
@@ -35,9 +40,14 @@ def main():
         L.fws_internal_gather_one_grid.argtypes = [ctypes.c_uint64]
         print(json.dumps({"cfg": name, "default_grid": L.fws_internal_gather_one_grid(len(w))}), flush=True)
         for rep in range(3):
-            for mode, blocks in ((0, 0), (1, 4608), (1, 0), (1, 6144), (1, 9216)):
-                L.fws_internal_set_gather_one(mode)
-                L.fws_internal_set_gather_blocks(blocks)
+            for mode, blocks in ((0, 0), (1, 0), (256, 3), (256, 5), (512, 2), (512, 3), (512, 4)):
+                # mode 0: plan + k_gather_fast; 1: k_gather_one default; 256 / 512: k_gather_one with that
+                # many threads per workgroup and `blocks` x the resident workgroups
+                L.fws_internal_set_gather_one(1 if mode else 0)
+                if mode > 1:
+                    L.fws_internal_set_gather_shape(mode, blocks)
+                else:
+                    L.fws_internal_set_gather_shape(256, 4)
                 for i in range(4):
                     gpu.unmask_gather(c, dsts[i % 4], src, dd, len(d))
                 torch.cuda.synchronize()
@@ -49,11 +59,11 @@ def main():
                 torch.cuda.synchronize()
                 ms = e0.elapsed_time(e1) / reps
                 outs[mode] = dsts[(reps - 1) % 4][:total].clone()
-                print(json.dumps({"cfg": name, "fragments": len(d), "gather_one": mode, "blocks": blocks, "rep": rep,
+                print(json.dumps({"lib": LIB, "cfg": name, "fragments": len(d), "gather_one": mode, "blocks": blocks, "rep": rep,
                                   "ms": round(ms, 4), "GiB_per_s": round(total / ms / 1e-3 / 2**30, 1)}), flush=True)
             assert torch.equal(outs[0], outs[1])
         L.fws_internal_set_gather_one(1)
-        L.fws_internal_set_gather_blocks(0)
+        L.fws_internal_set_gather_shape(256, 4)
         c.close()
         del src, dsts
 

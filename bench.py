@@ -758,7 +758,11 @@ def stream_decode_extra(ctx, wire_c2, dev, args):
             def estep(i):
                 rc = eng.run(jobs, stream=stream)
                 assert rc == 0, rc
-            te = _time(estep, 3, stream, warmup=1) / ENGINE_JOBS
+            # the median of 5 timed runs after 3 untimed ones (the first runs of a fresh
+            # engine come out ~5 % slower, profiles/r04/engine/sweep_schedules.jsonl)
+            for i in range(3):
+                estep(i)
+            te = sorted(_time(estep, 1, stream, warmup=0) for _ in range(5))[2] / ENGINE_JOBS
             for j in range(ENGINE_JOBS):
                 rj = gpu.read_result(ers[j])
                 assert int(rj["status"]) == 0 and int(rj["n_frames"]) == n_frames, (name, "engine", j, rj)

@@ -55,7 +55,7 @@ struct fws_decode_engine {
     fws_gpu_ctx *ctx[kSlots] = {};
     bool used[kSlots] = {};
     hipStream_t sx = nullptr, sy = nullptr;
-    hipEvent_t ev_in = nullptr, ev_out = nullptr;
+    hipEvent_t ev_in = nullptr, ev_jx = nullptr, ev_jy = nullptr;   // run start, the two streams' ends
     hipEvent_t ev_scan[kSlots] = {}, ev_done[kSlots] = {};
     uint64_t max_frames = 0, max_bytes = 0;
     bool utf8_ready = false;
@@ -73,8 +73,8 @@ static void engine_free(fws_decode_engine *e) {
         if (e->ev_done[k]) (void)hipEventDestroy(e->ev_done[k]);
         fws_gpu_ctx_destroy(e->ctx[k]);
     }
-    if (e->ev_in) (void)hipEventDestroy(e->ev_in);
-    if (e->ev_out) (void)hipEventDestroy(e->ev_out);
+    for (hipEvent_t ev : {e->ev_in, e->ev_jx, e->ev_jy})
+        if (ev) (void)hipEventDestroy(ev);
     if (e->sx) (void)hipStreamDestroy(e->sx);
     if (e->sy) (void)hipStreamDestroy(e->sy);
     delete e;
@@ -133,7 +133,8 @@ int fws_decode_engine_create(int device, uint64_t max_frames, uint64_t max_strea
     }
     const unsigned evf = hipEventDisableTiming;
     if (!r) r = fws_hip_status(hipEventCreateWithFlags(&e->ev_in, evf));
-    if (!r) r = fws_hip_status(hipEventCreateWithFlags(&e->ev_out, evf));
+    if (!r) r = fws_hip_status(hipEventCreateWithFlags(&e->ev_jx, evf));
+    if (!r) r = fws_hip_status(hipEventCreateWithFlags(&e->ev_jy, evf));
     for (int k = 0; k < kSlots && !r; ++k) {
         r = fws_hip_status(hipEventCreateWithFlags(&e->ev_scan[k], evf));
         if (!r) r = fws_hip_status(hipEventCreateWithFlags(&e->ev_done[k], evf));
@@ -148,6 +149,50 @@ int fws_decode_engine_create(int device, uint64_t max_frames, uint64_t max_strea
 }
 
 void fws_decode_engine_destroy(fws_decode_engine *e) { engine_free(e); }
+
+// Queues every job on the engine's streams (after ev_in); returns the first
+// failure, with the jobs before it queued.
+static int engine_queue(fws_decode_engine *e, const fws_decode_job *jobs, uint32_t n) {
+    int r;
+    if (e->mode == 0) {
+        // job j's whole decode on stream j % 2, workspace j % 2 (stream order
+        // serialises the jobs that share a workspace). Left alone the two streams
+        // fall into step (both scan, both resolve, both unmask: a kernel trace,
+        // profiles/r04/engine/); making each scan wait for the previous job's scan,
+        // so that scans alternate, measured slower (0.170-0.177 against
+        // 0.165 ms, profiles/r04/engine/sweep_scan_order.jsonl)
+        for (uint32_t j = 0; j < n; ++j) {
+            const fws_decode_job &q = jobs[j];
+            const uint32_t k = e->next;
+            e->next = (k + 1) % 2;
+            fws_gpu_ctx *c = e->ctx[k];
+            hipStream_t st = k ? e->sy : e->sx;
+            uint8_t *w = (uint8_t *)q.dev_wire;
+            if ((r = fws_decode_prepare(c, q.len, q.cap, q.dev_utf8_ok != nullptr))) return r;   // sized: no allocation
+            if ((r = fws_launch_decode(c, w, q.len, q.dev_frames, q.cap, q.dev_result, q.dev_utf8_ok, st))) return r;
+            if ((r = fws_decode_unmask(c, w, q.len, q.dev_frames, q.cap, q.dev_utf8_ok, st))) return r;
+        }
+        return 0;
+    }
+    for (uint32_t j = 0; j < n; ++j) {
+        const fws_decode_job &q = jobs[j];
+        const uint32_t k = e->next;
+        e->next = (k + 1) % kSlots;
+        fws_gpu_ctx *c = e->ctx[k];
+        uint8_t *w = (uint8_t *)q.dev_wire;
+        if ((r = fws_decode_prepare(c, q.len, q.cap, q.dev_utf8_ok != nullptr))) return r;
+        if (e->used[k] && (r = fws_hip_status(hipStreamWaitEvent(e->sx, e->ev_done[k], 0)))) return r;
+        if ((r = fws_launch_decode_scan(c, w, q.len, e->sx))) return r;
+        if ((r = fws_hip_status(hipEventRecord(e->ev_scan[k], e->sx)))) return r;
+        if ((r = fws_hip_status(hipStreamWaitEvent(e->sy, e->ev_scan[k], 0)))) return r;
+        if ((r = fws_launch_decode_resolve(c, w, q.len, q.dev_frames, q.cap, q.dev_result, q.dev_utf8_ok, e->sy)))
+            return r;
+        if ((r = fws_decode_unmask(c, w, q.len, q.dev_frames, q.cap, q.dev_utf8_ok, e->sy))) return r;
+        if ((r = fws_hip_status(hipEventRecord(e->ev_done[k], e->sy)))) return r;
+        e->used[k] = true;
+    }
+    return 0;
+}
 
 int fws_decode_engine_run(fws_decode_engine *e, const fws_decode_job *jobs, uint32_t n, void *stream) {
     if (!e || (n && !jobs)) return FWS_ERR_INVALID;
@@ -170,50 +215,14 @@ int fws_decode_engine_run(fws_decode_engine *e, const fws_decode_job *jobs, uint
     if ((r = fws_hip_status(hipEventRecord(e->ev_in, s))) || (r = fws_hip_status(hipStreamWaitEvent(e->sx, e->ev_in, 0))) ||
         (r = fws_hip_status(hipStreamWaitEvent(e->sy, e->ev_in, 0))))
         return r;
-    if (e->mode == 0) {
-        // job j's whole decode on stream j % 2, workspace j % 2 (stream order
-        // serialises the jobs that share a workspace). Left alone the two streams
-        // fall into step (both scan, both resolve, both unmask: a kernel trace,
-        // profiles/r04/engine/); making each scan wait for the previous job's scan,
-        // so that scans alternate, measured slower (0.170-0.177 against
-        // 0.165 ms, profiles/r04/engine/sweep_scan_order.jsonl)
-        for (uint32_t j = 0; j < n; ++j) {
-            const fws_decode_job &q = jobs[j];
-            const uint32_t k = e->next;
-            e->next = (k + 1) % 2;
-            fws_gpu_ctx *c = e->ctx[k];
-            hipStream_t st = k ? e->sy : e->sx;
-            uint8_t *w = (uint8_t *)q.dev_wire;
-            if ((r = fws_decode_prepare(c, q.len, q.cap, q.dev_utf8_ok != nullptr))) return r;
-            if ((r = fws_launch_decode(c, w, q.len, q.dev_frames, q.cap, q.dev_result, q.dev_utf8_ok, st))) return r;
-            if ((r = fws_decode_unmask(c, w, q.len, q.dev_frames, q.cap, q.dev_utf8_ok, st))) return r;
-        }
-        if ((r = fws_hip_status(hipEventRecord(e->ev_done[0], e->sx))) ||
-            (r = fws_hip_status(hipEventRecord(e->ev_done[1], e->sy))) ||
-            (r = fws_hip_status(hipStreamWaitEvent(s, e->ev_done[0], 0))))
-            return r;
-        return fws_hip_status(hipStreamWaitEvent(s, e->ev_done[1], 0));
-    }
-    for (uint32_t j = 0; j < n; ++j) {
-        const fws_decode_job &q = jobs[j];
-        const uint32_t k = e->next;
-        e->next = (k + 1) % kSlots;
-        fws_gpu_ctx *c = e->ctx[k];
-        uint8_t *w = (uint8_t *)q.dev_wire;
-        if ((r = fws_decode_prepare(c, q.len, q.cap, q.dev_utf8_ok != nullptr))) return r;   // sized: no allocation
-        if (e->used[k] && (r = fws_hip_status(hipStreamWaitEvent(e->sx, e->ev_done[k], 0)))) return r;
-        if ((r = fws_launch_decode_scan(c, w, q.len, e->sx))) return r;
-        if ((r = fws_hip_status(hipEventRecord(e->ev_scan[k], e->sx)))) return r;
-        if ((r = fws_hip_status(hipStreamWaitEvent(e->sy, e->ev_scan[k], 0)))) return r;
-        if ((r = fws_launch_decode_resolve(c, w, q.len, q.dev_frames, q.cap, q.dev_result, q.dev_utf8_ok, e->sy)))
-            return r;
-        if ((r = fws_decode_unmask(c, w, q.len, q.dev_frames, q.cap, q.dev_utf8_ok, e->sy))) return r;
-        if ((r = fws_hip_status(hipEventRecord(e->ev_done[k], e->sy)))) return r;
-        e->used[k] = true;
-    }
-    // every scan precedes its resolve on Y, so Y's end is the engine's end
-    if ((r = fws_hip_status(hipEventRecord(e->ev_out, e->sy)))) return r;
-    return fws_hip_status(hipStreamWaitEvent(s, e->ev_out, 0));
+    r = engine_queue(e, jobs, n);
+    // `stream` waits for both streams, also after a failure part-way (the jobs
+    // queued before it still run)
+    int j = fws_hip_status(hipEventRecord(e->ev_jx, e->sx));
+    if (!j) j = fws_hip_status(hipEventRecord(e->ev_jy, e->sy));
+    if (!j) j = fws_hip_status(hipStreamWaitEvent(s, e->ev_jx, 0));
+    if (!j) j = fws_hip_status(hipStreamWaitEvent(s, e->ev_jy, 0));
+    return r ? r : j;
 }
 
 }  // extern "C"

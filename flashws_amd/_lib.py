@@ -18,7 +18,10 @@ except ImportError:  # pragma: no cover - torch is part of the image
     torch = None
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG_DIR, "lib", "libfws_gpu.so")
+# FWS_LIB_VARIANT=<tag> loads an in-tree A/B build, lib/libfws_gpu_<tag>.so (make exp), e.g. to run
+# the parity tests on an experimental kernel; unset, the product library
+_VARIANT = os.environ.get("FWS_LIB_VARIANT", "")
+LIB_PATH = os.path.join(PKG_DIR, "lib", f"libfws_gpu_{_VARIANT}.so" if _VARIANT else "libfws_gpu.so")
 
 FWS_OK = 0
 FWS_ERR_RSV = -1

@@ -41,9 +41,6 @@ namespace fwsk {
 #ifndef FWS_SCAN_NT
 #define FWS_SCAN_NT 0
 #endif
-#ifndef FWS_SCAN_SEL
-#define FWS_SCAN_SEL 0                        // A/B: lean_parse_sel (no branches) for the node parse
-#endif
 constexpr bool kScanNT = FWS_SCAN_NT != 0;   // nontemporal stream loads
 constexpr uint32_t kSets = 2;                // tiles in flight per wavefront (register sets; 3 sets
                                              //   at 6 waves per SIMD measured slower)
@@ -261,11 +258,7 @@ __global__ __launch_bounds__(kScanThreads) __attribute__((amdgpu_waves_per_eu(8,
                     window16(wl, wh, p & 15u, d);
                     uint64_t plen = 0;
                     uint32_t key = 0;
-#if FWS_SCAN_SEL
-                    const int r = act ? lean_parse_sel(d, rem - p, plen, key) : -1;   // (p < rem)
-#else
                     const int r = act ? lean_parse(d, rem - p, plen, key) : -1;   // (p < rem)
-#endif
                     uint32_t ptr = kDeadLane;
                     if (r == 0) {
                         ptr = lane;                            // incomplete header at the stream end

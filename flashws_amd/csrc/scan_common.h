@@ -154,28 +154,6 @@ __device__ __forceinline__ int lean_parse(const uint32_t d[4], Avail avail, uint
     return avail < 14 ? 0 : 14;
 }
 
-// lean_parse without branches (the three length forms computed side by side and
-// selected): on random payload a wave's candidates take every form, so the
-// branchy form runs all three bodies under exec masks anyway. Same results.
-__device__ __forceinline__ int lean_parse_sel(const uint32_t d[4], uint32_t avail, uint64_t &plen, uint32_t &key) {
-    const uint32_t len7 = (d[0] >> 8) & 127u;
-    const bool f16 = len7 == 126u, f64 = len7 == 127u;
-    const uint32_t n = f64 ? 14u : (f16 ? 8u : 6u);
-    const uint32_t a2 = __builtin_amdgcn_alignbyte(d[1], d[0], 2u);          // bytes 2..5
-    const uint32_t a6 = __builtin_amdgcn_alignbyte(d[2], d[1], 2u);          // bytes 6..9
-    const uint32_t a10 = __builtin_amdgcn_alignbyte(d[3], d[2], 2u);         // bytes 10..13
-    const uint32_t l16 = ((d[0] >> 8) & 0xFF00u) | (d[0] >> 24);
-    const uint32_t hi = __builtin_bswap32(a2);
-    plen = f64 ? ((uint64_t(hi) << 32) | __builtin_bswap32(a6)) : (uint64_t)(f16 ? l16 : len7);
-    key = f64 ? a10 : (f16 ? d[1] : a2);
-    // :443-445 / :476-482 / :483-492 / :493-498 / :508-511, in that order: every
-    // form is incomplete below its own header length, except that a 64-bit
-    // length over 2^32 is refused once its 10 length bytes are there
-    const bool huge = f64 && plen > (1ull << 32);
-    const uint32_t nmin = f64 ? 10u : n;
-    return avail < nmin ? 0 : (huge ? FWS_ERR_TOO_LARGE : (avail < n ? 0 : (int)n));
-}
-
 // LDS of one dense_tile() wavefront. Tiles with <= kWCap candidates use
 // nodes[] as pos[kWCap] | nval[kWCap]; denser ones as nval[kTile].
 struct ScanWaveLds {

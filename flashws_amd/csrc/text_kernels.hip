@@ -226,14 +226,11 @@ __device__ __forceinline__ uint32_t lds_search(const uint64_t *base, uint32_t n,
     return lo;
 }
 
-// Requires dst 16-B aligned and 1 <= n <= kGatherLdsMax. 7 waves per SIMD
-// (72 VGPRs; the 2 spilled ones live only on the probe path of units past the
-// 64th per wave); the compiler's own choice is 74 VGPRs, 6 waves.
-#ifndef FWS_GATHER_WPE
-#define FWS_GATHER_WPE 7
-#endif
+// Requires dst 16-B aligned and 1 <= n <= kGatherLdsMax. 74 VGPRs, 6 waves per
+// SIMD; forced to 7 (72 VGPRs, 2 spilled on the probe path only) it measured
+// 0.096-0.101 against 0.085-0.089 ms on C4 (profiles/r04/ab_gather_shapes.jsonl).
 template <uint32_t kT>
-__global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(FWS_GATHER_WPE))) void k_gather_one(uint8_t *__restrict__ dst, const uint8_t *__restrict__ src,
+__global__ __launch_bounds__(kT) void k_gather_one(uint8_t *__restrict__ dst, const uint8_t *__restrict__ src,
                                                    const fws_frame_desc *__restrict__ d, uint32_t n) {
     constexpr uint32_t kGatherPer = kGatherLdsMax / kT;   // regions per thread in the block scan
     __shared__ uint64_t s_base[kGatherLdsMax + 1];
@@ -394,10 +391,16 @@ int fws_launch_utf8_descs(const uint8_t *base, const fws_frame_desc *descs, uint
 // leave a static tail (1 x resident: 0.095 ms on C4), more repeat the prefix
 // build (one unit per wave: 0.098 ms); 4 x: 0.0865 ms
 // (profiles/r04/ab_gather.jsonl). Fewer for a small reservation.
-static int g_gather_threads = 256, g_gather_mult = 4;   // tuning hook: k_gather_one shape
+// k_gather_one's shape: 512 threads (one prefix build per 8 waves) and 4 x the
+// resident workgroups; on C4 0.0850-0.0852 ms against 0.0864-0.0892 ms for
+// 256 threads x 4 and 0.0888-0.0897 for plan + k_gather_fast, in one process
+// (profiles/r04/ab_gather_shapes.jsonl; on a 64 MiB message 256 threads is
+// ~1 us faster). Tuning hook below.
+static int g_gather_threads = 512, g_gather_mult = 4;
+// threads 256 or 512 (0: the default), mult > 0 (0: the default)
 extern "C" __attribute__((visibility("default"))) int fws_internal_set_gather_shape(int threads, int mult) {
-    if (threads != 256 && threads != 512) return FWS_ERR_INVALID;
-    g_gather_threads = threads;
+    if (threads != 0 && threads != 256 && threads != 512) return FWS_ERR_INVALID;
+    g_gather_threads = threads ? threads : 512;
     g_gather_mult = mult > 0 ? mult : 4;
     return 0;
 }

@@ -93,14 +93,17 @@ def test_gather_one_small_context(cuda, gather_mode):
     c.close()
 
 
+@pytest.mark.parametrize("threads", [256, 512])
 @pytest.mark.parametrize("blocks", [1, 3, 0])
 @pytest.mark.parametrize("shape", ["c4_like", "small_2000", "exactly_2048"])
-def test_gather_one_grid_sizes(ctx, cuda, shape, blocks):
-    """The one-launch gather at a forced grid (fws_internal_set_gather_blocks):
-    1 and 3 workgroups leave hundreds of units per wave (past the 64 found up
-    front, one per lane: the per-unit probe path), 0 the default 4 x resident."""
+def test_gather_one_grid_sizes(ctx, cuda, shape, blocks, threads):
+    """The one-launch gather at a forced grid (fws_internal_set_gather_blocks)
+    and workgroup size (fws_internal_set_gather_shape): 1 and 3 workgroups
+    leave hundreds of units per wave (past the 64 found up front, one per
+    lane: the per-unit probe path), 0 the default 4 x resident."""
     L = _lib.lib()
     old_one, old_blocks = L.fws_internal_set_gather_one(1), L.fws_internal_set_gather_blocks(blocks)
+    assert L.fws_internal_set_gather_shape(threads, 0) == 0
     try:
         rng = np.random.default_rng(7 + blocks)
         host, regions = _regions(shape, rng)
@@ -120,3 +123,4 @@ def test_gather_one_grid_sizes(ctx, cuda, shape, blocks):
     finally:
         L.fws_internal_set_gather_one(old_one)
         L.fws_internal_set_gather_blocks(old_blocks)
+        L.fws_internal_set_gather_shape(0, 0)

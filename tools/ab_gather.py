@@ -47,7 +47,7 @@ def main():
                 if mode > 1:
                     L.fws_internal_set_gather_shape(mode, blocks)
                 else:
-                    L.fws_internal_set_gather_shape(256, 4)
+                    L.fws_internal_set_gather_shape(0, 0)       # the library's default shape
                 for i in range(4):
                     gpu.unmask_gather(c, dsts[i % 4], src, dd, len(d))
                 torch.cuda.synchronize()
@@ -63,7 +63,7 @@ def main():
                                   "ms": round(ms, 4), "GiB_per_s": round(total / ms / 1e-3 / 2**30, 1)}), flush=True)
             assert torch.equal(outs[0], outs[1])
         L.fws_internal_set_gather_one(1)
-        L.fws_internal_set_gather_shape(256, 4)
+        L.fws_internal_set_gather_shape(0, 0)
         c.close()
         del src, dsts
 

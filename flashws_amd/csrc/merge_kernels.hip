@@ -68,6 +68,9 @@ constexpr int kMWaves = kMThreads / 64;
 constexpr uint32_t kPer = kStCap / kMThreads;       // survivors per thread: i = kPer * tid + j
 constexpr uint32_t kWaveJump = 512;                 // k_merge: one wavefront pointer-jumps up to this many
 constexpr uint32_t kTailRun = 16;                   // EXIT tails of one super tile in its own tail-list run
+#ifndef FWS_LAND_WAVE
+#define FWS_LAND_WAVE 1                               // A/B: 0 = one thread per tail, stage slots only
+#endif
 constexpr uint32_t kLandCap = 256;                  // k_merge: EXIT tails whose landing survivor it looks up
 constexpr uint32_t kTailCapMax = 1u << 18;          // LDS bitmap of the path pruning
 constexpr uint32_t kCompCap = 32768;                // tails that are some tail's next (+ the root's)
@@ -725,7 +728,35 @@ __global__ __launch_bounds__(kMThreads) void k_merge(MergeParams P) {
     // is left to k_link (kNone), and so is every tail of a stream with dense
     // tiles (another k_merge workgroup may be rewriting a tile's count and
     // spill offset while this one reads them)
-    if (tid >= 64 && tid - 64 < L.n_tail && tid - 64 < kLandCap) {
+    if (FWS_LAND_WAVE && L.n_tail < kMThreads / 64u) {
+        // few tails (every dense-frame super tile): one wavefront per tail, so a
+        // spilled exit tile (more than 8 survivors: frames under ~250 B) is
+        // searched too -- its lanes read the spill run's offsets, one ballot --
+        // instead of k_link's binary search over it (a chain of dependent loads)
+        const uint32_t wv = tid >> 6, ln = tid & 63u;
+        if (wv >= 1u && wv - 1u < L.n_tail) {
+            const uint32_t k = wv - 1u;
+            uint32_t w = kNone;
+            if (!no_land) {
+                const uint64_t x = L.texit[k];
+                const uint32_t t = (uint32_t)(x / kTile);
+                const uint32_t tc = P.tile_count[t], tsp = P.tile_spill[t];
+                uint64_t o = ln < kSlots ? P.stage_info[t * kSlots + ln].hdr_off : ~0ull;   // with the counts
+                uint32_t id = t * kSlots + ln;
+                bool ok = true;
+                if (tsp != kNone) {                  // wave-uniform
+                    ok = tc <= 64u;
+                    id = P.spill_base + tsp + ln;
+                    o = ok && ln < tc ? P.spill_info[tsp + ln].hdr_off : ~0ull;
+                } else if (ln >= tc) {
+                    o = ~0ull;
+                }
+                const uint64_t m = __ballot(o == x);
+                if (ok) w = m ? (uint32_t)__builtin_amdgcn_readlane((int)id, (int)__builtin_ctzll(m)) : kTermDead;
+            }
+            if (ln == 0) L.tland[k] = w;
+        }
+    } else if (tid >= 64 && tid - 64 < L.n_tail && tid - 64 < kLandCap) {
         const uint32_t k = tid - 64;
         uint32_t w = kNone;                          // every looked-up slot is written (kNone: k_link's)
         if (!no_land) {

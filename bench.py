@@ -47,6 +47,7 @@ DENSE_FRAMES, DENSE_PAYLOAD = 200000, 64   # SURVEY §6 dense small-frame worklo
 # the next 10 (tools/c5_warmup_probe.py, profiles/r03/c5_warmup.txt)
 EXTRA_WARMUP = 10
 ENGINE_JOBS = 16               # batches per fws_decode_engine run (distinct buffers)
+EXTRA_WARM_S = 0.05            # and at least this long (s) of untimed calls before each extra config
 
 
 def parse():
@@ -624,11 +625,21 @@ def _step_roofline(alg_bytes, t, basis):
             "frac": round(a / HBM_PEAK_GBS, 4), "basis": basis, "alg_bytes_per_step": int(alg_bytes)}
 
 
-def _time(fn, steps, stream, warmup=1):
+def _time(fn, steps, stream, warmup=1, warm_s=EXTRA_WARM_S):
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    for i in range(warmup):
-        fn(i)
-    torch.cuda.synchronize()
+    # untimed calls in rounds of max(2, warmup) until both `warmup` calls and warm_s
+    # seconds have passed: a config whose timed region lasts a few ms otherwise runs
+    # on clocks still ramping up after the host-side setup before it (C4 measured
+    # 0.088 ms over its first 110 calls, 0.085 after; tools/c4_thermal_probe.py)
+    i = 0
+    t0 = time.perf_counter()
+    while True:
+        for _ in range(max(2, warmup)):
+            fn(i)
+            i += 1
+        torch.cuda.synchronize()
+        if i >= warmup and time.perf_counter() - t0 >= warm_s:
+            break
     ev0.record(stream)
     for i in range(steps):
         fn(i)

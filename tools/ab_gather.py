@@ -40,7 +40,7 @@ def main():
         L.fws_internal_gather_one_grid.argtypes = [ctypes.c_uint64]
         print(json.dumps({"cfg": name, "default_grid": L.fws_internal_gather_one_grid(len(w))}), flush=True)
         for rep in range(3):
-            for mode, blocks in ((0, 0), (1, 0), (256, 3), (256, 5), (512, 2), (512, 3), (512, 4)):
+            for mode, blocks in ((0, 0), (1, 0), (512, 5), (512, 6), (512, 8), (512, 4)):
                 # mode 0: plan + k_gather_fast; 1: k_gather_one default; 256 / 512: k_gather_one with that
                 # many threads per workgroup and `blocks` x the resident workgroups
                 L.fws_internal_set_gather_one(1 if mode else 0)

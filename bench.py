@@ -655,9 +655,14 @@ def batch_extra(ctx, bufs, dd, n, payload_bytes, args, stream):
     t = _time(lambda i: gpu.unmask_batch(ctx, bufs[i % args.nbuf], dd, n), steps, stream, warmup=EXTRA_WARMUP)
     gpu.unmask_plan(ctx, bufs[0], dd, n)
     tk = _time(lambda i: gpu.unmask_run(ctx, bufs[i % args.nbuf], dd, n), steps, stream, warmup=EXTRA_WARMUP)
+    # the same regions with the descriptor array permuted (planned in chunk space)
+    perm = torch.from_numpy(np.random.default_rng(5).permutation(n)).to(dd.device)
+    dp = dd.view(n, -1)[perm].reshape(-1).contiguous()
+    tp = _time(lambda i: gpu.unmask_batch(ctx, bufs[i % args.nbuf], dp, n), steps, stream, warmup=EXTRA_WARMUP)
     return {"GiB_per_s": round(payload_bytes / t / GIB, 1), "ms_per_step": round(t * 1e3, 4),
-            "k_unmask_desc_us": round(tk * 1e6, 2),
-            "path": "fws_gpu_unmask_batch: k_plan + k_unmask_desc (descriptors in any order)"}
+            "k_unmask_desc_us": round(tk * 1e6, 2), "permuted_ms_per_step": round(tp * 1e3, 4),
+            "path": "fws_gpu_unmask_batch: k_plan + k_unmask_desc (descriptors in any order; permuted_ms_per_step: "
+                    "the same batch with its descriptor array shuffled)"}
 
 
 def stream_decode_extra(ctx, wire_c2, dev, args):

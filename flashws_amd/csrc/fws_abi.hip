@@ -117,6 +117,8 @@ void fws_gpu_ctx_destroy(fws_gpu_ctx *ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     free_plan(ctx->plan);
+    dev_free(ctx->any_q);
+    dev_free(ctx->any_cnt);
     fws_decode_ws &d = ctx->dec;
     dev_free(d.tile_count);
     dev_free(d.cnt_base);
@@ -186,10 +188,50 @@ int fws_gpu_unmask_run(fws_gpu_ctx *ctx, void *dev_base, const fws_frame_desc *d
 
 int fws_gpu_unmask_batch(fws_gpu_ctx *ctx, void *dev_base, const fws_frame_desc *dev_descs,
                          uint32_t n, void *stream) {
+    if (fws_unmask_any_on()) {
+        // one launch, descriptor-major (+ the queued pieces of regions over 64 KiB):
+        // no plan; the same arguments and capacity checks as the planned form
+        if (!ctx || (n && (!dev_base || !dev_descs))) return FWS_ERR_INVALID;
+        if (n == 0) return 0;
+        if (ctx->cap_stream == 0 || n > ctx->cap_frames) return FWS_ERR_CAPACITY;
+        int r;
+        if ((r = fws_hip_status(hipSetDevice(ctx->device))) || (r = fws_ctx_ensure_any(ctx))) return r;
+        const uint32_t k = ctx->any_parity;
+        ctx->any_parity ^= 1u;
+        const uint32_t pg = ctx->any_qcap / 4u + 1u;
+        return fws_launch_unmask_any((uint8_t *)dev_base, dev_descs, n, ctx->any_q, ctx->any_qcap, ctx->any_cnt + k,
+                                     ctx->any_cnt + (k ^ 1u), pg < 2048u ? pg : 2048u, (hipStream_t)stream);
+    }
     int r = fws_gpu_unmask_plan(ctx, dev_base, dev_descs, n, stream);
     if (r) return r;
     return fws_gpu_unmask_run(ctx, dev_base, dev_descs, n, stream);
 }
+
+}  // extern "C"
+
+int fws_ctx_ensure_any(fws_gpu_ctx *ctx) {
+    // pieces come from regions over 64 KiB: at most the reserved span / 64 KiB of
+    // them (a batch past the reservation has its waves do their own pieces)
+    const uint64_t want = ctx->cap_stream / (64u * 1024u) + 64u;
+    const uint32_t cap = (uint32_t)(want < 0x7FFFFFFFull ? want : 0x7FFFFFFFull);
+    if (ctx->any_q && ctx->any_qcap >= cap) return 0;
+    hipError_t e = hipSuccess;
+    if (ctx->any_q) {
+        if ((e = hipDeviceSynchronize()) != hipSuccess) return fws_hip_status(e);   // (a regrowth: rare)
+        (void)hipFree(ctx->any_q);
+        ctx->any_q = nullptr;
+    }
+    if (!ctx->any_cnt) {
+        if ((e = hipMalloc((void **)&ctx->any_cnt, 2 * sizeof(uint32_t))) != hipSuccess) return fws_hip_status(e);
+        if ((e = hipMemset(ctx->any_cnt, 0, 2 * sizeof(uint32_t))) != hipSuccess) return fws_hip_status(e);
+        ctx->any_parity = 0;
+    }
+    if ((e = hipMalloc((void **)&ctx->any_q, (uint64_t)cap * sizeof(uint64_t))) != hipSuccess) return fws_hip_status(e);
+    ctx->any_qcap = cap;
+    return 0;
+}
+
+extern "C" {
 
 int fws_gpu_check_sorted(fws_gpu_ctx *ctx, const fws_frame_desc *dev_descs, uint32_t n, uint32_t *dev_bad,
                          void *stream) {

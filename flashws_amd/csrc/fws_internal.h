@@ -158,8 +158,13 @@ struct fws_gpu_ctx {
     void *pinned = nullptr;           // host staging for small readbacks
     uint32_t *seam = nullptr;         // fws_gpu_unmask_sorted_utf8: first / last unmasked dword per unit
     uint64_t seam_cap = 0;            // words
+    uint64_t *any_q = nullptr;        // fws_gpu_unmask_batch (one launch): queued pieces of long regions
+    uint32_t *any_cnt = nullptr;      // 2 words: queue counts by call parity
+    uint32_t any_qcap = 0;
+    uint32_t any_parity = 0;
 };
 int fws_ctx_ensure_seam(fws_gpu_ctx *ctx, uint64_t span);
+int fws_ctx_ensure_any(fws_gpu_ctx *ctx);             // the piece queue, sized from the reservation
 
 int fws_ctx_ensure_plan(fws_gpu_ctx *ctx, uint64_t frames, uint64_t units);
 
@@ -170,6 +175,11 @@ int fws_launch_plan(const uint8_t *base, const fws_frame_desc *d, uint32_t n, co
                     fws_plan_ws &ws, hipStream_t s);
 int fws_launch_unmask(uint8_t *base, const fws_frame_desc *d, uint32_t n, const uint32_t *n_dev,
                       const fws_plan_ws &ws, uint64_t max_chunks, hipStream_t s);
+// fws_gpu_unmask_batch in one launch (descriptor-major) + the queued pieces of
+// regions over 64 KiB; qcnt / qnext: this call's and the next call's count
+bool fws_unmask_any_on();
+int fws_launch_unmask_any(uint8_t *base, const fws_frame_desc *d, uint32_t n, uint64_t *queue, uint32_t qcap,
+                          uint32_t *qcnt, uint32_t *qnext, uint32_t piece_grid, hipStream_t s);
 int fws_launch_unmask_sorted(uint8_t *base, const fws_frame_desc *d, uint32_t n, uint64_t max_span,
                              hipStream_t s);
 // *bad = the first index breaking the sorted / disjoint contract, or ~0 (device word)

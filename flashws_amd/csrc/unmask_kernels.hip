@@ -174,6 +174,12 @@ __global__ __launch_bounds__(kBlock) void k_plan(const uint8_t *base, const fws_
     }
     if (cue > cap) cue = cap;                         // contract violation guard, never OOB
     if (bue > cap) bue = cap;
+    // byte space is used only for a sorted batch: once a block (or one before
+    // it) is out of order its records would be dead writes -- and a permuted
+    // batch's runs [po_f, po_{f+1}) span a third of the batch each (C2
+    // permuted: 1.43 ms of record writes before this, one 4096-frame block
+    // unsorted is enough to know)
+    if (!all_sorted) bue = bu;
     if (cue < cu) cue = cu;
     if (bue < bu) bue = bu;
     wave_fill_runs(a.unit_first, cu, (uint32_t)(cue - cu), (uint32_t)f, lane);
@@ -1298,6 +1304,121 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FWS_UTF8
     else unmask_sorted_body<kNT, false, true>(base, d, n, ok, seam, seam_units);
 }
 
+// ------------------------------------------------------------ one launch, any order
+// fws_gpu_unmask_batch without its plan launch: descriptor-major. One wavefront
+// per region (grid-stride); the region's aligned 16-B chunks inside it are
+// XORed whole (loads of 4 steps of 64 lanes issued before their stores), the
+// partial chunks at its ends byte by byte (a chunk shared with a neighbouring
+// region or piece is written only at this region's bytes, so regions in any
+// order never race). A region longer than kAnyPiece is cut: the wave unmasks
+// the first piece and queues the others (region index | piece << 32) for
+// k_unmask_pieces, which the host launches after it; the queue count runs on
+// two words by call parity (this call's, zeroed by the previous call's
+// k_unmask_any; the next call's, zeroed here). When the queue is full the wave
+// does the pieces itself.
+constexpr uint64_t kAnyPiece = 64u * 1024u;
+constexpr uint64_t kAnyEmpty = ~0ull;                // a queue slot no piece took
+
+// Bytes [lo, hi) of region (po, key, phase), lo < hi, hi - lo <= kAnyPiece:
+// every 16-B chunk meeting them is loaded in one batch (a partial chunk's other
+// bytes are only read), XORed with the key at its phase, and stored whole or,
+// for a partial chunk, byte by byte at this range's bytes only.
+template <bool kNT>
+__device__ __forceinline__ void unmask_range(uintptr_t po, uint32_t key, uint32_t phase, uintptr_t lo, uintptr_t hi,
+                                             int lane) {
+    // 5 steps of 64 chunks per round: a 4 KiB region off the 16-B grid (257
+    // chunks, the C2 shape) takes one round, so no load waits for a store
+    constexpr int kSteps = 5;
+    const uintptr_t c0 = lo & ~uintptr_t(15);
+    for (uintptr_t cs = c0; cs < hi; cs += (uintptr_t)kSteps * 1024u) {
+        u32x4 v[kSteps];
+#pragma unroll
+        for (int j = 0; j < kSteps; ++j) {
+            const uintptr_t c = cs + (uintptr_t)j * 1024u + (uintptr_t)lane * 16u;
+            if (c < hi) v[j] = gload16<kNT>(c);
+        }
+        // the whole chunks first, with no variable-count branch between their
+        // stores (the compiler then waits for no store before the next one)
+        uint32_t part = 0;
+#pragma unroll
+        for (int j = 0; j < kSteps; ++j) {
+            const uintptr_t c = cs + (uintptr_t)j * 1024u + (uintptr_t)lane * 16u;
+            const uint32_t rk = rotr32(key, 8u * ((uint32_t)(c - po + phase) & 3u));
+            v[j] = v[j] ^ u32x4{rk, rk, rk, rk};
+            if (c >= lo && c + 16u <= hi) gstore16<kNT>(c, v[j]);
+            else if (c < hi) part |= 1u << j;
+        }
+        // the range's partial chunks (at most its first and last), byte stores
+        if (__builtin_expect(part != 0, 0)) {
+#pragma unroll
+            for (int j = 0; j < kSteps; ++j) {
+                if (!((part >> j) & 1u)) continue;
+                const uintptr_t c = cs + (uintptr_t)j * 1024u + (uintptr_t)lane * 16u;
+                const uint32_t w[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
+#pragma unroll
+                for (int t = 0; t < 16; ++t)
+                    if (c + (uintptr_t)t >= lo && c + (uintptr_t)t < hi)
+                        *(uint8_t *)(c + (uintptr_t)t) = (uint8_t)(w[t >> 2] >> (8 * (t & 3)));
+            }
+        }
+    }
+}
+
+template <bool kNT>
+__global__ __launch_bounds__(kBlock) void k_unmask_any(uint8_t *base, const fws_frame_desc *__restrict__ d, uint32_t n,
+                                                       uint64_t *__restrict__ queue, uint32_t qcap,
+                                                       uint32_t *__restrict__ qcnt, uint32_t *__restrict__ qnext) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) *qnext = 0u;   // the next call's count (its pieces kernel is done)
+    const int lane = threadIdx.x & (kWave - 1);
+    const uint32_t nw = gridDim.x * (kBlock / kWave);
+    const uintptr_t b0 = (uintptr_t)base;
+    for (uint32_t i = blockIdx.x * (kBlock / kWave) + __builtin_amdgcn_readfirstlane(threadIdx.x / kWave); i < n; i += nw) {
+        const fws_frame_desc fd = d[i];
+        if (fd.payload_len == 0) continue;
+        const uintptr_t po = b0 + fd.payload_off, pe = po + fd.payload_len;
+        const uint32_t ph = fd.phase & 3u;
+        if (fd.payload_len <= kAnyPiece) {
+            unmask_range<kNT>(po, fd.key, ph, po, pe, lane);
+            continue;
+        }
+        const uint64_t np = (fd.payload_len + kAnyPiece - 1u) / kAnyPiece;   // pieces 1 .. np - 1 queued
+        uint32_t at = 0;
+        if (lane == 0) at = atomicAdd(qcnt, (uint32_t)(np - 1u));
+        at = __shfl(at, 0, 64);
+        const bool queued = (uint64_t)at + (np - 1u) <= qcap;
+        // (a refused reservation blanks the slots of it that lie below qcap: the
+        // pieces kernel reads up to qcap entries of a count that includes them)
+        for (uint64_t k = 1u + (uint64_t)lane; k < np; k += kWave)
+            if ((uint64_t)at + k - 1u < qcap) queue[at + k - 1u] = queued ? (uint64_t)i | (k << 32) : kAnyEmpty;
+        const uint64_t kend = queued ? 1u : np;       // queue full: every piece here
+        for (uint64_t k = 0; k < kend; ++k) {
+            const uintptr_t lo = po + k * kAnyPiece, hi = lo + kAnyPiece < pe ? lo + kAnyPiece : pe;
+            unmask_range<kNT>(po, fd.key, ph, lo, hi, lane);
+        }
+    }
+}
+
+// The queued pieces of this call (count: *qcnt, at most qcap of them listed).
+template <bool kNT>
+__global__ __launch_bounds__(kBlock) void k_unmask_pieces(uint8_t *base, const fws_frame_desc *__restrict__ d,
+                                                          const uint64_t *__restrict__ queue, uint32_t qcap,
+                                                          const uint32_t *__restrict__ qcnt) {
+    uint32_t cnt = *qcnt;
+    if (cnt > qcap) cnt = qcap;                      // (an overflowing wave did its own pieces)
+    const int lane = threadIdx.x & (kWave - 1);
+    const uint32_t nw = gridDim.x * (kBlock / kWave);
+    const uintptr_t b0 = (uintptr_t)base;
+    for (uint32_t e = blockIdx.x * (kBlock / kWave) + __builtin_amdgcn_readfirstlane(threadIdx.x / kWave); e < cnt; e += nw) {
+        const uint64_t q = queue[e];
+        if (q == kAnyEmpty) continue;
+        const fws_frame_desc fd = d[(uint32_t)q];
+        const uint64_t k = q >> 32;
+        const uintptr_t po = b0 + fd.payload_off, pe = po + fd.payload_len;
+        const uintptr_t lo = po + k * kAnyPiece, hi = lo + kAnyPiece < pe ? lo + kAnyPiece : pe;
+        unmask_range<kNT>(po, fd.key, fd.phase & 3u, lo, hi, lane);
+    }
+}
+
 }  // namespace fwsk
 
 // ---------------------------------------------------------------- launchers
@@ -1465,5 +1586,28 @@ int fws_launch_unmask(uint8_t *base, const fws_frame_desc *d, uint32_t n, const 
     const uint64_t units = (max_chunks + kUnitChunks - 1) / kUnitChunks;
     hipLaunchKernelGGL(k_unmask_desc<true>, dim3(grid_for_units(units)), dim3(kBlock), 0, s, base, d, n, ws.cbase,
                        ws.unit_first, (const u32x4 *)ws.unit_rec, ws.total, (const fws_plan_mode *)ws.mode, ws.unit_cap);
+    return fws_hip_status(hipGetLastError());
+}
+
+// tuning hook: fws_gpu_unmask_batch as k_unmask_any + k_unmask_pieces (1) or
+// k_plan + k_unmask_desc (0, the default: sorted C2 0.0906 ms against 0.1058,
+// permuted C2 0.142 against 0.123 -- DESIGN.md §4.3b)
+static int g_unmask_any = 0;
+extern "C" __attribute__((visibility("default"))) int fws_internal_set_unmask_any(int on) {
+    const int old = g_unmask_any;
+    g_unmask_any = on != 0;
+    return old;
+}
+bool fws_unmask_any_on() { return g_unmask_any != 0; }
+
+int fws_launch_unmask_any(uint8_t *base, const fws_frame_desc *d, uint32_t n, uint64_t *queue, uint32_t qcap,
+                          uint32_t *qcnt, uint32_t *qnext, uint32_t piece_grid, hipStream_t s) {
+    if (n == 0) return 0;
+    uint64_t blocks = (n + (kBlock / kWave) - 1) / (kBlock / kWave);
+    if (blocks > (1u << 20)) blocks = 1u << 20;      // grid-stride past it
+    hipLaunchKernelGGL(k_unmask_any<true>, dim3((unsigned)blocks), dim3(kBlock), 0, s, base, d, n, queue, qcap, qcnt,
+                       qnext);
+    hipLaunchKernelGGL(k_unmask_pieces<true>, dim3(piece_grid ? piece_grid : 1u), dim3(kBlock), 0, s, base, d, queue,
+                       qcap, qcnt);
     return fws_hip_status(hipGetLastError());
 }

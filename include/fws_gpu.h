@@ -116,7 +116,8 @@ int fws_gpu_mask(void *dev_ptr, uint64_t n, uint32_t key, void *stream);
  * share a 16-byte aligned chunk with payload bytes, between the batch's first
  * and last payload byte, are written back with their own value (no other
  * writer may change them during the call); bytes outside that span are never
- * written. */
+ * written. A permuted batch is planned in chunk space (C2 permuted: 0.142 ms
+ * against 0.091 sorted). */
 int fws_gpu_unmask_batch(fws_gpu_ctx *ctx, void *dev_base, const fws_frame_desc *dev_descs,
                          uint32_t n, void *stream);
 

@@ -7,7 +7,7 @@ import pytest
 import torch
 
 import orc
-from flashws_amd import gpu
+from flashws_amd import _lib, gpu
 
 pytestmark = pytest.mark.gpu
 
@@ -27,6 +27,25 @@ def oracle_unmask_regions(buf, descs):
         key = orc.orc().orc_rotr32(k, 8 * ph)   # phase == RotateR(key, 8*phase) (w_socket.h:758)
         orc.orc_mask("ws_mask_fast", out, key, o, n)
     return out
+
+
+@pytest.fixture(params=["any", "plan"])
+def batch_path(request):
+    """fws_gpu_unmask_batch's two forms: one launch, descriptor-major
+    (k_unmask_any + queued pieces, the default) and k_plan + k_unmask_desc."""
+    L = _lib.lib()
+    old = L.fws_internal_set_unmask_any(1 if request.param == "any" else 0)
+    yield request.param
+    L.fws_internal_set_unmask_any(old)
+
+
+@pytest.fixture
+def planned():
+    """The planned form only (the tests that read the plan's mode)."""
+    L = _lib.lib()
+    old = L.fws_internal_set_unmask_any(0)
+    yield
+    L.fws_internal_set_unmask_any(old)
 
 
 def run_batch(ctx, host, descs, cuda):
@@ -56,7 +75,7 @@ def test_mask_single_sweep(cuda):
                 assert np.array_equal(got, exp), (hex(key), off, n)
 
 
-def test_unmask_batch_alignment_sweep(ctx, cuda):
+def test_unmask_batch_alignment_sweep(ctx, cuda, batch_path):
     """One batch: every (offset mod 64, len 0..600, phase) region, packed with gaps."""
     rng = np.random.default_rng(2)
     regions = []
@@ -76,7 +95,7 @@ def test_unmask_batch_alignment_sweep(ctx, cuda):
     assert np.array_equal(got, exp)
 
 
-def test_unmask_batch_adjacent_regions(ctx, cuda):
+def test_unmask_batch_adjacent_regions(ctx, cuda, batch_path):
     """Regions sharing 16-B chunks (1..15-byte gaps and zero gaps)."""
     rng = np.random.default_rng(3)
     regions, pos = [], 3
@@ -92,7 +111,7 @@ def test_unmask_batch_adjacent_regions(ctx, cuda):
 
 
 @pytest.mark.parametrize("n_frames", [1, 7, 4096])
-def test_unmask_batch_c2_shape(ctx, cuda, n_frames):
+def test_unmask_batch_c2_shape(ctx, cuda, batch_path, n_frames):
     wire, descs, _ = gpu.config_c2(seed=7, n_frames=n_frames)
     got = run_batch(ctx, wire, descs, cuda)
     exp = wire.copy()
@@ -101,7 +120,7 @@ def test_unmask_batch_c2_shape(ctx, cuda, n_frames):
     assert np.array_equal(got, exp)
 
 
-def test_unmask_batch_c2_full(ctx, cuda):
+def test_unmask_batch_c2_full(ctx, cuda, batch_path):
     """BASELINE config 2 at full size: 65 536 x 4 KiB, seed 42, bit-exact."""
     wire, descs, _ = gpu.config_c2()
     got = run_batch(ctx, wire, descs, cuda)
@@ -111,7 +130,7 @@ def test_unmask_batch_c2_full(ctx, cuda):
     assert np.array_equal(got, exp)
 
 
-def test_unmask_batch_mixed(ctx, cuda):
+def test_unmask_batch_mixed(ctx, cuda, batch_path):
     wire, descs, _ = gpu.config_c3(seed=5, target=16 << 20)
     got = run_batch(ctx, wire, descs, cuda)
     exp = wire.copy()
@@ -120,7 +139,7 @@ def test_unmask_batch_mixed(ctx, cuda):
     assert np.array_equal(got, exp)
 
 
-def test_unmask_batch_involution(ctx, cuda):
+def test_unmask_batch_involution(ctx, cuda, batch_path):
     """Size-independent property at full C2 size: two passes restore the input."""
     wire, descs, _ = gpu.config_c2(seed=11)
     dev = torch.from_numpy(wire).to(cuda)
@@ -143,7 +162,7 @@ def _rand_regions(rng, n, max_len, max_gap, start=5):
 
 
 @pytest.mark.parametrize("permute", [False, True])
-def test_plan_mode_sorted_vs_permuted(ctx, cuda, permute):
+def test_plan_mode_sorted_vs_permuted(ctx, cuda, planned, permute):
     """The same regions sorted take the byte-space run, permuted the chunk-space
     run; both bit-exact (alignment sweep layout, gaps up to 70 B)."""
     rng = np.random.default_rng(21)
@@ -165,7 +184,7 @@ def test_plan_mode_sorted_vs_permuted(ctx, cuda, permute):
 
 @pytest.mark.parametrize("n,max_len,max_gap", [(1, 5, 0), (3, 20, 3), (1023, 64, 2), (1024, 64, 2),
                                                 (1025, 64, 2), (70000, 30, 3), (300000, 12, 1)])
-def test_plan_lookback_many_blocks(ctx, cuda, n, max_len, max_gap):
+def test_plan_lookback_many_blocks(ctx, cuda, planned, n, max_len, max_gap):
     """Frame counts around the 1024-frame plan block and far past it (the
     look-back runs over up to 293 blocks), tiny frames with 0-3-byte gaps."""
     rng = np.random.default_rng(n)
@@ -178,7 +197,7 @@ def test_plan_lookback_many_blocks(ctx, cuda, n, max_len, max_gap):
     assert np.array_equal(got, oracle_unmask_regions(host, descs))
 
 
-def test_plan_large_frames_block_fill(ctx, cuda):
+def test_plan_large_frames_block_fill(ctx, cuda, planned):
     """Frames spanning many 4 KiB units (unit maps filled by the whole block):
     16 MiB + 1 MiB + odd sizes, sorted then permuted."""
     rng = np.random.default_rng(31)
@@ -198,7 +217,7 @@ def test_plan_large_frames_block_fill(ctx, cuda):
         assert np.array_equal(got, oracle_unmask_regions(host, descs)), perm
 
 
-def test_plan_sparse_batch_takes_chunk_space(ctx, cuda):
+def test_plan_sparse_batch_takes_chunk_space(ctx, cuda, planned):
     """Sorted but sparse payloads (64 B every 1 MiB) stay in chunk space."""
     rng = np.random.default_rng(41)
     regions = [(i * (1 << 20) + 3, 64, int(rng.integers(0, 2**32)), 0) for i in range(64)]
@@ -315,7 +334,7 @@ def test_sorted_large_and_sparse(ctx, cuda):
     assert np.array_equal(run_sorted(ctx, host, descs, cuda), oracle_unmask_regions(host, descs))
 
 
-def test_sorted_matches_batch_and_involution(ctx, cuda):
+def test_sorted_matches_batch_and_involution(ctx, cuda, batch_path):
     """Full C2 size: _sorted and _batch agree, and two _sorted passes restore the input."""
     wire, descs, _ = gpu.config_c2(seed=43)
     dev = torch.from_numpy(wire).to(cuda)
@@ -331,7 +350,7 @@ def test_sorted_matches_batch_and_involution(ctx, cuda):
 
 
 @pytest.mark.parametrize("shift", [1, 7, 15])
-def test_batch_unaligned_base(ctx, cuda, shift):
+def test_batch_unaligned_base(ctx, cuda, batch_path, shift):
     """fws_gpu_unmask_batch with dev_base off 16-B alignment and the first
     payload within 15 B of it (the byte-space unit origin lies below the base)."""
     wire, descs, _ = gpu.config_c2(seed=47, n_frames=300)
@@ -415,3 +434,56 @@ def test_check_sorted_debug_mode_refuses(cuda, tmp_path):
 def _lib_invalid():
     from flashws_amd import _lib
     return _lib.FWS_ERR_INVALID
+
+
+# ---- fws_gpu_unmask_batch in one launch: long regions cut into queued pieces ----
+
+@pytest.mark.parametrize("permute", [False, True])
+def test_any_long_regions_pieces(ctx, cuda, permute):
+    """Regions of 64 KiB +- 1 (the piece size), 1 MiB + odd, 16 MiB, mixed with
+    small ones, at odd offsets, sorted and permuted: the first piece by the
+    region's wave, the rest from the queue (k_unmask_pieces)."""
+    L = _lib.lib()
+    old = L.fws_internal_set_unmask_any(1)
+    try:
+        rng = np.random.default_rng(77 + permute)
+        lens = [65535, 65536, 65537, 3, (1 << 20) + 13, 0, 16 << 20, 131072 * 3 + 5, 17, 4096]
+        regions, pos = [], 5
+        for ln in lens:
+            regions.append((pos, ln, int(rng.integers(0, 2**32)), int(rng.integers(0, 4))))
+            pos += ln + int(rng.integers(0, 20))
+        host = aligned_host(pos + 64)
+        host[:] = rng.integers(0, 256, len(host), dtype=np.uint8)
+        descs = np.array(regions, dtype=gpu.FRAME_DESC)
+        if permute:
+            descs = descs[rng.permutation(len(descs))]
+        got = run_batch(ctx, host, descs, cuda)
+        assert np.array_equal(got, oracle_unmask_regions(host, descs))
+    finally:
+        L.fws_internal_set_unmask_any(old)
+
+
+def test_any_queue_overflow(cuda):
+    """A context reserved for 1 MiB (a 80-entry piece queue) unmasking 40 regions
+    of 1-3 MiB (~1,100 pieces): the queue fills and the waves whose pieces do
+    not fit do them themselves. Twice, so the next call's count starts at zero."""
+    L = _lib.lib()
+    old = L.fws_internal_set_unmask_any(1)
+    c = gpu.Ctx(0, max_frames=64, max_stream_bytes=1 << 20)
+    try:
+        rng = np.random.default_rng(91)
+        regions, pos = [], 3
+        for _ in range(40):
+            ln = int(rng.integers(1 << 20, 3 << 20))
+            regions.append((pos, ln, int(rng.integers(0, 2**32)), int(rng.integers(0, 4))))
+            pos += ln + int(rng.integers(0, 9))
+        host = aligned_host(pos + 64)
+        host[:] = rng.integers(0, 256, len(host), dtype=np.uint8)
+        descs = np.array(regions, dtype=gpu.FRAME_DESC)
+        descs = descs[rng.permutation(len(descs))]
+        exp = oracle_unmask_regions(host, descs)
+        for _ in range(2):
+            assert np.array_equal(run_batch(c, host, descs, cuda), exp)
+    finally:
+        c.close()
+        L.fws_internal_set_unmask_any(old)

@@ -84,11 +84,16 @@ def test_sorted_utf8_edge_cases(ctx, cuda, max_pad, shift):
     assert np.array_equal(ok.astype(bool), exp), np.nonzero(ok.astype(bool) != exp)[0][:10]
 
 
-def test_sorted_utf8_long_frames(ctx, cuda):
-    """Frames of 4-40 KiB (fast-kind units, every unit seam inside a frame)."""
-    rng = np.random.default_rng(7)
+@pytest.mark.parametrize("max_pad", [14, 0, 2, 3, 6])
+def test_sorted_utf8_long_frames(ctx, cuda, max_pad):
+    """Frames of 4-40 KiB (fast-kind units, every unit seam inside a frame),
+    0-14 bytes apart, a third of them ending in a truncated sequence (its error
+    falls on the bytes after the frame: the frame's own, not the next's)."""
+    rng = np.random.default_rng(7 + max_pad)
     cases = _cases(rng, 0, 40, (1000, 12000))
-    plain, masked, descs = _layout(rng, cases, 14)
+    for i in range(0, len(cases), 3):                    # truncated sequences right at a frame end
+        cases[i] = cases[i] + [b"\xc3", b"\xe2\x82", b"\xf0\x9f\x98"][i % 3]
+    plain, masked, descs = _layout(rng, cases, max_pad)
     got, ok = _run(ctx, cuda, masked, descs)
     assert np.array_equal(got, plain)
     assert np.array_equal(ok.astype(bool), np.array([_valid(c) for c in cases]))

@@ -8,6 +8,9 @@
 // TEST INFRASTRUCTURE: the GPU test tests/test_gpu_dropin.py runs the built
 // client against the GPU-hooked drop-in server so the client's own HashArr
 // check (test_ws_client.cpp:260-277) sees bytes the MI355X unmasked.
+// With FWS_REFSERVER_GPU_HOOK the same header serves the reference's own echo
+// SERVER (tests/new-ws-echo/test_ws_server.cpp, compiled unchanged from its
+// place, oracle/Makefile `refserver`): see the end of this file.
 #pragma once
 #include <cstddef>
 #include <cstdint>
@@ -48,3 +51,42 @@ inline constexpr const char *log_data_file_path = "./log_data.csv";
 #define ENABLE_NO_DELAY 1
 
 }  // namespace test
+
+#ifdef FWS_REFSERVER_GPU_HOOK
+// The one added line of gpu_floop.hpp's recipe (hook.Enable(ws_socket) before
+// the listening socket goes to the loop), supplied without editing the server:
+// this header is included after flashws.h / ws_server_socket.h / floop.h
+// (test_ws_server.cpp:1-4), so a function-like macro on the name AddSocket
+// touches only the server's own call, ctx.loop.AddSocket(std::move(ws_socket),
+// ...) (test_ws_server.cpp:259), whose first argument passes through
+// fws_amd_refserver::hooked(): GpuRxHook::Enable on the listening socket, then
+// the same rvalue on to AddSocket. SIGTERM (the test's stop) prints the hook's
+// GPU read count and exits.
+#include <csignal>
+#include <cstdio>
+#include <unistd.h>
+#include <utility>
+#include "flashws_amd/gpu_floop.hpp"
+namespace fws_amd_refserver {
+inline fws_amd::GpuRxHookT<test::ENABLE_TLS> *g_hook = nullptr;
+inline void on_term(int) {
+    char b[64];
+    const int k = std::snprintf(b, sizeof b, "gpu_reads %llu\n",
+                                (unsigned long long)(g_hook ? g_hook->gpu_reads() : 0));
+    if (k > 0) (void)!::write(1, b, (size_t)k);
+    ::_exit(0);
+}
+template <class Sock>
+Sock &&hooked(Sock &&listen) {
+    static fws_amd::GpuContext gpu(0);
+    static fws_amd::GpuRxHookT<test::ENABLE_TLS> hook(gpu);
+    g_hook = &hook;
+    hook.Enable(listen);
+    std::signal(SIGTERM, on_term);
+    std::printf("gpu hook enabled\n");
+    std::fflush(stdout);
+    return std::move(listen);
+}
+}  // namespace fws_amd_refserver
+#define AddSocket(sock, ...) AddSocket(::fws_amd_refserver::hooked(sock), __VA_ARGS__)
+#endif

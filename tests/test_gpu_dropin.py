@@ -231,6 +231,44 @@ def test_reference_echo_client_through_gpu_hook(cuda, n_clients, batch, tmp_path
     assert st["gpu"] is True and st["gpu_reads"] > 0 and st["msgs"] == 40000
 
 
+REF_SERVER_GPU = os.path.join(ROOT, "oracle", "_ref", "ws_ref_server_gpu")
+
+
+@pytest.mark.parametrize("n_clients", [1, 8])
+def test_reference_echo_server_unchanged_with_gpu_hook(cuda, n_clients, tmp_path):
+    """Both ends of C1 are the reference's own code: tests/new-ws-echo/
+    test_ws_server.cpp and test_ws_client.cpp, compiled unchanged from their
+    place (oracle/Makefile `refserver` / `refclient`). The server's one hook line
+    (GpuRxHook::Enable on its listening socket) comes from our test_def.h, so
+    every read the server decodes goes through the MI355X; the client's HashArr
+    checks of the echo (test_ws_client.cpp:260-277) pass, and the hook's GPU
+    read count, printed at SIGTERM, is non-zero."""
+    if not os.path.exists(REF_SERVER_GPU):
+        pytest.fail(f"{REF_SERVER_GPU} not built (make -C oracle refserver in the build container)", pytrace=False)
+    exe = REF_CLIENTS[n_clients]
+    p = subprocess.Popen([REF_SERVER_GPU], stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                         cwd=str(tmp_path))
+    try:
+        seen = []
+        for line in p.stdout:
+            seen.append(line)
+            if line.startswith("gpu hook enabled"):
+                break
+        assert seen and seen[-1].startswith("gpu hook enabled"), ("".join(seen)[-2000:], p.poll())
+        r = subprocess.run([exe], capture_output=True, text=True, timeout=120, cwd=str(tmp_path))
+    finally:
+        p.terminate()
+        out, err = p.communicate(timeout=30)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-2000:])
+    data_hash = [ln.split(":")[1].strip() for ln in r.stdout.splitlines() if ln.startswith("data hash:")]
+    checks = [ln.rsplit("hash value:", 1)[1].split(",")[0].strip() for ln in r.stdout.splitlines()
+              if "hash value:" in ln]
+    assert len(data_hash) == 1 and len(checks) == 40000 // 16384, r.stdout[-3000:]
+    assert all(c == data_hash[0] for c in checks)
+    reads = [int(ln.split()[1]) for ln in out.splitlines() if ln.startswith("gpu_reads ")]
+    assert reads and reads[0] > 0, (out[-2000:], err[-2000:])
+
+
 @pytest.mark.parametrize("scenario", ["close_peers", "eof_with_data"])
 @pytest.mark.parametrize("mode", ["gpu", "gpu_batch"])
 def test_dropin_same_step_reads_match_reference(cuda, scenario, mode):

@@ -598,6 +598,40 @@ def c1_echo_extra(device=0):
                 "rc": r.returncode, "msgs": st.get("msgs"), "gpu_reads": st.get("gpu_reads"),
                 "client": "tests/new-ws-echo/test_ws_client.cpp unchanged (oracle/refclient/test_def.h: "
                           "127.0.0.1, 4 KiB, 40000 msgs)"}
+    # both ends the reference's own code: tests/new-ws-echo/test_ws_server.cpp compiled
+    # unchanged, plain (CPU OnRecvData) and with the GPU hook line supplied by our
+    # test_def.h (oracle/Makefile refserver), against the unchanged client
+    for hooked in (False, True):
+        exe = os.path.join(ROOT, "oracle", "_ref", "ws_ref_server_gpu" if hooked else "ws_ref_server")
+        if not (os.path.exists(exe) and os.path.exists(refcli)):
+            continue
+        with tempfile.TemporaryDirectory() as td:
+            p = subprocess.Popen([exe], stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, cwd=td)
+            try:
+                if hooked:                   # the hook line flushes once the socket listens
+                    for ln in p.stdout:
+                        if ln.startswith("gpu hook enabled"):
+                            break
+                else:
+                    time.sleep(1.0)
+                r = subprocess.run([refcli], capture_output=True, text=True, timeout=120, cwd=td)
+            finally:
+                p.terminate()
+                sout, _ = p.communicate(timeout=30)
+        lines = r.stdout.splitlines()
+        dh = [x.split(":")[1].strip() for x in lines if x.startswith("data hash:")]
+        hv = [x.rsplit("hash value:", 1)[1].split(",")[0].strip() for x in lines if "hash value:" in x]
+        gp = [float(x.split(":")[1].split()[0]) for x in lines if x.startswith("avg (rx+tx) goodput")]
+        lat = [x for x in lines if x.startswith("Latency (us)")]
+        gr = [int(x.split()[1]) for x in sout.splitlines() if x.startswith("gpu_reads ")]
+        out[f"reference_server_and_client_1_{'gpu_hook' if hooked else 'reference'}"] = {
+            "goodput_rx_tx_mbps": gp[0] if gp else None,
+            "rtt_us": {"p50": float(lat[0].split("P50:")[1].split(",")[0]) if lat else None,
+                       "p99": float(lat[0].split("P99:")[1].split(",")[0]) if lat else None},
+            "hash_checks_passed": len(hv) if (dh and hv and all(h == dh[0] for h in hv)) else 0,
+            "rc": r.returncode, "gpu_reads": gr[0] if gr else None,
+            "server": "tests/new-ws-echo/test_ws_server.cpp unchanged" + (" + GpuRxHook::Enable via test_def.h"
+                                                                          if hooked else "")}
     return out
 
 

@@ -182,6 +182,23 @@ def test_plan_mode_sorted_vs_permuted(ctx, cuda, planned, permute):
     assert np.array_equal(got, oracle_unmask_regions(host, descs))
 
 
+@pytest.mark.parametrize("where", [10, 2500, 4990], ids=["first_block", "middle", "last_block"])
+def test_plan_partly_sorted(ctx, cuda, planned, where):
+    """Sorted except for one swapped pair in one 1024-frame plan block: the
+    batch is planned in chunk space (k_plan writes byte-space records only while
+    the blocks up to its own are sorted, so some were written before the
+    unsorted block and are never read) and the result is bit-exact."""
+    rng = np.random.default_rng(33 + where)
+    regions, pos = _rand_regions(rng, 5000, 600, 20)
+    regions[where], regions[where + 1] = regions[where + 1], regions[where]
+    host = aligned_host(pos + 64)
+    host[:] = rng.integers(0, 256, len(host), dtype=np.uint8)
+    descs = np.array(regions, dtype=gpu.FRAME_DESC)
+    got = run_batch(ctx, host, descs, cuda)
+    assert gpu.plan_mode(ctx)["byte_space"] == 0
+    assert np.array_equal(got, oracle_unmask_regions(host, descs))
+
+
 @pytest.mark.parametrize("n,max_len,max_gap", [(1, 5, 0), (3, 20, 3), (1023, 64, 2), (1024, 64, 2),
                                                 (1025, 64, 2), (70000, 30, 3), (300000, 12, 1)])
 def test_plan_lookback_many_blocks(ctx, cuda, planned, n, max_len, max_gap):

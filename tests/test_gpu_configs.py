@@ -23,7 +23,7 @@ import numpy as np
 import pytest
 import torch
 
-from flashws_amd import gpu
+from flashws_amd import _lib, gpu
 
 pytestmark = pytest.mark.gpu
 
@@ -85,15 +85,27 @@ def test_decode_stream_full_config(ctx, cuda, name):
 
 
 @pytest.mark.parametrize("name", ["C2", "C3", "C5_16k_frames"])
-@pytest.mark.parametrize("path", ["sorted", "batch"])
+@pytest.mark.parametrize("path", ["sorted", "batch", "batch_permuted", "any_permuted"])
 def test_descriptor_unmask_full_config(ctx, cuda, name, path):
+    """Every descriptor-mode entry point on the full config against the golden
+    digest of the reference-unmasked bytes; `*_permuted`: the descriptor array
+    shuffled (any order is allowed), planned (chunk space) or by the opt-in
+    one-launch form (fws_internal_set_unmask_any)."""
     g, wire, descs, ok = _gen(name)
     dev = torch.from_numpy(wire).to(cuda)
+    if path.endswith("permuted"):
+        descs = descs[np.random.default_rng(9).permutation(len(descs))]
     dd = gpu.descs_to_device(descs, cuda)
     if path == "sorted":
         gpu.unmask_sorted(ctx, dev, dd, len(descs))
     else:
-        gpu.unmask_batch(ctx, dev, dd, len(descs))
+        L = _lib.lib()
+        old = L.fws_internal_set_unmask_any(1 if path == "any_permuted" else 0)
+        try:
+            gpu.unmask_batch(ctx, dev, dd, len(descs))
+            torch.cuda.synchronize()
+        finally:
+            L.fws_internal_set_unmask_any(old)
     assert sha(dev) == g["unmasked_sha256"]
 
 

@@ -48,6 +48,11 @@ DENSE_FRAMES, DENSE_PAYLOAD = 200000, 64   # SURVEY §6 dense small-frame worklo
 EXTRA_WARMUP = 10
 ENGINE_JOBS = 16               # batches per fws_decode_engine run (distinct buffers)
 EXTRA_WARM_S = 0.05            # and at least this long (s) of untimed calls before each extra config
+EXTRA_CONFIGS = ("c2s", "c3", "dense", "c4", "tx", "c5s", "c5d", "e2e", "c1", "batch")
+C5_STREAM_STEPS = 16           # timed C5 stream calls, each on its own freshly masked 4 GiB buffer
+# rocprofv3 kernel stats of each extra config, captured warm (bench.py --only <cfg> under
+# rocprofv3 --kernel-trace --stats; tools/gpu_round.sh prof_extras)
+PROFILE_DIR = "profiles/r05"
 
 
 def parse():
@@ -71,6 +76,9 @@ def parse():
     ap.add_argument("--share-device", action="store_true",
                     help="N > 1 validation on one GPU: every rank on device 0, gloo process group "
                          "(exercises the N-rank path on real HIP; not a scaling measurement)")
+    ap.add_argument("--only", default="",
+                    help="comma list of extra configs to run (c2s,c3,dense,c4,tx,c5s,c5d,e2e,c1,batch): one "
+                         "config per process, e.g. under rocprofv3 (profiles/r05/*_kernel_stats.csv)")
     ap.add_argument("--launcher-selftest", action="store_true",
                     help="CPU only (gloo): exercise the N-rank launch, barrier and max-over-ranks timing on a "
                          "host XOR of each rank's shard; prints a self-test line, not the metric")
@@ -79,7 +87,19 @@ def parse():
         a.extra = a.c5 = True
     if a.no_extra:
         a.extra = a.c5 = False
+    a.only = {x.strip() for x in a.only.split(",") if x.strip()}
+    bad = a.only - set(EXTRA_CONFIGS)
+    if bad:
+        ap.error(f"--only: unknown config(s) {sorted(bad)}; known: {EXTRA_CONFIGS}")
+    if a.only:
+        a.extra = True
+        a.c5 = bool(a.only & {"c5s", "c5d"})
     return a
+
+
+def want(args, name):
+    """extra config `name` runs: every config by default, only the listed ones with --only"""
+    return not args.only or name in args.only
 
 
 def launch_ranks(args):
@@ -138,20 +158,23 @@ def dist_env():
 
 
 def setup_dist(world, local, share_device=False):
-    """One process per GPU; the process group only carries the barriers and the
-    max-over-ranks reduction of the step time (outside the timed region).
-    share_device (validation on a one-GPU box): every rank on device 0 and a
-    gloo group -- RCCL will not put two ranks on one GPU -- so the N-rank path
-    (shard seeds, C5 split, max over ranks) runs on real HIP; its times are
-    contended and not a scaling claim."""
-    if world > 1 and share_device:
-        torch.cuda.set_device(0)
+    """One process per GPU. The data path has no exchange step:
+    the process group only carries the barriers, the max-over-ranks reduction
+    of the step time and the flag check, all outside the timed region and all
+    on CPU tensors, so it is a gloo group and no device collective (RCCL) is
+    initialised at all. share_device (validation on a one-GPU box): every rank
+    on device 0, so the N-rank path (shard seeds, C5 split, max over ranks) runs
+    on real HIP; its times are contended and not a scaling claim."""
+    torch.cuda.set_device(0 if (share_device or world == 1) else local)
+    init_group(world)
+
+
+def init_group(world):
+    """the N > 1 control group: gloo (CPU tensors only; tests/test_dist_cpu.py)"""
+    if world > 1:
         dist.init_process_group(backend="gloo")
-    elif world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(0)
+        return dist.get_backend()
+    return None
 
 
 def barrier(world):
@@ -163,8 +186,7 @@ def max_over_ranks(world, x):
     """Slowest rank's value (the timed region ends when every rank is done)."""
     if world == 1:
         return x
-    dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
-    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    t = torch.tensor([x], dtype=torch.float64)          # CPU tensor on the gloo group
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -414,11 +436,12 @@ def main():
     kern_s = min(ev0.elapsed_time(ev1) / 1e3 / args.steps, own_s)
 
     extra = {}
-    if not args.no_batch_extra and world == 1:
+    if not args.no_batch_extra and world == 1 and want(args, "batch"):
         extra["C2_unmask_batch_any_order"] = batch_extra(ctx, bufs, dd, n, payload_bytes, args, stream)
     if args.extra:
         extra.update(stream_decode_extra(ctx, wire, dev, args)["extra"])
-        extra["C1_echo"] = c1_echo_extra(local)
+        if want(args, "c1"):
+            extra["C1_echo"] = c1_echo_extra(local)
     del bufs
     if world > 1 and not args.no_c5_split:
         extra["C5_batch_split"] = c5_split(args, world, rank, local, dev)
@@ -468,53 +491,58 @@ def c5_split(args, world, rank, local, dev):
     its own 4 GiB of 16 KiB TEXT frames (seed 42 + rank), descriptor mode
     (fws_gpu_unmask_sorted_utf8) and as a raw stream (fws_gpu_decode_stream with
     UTF-8 flags); barrier + synchronize around K steps, slowest rank's time,
-    aggregate = all ranks' payload / that time. Flags are checked against the
-    generator on every rank before timing."""
+    aggregate = all ranks' payload / that time. As in c5_extra, every timed call
+    decodes its own freshly masked copy (K + 1 copies per rank: K timed, one for
+    the untimed warm-up calls); the flags of the last timed call of each mode
+    are checked against the generator on every rank."""
     w5, d5, ok5 = gpu.config_c5(seed=shard_seed(rank))
     n5 = len(d5)
     pl5 = int(d5["payload_len"].sum())
+    expect = np.asarray(ok5, dtype=np.uint8)[:n5]
     c = gpu.Ctx(local, max_frames=n5 + 64, max_stream_bytes=len(w5))
-    wd = torch.from_numpy(w5).to(dev)
+    master = torch.from_numpy(w5).to(dev)
     del w5
+    k = max(2, min(args.steps, 8))
+    warm = master.clone()
+    bufs = [master.clone() for _ in range(k)]
     dd5 = gpu.descs_to_device(d5, dev)
     ok = torch.empty(n5, dtype=torch.uint8, device=dev)
-    gpu.unmask_sorted_utf8(c, wd, dd5, n5, ok)             # one pass: unmasked, flags valid
-    torch.cuda.synchronize()
-    flags_ok = bool(np.array_equal(ok.cpu().numpy(), np.asarray(ok5, dtype=np.uint8)))
-    gpu.unmask_sorted_utf8(c, wd, dd5, n5, ok)             # masked again (XOR involution)
-    steps = max(2, min(args.steps, 20)) // 2 * 2
 
     def timed(fn):
+        _warm(lambda i: fn(warm), warmup=EXTRA_WARMUP)
         torch.cuda.synchronize()
         barrier(world)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for i in range(steps):
-            fn(i)
+        for b in bufs:
+            fn(b)
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         barrier(world)
-        return max_over_ranks(world, (t1 - t0) / steps), (t1 - t0) / steps
+        return max_over_ranks(world, (t1 - t0) / k), (t1 - t0) / k
 
-    t_desc, own_desc = timed(lambda i: gpu.unmask_sorted_utf8(c, wd, dd5, n5, ok))
+    t_desc, own_desc = timed(lambda b: gpu.unmask_sorted_utf8(c, b, dd5, n5, ok))
+    flags_ok = bool(np.array_equal(ok.cpu().numpy(), expect))
+    for b in bufs:
+        b.copy_(master)
+    warm.copy_(master)
     cap = n5 + 64
     frames = torch.empty(cap * gpu.FRAME_INFO.itemsize, dtype=torch.uint8, device=dev)
     res = torch.empty(gpu.DECODE_RESULT.itemsize, dtype=torch.uint8, device=dev)
     okd = torch.zeros(cap, dtype=torch.uint8, device=dev)
 
-    def dec(i):
-        rc, _, _, _ = gpu.decode_stream(c, wd, cap, frames=frames, result=res, utf8_ok=okd)
+    def dec(b):
+        rc, _, _, _ = gpu.decode_stream(c, b, cap, frames=frames, result=res, utf8_ok=okd)
         assert rc == 0, rc
 
-    dec(0)
-    torch.cuda.synchronize()
+    t_str, own_str = timed(dec)
     r = gpu.read_result(res)
     stream_ok = int(r["status"]) == 0 and int(r["n_frames"]) == n5 and bool(
-        np.array_equal(okd[:n5].cpu().numpy(), np.asarray(ok5, dtype=np.uint8)))
-    dec(1)
-    t_str, own_str = timed(dec)
+        np.array_equal(okd[:n5].cpu().numpy(), expect))
     all_ok = max_over_ranks(world, 0.0 if (flags_ok and stream_ok) else 1.0) == 0.0
     c.close()
+    del master, warm, bufs
+    torch.cuda.empty_cache()
     return {"workload": "C5: per GPU 262144 x 16 KiB masked TEXT frames (4 GiB payload), unmask + per-frame "
                         "UTF-8 flags; ranks split the 8 x 4 GiB job, no collective on the data path",
             "descriptor_mode": {"GiB_per_s": round(world * pl5 / t_desc / GIB, 1),
@@ -523,7 +551,8 @@ def c5_split(args, world, rank, local, dev):
             "stream_decode": {"GiB_per_s": round(world * pl5 / t_str / GIB, 1),
                               "ms_per_step": round(t_str * 1e3, 4),
                               "path": "fws_gpu_decode_stream + UTF-8 flags"},
-            "payload_bytes_per_gpu": pl5, "steps": steps, "n_gpus": world,
+            "payload_bytes_per_gpu": pl5, "steps": k, "n_gpus": world,
+            "timed_input": f"{k} freshly masked copies per rank, one per timed call",
             "flags_match_generator_all_ranks": all_ok}
 
 
@@ -645,10 +674,17 @@ def check_c5_stream(rec):
                    f"{rec.get('utf8_invalid_frames_expected')}")
     if rec.get("flags_match_generator") is not True:
         bad.append("per-frame UTF-8 flags differ from the generator's")
-    if rec.get("first_call_status") != 0 or rec.get("first_call_frames") != rec.get("frames"):
-        bad.append(f"first call status {rec.get('first_call_status')} frames {rec.get('first_call_frames')}")
+    if rec.get("checked_call_status") != 0 or rec.get("checked_call_frames") != rec.get("frames"):
+        bad.append(f"checked call status {rec.get('checked_call_status')} frames {rec.get('checked_call_frames')}")
     if bad:
         raise RuntimeError("C5 stream decode record failed its checks: " + "; ".join(bad))
+    return rec
+
+
+def _profile(rec, cfg):
+    """name the warm rocprofv3 kernel summary of this config in its roofline block"""
+    path = f"{PROFILE_DIR}/{cfg}_kernel_stats.csv"
+    rec.setdefault("roofline", {})["profile"] = path if os.path.exists(os.path.join(ROOT, path)) else None
     return rec
 
 
@@ -659,12 +695,11 @@ def _step_roofline(alg_bytes, t, basis):
             "frac": round(a / HBM_PEAK_GBS, 4), "basis": basis, "alg_bytes_per_step": int(alg_bytes)}
 
 
-def _time(fn, steps, stream, warmup=1, warm_s=EXTRA_WARM_S):
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    # untimed calls in rounds of max(2, warmup) until both `warmup` calls and warm_s
-    # seconds have passed: a config whose timed region lasts a few ms otherwise runs
-    # on clocks still ramping up after the host-side setup before it (C4 measured
-    # 0.088 ms over its first 110 calls, 0.085 after; tools/c4_thermal_probe.py)
+def _warm(fn, warmup=1, warm_s=EXTRA_WARM_S):
+    """untimed calls in rounds of max(2, warmup) until both `warmup` calls and warm_s
+    seconds have passed: a config whose timed region lasts a few ms otherwise runs
+    on clocks still ramping up after the host-side setup before it (C4 measured
+    0.088 ms over its first 110 calls, 0.085 after; tools/c4_thermal_probe.py)"""
     i = 0
     t0 = time.perf_counter()
     while True:
@@ -673,7 +708,12 @@ def _time(fn, steps, stream, warmup=1, warm_s=EXTRA_WARM_S):
             i += 1
         torch.cuda.synchronize()
         if i >= warmup and time.perf_counter() - t0 >= warm_s:
-            break
+            return
+
+
+def _time(fn, steps, stream, warmup=1, warm_s=EXTRA_WARM_S):
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    _warm(fn, warmup, warm_s)
     ev0.record(stream)
     for i in range(steps):
         fn(i)
@@ -706,7 +746,7 @@ def stream_decode_extra(ctx, wire_c2, dev, args):
     steps = max(4, min(args.steps, 50)) // 2 * 2         # even: in-place XOR restores the input
     out = {}
 
-    def decode_cfg(name, wire, n_frames, utf8=False, nbuf=None, pipelined=True, expect_ok=None):
+    def decode_cfg(name, wire, n_frames, nbuf=None, pipelined=True):
         if nbuf is None:
             # rotate >= 1 GiB of distinct batches so the 256 MB Infinity Cache cannot
             # serve a step from the one before: 4 for C2 / C3, 77 of the
@@ -717,29 +757,9 @@ def stream_decode_extra(ctx, wire_c2, dev, args):
         cap = n_frames + 64
         frames = torch.empty(cap * gpu.FRAME_INFO.itemsize, dtype=torch.uint8, device=dev)
         res = torch.empty(gpu.DECODE_RESULT.itemsize, dtype=torch.uint8, device=dev)
-        ok = torch.zeros(cap, dtype=torch.uint8, device=dev) if utf8 else None
         def step(i):
-            rc, _, _, _ = gpu.decode_stream(c, bufs[i % nbuf], cap, frames=frames, result=res, utf8_ok=ok)
+            rc, _, _, _ = gpu.decode_stream(c, bufs[i % nbuf], cap, frames=frames, result=res)
             assert rc == 0, rc
-        checks = {}
-        if utf8:
-            # the flags are only meaningful on masked input: take them from the first
-            # call on the fresh (masked) batch, before the timed loop, then XOR the
-            # batch back (in-place unmask is an involution). In the timed loop below
-            # every call unmasks the previous call's output in place, so with one
-            # buffer the calls alternate between masked text and the re-masked result
-            # (whose flags say "invalid"); the flags read after it are not reported.
-            step(0)
-            torch.cuda.synchronize()
-            r0 = gpu.read_result(res)
-            checks["utf8_invalid_frames"] = int((ok[:n_frames] == 0).sum().item())
-            if expect_ok is not None:
-                checks["flags_match_generator"] = bool(np.array_equal(
-                    ok[:n_frames].cpu().numpy(), np.asarray(expect_ok, dtype=np.uint8)[:n_frames]))
-            checks["first_call_status"] = int(r0["status"])
-            checks["first_call_frames"] = int(r0["n_frames"])
-            step(1)
-            torch.cuda.synchronize()
         t = _time(step, steps, stream, warmup=EXTRA_WARMUP)
         r = gpu.read_result(res)
         assert int(r["status"]) == 0 and int(r["n_frames"]) == n_frames, (name, r)
@@ -753,11 +773,6 @@ def stream_decode_extra(ctx, wire_c2, dev, args):
                "roofline": {"bound": "hbm", "achieved": round(alg, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                             "frac": round(alg / HBM_PEAK_GBS, 4), "basis": "whole fws_gpu_decode_stream step",
                             "alg_bytes_per_step": len(wire) + payload}}
-        if utf8:
-            rec.update(checks)
-            rec["timed_input"] = (f"{nbuf} in-place buffer(s): the timed calls alternate between masked text and "
-                                  "its unmasked output (XOR involution); utf8_invalid_frames is from the call on "
-                                  "the masked batch before timing")
         if pipelined and nbuf >= 4:
             # two batches in flight (two connections' reads): a context, a frame list and a
             # stream each, so one batch's latency-bound resolve overlaps the other's streaming
@@ -828,16 +843,35 @@ def stream_decode_extra(ctx, wire_c2, dev, args):
         c.close()
         return rec
 
-    out["C2_stream_decode"] = decode_cfg("C2", wire_c2, args.frames)
-    w3, d3, _ = gpu.config_c3()
-    out["C3_mixed_stream_decode"] = decode_cfg("C3", w3, len(d3))
-    del w3
+    if want(args, "c2s"):
+        out["C2_stream_decode"] = decode_cfg("C2", wire_c2, args.frames)
+        _profile(out["C2_stream_decode"], "c2s")
+    if want(args, "c3"):
+        w3, d3, _ = gpu.config_c3()
+        out["C3_mixed_stream_decode"] = decode_cfg("C3", w3, len(d3))
+        _profile(out["C3_mixed_stream_decode"], "c3")
+        del w3
     # SURVEY §6's dense workload: 200 000 x 64 B frames (~3 700 headers per 256 KiB super
     # tile: the big-ST resolve path); the reference's 1-core rate is cpu_baseline.dense_64B_one_core
-    wd, dd, _ = gpu.config_c2(n_frames=DENSE_FRAMES, payload=DENSE_PAYLOAD)
-    out["dense_64B_stream_decode"] = decode_cfg("dense", wd, DENSE_FRAMES, pipelined=False)
-    del wd
-    # C4: one 256 MiB fragmented message, unmask + reassemble out of place
+    if want(args, "dense"):
+        wd, dd, _ = gpu.config_c2(n_frames=DENSE_FRAMES, payload=DENSE_PAYLOAD)
+        out["dense_64B_stream_decode"] = decode_cfg("dense", wd, DENSE_FRAMES, pipelined=False)
+        _profile(out["dense_64B_stream_decode"], "dense")
+        del wd
+    if want(args, "c4"):
+        out.update(c4_extra(dev, steps, stream))
+    if want(args, "tx"):
+        out.update(tx_extra(dev, args, steps, stream))
+    if args.c5 and (want(args, "c5s") or want(args, "c5d")):
+        out.update(c5_extra(dev, args, stream))
+    if want(args, "e2e"):
+        out.update(e2e_extra(ctx, wire_c2, dev, args, stream))
+    return {"extra": out}
+
+
+def c4_extra(dev, steps, stream):
+    """C4: one 256 MiB fragmented message, unmask + reassemble out of place"""
+    out = {}
     w4, d4, _ = gpu.config_c4()
     c = gpu.Ctx(dev.index or 0, max_frames=len(d4) + 8, max_stream_bytes=len(w4))
     src = torch.from_numpy(w4).to(dev)
@@ -848,10 +882,16 @@ def stream_decode_extra(ctx, wire_c2, dev, args):
     out["C4_fragmented_reassemble"] = {"GiB_per_s": round(total / t / GIB, 1), "ms_per_step": round(t * 1e3, 4),
                                        "fragments": len(d4), "alg_GB_per_s": round((len(w4) + total) / t / 1e9, 1),
                                        "roofline": _step_roofline(len(w4) + total, t, "whole fws_gpu_unmask_gather step: wire read + payload written out of place")}
+    _profile(out["C4_fragmented_reassemble"], "c4")
     c.close()
     del src, dsts, w4
-    # TX: the C2 shape sent by a client -- 65 536 x 4 KiB payloads (back to
-    # back in HBM) framed and masked into one wire buffer by fws_gpu_encode_frames
+    return out
+
+
+def tx_extra(dev, args, steps, stream):
+    """TX: the C2 shape sent by a client -- 65 536 x 4 KiB payloads (back to
+    back in HBM) framed and masked into one wire buffer by fws_gpu_encode_frames"""
+    out = {}
     n = args.frames
     pl = args.payload
     rng = np.random.default_rng(7)
@@ -875,37 +915,100 @@ def stream_decode_extra(ctx, wire_c2, dev, args):
                            "frames": n, "alg_GB_per_s": round((n * pl + tx_total) / t / 1e9, 1),
                            "path": "fws_gpu_encode_frames: client frames (header + key + masked payload)",
                            "roofline": _step_roofline(n * pl + tx_total, t, "whole fws_gpu_encode_frames step: payload read + frames written")}
+    _profile(out["C2_tx_encode"], "tx")
     c.close()
     del touts, tsrc
-    # C5 per-GPU share: 262 144 x 16 KiB TEXT frames (4 GiB), decode + fused-launch UTF-8 flags
-    if args.c5:
-        w5, d5, ok5 = gpu.config_c5()
-        rec = decode_cfg("C5", w5, len(d5), utf8=True, nbuf=1, expect_ok=ok5)
-        rec["utf8_invalid_frames_expected"] = int((ok5 == 0).sum())
+    return out
+
+
+def c5_extra(dev, args, stream):
+    """C5 per-GPU share: 262 144 x 16 KiB TEXT frames (4 GiB), unmask + per-frame UTF-8 flags,
+    as a raw stream (fws_gpu_decode_stream) and in descriptor mode (fws_gpu_unmask_sorted_utf8).
+    Both decode in place, and an in-place unmask of already unmasked text is a different
+    workload (plain text in, masked bytes out, every flag "invalid"), so every timed call
+    gets its own freshly masked copy of the batch: C5_STREAM_STEPS device copies (~69 GB of
+    the 288 GB HBM), re-masked by device copies between the two modes; the untimed warm-up
+    calls run on one more copy. The flags of every timed call are valid; the last call's
+    are checked against the generator's."""
+    out = {}
+    w5, d5, ok5 = gpu.config_c5()
+    n5 = len(d5)
+    pl5 = int(d5["payload_len"].sum())
+    expect = np.asarray(ok5, dtype=np.uint8)[:n5]
+    master = torch.from_numpy(w5).to(dev)
+    k = C5_STREAM_STEPS
+    warm = master.clone()
+    bufs = [master.clone() for _ in range(k)]
+    c = gpu.Ctx(dev.index or 0, max_frames=n5 + 64, max_stream_bytes=len(w5))
+
+    def timed(fn):
+        _warm(lambda i: fn(warm), warmup=EXTRA_WARMUP)
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        ev0.record(stream)
+        for b in bufs:
+            fn(b)
+        ev1.record(stream)
+        torch.cuda.synchronize()
+        return ev0.elapsed_time(ev1) / 1e3 / k
+
+    if want(args, "c5s"):
+        cap = n5 + 64
+        frames = torch.empty(cap * gpu.FRAME_INFO.itemsize, dtype=torch.uint8, device=dev)
+        res = torch.empty(gpu.DECODE_RESULT.itemsize, dtype=torch.uint8, device=dev)
+        ok = torch.zeros(cap, dtype=torch.uint8, device=dev)
+
+        def dec(b):
+            rc, _, _, _ = gpu.decode_stream(c, b, cap, frames=frames, result=res, utf8_ok=ok)
+            assert rc == 0, rc
+        t = timed(dec)
+        r = gpu.read_result(res)
+        flags = ok[:n5].cpu().numpy()
+        payload = int(gpu.read_frames(frames, n5)["payload_len"].sum())
+        rec = {"GiB_per_s": round(payload / t / GIB, 1), "ms_per_step": round(t * 1e3, 4), "frames": n5,
+               "wire_bytes": len(w5), "alg_GB_per_s": round((len(w5) + payload) / t / 1e9, 1),
+               "rotating_buffers": k, "big_super_tiles": gpu.decode_counters(c)["big_super_tiles"],
+               "roofline": _step_roofline(len(w5) + payload, t, "whole fws_gpu_decode_stream step"),
+               "utf8_invalid_frames": int((flags == 0).sum()),
+               "utf8_invalid_frames_expected": int((expect == 0).sum()),
+               "flags_match_generator": bool(np.array_equal(flags, expect)),
+               "checked_call_status": int(r["status"]), "checked_call_frames": int(r["n_frames"]),
+               "timed_input": f"{k} distinct freshly masked copies of the batch, one per timed call (the "
+                              "warm-up calls run on another); status, frame count and flags checked on the "
+                              "last timed call"}
         check_c5_stream(rec)
+        _profile(rec, "c5s")
         out["C5_utf8_text_decode"] = rec
+        for b in bufs:
+            b.copy_(master)                                  # masked again for the descriptor mode
+        warm.copy_(master)
+        del frames, res, ok
+    if want(args, "c5d"):
         # the same batch in descriptor mode (a batch split at frame boundaries knows its
         # frames): one pass of unmask + UTF-8 flags, fws_gpu_unmask_sorted_utf8
-        c = gpu.Ctx(dev.index or 0, max_frames=len(d5) + 8, max_stream_bytes=len(w5))
-        wd = torch.from_numpy(w5).to(dev)
         dd5 = gpu.descs_to_device(d5, dev)
-        ok = torch.empty(len(d5), dtype=torch.uint8, device=dev)
-        gpu.unmask_sorted_utf8(c, wd, dd5, len(d5), ok)
-        torch.cuda.synchronize()
-        flags_ok = bool(np.array_equal(ok.cpu().numpy(), np.asarray(ok5, dtype=np.uint8)[:len(d5)]))
+        ok = torch.empty(n5, dtype=torch.uint8, device=dev)
+        t = timed(lambda b: gpu.unmask_sorted_utf8(c, b, dd5, n5, ok))
+        flags_ok = bool(np.array_equal(ok.cpu().numpy(), expect))
         if not flags_ok:
             raise RuntimeError("C5 descriptor mode: UTF-8 flags differ from the generator's")
-        gpu.unmask_sorted_utf8(c, wd, dd5, len(d5), ok)       # masked again (XOR involution)
-        t = _time(lambda i: gpu.unmask_sorted_utf8(c, wd, dd5, len(d5), ok), 10, stream, warmup=EXTRA_WARMUP)
-        pl5 = int(d5["payload_len"].sum())
         out["C5_utf8_descriptor"] = {"GiB_per_s": round(pl5 / t / GIB, 1), "ms_per_step": round(t * 1e3, 4),
-                                     "frames": len(d5), "alg_GB_per_s": round((len(w5) + pl5) / t / 1e9, 1),
-                                     "flags_match_generator": flags_ok,
+                                     "frames": n5, "alg_GB_per_s": round((len(w5) + pl5) / t / 1e9, 1),
+                                     "flags_match_generator": flags_ok, "rotating_buffers": k,
+                                     "timed_input": f"{k} distinct freshly masked copies, one per timed call; "
+                                                    "flags of the last call checked",
                                      "path": "fws_gpu_unmask_sorted_utf8: k_unmask_sorted_utf8 + k_utf8_seam_sorted",
                                      "roofline": _step_roofline(len(w5) + pl5, t, "whole fws_gpu_unmask_sorted_utf8 step: wire read + payload written")}
-        c.close()
-        del w5, wd
-    # end-to-end: pinned host -> HBM -> unmask -> host (PCIe-inclusive), C2
+        _profile(out["C5_utf8_descriptor"], "c5d")
+    c.close()
+    del master, warm, bufs, w5
+    torch.cuda.empty_cache()
+    return out
+
+
+def e2e_extra(ctx, wire_c2, dev, args, stream):
+    """end-to-end: pinned host -> HBM -> unmask -> host (PCIe-inclusive), C2"""
+    out = {}
     n = args.frames
     host_in = torch.from_numpy(wire_c2).pin_memory()
     host_out = torch.empty_like(host_in).pin_memory()
@@ -951,7 +1054,7 @@ def stream_decode_extra(ctx, wire_c2, dev, args):
                 "bound by PCIe: H2D and D2H do not overlap on this box (profiles/r01/pcie_probe.json)",
         "batches": k}
     pipe.close()
-    return {"extra": out}
+    return out
 
 
 if __name__ == "__main__":

@@ -144,20 +144,47 @@ __device__ __forceinline__ uint32_t sel_bytes(uintptr_t w, uintptr_t lo, uintptr
     return (0xFFFFFFFFu << (8u * s)) & (0xFFFFFFFFu >> (8u * e));
 }
 
-// UTF-8 error flags (bit 7 of each byte) of the 4 bytes of x, p = the dword
-// before x. Bytes outside the region are zero, so a sequence cut by the region
-// end fails the continuation rule at the first zero byte after it.
-//   continuation (10xxxxxx) <=> prev1 >= C0 or prev2 >= E0 or prev3 >= F0
-//   never C0, C1, F5..FF
-//   after E0: >= A0, after ED: <= 9F, after F0: >= 90, after F4: <= 8F
-// Lead flags (>= C0 / E0 / F0 at bit 7) are computed once per dword and
-// byte-aligned (v_alignbyte) to the prev1..3 positions; the four second-byte
-// rules test prev1 & 1F (00 / 0D / 10 / 14 under prev1 >= E0) with one add
-// each and select by bit 5 / bits 5|4 of x (v_bfi). ~38 VALU ops per dword
-// (was ~60); inlined chains share the flags of the dword between two calls.
-// Equivalent to the per-rule form on every (prev3, prev2, prev1, x) of 28
-// boundary bytes at every alignment and 2e8 random dword pairs (host check).
-__device__ __forceinline__ uint32_t utf8_err(uint32_t x, uint32_t p) {
+// UTF-8 error flags of the 4 bytes of x, p = the dword before x: byte k of the
+// result is nonzero iff byte k of x is in error. Bytes outside the region are
+// zero, so a sequence cut by the region end fails rule (A) at the first zero
+// byte after it. Unicode Table 3-7 / RFC 3629 as two rules:
+//  (A) x is a continuation (10xxxxxx) <=> prev1 >= C0 or prev2 >= E0 or
+//      prev3 >= F0 (bit 7 of each byte);
+//  (B) prev1 in {C0, C1, F5..FF} and x a continuation; E0 and x < A0; ED and
+//      x > 9F; F0 and x < 90; F4 and x > 8F (bits 0..6).
+// (B) is three v_perm_b32 lookups on prev1 -- bits 7:5, 4:2 and 2:0, 8-entry
+// tables whose AND is exact on every byte, one flag per rule -- against one on
+// x's bits 6:4 (exact on continuation bytes; when a non-continuation follows a
+// flagged prev1, (A) fails anyway). The lead flags of (A) come from the same
+// tables (bit 7: bits 7:5 == 111 is >= E0, and with bit 4 it is >= F0), so
+// only >= C0 is computed by shifts. An invalid byte (C0, C1, F5..FF) is flagged
+// at the byte after it (by (A) or (B)); the walks run 3 zero bytes past every
+// region, so a frame's verdict is the per-rule form's (r02-r04 SWAR, ~36 VALU
+// per dword; this form ~22 with the x-side values shared by the chain's next
+// call). tools/utf8_lookup_check.c proves the per-byte equivalence on every
+// (prev3, prev2) of 48 boundary bytes x every (prev1, x) at each position, and
+// on 4e8 random dword pairs.
+__device__ __forceinline__ uint32_t utf8_lead_tables(uint32_t x, uint32_t &ta) {
+    const uint32_t m = 0x07070707u;
+    ta = __builtin_amdgcn_perm(0xFE010000u, 0x00000000u, (x >> 5) & m);     // bits 7:5
+    const uint32_t tb = __builtin_amdgcn_perm(0x8282C4A0u, 0x10000009u, (x >> 2) & m);   // bits 4:2
+    const uint32_t tc = __builtin_amdgcn_perm(0x868696C2u, 0x828283ABu, x & m);          // bits 2:0
+    return ta & tb & tc;
+}
+__device__ __forceinline__ uint32_t utf8_err_lookup(uint32_t x, uint32_t p) {
+    uint32_t tax, tap;
+    const uint32_t b1x = utf8_lead_tables(x, tax), b1p = utf8_lead_tables(p, tap);
+    const uint32_t x1 = x << 1, tx = x & x1, tp = p & (p << 1);
+    const uint32_t req = __builtin_amdgcn_alignbyte(tx, tp, 3u) | __builtin_amdgcn_alignbyte(tax, tap, 2u) |
+                         __builtin_amdgcn_alignbyte(b1x, b1p, 1u);
+    const uint32_t ea = (x & ~x1) ^ req;
+    const uint32_t b2 = __builtin_amdgcn_perm(0u, 0x57574F2Fu, (x >> 4) & 0x07070707u);
+    return (ea & 0x80808080u) | (__builtin_amdgcn_alignbyte(b1x, b1p, 3u) & b2);
+}
+
+// r02-r04 form (bit 7 of each byte = error; invalid bytes flagged at their own
+// position), kept for the A/B build FWS_UTF8_SWAR
+__device__ __forceinline__ uint32_t utf8_err_swar(uint32_t x, uint32_t p) {
     const uint32_t H = 0x80808080u;
     const uint32_t x1 = x << 1, x2 = x << 2, x3 = x << 3;
     const uint32_t tx = x & x1, ux = tx & x2, wx = ux & x3;
@@ -176,6 +203,16 @@ __device__ __forceinline__ uint32_t utf8_err(uint32_t x, uint32_t p) {
     const uint32_t bF = (s54 & nzF4) | (~s54 & nzF0);
     err |= e1 & ~(bE & bF);
     return err & H;
+}
+
+#ifndef FWS_UTF8_SWAR
+#define FWS_UTF8_SWAR 0
+#endif
+// callers test byte k != 0 (masks 0xFF000000 / 0x00FFFFFF select bytes), which
+// both forms satisfy
+__device__ __forceinline__ uint32_t utf8_err(uint32_t x, uint32_t p) {
+    if constexpr (FWS_UTF8_SWAR != 0) return utf8_err_swar(x, p);
+    else return utf8_err_lookup(x, p);
 }
 
 }  // namespace fwsk

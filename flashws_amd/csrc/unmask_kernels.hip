@@ -351,7 +351,7 @@ __device__ __forceinline__ bool utf8_chunk_bad(const u32x4 &u, uint32_t prev, ui
     if (!(c >= lo + 4u && c <= hi)) p &= sel_bytes(c - 4u, lo, hi);
     if (!((x.x | x.y | x.z | x.w | p) & 0x80808080u)) return false;   // ASCII, no open sequence
     uint32_t e0 = utf8_err(x.x, p);
-    if (skip) e0 &= 0x80000000u;                     // bytes 0..2 are judged by k_utf8_seam
+    if (skip) e0 &= 0xFF000000u;                     // bytes 0..2 are judged by k_utf8_seam
     return (e0 | utf8_err(x.y, x.x) | utf8_err(x.z, x.y) | utf8_err(x.w, x.z)) != 0u;
 }
 
@@ -376,7 +376,7 @@ __device__ __forceinline__ uint32_t utf8_chunk_err32(const u32x4 &u, uint32_t pr
     }
     if (!(r >= lo + 4 && r <= hi)) p &= sel_bytes32(r - 4, lo, hi);
     uint32_t e0 = utf8_err(x.x, p);
-    if (skip) e0 &= 0x80000000u;
+    if (skip) e0 &= 0xFF000000u;
     return e0 | utf8_err(x.y, x.x) | utf8_err(x.z, x.y) | utf8_err(x.w, x.z);
 }
 
@@ -540,7 +540,7 @@ __global__ __launch_bounds__(kBlock) void k_unmask_stream(uint8_t *base, uint64_
                     const uint32_t prev = __builtin_amdgcn_update_dpp(carry, x[j].w, 0x138, 0xF, 0xF, false);
                     carry = __builtin_amdgcn_readlane(x[j].w, 63);
                     uint32_t e0 = utf8_err(x[j].x, prev);
-                    if (j == 0 && lane == 0) e0 &= 0x80000000u;   // bytes 0..2: k_utf8_seam's
+                    if (j == 0 && lane == 0) e0 &= 0xFF000000u;   // bytes 0..2: k_utf8_seam's
                     err |= e0 | utf8_err(x[j].y, x[j].x) | utf8_err(x[j].z, x[j].y) | utf8_err(x[j].w, x[j].z);
                 }
                 if (__any(err != 0u) && lane == 0) ok[flo] = 0;
@@ -625,7 +625,7 @@ __global__ __launch_bounds__(kBlock) void k_utf8_seam(const uint8_t *base, uint6
         const StreamFrame sf = stream_frame(fr[g], N);
         if (!sf.text || P + 3u <= sf.po || P >= sf.pe + 3u) continue;
         const uint32_t x = cur & sel_bytes(P, sf.po, sf.pe), p = prev & sel_bytes(P - 4u, sf.po, sf.pe);
-        if (utf8_err(x, p) & 0x00808080u) ok[g] = 0;
+        if (utf8_err(x, p) & 0x00FFFFFFu) ok[g] = 0;
     }
 }
 
@@ -1018,7 +1018,7 @@ __device__ __forceinline__ void unmask_sorted_body(uint8_t *base, const fws_fram
                     const uint32_t prev = __builtin_amdgcn_update_dpp(carry, x[j].w, 0x138, 0xF, 0xF, false);
                     carry = __builtin_amdgcn_readlane(x[j].w, 63);
                     uint32_t e0 = utf8_err(x[j].x, prev);
-                    if (j == 0 && lane == 0) e0 &= 0x80000000u;   // bytes 0..2: k_utf8_seam_sorted's
+                    if (j == 0 && lane == 0) e0 &= 0xFF000000u;   // bytes 0..2: k_utf8_seam_sorted's
                     err |= e0 | utf8_err(x[j].y, x[j].x) | utf8_err(x[j].z, x[j].y) | utf8_err(x[j].w, x[j].z);
                 }
                 if (__any(err != 0u) && lane == 0) ok[A] = 0;
@@ -1152,7 +1152,7 @@ __global__ __launch_bounds__(kBlock) void k_utf8_seam_sorted(const uint8_t *base
         if (pe + 3u <= P) break;
         if (!fd.payload_len || po >= P + 3u) continue;
         const uint32_t x = cur & sel_bytes(P, po, pe), p = prev & sel_bytes(P - 4u, po, pe);
-        if (utf8_err(x, p) & 0x00808080u) ok[f] = 0;
+        if (utf8_err(x, p) & 0x00FFFFFFu) ok[f] = 0;
     }
     }
 }
@@ -1186,7 +1186,8 @@ struct SortedUnit {
 
 template <bool kNT>
 __device__ __forceinline__ void unmask_sorted_utf8_pipe(uint8_t *base, const fws_frame_desc *__restrict__ d,
-                                                        uint32_t n, uint8_t *__restrict__ ok) {
+                                                        uint32_t n, uint8_t *__restrict__ ok,
+                                                        uint32_t *__restrict__ seam, uint64_t seam_units) {
     if (n == 0) return;
     const int lane = threadIdx.x & (kWave - 1);
     const uintptr_t b0 = (uintptr_t)base;
@@ -1240,7 +1241,18 @@ __device__ __forceinline__ void unmask_sorted_utf8_pipe(uint8_t *base, const fws
     for (;;) {
         const uint64_t c0 = cur.U0 + uint64_t(lane) * 16u;
         u32x4 x[kUnmaskU];
-        if (!cur.gap) {
+        // one key: the unit lies wholly inside A's payload and B has no byte in it (the
+        // common unit of large frames, as in unmask_sorted_body)
+        const bool onekey = !cur.slow && cur.rec.z == (4096u << 13) &&
+                            ((cur.rec.w >> 13) & 0x1FFFu) <= (cur.rec.w & 0x1FFFu);
+        if (onekey) {
+            const uint32_t rk = cur.rec.x;
+#pragma unroll
+            for (int j = 0; j < kUnmaskU; ++j) {
+                x[j] = v[j] ^ u32x4{rk, rk, rk, rk};
+                gstore16<kNT>(c0 + uint64_t(j) * 1024u, x[j]);
+            }
+        } else if (!cur.gap) {
             u32x4 m[kUnmaskU];
             if (cur.slow) slow_unit_masks(d, n, cur.A, b0, cur.U0, lane, m);
             else fast_unit_masks(cur.rec, lane, m);
@@ -1262,7 +1274,23 @@ __device__ __forceinline__ void unmask_sorted_utf8_pipe(uint8_t *base, const fws
             nx = lookup(un);
             load(nx, v);
         }
-        if (!cur.gap) {
+        // the unit's first and last unmasked dwords for k_utf8_seam_sorted
+        if (!cur.gap && u < seam_units) {
+            if (lane == 0) seam[2u * u] = x[0].x;
+            if (lane == 63) seam[2u * u + 1u] = x[kUnmaskU - 1].w;
+        }
+        if (onekey) {
+            uint32_t err = 0, carry = 0;
+#pragma unroll
+            for (int j = 0; j < kUnmaskU; ++j) {
+                const uint32_t prev = __builtin_amdgcn_update_dpp(carry, x[j].w, 0x138, 0xF, 0xF, false);
+                carry = __builtin_amdgcn_readlane(x[j].w, 63);
+                uint32_t e0 = utf8_err(x[j].x, prev);
+                if (j == 0 && lane == 0) e0 &= 0xFF000000u;   // bytes 0..2: k_utf8_seam_sorted's
+                err |= e0 | utf8_err(x[j].y, x[j].x) | utf8_err(x[j].z, x[j].y) | utf8_err(x[j].w, x[j].z);
+            }
+            if (__any(err != 0u) && lane == 0) ok[cur.A] = 0;
+        } else if (!cur.gap) {
             bool badA = false, badB = false;
             uint32_t carry = 0;
 #pragma unroll
@@ -1300,7 +1328,7 @@ template <bool kNT, bool kPipe>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FWS_UTF8_WPE))) void k_unmask_sorted_utf8(uint8_t *base, const fws_frame_desc *__restrict__ d,
                                                                uint32_t n, uint8_t *__restrict__ ok,
                                                                uint32_t *__restrict__ seam, uint64_t seam_units) {
-    if (kPipe) unmask_sorted_utf8_pipe<kNT>(base, d, n, ok);
+    if (kPipe) unmask_sorted_utf8_pipe<kNT>(base, d, n, ok, seam, seam_units);
     else unmask_sorted_body<kNT, false, true>(base, d, n, ok, seam, seam_units);
 }
 
@@ -1538,13 +1566,13 @@ int fws_launch_unmask_sorted_utf8(uint8_t *base, const fws_frame_desc *d, uint32
     const uint64_t units = max_span / 4096u + 2u;
     if (g_sorted_utf8_pipe)
         hipLaunchKernelGGL((k_unmask_sorted_utf8<true, true>), dim3(grid_for_units(units, kCapSortedUtf8)), dim3(kBlock), 0, s, base, d,
-                           n, ok, nullptr, 0ull);
+                           n, ok, seam, seam_units);
     else
         hipLaunchKernelGGL((k_unmask_sorted_utf8<true, false>), dim3(grid_for_units(units, kCapSortedUtf8)), dim3(kBlock), 0, s, base,
                            d, n, ok, seam, seam_units);
     const uint64_t seam_blocks = (units + kBlock - 1) / kBlock;   // grid-stride: any span is covered
     hipLaunchKernelGGL(k_utf8_seam_sorted, dim3((unsigned)(seam_blocks < 4096u ? seam_blocks : 4096u)), dim3(kBlock), 0, s,
-                       (const uint8_t *)base, d, n, ok, g_sorted_utf8_pipe ? nullptr : seam, seam_units);
+                       (const uint8_t *)base, d, n, ok, seam, seam_units);
     return fws_hip_status(hipGetLastError());
 }
 

@@ -1,7 +1,8 @@
 """CPU, world_size 2 over gloo: the multi-GPU path of bench.py (one process
 per GPU, independent shards, barrier + max-over-ranks timing, aggregate =
 sum of shards / slowest rank) with the oracle standing in for the device
-decode. No collective touches frame data."""
+decode. No collective touches frame data; bench.py's control group is gloo at
+every N (bench.init_group), so no RCCL initialisation is on the N > 1 path."""
 import os
 import socket
 
@@ -23,9 +24,9 @@ def _worker(rank, world, port, q):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path.insert(0, root)
     sys.path.insert(0, os.path.join(root, "tests"))
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     import bench
+    backend = bench.init_group(world)                # bench.py's own N > 1 control group
     import orc
     from flashws_amd import gpu
     wire, descs, _ = gpu.config_c2(seed=bench.shard_seed(rank), n_frames=512)
@@ -42,7 +43,7 @@ def _worker(rank, world, port, q):
     digest = torch.tensor([int(buf[:4096].sum())], dtype=torch.int64)
     gathered = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
     dist.all_gather(gathered, digest)          # test-only check that shards differ
-    q.put((rank, ret, len(frames), step, t1 - t0, agg, payload, [int(g) for g in gathered]))
+    q.put((rank, ret, len(frames), step, t1 - t0, agg, payload, [int(g) for g in gathered], backend))
     dist.destroy_process_group()
 
 
@@ -59,7 +60,8 @@ def test_two_rank_batch_split_gloo():
         assert p.exitcode == 0
     steps = [r[3] for r in res]
     assert steps[0] == steps[1] == max(r[4] for r in res)        # both report the slowest rank
-    for rank, ret, nf, step, own, agg, payload, gathered in res:
+    for rank, ret, nf, step, own, agg, payload, gathered, backend in res:
+        assert backend == "gloo"                                   # no device collective is initialised
         assert ret == 0 and nf == 512
         assert np.isclose(agg, world * payload / step / (1 << 30))
     assert res[0][7][0] != res[0][7][1]                           # independent shards
@@ -112,9 +114,9 @@ def test_c5_stream_record_check_fails_loudly():
     (a record once showed 262144 invalid frames against 2692)."""
     import bench
     good = {"frames": 262144, "utf8_invalid_frames": 2692, "utf8_invalid_frames_expected": 2692,
-            "flags_match_generator": True, "first_call_status": 0, "first_call_frames": 262144}
+            "flags_match_generator": True, "checked_call_status": 0, "checked_call_frames": 262144}
     assert bench.check_c5_stream(dict(good)) == good
     for bad in ({"utf8_invalid_frames": 262144}, {"utf8_invalid_frames_expected": 2693},
-                {"flags_match_generator": False}, {"first_call_status": -1}, {"first_call_frames": 5}):
+                {"flags_match_generator": False}, {"checked_call_status": -1}, {"checked_call_frames": 5}):
         with pytest.raises(RuntimeError):
             bench.check_c5_stream({**good, **bad})

@@ -422,22 +422,32 @@ def test_utf8_flags_mixed_stream(ctx, cuda, seed):
 
 
 def test_utf8_flags_unit_seams(ctx, cuda):
-    """TEXT frames placed so that multi-byte sequences, cut sequences and frame
-    ends straddle 4 KiB stream-unit boundaries (the seam kernel's bytes)."""
+    """TEXT frames placed so that multi-byte sequences, cut sequences, invalid
+    bytes and frame ends straddle 4 KiB stream-unit boundaries (the seam
+    kernel's bytes)."""
     rng = np.random.default_rng(77)
     parts, bodies = [], []
     pos = 0
-    for k in range(60):
+    for k in range(150):
         # the payload end lands at unit boundary + d, d in -3..3
         d = int(rng.integers(-3, 4))
         target = (pos // 4096 + 2) * 4096 + d
         seq = rng.choice([b"\xe2\x82\xac", b"\xf0\x9d\x84\x9e", b"\xc3\xa9", b"a"])
         n = target - pos - 8
         body = bytearray((seq * (n // len(seq) + 2))[:n])
-        if k % 3 == 1:
+        if k % 5 == 1:
             body[-1] = 0xE2                              # cut at the end
-        elif k % 3 == 2:
+        elif k % 5 == 2:
             body[-int(rng.integers(1, 4))] = 0x80        # stray continuation near the end
+        elif k % 5 == 3:
+            # an invalid byte at or near the end: the table check flags it at the byte after
+            # it, which may be the next unit's first bytes or the zero bytes past the payload
+            body[-int(rng.integers(1, 5))] = int(rng.choice([0xC0, 0xC1, 0xF5, 0xF8, 0xFF]))
+        elif k % 5 == 4:
+            # ... or at a unit seam inside the payload
+            at = ((pos + 8) // 4096 + 1) * 4096 + int(rng.integers(-4, 4)) - pos - 8
+            if 0 <= at < len(body):
+                body[at] = int(rng.choice([0xC0, 0xC1, 0xF5, 0xF8, 0xFF]))
         parts.append(frame(1, bytes(body), key=int(rng.integers(0, 2**32)), len_form=126))
         bodies.append(bytes(body))
         pos += len(parts[-1])

@@ -14,6 +14,15 @@ from test_gpu_unmask import aligned_host, oracle_unmask_regions
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True, params=[0, 1], ids=["plain", "pipe"])
+def utf8_pipe(request):
+    """every test runs on both forms of k_unmask_sorted_utf8 (plain and software-pipelined)"""
+    from flashws_amd import lib
+    old = lib().fws_internal_set_sorted_utf8_pipe(request.param)
+    yield request.param
+    lib().fws_internal_set_sorted_utf8_pipe(old)
+
+
 def _valid(b):
     try:
         b.decode("utf-8")
@@ -160,3 +169,31 @@ def test_sorted_utf8_unreserved_ctx_wide_frames(cuda):
         c.close()
     assert np.array_equal(got, plain)
     assert np.array_equal(ok.astype(bool), np.array([_valid(x) for x in cases]))
+
+
+def test_sorted_utf8_invalid_bytes_at_seams(ctx, cuda):
+    """An invalid byte (C0, C1, F5, F8, FF) or a lead whose sequence is cut, at
+    every offset -4..+4 around a 4 KiB unit seam and as a frame's last byte: the
+    table form flags an invalid byte at the byte after it, which may be the next
+    unit's first bytes (k_utf8_seam_sorted's) or the 3 zero bytes past the frame."""
+    rng = np.random.default_rng(41)
+    base = "".join(chr(int(c)) for c in rng.integers(0x20, 0x7F, 30000)).encode()   # ASCII: byte = char
+    cases = []
+    for bad in (b"\xc0", b"\xc1", b"\xf5", b"\xf8", b"\xff", b"\xe2\x82", b"\xc3"):
+        for seam in (4096, 8192, 12288):
+            for d in range(-4, 5):
+                b = bytearray(base[:20000])
+                # the frame starts 16-B aligned plus the layout's offset; seams are relative to
+                # the batch origin, so cover them by position within the frame as well
+                at = seam + d
+                b[at:at + len(bad)] = bad
+                cases.append(bytes(b))
+        cases.append(bytes(base[:9000]) + bad)                        # the frame's last byte(s)
+        cases.append(bytes(base[:4096 - len(bad)]) + bad)            # ends right before a seam
+        cases.append(b"\xe2\x82\xac" * 1365 + bad)                    # ends at 4095 + len(bad)
+    plain, masked, descs = _layout(rng, cases, 0)
+    got, ok = _run(ctx, cuda, masked, descs)
+    assert np.array_equal(got, plain)
+    exp = np.array([_valid(c) for c in cases])
+    assert not exp.any()
+    assert np.array_equal(ok.astype(bool), exp), np.nonzero(ok.astype(bool) != exp)[0][:10]

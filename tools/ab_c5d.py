@@ -1,0 +1,60 @@
+#!/usr/bin/env python3
+"""A/B timing of the C5 descriptor-mode passes on one 4 GiB C5 batch, in one
+process (the library variant from FWS_LIB_VARIANT): the plain unmask
+(k_unmask_sorted, the HBM floor of the pass), fws_gpu_unmask_sorted_utf8 in
+its plain form (pipe 0) and its early-load form (pipe 1). HIP events, 20 calls
+per repetition after a warm-up of >= 0.5 s; prints one JSON line per mode."""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from flashws_amd import gpu  # noqa: E402
+from flashws_amd._lib import lib  # noqa: E402
+
+
+def main(calls=20, reps=3):
+    dev = torch.device("cuda:0")
+    w5, d5, ok5 = gpu.config_c5()
+    n = len(d5)
+    ctx = gpu.Ctx(0, max_frames=n + 64, max_stream_bytes=len(w5))
+    w = torch.from_numpy(w5).to(dev)
+    dd = gpu.descs_to_device(d5, dev)
+    ok = torch.zeros(n, dtype=torch.uint8, device=dev)
+    s = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    modes = {"plain_unmask": lambda: gpu.unmask_sorted(ctx, w, dd, n),
+             "utf8_pipe0": lambda: (lib().fws_internal_set_sorted_utf8_pipe(0), gpu.unmask_sorted_utf8(ctx, w, dd, n, ok)),
+             "utf8_pipe1": lambda: (lib().fws_internal_set_sorted_utf8_pipe(1), gpu.unmask_sorted_utf8(ctx, w, dd, n, ok))}
+    for name in list(modes) + list(modes)[::-1]:
+        fn = modes[name]
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < 0.5:
+            for _ in range(4):
+                fn()
+            torch.cuda.synchronize()
+        ms = []
+        for _ in range(reps):
+            e0.record(s)
+            for _ in range(calls):
+                fn()
+            e1.record(s)
+            torch.cuda.synchronize()
+            ms.append(round(e0.elapsed_time(e1) / calls, 4))
+        print(json.dumps({"variant": os.environ.get("FWS_LIB_VARIANT", "") or "product", "mode": name,
+                          "ms": sorted(ms)[len(ms) // 2], "reps": ms}), flush=True)
+    lib().fws_internal_set_sorted_utf8_pipe(0)
+    # correctness of the product setting on the masked batch
+    w.copy_(torch.from_numpy(w5).to(dev))
+    gpu.unmask_sorted_utf8(ctx, w, dd, n, ok)
+    torch.cuda.synchronize()
+    assert np.array_equal(ok.cpu().numpy(), np.asarray(ok5, dtype=np.uint8)[:n]), "utf8 flags differ"
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()

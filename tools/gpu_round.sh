@@ -18,7 +18,7 @@
 #   trace        phase clocks of k_scan and per-workgroup timelines of the resolve kernels
 #                (FWS_SCAN_PROF build: make -C flashws_amd/csrc prof, built beforehand)
 set -o pipefail
-ROUND=${ROUND:-r04}
+ROUND=${ROUND:-r05}
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 O=$R/gpurun_out/$ROUND
 mkdir -p "$O"
@@ -89,6 +89,20 @@ for step in "$@"; do
             prof "kdec_$c" 300 --kernel-trace --stats -f csv -d "$O/kdec_$c" -o run -- python3 "$R/tools/run_decode.py" $c 20
         done
         for c in c3 dense; do cut -d, -f1-5 "$O/kdec_$c/run_kernel_stats.csv" | head -12; done ;;
+    utf8tests)
+        timeout -k 10 600 python -u -m pytest tests/test_gpu_sorted_utf8.py tests/test_gpu_decode.py tests/test_gpu_configs.py -k "utf8 or c5 or C5 or text" -x -v --timeout 120 --timeout-method thread \
+            > "$O/utf8_tests.log" 2>&1 || fail utf8tests $? "$O/utf8_tests.log"
+        tail -1 "$O/utf8_tests.log" ;;
+    ab_c5)       # A/B: UTF-8 check forms (FWS_LIB_VARIANT=swar: make exp EXP_TAG=swar EXP_DEFS=-DFWS_UTF8_SWAR=1)
+        for v in swar "" swar ""; do
+            FWS_LIB_VARIANT=$v timeout -k 10 300 python bench.py --only c5d,c5s --no-cpu --no-batch-extra --steps 20 --warmup 5 \
+                >> "$O/ab_c5.jsonl" 2>> "$O/ab_c5.err" || fail ab_c5 $? "$O/ab_c5.err"
+            python3 -c "import json,sys;d=json.loads(open('$O/ab_c5.jsonl').read().splitlines()[-1]);e=d['extra'];print('variant=${v:-product}', e['C5_utf8_descriptor']['ms_per_step'], e['C5_utf8_text_decode']['ms_per_step'])"
+        done ;;
+    prof_extras)  # warm kernel stats, one config per process under bench.py's own warm-up
+        for c in c3 dense c2s c4 tx c5d c5s; do
+            prof "prof_$c" 400 --kernel-trace --stats -f csv -d "$O/prof_$c" -o run -- python3 "$R/bench.py" --only $c --no-cpu --no-batch-extra --steps 20 --warmup 5
+        done ;;
     *) echo "unknown step $step"; exit 2 ;;
     esac
 done

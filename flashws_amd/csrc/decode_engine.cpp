@@ -80,6 +80,11 @@ static void engine_free(fws_decode_engine *e) {
     delete e;
 }
 
+// Workspaces in use: the default schedule (mode 0) alternates two, the
+// split-phase schedule keeps kSlots decodes in flight (the third
+// full-size workspace sat unused in mode 0).
+static int engine_slots(const fws_decode_engine *e) { return e->mode == 0 ? 2 : kSlots; }
+
 // Workspaces for jobs of up to `frames` frames / `bytes` bytes (and UTF-8
 // seams): a growth drains the engine first (the workspaces may be in use).
 static int engine_reserve(fws_decode_engine *e, uint64_t frames, uint64_t bytes, bool utf8) {
@@ -90,7 +95,7 @@ static int engine_reserve(fws_decode_engine *e, uint64_t frames, uint64_t bytes,
     const uint64_t f = frames > e->max_frames ? frames : e->max_frames;
     const uint64_t b = bytes > e->max_bytes ? bytes : e->max_bytes;
     if (f > 0xFFFFFFFFull) return FWS_ERR_CAPACITY;
-    for (int k = 0; k < kSlots; ++k) {
+    for (int k = 0; k < engine_slots(e); ++k) {
         if ((r = fws_gpu_ctx_reserve(e->ctx[k], f, b))) return r;
         if ((r = fws_decode_prepare(e->ctx[k], b, (uint32_t)f, utf8 || e->utf8_ready))) return r;
     }

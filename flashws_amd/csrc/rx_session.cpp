@@ -251,7 +251,11 @@ int fws_wait_flag(const volatile uint32_t *flag, uint32_t seq, hipStream_t s) {
     for (uint32_t i = 0;; ++i) {
         if (__atomic_load_n(f, __ATOMIC_ACQUIRE) == seq) return 0;
         if ((i & 255u) == 255u && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(200)) break;
+#if defined(__x86_64__) || defined(__i386__)
         __builtin_ia32_pause();
+#elif defined(__aarch64__)
+        __asm__ __volatile__("yield");
+#endif
     }
     // a long decode (or a failed launch): block on the stream instead of spinning
     const hipError_t e = hipStreamSynchronize(s);
@@ -564,8 +568,7 @@ struct fws_rx_mux {
     uint64_t mcap = 0;
     std::vector<uint8_t> seen;        // per connection: fed in this call
     uint64_t zc_max = 0;              // batches up to this many bytes: kernels on the pinned buffers
-    uint32_t *dctr = nullptr;         // host_done counter of the zero-copy launch (monotonic)
-    uint32_t ctr_total = 0;
+    uint32_t *dctr = nullptr;         // host_done counter of the zero-copy launch (reset by its last workgroup)
     uint32_t *hflag = nullptr;        // and its flag (coherent pinned word)
     uint32_t seq = 0;
 
@@ -756,11 +759,10 @@ int fws_rx_mux_feed(fws_rx_mux *m, const fws_rx_read *reads, uint32_t n, fws_rx_
         if (bytes <= m->zc_max) {
             fws_decode_result *hr = (fws_decode_result *)(m->hmeta + desc_bytes);
             fws_frame_info *hf = (fws_frame_info *)(m->hmeta + desc_bytes + res_bytes);
-            const uint32_t target = m->ctr_total + nseg, seq = ++m->seq;
+            const uint32_t seq = ++m->seq;
             if ((r = fws_launch_decode_segments(m->hbuf, (const fws_seg_desc *)m->hmeta, nseg, hf, hr, st, m->dctr,
-                                                target, m->hflag, seq)))
+                                                nseg, m->hflag, seq)))
                 return r;
-            m->ctr_total = target;
             if ((r = fws_wait_flag(m->hflag, seq, st))) return r;
         } else {
             fws_decode_result *dres = (fws_decode_result *)(m->dmeta + desc_bytes);

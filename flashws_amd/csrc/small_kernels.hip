@@ -190,8 +190,10 @@ __device__ __forceinline__ void decode_segment(uint8_t *__restrict__ batch, cons
 // stores, the workgroup meets, and one lane releases at system scope and
 // stores `seq` to the flag in host memory. With a counter (several
 // workgroups), each workgroup releases and counts; the one completing the
-// count stores the flag. The counter is monotonic across launches (the host
-// passes the value this launch completes).
+// count (target = the launch's workgroups) stores 0 back and then the flag, so
+// every launch starts from 0 whatever an earlier launch's host-side status said
+// (a monotonic count drifted for good after one misreported launch;
+// launches on the mux's one stream never overlap).
 __device__ __forceinline__ void host_done(uint32_t *ctr, uint32_t target, uint32_t *flag, uint32_t seq) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -202,6 +204,7 @@ __device__ __forceinline__ void host_done(uint32_t *ctr, uint32_t target, uint32
         const uint32_t v = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) + 1u;
         if (v != target) return;
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "");
+        __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     __hip_atomic_store(flag, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }

@@ -56,7 +56,9 @@
 // Zero copy (default on): each read buffer the loop hands over is a MemPool
 // slot (RequestBuf, buffer_manager.h:90-95 -> MemPool::allocate, flash_alloc.h:
 // 137-244: a power-of-two slot inside a block the pool never frees); the hook
-// registers every slot it sees once (fws_gpu_host_register), and the GPU then
+// registers every slot it sees once (fws_gpu_host_register) over the extent
+// the pool's own metadata records for it (a buffer the pool does not know is
+// staged, never registered on a guess), and the GPU then
 // decodes the read where it lies -- no copy into pinned staging and back
 // (rx_session.cpp: reads whose parts start on the 16-B chunk grid and need no
 // staged header bytes). SetZeroCopy(false) keeps every read staged.
@@ -200,12 +202,16 @@ public:
         for (uint8_t *p : registered_) (void)fws_gpu_host_unregister(p);
     }
 
-    // Register the read buffers for in-place decode (default), or not.
+    // Register the read buffers for in-place decode (default), or not. Only
+    // buffers the reference's MemPool allocated (RequestBuf) are registered, each
+    // over the slot the pool recorded for it (PoolSlot); any other IOBuffer is
+    // staged through pinned memory as with SetZeroCopy(false).
     void SetZeroCopy(bool on) { zero_copy_ = on; }
 
     size_t connections() const { return conns_.size(); }
     uint64_t gpu_reads() const { return gpu_reads_; }
     uint64_t gpu_batches() const { return gpu_batches_; }
+    size_t zero_copy_slots() const { return registered_.size(); }   // MemPool slots decoded in place
 
 private:
     static constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
@@ -399,15 +405,34 @@ private:
         for (USock *u : d) delete_fd_(static_cast<void *>(u));   // FLoop::DeleteFd: a no-op if gone
     }
 
-    // A read buffer's MemPool slot, registered once (the pool never frees its
-    // blocks, so the registration stays valid; flash_alloc.h:137-244).
+    // The pool's own record of a live allocation (register only what is
+    // proven to be a MemPool slot): MemPool::allocate records every allocation of
+    // >= 1 KiB in mem_meta_map_ with its size class (flash_alloc.h:145-157, 201-212),
+    // and the slot is power2 = 1 << log2 bytes of memory_buffers_[log2], which the
+    // pool never frees (only deallocate's index stack changes, :286-321). A buffer
+    // that is not in the map (not from RequestBuf, buffer_manager.h:90-95) is staged.
+    struct PoolSlot : fws::MemPool {
+        static bool Extent(const void *p, size_t &bytes) {
+            fws::MemPool &pool = fws::MemPoolEnv::instance();
+            const auto &meta = pool.*(&PoolSlot::mem_meta_map_);   // protected: via a pointer to member
+            const auto it = meta.find(const_cast<void *>(p));
+            if (it == meta.end() || it->second.log2 >= 48) return false;
+            bytes = size_t(1) << it->second.log2;
+            return true;
+        }
+    };
+
+    // A read buffer's MemPool slot, registered once over its exact extent (the
+    // pool never frees its blocks, so the registration stays valid and the range
+    // never changes owner outside the pool).
     void EnsureRegistered(const fws::IOBuffer &b) {
         if (!zero_copy_ || !b.data || b.capacity < 4096) return;
         if (registered_.count(b.data) || unregistrable_.count(b.data)) return;
-        size_t slot = 4096;
-        while (slot < b.capacity) slot <<= 1;              // RoundUpPow2 of the request (MemPool::allocate)
-        if (fws_gpu_host_register(b.data, slot) == 0) registered_.insert(b.data);
-        else unregistrable_.insert(b.data);              // staged from then on
+        size_t slot = 0;
+        if (PoolSlot::Extent(b.data, slot) && slot >= b.capacity && fws_gpu_host_register(b.data, slot) == 0)
+            registered_.insert(b.data);
+        else
+            unregistrable_.insert(b.data);               // staged from then on
     }
 
     // ws_server_socket.h:172-196 with OnRecvData on the GPU.

@@ -17,6 +17,7 @@ import orc
 from flashws_amd import gpu
 from test_gpu_mux import _random_stream
 from test_gpu_session import _out_matches, session_view
+from wsframes import frame
 
 pytestmark = pytest.mark.gpu
 
@@ -115,3 +116,56 @@ def test_mux_in_place_random_vs_sessions(ictx, arena):
     mux.close()
     for s in ref:
         s.close()
+
+
+def _declined_reads(rng, n_tiny):
+    """A continuation of 48 B (a multiple of 16, so the header stream after it
+    stays on the 16-B grid) followed by n_tiny frames of 0-6 B payload: more
+    than kSmallFrames (256) headers, so the in-place one-launch decode declines
+    and the parallel decode runs on the registered bytes (rx_session.cpp, the
+    FWS_SMALL_DECLINED branch after k_decode_one)."""
+    big = frame(2, rng.integers(0, 256, 1000, dtype=np.uint8).tobytes(), key=int(rng.integers(0, 2**32)))
+    tiny = b"".join(frame(int(rng.choice([1, 2])), rng.integers(0x20, 0x7F, int(rng.integers(0, 7)),
+                                                                 dtype=np.uint8).tobytes(),
+                          key=int(rng.integers(0, 2**32))) for _ in range(n_tiny))
+    return [big[:-48], big[-48:] + tiny]
+
+
+@pytest.mark.parametrize("n_tiny", [300, 2000])
+def test_session_in_place_declined_small_read(ictx, arena, n_tiny):
+    """the declined in-place path (continuation unmasked in place by
+    k_decode_one, then the parallel decode on the registered alias) against an
+    unregistered session fed the same reads."""
+    rng = np.random.default_rng(900 + n_tiny)
+    reads = _declined_reads(rng, n_tiny)
+    s, ref = gpu.RxSession(ictx), gpu.RxSession(ictx)
+    for rd in reads:
+        ret, buf, ev, ctl = s.feed(rd, arena=arena, align_off=0)
+        eret, ebuf, eev, ectl = ref.feed(rd)
+        assert ret == eret == 0
+        assert bytes(buf) == bytes(ebuf)
+        assert session_view(ev, ctl) == session_view(eev, ectl)
+    assert len(ev) >= n_tiny                             # an event per tiny frame at least
+    s.close()
+    ref.close()
+
+
+@pytest.mark.parametrize("zc", ["copy", "zero-copy"])
+def test_mux_in_place_declined_small_read(ictx, arena, zc, monkeypatch):
+    """The same reads on three connections of one mux (registered, in place),
+    against unregistered standalone sessions."""
+    monkeypatch.setenv("FWS_MUX_ZC_MAX", "0" if zc == "copy" else str(1 << 40))
+    rng = np.random.default_rng(77)
+    conns = [_declined_reads(rng, k) for k in (300, 40, 1200)]
+    mux = gpu.RxMux(ictx, len(conns))
+    ref = [gpu.RxSession(ictx) for _ in conns]
+    for r in range(2):
+        got = mux.feed([(i, conns[i][r]) for i in range(len(conns))], arena=arena)
+        for i, (ret, buf, ev, ctl) in enumerate(got):
+            eret, ebuf, eev, ectl = ref[i].feed(conns[i][r])
+            assert ret == eret == 0, (i, r)
+            assert bytes(buf) == bytes(ebuf), (i, r)
+            assert session_view(ev, ctl) == session_view(eev, ectl), (i, r)
+    mux.close()
+    for x in ref:
+        x.close()

@@ -31,8 +31,9 @@ def oracle_unmask_regions(buf, descs):
 
 @pytest.fixture(params=["any", "plan"])
 def batch_path(request):
-    """fws_gpu_unmask_batch's two forms: one launch, descriptor-major
-    (k_unmask_any + queued pieces, the default) and k_plan + k_unmask_desc."""
+    """fws_gpu_unmask_batch's two forms: k_plan + k_unmask_desc (the default)
+    and one launch, descriptor-major (k_unmask_any + queued pieces; opt-in
+    through fws_internal_set_unmask_any(1))."""
     L = _lib.lib()
     old = L.fws_internal_set_unmask_any(1 if request.param == "any" else 0)
     yield request.param

@@ -44,13 +44,13 @@ int fws_ctx_ensure_plan(fws_gpu_ctx *ctx, uint64_t frames, uint64_t units) {
     if ((r = dev_alloc(&ctx->plan.unit_first, units + 2))) return r;
     if ((r = dev_alloc(&ctx->plan.unit_rec, 4 * (units + 2)))) return r;
     if ((r = dev_alloc(&ctx->plan.total, 2))) return r;
-    if ((r = dev_alloc(&ctx->plan.status, frames / 64 + 2))) return r;
+    if ((r = dev_alloc(&ctx->plan.status, frames / 8 + 2))) return r;
     if ((r = dev_alloc(&ctx->plan.ticket, 2))) return r;
     if ((r = dev_alloc(&ctx->plan.mode, sizeof(fws_plan_mode) / 8))) return r;
-    if ((r = fws_hip_status(hipMemset(ctx->plan.status, 0, (frames / 64 + 2) * 8)))) return r;
+    if ((r = fws_hip_status(hipMemset(ctx->plan.status, 0, (frames / 8 + 2) * 8)))) return r;
     if ((r = fws_hip_status(hipMemset(ctx->plan.ticket, 0, 8)))) return r;
     if ((r = fws_hip_status(hipMemset(ctx->plan.mode, 0, sizeof(fws_plan_mode))))) return r;
-    ctx->plan.status_cap = frames / 64 + 2;
+    ctx->plan.status_cap = frames / 8 + 2;             // k_tx_one: >= 8 frames per workgroup
     ctx->plan.epoch = 0;
     ctx->cap_frames = frames;
     ctx->cap_units = units;

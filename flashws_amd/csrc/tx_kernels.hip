@@ -19,7 +19,7 @@
 // on a frame seam are built bytewise. HBM bytes = payload read + frames written.
 #include "fws_device.h"
 #include "fws_internal.h"
-#include "plan_common.h"
+#include "outplan_common.h"    // out_size; plan_common.h: the look-back
 
 namespace fwsk {
 
@@ -161,6 +161,113 @@ __device__ __forceinline__ void tx_store_tail(uint8_t *out, uint64_t a, uint64_t
     for (uint64_t b = a; b < total && b < a + 16u; ++b) out[b] = (uint8_t)(xw[(b - a) >> 2] >> (8u * ((b - a) & 3u)));
 }
 
+// One 4 KiB output unit of a wave: lane chunks a0 + 1024 j (j < 4). Frames flo
+// .. fhi (indices into d / obase, which may be global or a workgroup's LDS copy)
+// cover the unit; chunks at or past own_end belong to another unit owner and are
+// skipped; no byte at or past total is written.
+template <typename DescP, typename OffP>
+__device__ __forceinline__ void tx_unit(uint8_t *__restrict__ out, const uint8_t *__restrict__ src, DescP d,
+                                        OffP obase, uint32_t flo, uint32_t fhi, const fws_tx_desc &dA,
+                                        const fws_tx_desc &dB, uint64_t OA, uint64_t OB, uint64_t a0,
+                                        uint64_t own_end, uint64_t total) {
+    if (fhi - flo >= 2u) {                             // small frames: bytewise with a search
+        for (int j = 0; j < 4; ++j) {
+            const uint64_t a = a0 + (uint64_t)j * 1024u;
+            if (a >= own_end) break;
+            const uint32_t f = find_frame(obase, flo, fhi, a);
+            tx_bytes(out, src, d, obase, f, a, total);
+        }
+        return;
+    }
+    // at most two frames: uniform metadata (dA, dB = d[flo], d[fhi] at OA, OB);
+    // payload k of frame X covers [PX, EX)
+    TxSeam z;
+    z.PA = OA + tx_hdr_len(dA);
+    z.EA = z.PA + dA.len;
+    z.PB = OB + tx_hdr_len(dB);
+    z.EB = z.PB + dB.len;
+    const bool two = fhi != flo;
+    const bool any_pay = dA.len != 0 || (two && dB.len != 0);          // wave-uniform
+    const uint8_t *const safe = src + (dA.len != 0 ? dA.src_off : dB.src_off);
+    const uintptr_t safe16 = (uintptr_t)safe & ~uintptr_t(15);
+    const uintptr_t SA = (uintptr_t)(src + dA.src_off) - (uintptr_t)z.PA;   // src of output byte a: S + a
+    const uintptr_t SB = (uintptr_t)(src + dB.src_off) - (uintptr_t)z.PB;
+    uintptr_t sb[4];
+    uint32_t sh[4], rk[4];
+    uint32_t full = 0, seam = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint64_t a = a0 + (uint64_t)j * 1024u;
+        const bool own = a < own_end;
+        const bool inA = own && a >= z.PA && a + 16 <= z.EA;
+        const bool inB = own && two && a >= z.PB && a + 16 <= z.EB;
+        if (inA || inB) full |= 1u << j;
+        else if (own && a < total) seam |= 1u << j;
+        const uintptr_t sa = (inB ? SB : SA) + (uintptr_t)a;
+        sb[j] = (inA || inB) ? (sa & ~uintptr_t(15)) : safe16;
+        sh[j] = (uint32_t)(sa & 15u);
+        const fws_tx_desc &dx = inB ? dB : dA;
+        const uint32_t ph = (uint32_t)(a - (inB ? z.PB : z.PA));
+        rk[j] = dx.masked ? rotr32(dx.key, 8u * (ph & 3u)) : 0u;
+    }
+    // one batch of loads: the full chunks' two aligned source blocks and the
+    // A and B source blocks of this lane's first seam chunk
+    u32x4 v0[4], v1[4], sa0, sa1, sb0, sb1;
+    const int js = seam ? __builtin_ctz(seam) : 0;
+    const uint64_t as = a0 + (uint64_t)js * 1024u;
+    const uintptr_t sA0 = (uintptr_t)(src + dA.src_off), sB0 = (uintptr_t)(src + dB.src_off);
+    uintptr_t qa0, qa1, qb0, qb1;
+    uint32_t sha, shb;
+    tx_seam_blocks(as, SA, sA0, dA.len, safe16, qa0, qa1, sha);
+    tx_seam_blocks(as, SB, sB0, two ? dB.len : 0, safe16, qb0, qb1, shb);
+    if (any_pay) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            // default-policy loads: the second block of lane L is the first of lane
+            // L + 1, so it must stay in cache (a nontemporal pair reads it twice)
+            uintptr_t s1 = sh[j] && ((full >> j) & 1u) ? sb[j] + 16u : sb[j];
+            asm volatile("" : "+v"(s1));            // opaque: no "same address as v0" copy
+            v0[j] = gload16<false>(sb[j]);          // (a copy would wait for the load)
+            v1[j] = gload16<false>(s1);
+        }
+        sa0 = gload16<false>(qa0);
+        sa1 = gload16<false>(qa1);
+        sb0 = gload16<false>(qb0);
+        sb1 = gload16<false>(qb1);
+        __builtin_amdgcn_sched_barrier(0);          // keep every load ahead of the first use
+    } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v0[j] = v1[j] = u32x4{0u, 0u, 0u, 0u};
+        sa0 = sa1 = sb0 = sb1 = u32x4{0u, 0u, 0u, 0u};
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+        if ((full >> j) & 1u)
+            gstore16<true>((uintptr_t)(out + a0 + (uint64_t)j * 1024u), tx_shr_bytes(v0[j], v1[j], sh[j]) ^ rk[j]);
+    auto seam_chunk = [&](uint64_t a, const u32x4 &A0, const u32x4 &A1, uint32_t shA, const u32x4 &B0,
+                          const u32x4 &B1, uint32_t shB) {
+        const uint32_t rka = dA.masked ? rotr32(dA.key, 8u * ((uint32_t)(a - z.PA) & 3u)) : 0u;
+        const uint32_t rkb = dB.masked ? rotr32(dB.key, 8u * ((uint32_t)(a - z.PB) & 3u)) : 0u;
+        const u32x4 x = tx_seam_combine(a, dA, OA, dB, OB, two, z, total, tx_shr_bytes(A0, A1, shA) ^ rka,
+                                        tx_shr_bytes(B0, B1, shB) ^ rkb);
+        if (a + 16u <= total) gstore16<true>((uintptr_t)(out + a), x);
+        else tx_store_tail(out, a, total, x);
+    };
+    if (seam) {
+        seam_chunk(as, sa0, sa1, sha, sb0, sb1, shb);
+        seam &= seam - 1u;
+    }
+    if (!__any(seam)) return;                          // a lane with a second seam chunk (rare)
+#pragma unroll 1
+    for (int j = 0; j < 4; ++j) {
+        if (!((seam >> j) & 1u)) continue;
+        const uint64_t a = a0 + (uint64_t)j * 1024u;
+        tx_seam_blocks(a, SA, sA0, dA.len, safe16, qa0, qa1, sha);
+        tx_seam_blocks(a, SB, sB0, two ? dB.len : 0, safe16, qb0, qb1, shb);
+        seam_chunk(a, gload16<true>(qa0), gload16<true>(qa1), sha, gload16<true>(qb0), gload16<true>(qb1), shb);
+    }
+}
+
 __device__ __forceinline__ void tx_encode_body(uint8_t *__restrict__ out, const uint8_t *__restrict__ src,
                                                       const fws_tx_desc *__restrict__ d, uint32_t n,
                                                       const uint64_t *__restrict__ obase,
@@ -182,103 +289,98 @@ __device__ __forceinline__ void tx_encode_body(uint8_t *__restrict__ out, const 
         }
         const uint32_t flo = uf0;
         const uint32_t fhi = (u + 1 < n_units) ? uf1 : n - 1;
-        const uint64_t a0 = u * kTxUnit + (uint64_t)lane * 16u;
-        if (fhi - flo >= 2u) {                         // small frames: bytewise with a search
-            for (int j = 0; j < 4; ++j) {
-                const uint64_t a = a0 + (uint64_t)j * 1024u;
-                if (a >= total) break;
-                const uint32_t f = find_frame(obase, flo, fhi, a);
-                tx_bytes(out, src, d, obase, f, a, total);
-            }
-            continue;
-        }
-        // at most two frames: uniform metadata; payload k of frame X covers [PX, EX)
-        const fws_tx_desc dA = d[flo], dB = d[fhi];
-        const uint64_t OA = obase[flo], OB = obase[fhi];
-        TxSeam z;
-        z.PA = OA + tx_hdr_len(dA);
-        z.EA = z.PA + dA.len;
-        z.PB = OB + tx_hdr_len(dB);
-        z.EB = z.PB + dB.len;
-        const bool two = fhi != flo;
-        const bool any_pay = dA.len != 0 || (two && dB.len != 0);          // wave-uniform
-        const uint8_t *const safe = src + (dA.len != 0 ? dA.src_off : dB.src_off);
-        const uintptr_t safe16 = (uintptr_t)safe & ~uintptr_t(15);
-        const uintptr_t SA = (uintptr_t)(src + dA.src_off) - (uintptr_t)z.PA;   // src of output byte a: S + a
-        const uintptr_t SB = (uintptr_t)(src + dB.src_off) - (uintptr_t)z.PB;
-        uintptr_t sb[4];
-        uint32_t sh[4], rk[4];
-        uint32_t full = 0, seam = 0;
+        tx_unit(out, src, d, obase, flo, fhi, d[flo], d[fhi], obase[flo], obase[fhi], u * kTxUnit + (uint64_t)lane * 16u,
+                total, total);
+    }
+}
+
+// ------------------------------------------------------------ one launch
+// fws_gpu_encode_frames without the plan launch (r05): frame-major. Workgroup
+// b (in ticket order) takes frames [F b, F b + F): one block scan of their
+// sizes (+ up to kTxLook frames after them, whose bytes can share the span's
+// last 16-B chunk), a decoupled look-back over the workgroups' sums for the
+// span's output offset O0 (plan_common.h: the k_out_plan words), then the
+// span's 16-B chunks whose first byte lies in [O0, O1) in 4 KiB units, one per
+// wave at a time, through tx_unit with the frames' descriptors and offsets in
+// LDS. Every chunk has one owner (the workgroup holding its first byte), so
+// all but the batch's last chunk are full 16-B stores.
+__device__ __forceinline__ uint64_t sgpr64(uint64_t v) {   // a wave-uniform value into SGPRs
+    return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
+           __builtin_amdgcn_readfirstlane((uint32_t)v);
+}
+__device__ __forceinline__ void sgpr_copy(const fws_tx_desc &x, fws_tx_desc &y) {
+    static_assert(sizeof(fws_tx_desc) == 24, "6 words");
+    const uint32_t *a = reinterpret_cast<const uint32_t *>(&x);
+    uint32_t *b = reinterpret_cast<uint32_t *>(&y);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const uint64_t a = a0 + (uint64_t)j * 1024u;
-            const bool inA = a >= z.PA && a + 16 <= z.EA;
-            const bool inB = two && a >= z.PB && a + 16 <= z.EB;
-            if (inA || inB) full |= 1u << j;
-            else if (a < total) seam |= 1u << j;
-            const uintptr_t sa = (inB ? SB : SA) + (uintptr_t)a;
-            sb[j] = (inA || inB) ? (sa & ~uintptr_t(15)) : safe16;
-            sh[j] = (uint32_t)(sa & 15u);
-            const fws_tx_desc &dx = inB ? dB : dA;
-            const uint32_t ph = (uint32_t)(a - (inB ? z.PB : z.PA));
-            rk[j] = dx.masked ? rotr32(dx.key, 8u * (ph & 3u)) : 0u;
-        }
-        // one batch of loads: the full chunks' two aligned source blocks and the
-        // A and B source blocks of this lane's first seam chunk
-        u32x4 v0[4], v1[4], sa0, sa1, sb0, sb1;
-        const int js = seam ? __builtin_ctz(seam) : 0;
-        const uint64_t as = a0 + (uint64_t)js * 1024u;
-        const uintptr_t sA0 = (uintptr_t)(src + dA.src_off), sB0 = (uintptr_t)(src + dB.src_off);
-        uintptr_t qa0, qa1, qb0, qb1;
-        uint32_t sha, shb;
-        tx_seam_blocks(as, SA, sA0, dA.len, safe16, qa0, qa1, sha);
-        tx_seam_blocks(as, SB, sB0, two ? dB.len : 0, safe16, qb0, qb1, shb);
-        if (any_pay) {
+    for (int i = 0; i < 6; ++i) b[i] = __builtin_amdgcn_readfirstlane(a[i]);
+}
+
+constexpr uint32_t kTxLook = 8;        // frames >= 2 B: 8 of them cover a chunk's 15 bytes past O1
+constexpr uint32_t kTxOneMaxF = kBlock - kTxLook;
+
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) void k_tx_one(
+    uint8_t *__restrict__ out, const uint8_t *__restrict__ src, const fws_tx_desc *__restrict__ d, uint32_t n,
+    uint32_t F, uint64_t out_cap, uint64_t *__restrict__ out_len, uint64_t *__restrict__ status,
+    uint32_t *__restrict__ ticket, uint32_t epoch) {
+    __shared__ fws_tx_desc s_d[kBlock];
+    __shared__ uint64_t s_ob[kBlock + 1];
+    __shared__ uint64_t s_wsum[kBlock / kWave];
+    const uint32_t blk = plan_block_order(ticket);
+    const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+    const uint64_t fb = (uint64_t)blk * F;
+    const uint32_t nf = (uint32_t)(n - fb < F ? n - fb : F);                     // this span's frames
+    const uint32_t nl = (uint32_t)(n - fb < (uint64_t)nf + kTxLook ? n - fb : nf + kTxLook);   // + look-ahead
+    uint64_t sz = 0;
+    if (threadIdx.x < nl) {
+        const fws_tx_desc x = d[fb + threadIdx.x];
+        s_d[threadIdx.x] = x;
+        sz = out_size(x);
+    }
+    const uint64_t inc = wave_incl_scan64(sz, lane);
+    if (lane == kWave - 1) s_wsum[w] = inc;
+    __syncthreads();
+    uint64_t rel = inc - sz;                           // offset of frame t from O0
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                // default-policy loads: the second block of lane L is the first of lane
-                // L + 1, so it must stay in cache (a nontemporal pair reads it twice)
-                uintptr_t s1 = sh[j] && ((full >> j) & 1u) ? sb[j] + 16u : sb[j];
-                asm volatile("" : "+v"(s1));            // opaque: no "same address as v0" copy
-                v0[j] = gload16<false>(sb[j]);          // (a copy would wait for the load)
-                v1[j] = gload16<false>(s1);
-            }
-            sa0 = gload16<false>(qa0);
-            sa1 = gload16<false>(qa1);
-            sb0 = gload16<false>(qb0);
-            sb1 = gload16<false>(qb1);
-            __builtin_amdgcn_sched_barrier(0);          // keep every load ahead of the first use
-        } else {
+    for (int i = 0; i < kBlock / kWave; ++i) rel += i < w ? s_wsum[i] : 0;
+    if (threadIdx.x <= nl) s_ob[threadIdx.x] = rel;    // t = nl: the end of the loaded frames
+    __syncthreads();
+    const uint64_t agg = sgpr64(s_ob[nf]);             // the span's own bytes
+    bool unused;
+    const uint64_t O0 = sgpr64(block_lookback(status, blk, agg, true, epoch, &unused));
+    const uint64_t O1 = O0 + agg, Lend = O0 + sgpr64(s_ob[nl]);
+    const bool last = fb + nf >= n;
+    if (last && threadIdx.x == 0) *out_len = O1 <= out_cap ? O1 : ~0ull;
+    __syncthreads();                                   // every thread read s_ob[nf], s_ob[nl]
+    if (threadIdx.x <= nl) s_ob[threadIdx.x] += O0;
+    __syncthreads();
+    // bytes past the batch (Lend = O1 for the last span) and past out_cap are never written
+    const uint64_t clip = Lend < out_cap ? Lend : out_cap;
+    const uint64_t A0 = (O0 + 15u) & ~uint64_t(15);    // first chunk whose first byte is ours
+    const uint64_t n_units = O1 > A0 ? (O1 - A0 + kTxUnit - 1) / kTxUnit : 0;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    for (uint64_t k = wave; k < n_units; k += kBlock / kWave) {
+        const uint64_t U0 = A0 + k * kTxUnit;
+        if (U0 >= clip) break;                         // wave-uniform
+        const uint64_t Ue = (U0 + kTxUnit < clip ? U0 + kTxUnit : clip) - 1u;   // the unit's last byte
+        // the frames holding U0 and Ue: count the offsets <= pos (nl + 1 of them, 4 per lane)
+        uint32_t flo = 0, fhi = 0;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) v0[j] = v1[j] = u32x4{0u, 0u, 0u, 0u};
-            sa0 = sa1 = sb0 = sb1 = u32x4{0u, 0u, 0u, 0u};
+        for (int q = 0; q < kBlock / kWave; ++q) {
+            const uint32_t i = (uint32_t)q * kWave + (uint32_t)lane;
+            const uint64_t o = i < nl ? s_ob[i] : ~0ull;
+            flo += (uint32_t)__popcll(__ballot(o <= U0));
+            fhi += (uint32_t)__popcll(__ballot(o <= Ue));
         }
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-            if ((full >> j) & 1u)
-                gstore16<true>((uintptr_t)(out + a0 + (uint64_t)j * 1024u), tx_shr_bytes(v0[j], v1[j], sh[j]) ^ rk[j]);
-        auto seam_chunk = [&](uint64_t a, const u32x4 &A0, const u32x4 &A1, uint32_t shA, const u32x4 &B0,
-                              const u32x4 &B1, uint32_t shB) {
-            const uint32_t rka = dA.masked ? rotr32(dA.key, 8u * ((uint32_t)(a - z.PA) & 3u)) : 0u;
-            const uint32_t rkb = dB.masked ? rotr32(dB.key, 8u * ((uint32_t)(a - z.PB) & 3u)) : 0u;
-            const u32x4 x = tx_seam_combine(a, dA, OA, dB, OB, two, z, total, tx_shr_bytes(A0, A1, shA) ^ rka,
-                                            tx_shr_bytes(B0, B1, shB) ^ rkb);
-            if (a + 16u <= total) gstore16<true>((uintptr_t)(out + a), x);
-            else tx_store_tail(out, a, total, x);
-        };
-        if (seam) {
-            seam_chunk(as, sa0, sa1, sha, sb0, sb1, shb);
-            seam &= seam - 1u;
-        }
-        if (!__any(seam)) continue;                    // a lane with a second seam chunk (rare)
-#pragma unroll 1
-        for (int j = 0; j < 4; ++j) {
-            if (!((seam >> j) & 1u)) continue;
-            const uint64_t a = a0 + (uint64_t)j * 1024u;
-            tx_seam_blocks(a, SA, sA0, dA.len, safe16, qa0, qa1, sha);
-            tx_seam_blocks(a, SB, sB0, two ? dB.len : 0, safe16, qb0, qb1, shb);
-            seam_chunk(a, gload16<true>(qa0), gload16<true>(qa1), sha, gload16<true>(qb0), gload16<true>(qb1), shb);
-        }
+        flo -= 1u;
+        fhi -= 1u;
+        // the two frames' words from LDS into SGPRs (wave-uniform; LDS loads land in VGPRs)
+        fws_tx_desc dA, dB;
+        sgpr_copy(s_d[flo], dA);
+        sgpr_copy(s_d[fhi], dB);
+        const uint64_t OA = sgpr64(s_ob[flo]), OB = sgpr64(s_ob[fhi]);
+        tx_unit(out, src, (const fws_tx_desc *)s_d, (const uint64_t *)s_ob, flo, fhi, dA, dB, OA, OB,
+                U0 + (uint64_t)lane * 16u, O1, clip);
     }
 }
 
@@ -319,6 +421,20 @@ extern "C" __attribute__((visibility("default"))) int fws_internal_set_tx_w5(int
     return old;
 }
 
+// tuning hook: the one-launch form k_tx_one (1, the default for batches whose
+// frames average <= kTxOneMaxAvg bytes of out_cap; 2 = for every batch, tests)
+// or plan + encode (0); and the output bytes per k_tx_one workgroup (its frames
+// F = span / average frame)
+static int g_tx_one = 1;
+static uint64_t g_tx_one_span = 64u << 10;
+constexpr uint64_t kTxOneMaxAvg = 16u << 10;
+extern "C" __attribute__((visibility("default"))) int fws_internal_set_tx_one(int on, int span_kib) {
+    const int old = g_tx_one;
+    g_tx_one = on < 0 ? 0 : (on > 2 ? 2 : on);
+    if (span_kib > 0) g_tx_one_span = (uint64_t)span_kib << 10;
+    return old;
+}
+
 using namespace fwsk;
 
 extern "C" {
@@ -345,6 +461,22 @@ int fws_gpu_encode_frames(fws_gpu_ctx *ctx, void *dev_out, uint64_t out_cap, con
     if (r) return r;
     if (n == 0) return fws_hip_status(hipMemsetAsync(dev_out_len, 0, sizeof(uint64_t), s));
     const uint64_t units = out_cap / kTxUnit + 2;
+    const uint64_t avg = out_cap / n;
+    if (g_tx_one == 2 || (g_tx_one == 1 && avg <= kTxOneMaxAvg)) {
+        // one launch: ~g_tx_one_span output bytes (F frames) per workgroup
+        if ((r = fws_ctx_ensure_plan(ctx, n, 2))) return r;
+        fws_plan_ws &ws = ctx->plan;
+        uint64_t F = g_tx_one_span / (avg ? avg : 1u);
+        if (F < 8u) F = 8u;
+        if (F > kTxOneMaxF) F = kTxOneMaxF;
+        const uint64_t nb = (n + F - 1) / F;
+        if (nb > ws.status_cap || nb > (1u << 30)) return FWS_ERR_CAPACITY;
+        if ((r = fws_plan_next_epoch(ws, s))) return r;
+        hipLaunchKernelGGL(k_tx_one, dim3((unsigned)nb), dim3(kBlock), 0, s, (uint8_t *)dev_out,
+                           (const uint8_t *)dev_src, dev_descs, n, (uint32_t)F, out_cap, dev_out_len, ws.status,
+                           ws.ticket, ws.epoch);
+        return fws_hip_status(hipGetLastError());
+    }
     if ((r = fws_ctx_ensure_plan(ctx, n, units))) return r;
     fws_plan_ws &ws = ctx->plan;
     if ((r = fws_launch_tx_plan(dev_descs, n, ws, out_cap, dev_out_len, s))) return r;

@@ -326,8 +326,11 @@ void fws_tx_next(uint32_t frame_type, int last_frame_if_possible, uint8_t *last_
                  uint8_t *fin);
 
 /* dev_out (16-B aligned) = the frames of dev_descs[0..n) back to back;
- * *dev_out_len (device u64) = their total size, or ~0 if it exceeds out_cap
- * (then nothing is written). One launch sequence for any mix of sizes. */
+ * *dev_out_len (device u64) = their total size, or ~0 if it exceeds out_cap.
+ * No byte at or past out_cap is ever written; when the total exceeds out_cap
+ * the bytes below it are unspecified (the one-launch form writes the frames
+ * that fit). One launch (k_tx_one) when the frames average <= 16 KiB of
+ * out_cap, else plan + encode. */
 int fws_gpu_encode_frames(fws_gpu_ctx *ctx, void *dev_out, uint64_t out_cap, const void *dev_src,
                           const fws_tx_desc *dev_descs, uint32_t n, uint64_t *dev_out_len, void *stream);
 

@@ -6,7 +6,8 @@ SendFrame bytes (net/w_socket.h:832-944), bit-exact.
 * random batches vs the oracle's orc_tx_frame: every length form, masked and
   unmasked frames mixed, payloads at arbitrary source offsets, batches of tiny
   frames (the bytewise path) and large ones (the shifted 16-B path);
-* capacity overflow (~0, nothing written), the empty batch;
+* capacity overflow (~0; nothing at or past out_cap, and with the plan form
+  nothing at all), the empty batch; both forms (one launch, plan + encode);
 * round trip: client frames encoded here, decoded by fws_gpu_decode_stream.
 """
 import numpy as np
@@ -19,6 +20,16 @@ from flashws_amd._lib import TX_DESC
 from test_tx_cpu import SESSIONS, frame_matches, tx_payload
 
 pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True, params=["one", "plan"])
+def tx_form(request):
+    """every test runs on both forms of fws_gpu_encode_frames: one launch
+    (k_tx_one, forced for every batch) and k_out_plan + k_tx_encode"""
+    from flashws_amd._lib import lib
+    old = lib().fws_internal_set_tx_one(2 if request.param == "one" else 0, 0)
+    yield request.param
+    lib().fws_internal_set_tx_one(old, 0)
 
 
 def build_batch(payloads, metas, rng, gap_max=40):
@@ -39,12 +50,14 @@ def encode(ctx, cuda, src, d, out_cap=None, fill=0xEE):
     total = sum(int(x["len"]) + 2 + 4 * int(x["masked"]) + (0 if x["len"] < 126 else 2 if x["len"] < 65536 else 8)
                 for x in d)
     cap = total if out_cap is None else out_cap
-    out = torch.full((max(cap, 1),), fill, dtype=torch.uint8, device=cuda)
+    out = torch.full((max(cap, 1) + 64,), fill, dtype=torch.uint8, device=cuda)   # + a guard band
     dsrc = torch.from_numpy(src).to(cuda)
     dd = torch.from_numpy(d.view(np.uint8).copy()).to(cuda)
     ol = gpu.encode_frames(ctx, out[:cap] if cap else out[:0], dsrc, dd, len(d))
     torch.cuda.synchronize()
-    return out.cpu().numpy().tobytes(), int(ol.cpu().item()), total
+    o = out.cpu().numpy().tobytes()
+    assert o[max(cap, 1):] == bytes([fill]) * 64                               # nothing past out_cap
+    return o[:max(cap, 1)], int(ol.cpu().item()), total
 
 
 def oracle_frames(payloads, metas):
@@ -110,14 +123,20 @@ def test_encode_random_vs_oracle(ctx, cuda, mode):
         pytest.fail(f"{len(diff)} bytes differ, first at {diff[0]}")
 
 
-def test_encode_overflow_and_empty(ctx, cuda):
+def test_encode_overflow_and_empty(ctx, cuda, tx_form):
     rng = np.random.default_rng(9)
     payloads = [rng.integers(0, 256, 5000, dtype=np.uint8).tobytes() for _ in range(4)]
     metas = [(2, 1, 0x01020304, 1)] * 4
     src, d = build_batch(payloads, metas, rng)
-    out, got, total = encode(ctx, cuda, src, d, out_cap=4 * 5000)            # 32 bytes short
-    assert got == -1                                                           # ~0 as int64
-    assert out == b"\xEE" * len(out)                                           # nothing written
+    for cap in (4 * 5000, 5007, 17):                                           # 32 bytes short .. one frame
+        out, got, total = encode(ctx, cuda, src, d, out_cap=cap)
+        assert got == -1                                                       # ~0 as int64
+        if tx_form == "plan":
+            assert out == b"\xEE" * len(out)                                   # nothing written at all
+        else:                                                                  # the frames that fit, exact
+            exp = b"".join(oracle_frames(payloads, metas))
+            k = max(j for j in range(5) if sum(5008 for _ in range(j)) <= cap)
+            assert out[:5008 * k] == exp[:5008 * k]
     out, got, total = encode(ctx, cuda, src, d, out_cap=total)
     assert got == total
     # the empty batch: length 0

@@ -1,12 +1,13 @@
 #!/usr/bin/env python3
-"""A/B of k_tx_encode grid sizes on the bench's TX workload (C2 shape: 65 536 x
-4 KiB payloads framed + masked by fws_gpu_encode_frames): one wave per output
-unit (0, the default) against grid caps of k x the resident workgroups
-(fws_internal_set_tx_blocks), HIP events over back-to-back calls rotating four
-outputs, modes alternated in one process; outputs compared across modes. One
-JSON line per (mode, rep).
+"""A/B of fws_gpu_encode_frames forms on the bench's TX workload (C2 shape:
+65 536 x 4 KiB payloads framed + masked): k_out_plan + k_tx_encode ("plan")
+against the one-launch k_tx_one at several output spans per workgroup
+(fws_internal_set_tx_one), HIP events over back-to-back calls rotating four
+outputs, modes alternated in one process (order reversed every other
+repetition); outputs compared across modes. One JSON line per (mode, rep).
+(r04 used it for k_tx_encode grid caps, profiles/r04/ab_tx.jsonl.)
 
-usage: python tools/ab_tx.py [reps]"""
+usage: python tools/ab_tx.py [reps] [mode,mode,...]"""
 import json
 import os
 import sys
@@ -36,9 +37,18 @@ def main():
     outs = [torch.empty(total, dtype=torch.uint8, device=dev) for _ in range(4)]
     olen = torch.empty(1, dtype=torch.int64, device=dev)
     ref = None
+    modes = [("plan", 0, 0)] + [(f"one_span{k}k", 1, k) for k in (32, 64, 128, 256)]
+    if len(sys.argv) > 2:
+        modes = [m for m in modes if m[0] in sys.argv[2].split(",")]
+    # warm the clocks before the first timed mode (tools/c4_thermal_probe.py)
+    import time
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < 0.5:
+        gpu.encode_frames(c, outs[0], tsrc, tdd, n, out_len=olen)
+        torch.cuda.synchronize()
     for rep in range(3):
-        for blocks in (0, 2560, 5120, 7680, 10240):
-            L.fws_internal_set_tx_blocks(blocks)
+        for name, one, span in (modes if rep % 2 == 0 else modes[::-1]):
+            L.fws_internal_set_tx_one(one, span)
             for i in range(4):
                 gpu.encode_frames(c, outs[i % 4], tsrc, tdd, n, out_len=olen)
             torch.cuda.synchronize()
@@ -53,10 +63,10 @@ def main():
             if ref is None:
                 ref = got.clone()
             same = bool(torch.equal(ref, got))
-            print(json.dumps({"tx_blocks": blocks, "rep": rep, "ms": round(ms, 4),
+            print(json.dumps({"mode": name, "rep": rep, "ms": round(ms, 4),
                               "frac": round((n * pl + total) / ms / 1e-3 / 8e12, 4), "same_output": same}), flush=True)
             assert same
-    L.fws_internal_set_tx_blocks(0)
+    L.fws_internal_set_tx_one(1, 64)
     c.close()
 
 

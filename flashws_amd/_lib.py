@@ -84,6 +84,7 @@ SIGNATURES = [
     ("fws_gpu_ctx_create", _I, [_I, C.POINTER(C.c_void_p)]),
     ("fws_gpu_ctx_destroy", None, [_P]),
     ("fws_gpu_ctx_reserve", _I, [_P, _U64, _U64]),
+    ("fws_gpu_ctx_set_rx_persistent", _I, [_P, _U32]),
     ("fws_gpu_mask", _I, [_P, _U64, _U32, _P]),
     ("fws_gpu_unmask_batch", _I, [_P, _P, _P, _U32, _P]),
     ("fws_gpu_unmask_sorted", _I, [_P, _P, _P, _U32, _P]),

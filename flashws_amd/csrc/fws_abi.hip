@@ -116,6 +116,8 @@ int fws_gpu_ctx_create(int device, fws_gpu_ctx **out) {
 void fws_gpu_ctx_destroy(fws_gpu_ctx *ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
+    fws_rx_service_destroy(ctx->svc);    // its grid drained before the buffers it names go
+    ctx->svc = nullptr;
     free_plan(ctx->plan);
     dev_free(ctx->any_q);
     dev_free(ctx->any_cnt);

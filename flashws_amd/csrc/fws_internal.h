@@ -52,6 +52,48 @@ int fws_launch_decode_one(uint8_t *batch, const fws_seg_desc &d, fws_frame_info 
 // synchronize the stream (which also reports a failed launch)
 int fws_wait_flag(const volatile uint32_t *flag, uint32_t seq, hipStream_t s);
 
+// ---- the persistent receive service (r05; small_kernels.hip k_rx_service,
+// rx_session.cpp fws_rx_service): the small-read decodes of fws_rx_session and
+// fws_rx_mux without a kernel launch per read. One lingering grid: a poller
+// workgroup reads a mailbox in coherent pinned memory and republishes each
+// request in device memory; `workers` workgroups decode its segments
+// (decode_segment, as k_decode_segments does) and the last one stores the
+// request's host flag. state = (seq << 1) | running: the host publishes a
+// request by a CAS from (s, running) to (s + 1, running), and launches a new
+// grid when the running bit is clear; the poller clears it by a CAS after
+// `linger` ticks without a request (or once `life` ticks have passed), so an
+// idle grid always exits and a request is never lost between the two.
+struct fws_svc_req {
+    uint64_t base;                     // segment offsets are relative to it (mod 2^64)
+    uint64_t descs;                    // fws_seg_desc[nseg] (host or device memory), or 0: `one`
+    uint64_t frames;                   // fws_frame_info*
+    uint64_t res;                      // fws_decode_result[nseg]
+    uint64_t flag;                     // uint32_t* in host memory: flag_seq is stored there when done
+    uint32_t nseg, flag_seq, kind, pad;   // kind 1: quit
+    fws_seg_desc one;
+};
+static_assert(sizeof(fws_svc_req) % 8 == 0, "8-B words");
+struct alignas(128) fws_svc_mail {     // coherent pinned host memory
+    uint64_t state;
+    uint64_t pad[15];
+    fws_svc_req req;                   // written before the CAS that publishes its seq
+};
+struct alignas(128) fws_svc_dev {      // device memory, zeroed before each launch
+    uint32_t seq, quit, ctr, pad[29];
+    fws_svc_req req;
+};
+int fws_launch_rx_service(fws_svc_mail *mail, fws_svc_dev *dv, uint32_t seq0, uint32_t workers, uint64_t linger_ticks,
+                          uint64_t life_ticks, hipStream_t s);
+struct fws_rx_service;
+// the context's service (created on first use when enabled), or null: not enabled
+fws_rx_service *fws_ctx_rx_service(fws_gpu_ctx *ctx);
+void fws_rx_service_destroy(fws_rx_service *v);
+// one request through the service, waited for: segments [0, nseg) of `descs`
+// (or the one `*one`) relative to base; returns 0 once flag == flag_seq
+int fws_rx_service_run(fws_rx_service *v, uint8_t *base, const fws_seg_desc *descs, const fws_seg_desc *one,
+                       uint32_t nseg, fws_frame_info *frames, fws_decode_result *res, uint32_t *flag,
+                       uint32_t flag_seq);
+
 // Device workspace for the chunk plan of one descriptor batch.
 // Descriptor batches are planned two ways in one launch (k_plan): chunk space
 // (cbase / unit_first: any descriptor order) and byte space (unit_first_s:
@@ -162,6 +204,8 @@ struct fws_gpu_ctx {
     uint32_t *any_cnt = nullptr;      // 2 words: queue counts by call parity
     uint32_t any_qcap = 0;
     uint32_t any_parity = 0;
+    uint32_t svc_workers = 0;         // fws_gpu_ctx_set_rx_persistent: 0 = off
+    fws_rx_service *svc = nullptr;
 };
 int fws_ctx_ensure_seam(fws_gpu_ctx *ctx, uint64_t span);
 int fws_ctx_ensure_any(fws_gpu_ctx *ctx);             // the piece queue, sized from the reservation

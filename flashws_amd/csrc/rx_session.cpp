@@ -405,8 +405,12 @@ static int feed_impl(fws_rx_session *s, uint8_t *buf, uint64_t size, uint64_t bu
         d.L = (uint32_t)(rest ? L : 0);
         d.fcap = segcap;
         const uint32_t seq = ++s->seq;
-        if ((r = fws_launch_decode_one(dev, d, s->hframes, s->hres, st, s->hflag, seq))) return r;
-        if ((r = fws_wait_flag(s->hflag, seq, st))) return r;
+        if (fws_rx_service *v = fws_ctx_rx_service(s->ctx)) {          // the resident grid, no launch
+            if ((r = fws_rx_service_run(v, dev, nullptr, &d, 1, s->hframes, s->hres, s->hflag, seq))) return r;
+        } else {
+            if ((r = fws_launch_decode_one(dev, d, s->hframes, s->hres, st, s->hflag, seq))) return r;
+            if ((r = fws_wait_flag(s->hflag, seq, st))) return r;
+        }
         frames_here = true;
         if (rest && s->hres->status == FWS_SMALL_DECLINED) {
             if ((r = launch(dev + u, false))) return r;       // the parallel decode, in place
@@ -438,8 +442,12 @@ static int feed_impl(fws_rx_session *s, uint8_t *buf, uint64_t size, uint64_t bu
         d.fcap = segcap;
         d.fbase = 0;
         const uint32_t seq = ++s->seq;
-        if ((r = fws_launch_decode_one(s->hstage, d, s->hframes, s->hres, st, s->hflag, seq))) return r;
-        if ((r = fws_wait_flag(s->hflag, seq, st))) return r;
+        if (fws_rx_service *v = fws_ctx_rx_service(s->ctx)) {
+            if ((r = fws_rx_service_run(v, s->hstage, nullptr, &d, 1, s->hframes, s->hres, s->hflag, seq))) return r;
+        } else {
+            if ((r = fws_launch_decode_one(s->hstage, d, s->hframes, s->hres, st, s->hflag, seq))) return r;
+            if ((r = fws_wait_flag(s->hflag, seq, st))) return r;
+        }
         frames_here = true;
         if (rest && s->hres->status == FWS_SMALL_DECLINED) {
             // more than kSmallFrames headers: the parallel decode on the same bytes
@@ -760,10 +768,16 @@ int fws_rx_mux_feed(fws_rx_mux *m, const fws_rx_read *reads, uint32_t n, fws_rx_
             fws_decode_result *hr = (fws_decode_result *)(m->hmeta + desc_bytes);
             fws_frame_info *hf = (fws_frame_info *)(m->hmeta + desc_bytes + res_bytes);
             const uint32_t seq = ++m->seq;
-            if ((r = fws_launch_decode_segments(m->hbuf, (const fws_seg_desc *)m->hmeta, nseg, hf, hr, st, m->dctr,
-                                                nseg, m->hflag, seq)))
-                return r;
-            if ((r = fws_wait_flag(m->hflag, seq, st))) return r;
+            if (fws_rx_service *v = fws_ctx_rx_service(m->ctx)) {      // the resident grid, no launch
+                if ((r = fws_rx_service_run(v, m->hbuf, (const fws_seg_desc *)m->hmeta, nullptr, nseg, hf, hr, m->hflag,
+                                            seq)))
+                    return r;
+            } else {
+                if ((r = fws_launch_decode_segments(m->hbuf, (const fws_seg_desc *)m->hmeta, nseg, hf, hr, st, m->dctr,
+                                                    nseg, m->hflag, seq)))
+                    return r;
+                if ((r = fws_wait_flag(m->hflag, seq, st))) return r;
+            }
         } else {
             fws_decode_result *dres = (fws_decode_result *)(m->dmeta + desc_bytes);
             fws_frame_info *dfr = (fws_frame_info *)(m->dmeta + desc_bytes + res_bytes);

@@ -229,7 +229,100 @@ __global__ __launch_bounds__(kSThreads) void k_decode_one(uint8_t *__restrict__ 
     host_done(nullptr, 0u, flag, seq);
 }
 
+// ------------------------------------------------------------ persistent service
+// fws_rx_service (fws_internal.h): block 0 is the poller (one lane: a
+// system-scope load of the mailbox state per ~0.1 us), blocks 1..workers the
+// decoders. A worker takes segments w, w + workers, ... of each request; all
+// workers count in dv->ctr and the last one stores the request's flag
+// (host_done). Host memory the request names (descriptors, reads in place,
+// frame records) is read after a system-scope acquire by each worker, so no L2
+// line of an earlier request is reused; the flag follows a system-scope release.
+__device__ __forceinline__ uint64_t svc_load64(const uint64_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ __launch_bounds__(kSThreads) void k_rx_service(fws_svc_mail *mail, fws_svc_dev *dv, uint32_t seq0,
+                                                          uint32_t workers, uint64_t linger, uint64_t life) {
+    if (blockIdx.x == 0) {
+        if (threadIdx.x != 0) return;
+        uint32_t last = seq0;
+        const uint64_t t0 = wall_clock64();
+        uint64_t tl = t0;
+        for (;;) {
+            const uint64_t st = __hip_atomic_load(&mail->state, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+            const uint32_t sq = (uint32_t)(st >> 1);
+            if (sq != last) {
+                // the request, word by word from the coherent mailbox into device memory
+                const uint64_t *src = reinterpret_cast<const uint64_t *>(&mail->req);
+                uint64_t *dst = reinterpret_cast<uint64_t *>(&dv->req);
+                for (uint32_t i = 0; i < sizeof(fws_svc_req) / 8; ++i) dst[i] = svc_load64(src + i);
+                last = sq;
+                if (dv->req.kind == 1u) {                      // quit: stop and tell the workers
+                    __hip_atomic_store(&mail->state, (uint64_t)sq << 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+                    __hip_atomic_store(&dv->quit, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                    return;
+                }
+                __hip_atomic_store(&dv->seq, sq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                tl = wall_clock64();
+                continue;
+            }
+            const uint64_t now = wall_clock64();
+            if (now - tl > linger || now - t0 > life) {
+                uint64_t exp = ((uint64_t)last << 1) | 1u;
+                if (__hip_atomic_compare_exchange_strong(&mail->state, &exp, (uint64_t)last << 1, __ATOMIC_ACQ_REL,
+                                                         __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM)) {
+                    __hip_atomic_store(&dv->quit, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                    return;
+                }
+                continue;                                      // a request came in meanwhile
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+    }
+    __shared__ uint32_t s_cmd[2];
+    const uint32_t w = blockIdx.x - 1u;
+    uint32_t wlast = seq0;
+    for (;;) {
+        if (threadIdx.x == 0) {
+            uint32_t v, q;
+            for (;;) {
+                v = __hip_atomic_load(&dv->seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+                if ((int32_t)(v - wlast) > 0) { q = 0; break; }
+                q = __hip_atomic_load(&dv->quit, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+                if (q) break;
+                __builtin_amdgcn_s_sleep(2);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");      // system scope: host bytes fresh
+            s_cmd[0] = v;
+            s_cmd[1] = q;
+        }
+        __syncthreads();
+        const uint32_t v = s_cmd[0];
+        if (s_cmd[1]) return;
+        const fws_svc_req rq = dv->req;
+        uint8_t *const base = reinterpret_cast<uint8_t *>(rq.base);
+        fws_frame_info *const frames = reinterpret_cast<fws_frame_info *>(rq.frames);
+        fws_decode_result *const res = reinterpret_cast<fws_decode_result *>(rq.res);
+        for (uint32_t i = w; i < rq.nseg; i += workers) {
+            const fws_seg_desc d = rq.descs ? reinterpret_cast<const fws_seg_desc *>(rq.descs)[i] : rq.one;
+            decode_segment(base, d, frames, res + i);
+            __syncthreads();                                   // LDS reused by the next segment
+        }
+        host_done(&dv->ctr, workers, reinterpret_cast<uint32_t *>(rq.flag), rq.flag_seq);
+        wlast = v;
+        __syncthreads();                                       // s_cmd rewritten next round
+    }
+}
+
 }  // namespace fwsk
+
+int fws_launch_rx_service(fws_svc_mail *mail, fws_svc_dev *dv, uint32_t seq0, uint32_t workers, uint64_t linger_ticks,
+                          uint64_t life_ticks, hipStream_t s) {
+    if (!workers) return FWS_ERR_INVALID;
+    hipLaunchKernelGGL(fwsk::k_rx_service, dim3(workers + 1u), dim3(fwsk::kSThreads), 0, s, mail, dv, seq0, workers,
+                       linger_ticks, life_ticks);
+    return fws_hip_status(hipGetLastError());
+}
 
 int fws_launch_decode_segments(uint8_t *batch, const fws_seg_desc *segs, uint32_t n, fws_frame_info *frames,
                                fws_decode_result *res, hipStream_t s, uint32_t *ctr, uint32_t target, uint32_t *flag,

@@ -78,6 +78,17 @@ class Ctx:
     def reserve(self, max_frames, max_stream_bytes):
         check("fws_gpu_ctx_reserve", lib().fws_gpu_ctx_reserve(self.h, max_frames, max_stream_bytes))
 
+    def set_rx_persistent(self, workers):
+        """fws_gpu_ctx_set_rx_persistent: the context's small reads decoded by a
+        resident grid of `workers` workgroups (0 = a launch per read)."""
+        check("fws_gpu_ctx_set_rx_persistent", lib().fws_gpu_ctx_set_rx_persistent(self.h, workers))
+
+    def rx_service_stats(self):
+        """(grid launches, requests) of the persistent receive decode"""
+        out = (C.c_uint64 * 2)()
+        check("fws_internal_rx_service_stats", lib().fws_internal_rx_service_stats(self.h, out))
+        return int(out[0]), int(out[1])
+
     def close(self):
         if self.h:
             lib().fws_gpu_ctx_destroy(self.h)

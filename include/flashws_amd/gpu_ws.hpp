@@ -44,6 +44,11 @@ public:
     GpuContext(const GpuContext &) = delete;
     GpuContext &operator=(const GpuContext &) = delete;
     fws_gpu_ctx *get() const { return ctx_; }
+    // the persistent receive decode (fws_gpu_ctx_set_rx_persistent): reads
+    // decoded by a resident grid of `workers` workgroups, no launch per read
+    void SetPersistent(uint32_t workers) {
+        if (fws_gpu_ctx_set_rx_persistent(ctx_, workers) != 0) throw std::runtime_error("set_rx_persistent failed");
+    }
 
 private:
     fws_gpu_ctx *ctx_ = nullptr;

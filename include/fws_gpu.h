@@ -103,6 +103,15 @@ int fws_gpu_ctx_create(int device, fws_gpu_ctx **out);
 void fws_gpu_ctx_destroy(fws_gpu_ctx *ctx);
 /* Pre-size the workspace so later calls never allocate (hipGraph-capturable). */
 int fws_gpu_ctx_reserve(fws_gpu_ctx *ctx, uint64_t max_frames, uint64_t max_stream_bytes);
+/* Persistent receive decode (r05): with workers > 0, the small reads of the
+ * context's fws_rx_session / fws_rx_mux calls (reads of <= 128 KiB in pinned
+ * or registered host memory, the per-read and per-loop-step hot path of
+ * OnRecvData, w_socket.h:543-769) are decoded by a resident grid of `workers`
+ * workgroups (+ one poller) that the context launches on first use and that
+ * exits by itself after ~250 us without a read -- no kernel launch per read
+ * while reads keep coming. 0 (the default) = a launch per read. The grid holds
+ * `workers` CUs' LDS and one hardware queue while it is resident. */
+int fws_gpu_ctx_set_rx_persistent(fws_gpu_ctx *ctx, uint32_t workers);
 
 /* seam 1 -- device twin of WSMaskBytesFast (ws_mask.h:175): XOR n bytes at
  * dev_ptr with key, in place, on `stream`. Any alignment, any n. */

@@ -1,0 +1,172 @@
+"""GPU: the persistent receive decode (fws_gpu_ctx_set_rx_persistent, r05).
+A context with the service decodes its sessions' and muxes' small reads on a
+resident grid instead of a launch per read; the results must be exactly the
+launch path's: every tests/golden/ KAT case replayed read by read against the
+compiled reference's results (w_socket.h:543-769), in place (registered
+memory) and staged (pinned), through a session and through a mux; random
+multi-connection traffic and the declined (>256 headers) path against
+standalone sessions on a context without the service; the grid's lifecycle
+(exit after its linger time, relaunch on the next read, teardown while it is
+resident)."""
+import time
+
+import numpy as np
+import pytest
+
+from flashws_amd import gpu
+from test_gpu_inplace import CASES, _declined_reads, _state
+from test_gpu_mux import _random_stream
+from test_gpu_session import _out_matches, session_view
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def sctx(cuda):
+    c = gpu.Ctx(0, max_frames=1 << 16, max_stream_bytes=1 << 24)
+    c.set_rx_persistent(16)
+    yield c
+    c.close()
+
+
+@pytest.fixture(scope="module")
+def plain_ctx(cuda):
+    c = gpu.Ctx(0, max_frames=1 << 16, max_stream_bytes=1 << 24)
+    yield c
+    c.close()
+
+
+@pytest.fixture(scope="module")
+def arena(cuda):
+    a = gpu.HostArena(32 << 20)
+    yield a
+    a.close()
+
+
+@pytest.mark.parametrize("align_off", [0, 5], ids=["in_place", "staged"])
+def test_service_session_kat(sctx, arena, align_off):
+    before = sctx.rx_service_stats()
+    for name in sorted(CASES):
+        case = CASES[name]
+        s = gpu.RxSession(sctx)
+        for i, (rd, exp) in enumerate(zip(case["reads"], case["expected"])):
+            ret, buf, ev, ctl = s.feed(bytes.fromhex(rd), arena=arena, align_off=align_off)
+            assert ret == exp["ret"], (name, i)
+            assert _out_matches(exp["out"], buf), (name, i)
+            assert session_view(ev, ctl) == exp["events"], (name, i)
+            if ret < 0:
+                break
+            assert _state(s.state()) == exp["state"], (name, i)
+        s.close()
+    launches, requests = sctx.rx_service_stats()
+    assert requests - before[1] > 100                  # the reads went through the resident grid
+    assert launches - before[0] < requests - before[1]  # which was not relaunched per read
+
+
+def test_service_mux_kat(sctx, arena, monkeypatch):
+    monkeypatch.setenv("FWS_MUX_ZC_MAX", str(1 << 40))
+    names = sorted(CASES)
+    mux = gpu.RxMux(sctx, len(names))
+    closed = set()
+    before = sctx.rx_service_stats()[1]
+    for r in range(max(len(CASES[n]["reads"]) for n in names)):
+        live = [ci for ci, n in enumerate(names) if r < len(CASES[n]["reads"]) and ci not in closed]
+        got = mux.feed([(ci, bytes.fromhex(CASES[names[ci]]["reads"][r])) for ci in live], arena=arena,
+                       align_off=lambda i: 7 if i % 3 == 2 else 0)
+        for ci, (ret, buf, ev, ctl) in zip(live, got):
+            name, exp = names[ci], CASES[names[ci]]["expected"][r]
+            assert ret == exp["ret"], (name, r)
+            assert _out_matches(exp["out"], buf), (name, r)
+            assert session_view(ev, ctl) == exp["events"], (name, r)
+            if ret < 0:
+                closed.add(ci)
+            else:
+                assert _state(mux.state(ci)) == exp["state"], (name, r)
+    mux.close()
+    assert sctx.rx_service_stats()[1] > before
+
+
+def test_service_mux_random_vs_sessions(sctx, plain_ctx, arena):
+    rng = np.random.default_rng(505)
+    n = 48
+    streams = [_random_stream(rng, int(rng.integers(5, 40))) for _ in range(n)]
+    cuts = []
+    for st in streams:
+        pos, c = 0, []
+        while pos < len(st):
+            k = int(rng.choice([1, 7, 100, 4096, 5000, 70000]))
+            c.append(st[pos:pos + k])
+            pos += k
+        cuts.append(c)
+    mux = gpu.RxMux(sctx, n)
+    ref = [gpu.RxSession(plain_ctx) for _ in range(n)]
+    dead = set()
+    for r in range(max(len(c) for c in cuts)):
+        live = [i for i in range(n) if r < len(cuts[i]) and i not in dead]
+        got = mux.feed([(i, cuts[i][r]) for i in live], arena=arena)
+        for i, (ret, buf, ev, ctl) in zip(live, got):
+            eret, ebuf, eev, ectl = ref[i].feed(cuts[i][r])
+            assert ret == eret, (i, r)
+            assert bytes(buf) == bytes(ebuf), (i, r)
+            assert session_view(ev, ctl) == session_view(eev, ectl), (i, r)
+            if ret < 0:
+                dead.add(i)
+    mux.close()
+    for s in ref:
+        s.close()
+
+
+def test_service_declined_small_read(sctx, plain_ctx, arena):
+    rng = np.random.default_rng(606)
+    reads = _declined_reads(rng, 700)
+    s, ref = gpu.RxSession(sctx), gpu.RxSession(plain_ctx)
+    for rd in reads:
+        ret, buf, ev, ctl = s.feed(rd, arena=arena, align_off=0)
+        eret, ebuf, eev, ectl = ref.feed(rd)
+        assert ret == eret == 0
+        assert bytes(buf) == bytes(ebuf)
+        assert session_view(ev, ctl) == session_view(eev, ectl)
+    s.close()
+    ref.close()
+
+
+def test_service_relaunch_after_linger(cuda, arena):
+    """The grid leaves after its linger time without a read; the next read
+    relaunches it and decodes as before."""
+    from flashws_amd._lib import lib
+    old = lib().fws_internal_set_rx_linger_us(40)
+    c = gpu.Ctx(0)
+    try:
+        c.set_rx_persistent(4)
+        rng = np.random.default_rng(7)
+        data = _random_stream(rng, 30)
+        s, ref_ctx = gpu.RxSession(c), gpu.Ctx(0)
+        ref = gpu.RxSession(ref_ctx)
+        for k in range(6):
+            rd = data[k * 500:(k + 1) * 500] if k < 5 else data[2500:]
+            got, exp = s.feed(rd, arena=arena), ref.feed(rd)
+            assert got[0] == exp[0] and bytes(got[1]) == bytes(exp[1])
+            assert session_view(got[2], got[3]) == session_view(exp[2], exp[3])
+            time.sleep(0.005)                                # >> 40 us: the grid has left
+        launches, requests = c.rx_service_stats()
+        assert requests >= 6 and launches >= 3
+        s.close()
+        ref.close()
+        ref_ctx.close()
+    finally:
+        c.close()
+        lib().fws_internal_set_rx_linger_us(old)
+
+
+def test_service_teardown_while_resident(cuda, arena):
+    """Closing a context whose grid is resident (default linger) sends the quit
+    request and waits for the grid to drain; a new context works after it."""
+    for _ in range(3):
+        c = gpu.Ctx(0)
+        c.set_rx_persistent(8)
+        s = gpu.RxSession(c)
+        ret, buf, ev, ctl = s.feed(bytes.fromhex(CASES[sorted(CASES)[0]]["reads"][0]), arena=arena)
+        s.close()
+        t0 = time.perf_counter()
+        c.close()                                            # the grid is still lingering
+        assert time.perf_counter() - t0 < 1.0

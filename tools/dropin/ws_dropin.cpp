@@ -60,6 +60,7 @@ struct Opts {
     int port = 0;
     bool gpu = false;
     bool gpu_batch = false;             // --gpu-batch: GpuRxHook::EnableBatched
+    int persistent = 0;                 // --persistent N: the context's resident decode grid (N workgroups)
     int device = 0;
     int conns = 1;
     int clients = 1;
@@ -174,6 +175,7 @@ int RunServer(const Opts &o) {
     std::unique_ptr<fws_amd::GpuRxHookT<kTls>> hook;
     if (o.gpu) {
         gpu = std::make_unique<fws_amd::GpuContext>(o.device);
+        if (o.persistent > 0) gpu->SetPersistent(uint32_t(o.persistent));
         hook = std::make_unique<fws_amd::GpuRxHookT<kTls>>(*gpu);
         if (o.gpu_batch) hook->EnableBatched(ws, srv.loop);   // (or: every read of a loop step in one GPU batch)
         else hook->Enable(ws);                 // the one added line
@@ -351,6 +353,7 @@ int main(int argc, char **argv) {
         else if (a == "--gpu") o.gpu = true;
         else if (a == "--gpu-batch") o.gpu = o.gpu_batch = true;
         else if (a == "--device") o.device = std::atoi(next().c_str());
+        else if (a == "--persistent") o.persistent = std::atoi(next().c_str());
         else if (a == "--conns") o.conns = std::atoi(next().c_str());
         else if (a == "--clients") o.clients = std::atoi(next().c_str());
         else if (a == "--msg-len") o.msg_len = std::strtoull(next().c_str(), nullptr, 10);

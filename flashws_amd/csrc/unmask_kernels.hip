@@ -385,7 +385,11 @@ __device__ __forceinline__ uint32_t utf8_chunk_err32(const u32x4 &u, uint32_t pr
 #endif
 constexpr bool kUnmaskPre = FWS_UNMASK_PRE != 0;   // A/B: every unit's loads before its frame lookup
 
-template <bool kNT, bool kUtf8, bool kRev>
+// kPf (UTF-8 only, r05): the next unit's loads go out at the top of each unit,
+// so they are in flight during this unit's lookup and UTF-8 work (the check
+// is ~28 VALU per dword; without the prefetch a wave has no load in flight
+// while it runs, and the pass ran 10-15 % above the plain unmask's time)
+template <bool kNT, bool kUtf8, bool kRev, bool kPf = false>
 __global__ __launch_bounds__(kBlock) void k_unmask_stream(uint8_t *base, uint64_t N,
                                                           const fws_frame_info *__restrict__ fr, uint32_t cap,
                                                           const uint32_t *__restrict__ n_dev,
@@ -399,22 +403,37 @@ __global__ __launch_bounds__(kBlock) void k_unmask_stream(uint8_t *base, uint64_
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const uint64_t nwaves = uint64_t(gridDim.x) * (kBlock / kWave);
     const uintptr_t b0 = (uintptr_t)base;
-    for (uint64_t ui = uint64_t(blockIdx.x) * (kBlock / kWave) + wave; ui < n_units; ui += nwaves) {
+    const uint64_t last = (N - 1u) & ~uint64_t(15);
+    auto unit_of = [&](uint64_t ui) -> uint64_t { return kRev ? n_units - 1u - ui : ui; };
+    auto load_unit = [&](uint64_t u, u32x4 (&dst)[kUnmaskU]) {
+        const uint64_t c0 = u * 4096u + uint64_t(lane) * 16u;
+#pragma unroll
+        for (int j = 0; j < kUnmaskU; ++j) {
+            const uint64_t c = c0 + uint64_t(j) * 1024u;
+            dst[j] = gload16<kNT>(b0 + (c < N ? c : last));
+        }
+    };
+    u32x4 nxt[kUnmaskU];
+    const uint64_t ui0 = uint64_t(blockIdx.x) * (kBlock / kWave) + wave;
+    if constexpr (kPf) {
+        if (ui0 < n_units) load_unit(unit_of(ui0), nxt);
+    }
+    for (uint64_t ui = ui0; ui < n_units; ui += nwaves) {
         // kRev: the first-dispatched waves take the END of the stream, which the
         // decode's scan read last -- those lines are still in the 256 MB
         // Infinity Cache (MALL) when this pass re-reads them
-        const uint64_t u = kRev ? n_units - 1u - ui : ui;
+        const uint64_t u = unit_of(ui);
         const uint64_t c0 = u * 4096u + uint64_t(lane) * 16u;
         // kUtf8 (VALU-heavier per unit): the unit's loads are issued before the frame
         // lookup, whose dependent round trips then overlap them
         u32x4 pre[kUnmaskU];
-        if constexpr (kUtf8 || kUnmaskPre) {
-            const uint64_t last = (N - 1u) & ~uint64_t(15);
+        if constexpr (kPf) {
 #pragma unroll
-            for (int j = 0; j < kUnmaskU; ++j) {
-                const uint64_t c = c0 + uint64_t(j) * 1024u;
-                pre[j] = gload16<kNT>(b0 + (c < N ? c : last));
-            }
+            for (int j = 0; j < kUnmaskU; ++j) pre[j] = nxt[j];
+            if (ui + nwaves < n_units) load_unit(unit_of(ui + nwaves), nxt);
+            asm volatile("" ::: "memory");
+        } else if constexpr (kUtf8 || kUnmaskPre) {
+            load_unit(u, pre);
             asm volatile("" ::: "memory");           // issued here, not sunk into the branches
         }
         const uint32_t flo = unit_first[u];
@@ -1484,6 +1503,12 @@ extern "C" __attribute__((visibility("default"))) int fws_internal_set_sorted_ut
 // tuning hook: k_unmask_stream variant -- 0 forward nontemporal, 1 reverse
 // nontemporal, 2 forward default policy, 3 reverse default policy
 static int g_stream_variant = 0;
+static int g_stream_utf8_pf = 1;   // tuning hook: k_unmask_stream<utf8> with the cross-unit prefetch (kPf)
+extern "C" __attribute__((visibility("default"))) int fws_internal_set_stream_utf8_pf(int on) {
+    const int old = g_stream_utf8_pf;
+    g_stream_utf8_pf = on != 0;
+    return old;
+}
 extern "C" __attribute__((visibility("default"))) int fws_internal_set_stream_variant(int v) {
     const int old = g_stream_variant;
     if (v >= 0 && v <= 3) g_stream_variant = v;
@@ -1597,7 +1622,13 @@ int fws_launch_unmask_stream(uint8_t *base, uint64_t N, const fws_frame_info *fr
             hipLaunchKernelGGL((k_unmask_stream<false, false, true>), grid, blk, 0, s, (uint8_t *)base, N, frames,
                                cap, n_dev, unit_first, units, nullptr, nullptr);
     } else {
-        if (v == 1 || v == 3)
+        if (g_stream_utf8_pf && (v == 1 || v == 3))
+            hipLaunchKernelGGL((k_unmask_stream<true, true, true, true>), grid, blk, 0, s, (uint8_t *)base, N, frames,
+                               cap, n_dev, unit_first, units, utf8_ok, seam);
+        else if (g_stream_utf8_pf)
+            hipLaunchKernelGGL((k_unmask_stream<true, true, false, true>), grid, blk, 0, s, (uint8_t *)base, N, frames,
+                               cap, n_dev, unit_first, units, utf8_ok, seam);
+        else if (v == 1 || v == 3)
             hipLaunchKernelGGL((k_unmask_stream<true, true, true>), grid, blk, 0, s, (uint8_t *)base, N, frames, cap,
                                n_dev, unit_first, units, utf8_ok, seam);
         else

@@ -356,7 +356,16 @@ def test_candidate_counts_at_node_limits(ctx, cuda, seed):
     check(ctx, cuda, b"".join(parts))
 
 
-def test_utf8_flags_c5_shape(ctx, cuda):
+@pytest.fixture(params=[1, 0], ids=["pf", "no_pf"])
+def stream_utf8_pf(request):
+    """k_unmask_stream<utf8> with (default) and without the cross-unit prefetch"""
+    from flashws_amd._lib import lib
+    old = lib().fws_internal_set_stream_utf8_pf(request.param)
+    yield request.param
+    lib().fws_internal_set_stream_utf8_pf(old)
+
+
+def test_utf8_flags_c5_shape(ctx, cuda, stream_utf8_pf):
     wire, descs, ok = gpu.config_c5(seed=5, n_frames=512, payload=16384, invalid_permille=100)
     dev = torch.from_numpy(wire).to(cuda)
     flags = torch.zeros(len(descs), dtype=torch.uint8, device=cuda)
@@ -380,7 +389,7 @@ def _utf8_payload(rng, n_chars, corrupt):
 
 
 @pytest.mark.parametrize("seed", range(4))
-def test_utf8_flags_mixed_stream(ctx, cuda, seed):
+def test_utf8_flags_mixed_stream(ctx, cuda, seed, stream_utf8_pf):
     """Fused decode + UTF-8 flags on TEXT frames of every size (tiny frames take
     the per-chunk unmask path, big ones the uniform path), misaligned against
     the 4 KiB stream units and 16-B chunks, next to BIN / non-FIN / control
@@ -421,7 +430,7 @@ def test_utf8_flags_mixed_stream(ctx, cuda, seed):
         assert bool(got[i]) == exp, (i, op, fin, body[-8:])
 
 
-def test_utf8_flags_unit_seams(ctx, cuda):
+def test_utf8_flags_unit_seams(ctx, cuda, stream_utf8_pf):
     """TEXT frames placed so that multi-byte sequences, cut sequences, invalid
     bytes and frame ends straddle 4 KiB stream-unit boundaries (the seam
     kernel's bytes)."""

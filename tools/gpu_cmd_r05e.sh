@@ -10,6 +10,8 @@ for l in open('$O/ab_tx.jsonl'): r=json.loads(l); d[r['mode']].append(r['ms'])
 print({k:sorted(v) for k,v in d.items()})"
 bash tools/gpu_round.sh utf8tests || exit 1
 $T 200 python tools/ab_c5d.py > $O/ab_c5d_b.jsonl 2>> $O/ab_c5d.err || exit 1
+$T 200 python tools/ab_c5s.py > $O/ab_c5s.jsonl 2>> $O/ab_c5s.err || exit 1
+cat $O/ab_c5s.jsonl
 cat $O/ab_c5d_b.jsonl
 $T 600 python -u -m pytest tests/test_gpu_inplace.py tests/test_gpu_mux.py tests/test_gpu_engine.py -x -q --timeout 120 --timeout-method thread > $O/host_tests.log 2>&1 || { tail -30 $O/host_tests.log; exit 1; }
 tail -1 $O/host_tests.log

@@ -79,6 +79,9 @@ def parse():
     ap.add_argument("--only", default="",
                     help="comma list of extra configs to run (c2s,c3,dense,c4,tx,c5s,c5d,e2e,c1,batch): one "
                          "config per process, e.g. under rocprofv3 (profiles/r05/*_kernel_stats.csv)")
+    ap.add_argument("--no-pipelined", action="store_true",
+                    help="skip the two-in-flight and engine runs of the stream configs (profiling: a config's "
+                         "timed calls are then the last dispatches of its kernels, tools/prof_window.py)")
     ap.add_argument("--launcher-selftest", action="store_true",
                     help="CPU only (gloo): exercise the N-rank launch, barrier and max-over-ranks timing on a "
                          "host XOR of each rank's shard; prints a self-test line, not the metric")
@@ -773,7 +776,7 @@ def stream_decode_extra(ctx, wire_c2, dev, args):
                "roofline": {"bound": "hbm", "achieved": round(alg, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                             "frac": round(alg / HBM_PEAK_GBS, 4), "basis": "whole fws_gpu_decode_stream step",
                             "alg_bytes_per_step": len(wire) + payload}}
-        if pipelined and nbuf >= 4:
+        if pipelined and nbuf >= 4 and not args.no_pipelined:
             # two batches in flight (two connections' reads): a context, a frame list and a
             # stream each, so one batch's latency-bound resolve overlaps the other's streaming
             c2 = gpu.Ctx(dev.index or 0, max_frames=n_frames + 64, max_stream_bytes=len(wire))

@@ -99,9 +99,16 @@ for step in "$@"; do
                 >> "$O/ab_c5.jsonl" 2>> "$O/ab_c5.err" || fail ab_c5 $? "$O/ab_c5.err"
             python3 -c "import json,sys;d=json.loads(open('$O/ab_c5.jsonl').read().splitlines()[-1]);e=d['extra'];print('variant=${v:-product}', e['C5_utf8_descriptor']['ms_per_step'], e['C5_utf8_text_decode']['ms_per_step'])"
         done ;;
-    prof_extras)  # warm kernel stats, one config per process under bench.py's own warm-up
-        for c in c3 dense c2s c4 tx c5d c5s; do
-            prof "prof_$c" 400 --kernel-trace --stats -f csv -d "$O/prof_$c" -o run -- python3 "$R/bench.py" --only $c --no-cpu --no-batch-extra --steps 20 --warmup 5
+    prof_extras)  # warm kernel stats per config: bench.py --only CFG under rocprofv3, stats of the timed window
+        mkdir -p "$O/profiles"
+        for c in ${PROF_CFGS:-c3 dense c2s c4 tx c5d c5s}; do
+            prof "prof_$c" 400 --kernel-trace --stats -f csv -d "$O/prof_$c" -o run -- python3 "$R/bench.py" --only $c --no-cpu --no-batch-extra --no-pipelined --steps 20 --warmup 5
+            grep '^{"metric"' "$O/prof_$c.log" | tail -1 > "$O/profiles/${c}_bench_line.json"
+            last=20; case $c in c5*) last=16 ;; esac
+            python3 tools/prof_window.py "$O/prof_$c/run_kernel_trace.csv" --last $last --out "$O/profiles/${c}_kernel_stats.csv" \
+                --json "$O/profiles/${c}_window.json" --bench "$O/profiles/${c}_bench_line.json" > /dev/null || fail "window_$c" 1 "$O/prof_$c.log"
+            cp "$O/prof_$c/run_kernel_stats.csv" "$O/profiles/${c}_kernel_stats_all.csv"
+            python3 -c "import json;d=json.load(open('$O/profiles/${c}_window.json'));k=sorted(d['kernels'].items(),key=lambda x:-x[1]['window_avg_us'])[:3];print('$c',d.get('bench_ms_per_step'),[(n[:40],v['window_avg_us']) for n,v in k])"
         done ;;
     *) echo "unknown step $step"; exit 2 ;;
     esac

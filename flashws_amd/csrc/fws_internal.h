@@ -73,11 +73,18 @@ struct fws_svc_req {
     fws_seg_desc one;
 };
 static_assert(sizeof(fws_svc_req) % 8 == 0, "8-B words");
+// One 128-B line: the poller's wave reads all of it with one coalesced load per
+// poll (one PCIe round trip for the state and the request together). `tag` =
+// the request's seq, written with the request (a later 64-B half than the
+// state word): a read that sees the new state and the new tag saw the whole
+// request, since the host writes the request, then the tag, then CASes state.
 struct alignas(128) fws_svc_mail {     // coherent pinned host memory
     uint64_t state;
-    uint64_t pad[15];
     fws_svc_req req;                   // written before the CAS that publishes its seq
+    uint64_t tag;
+    uint64_t pad[2];
 };
+static_assert(sizeof(fws_svc_mail) == 128, "one line");
 struct alignas(128) fws_svc_dev {      // device memory, zeroed before each launch
     uint32_t seq, quit, ctr, pad[29];
     fws_svc_req req;

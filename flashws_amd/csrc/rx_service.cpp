@@ -75,6 +75,7 @@ void fws_rx_service_destroy(fws_rx_service *v) {
         uint64_t old = __atomic_load_n(&v->mail->state, __ATOMIC_ACQUIRE);
         if (old & 1u) {                // a grid is running: a quit request
             v->mail->req.kind = 1u;
+            __atomic_store_n(&v->mail->tag, (old >> 1) + 1u, __ATOMIC_RELEASE);
             uint64_t e = old;
             (void)__atomic_compare_exchange_n(&v->mail->state, &e, (((old >> 1) + 1u) << 1) | 1u, false,
                                               __ATOMIC_SEQ_CST, __ATOMIC_SEQ_CST);   // fails: it just stopped
@@ -103,6 +104,9 @@ int fws_rx_service_run(fws_rx_service *v, uint8_t *base, const fws_seg_desc *des
     q.kind = 0;
     if (!descs) q.one = *one;
     uint64_t old = __atomic_load_n(&v->mail->state, __ATOMIC_ACQUIRE);
+    // the tag names the seq this request is published as (the poller reads the
+    // line in one load and trusts the request only when the tag matches)
+    __atomic_store_n(&v->mail->tag, (old >> 1) + 1u, __ATOMIC_RELEASE);
     bool published = false;
     if (old & 1u) {                    // a grid is running: hand it the request
         uint64_t e = old;

@@ -244,37 +244,55 @@ __device__ __forceinline__ uint64_t svc_load64(const uint64_t *p) {
 __global__ __launch_bounds__(kSThreads) void k_rx_service(fws_svc_mail *mail, fws_svc_dev *dv, uint32_t seq0,
                                                           uint32_t workers, uint64_t linger, uint64_t life) {
     if (blockIdx.x == 0) {
-        if (threadIdx.x != 0) return;
+        // the poller: wave 0, every lane i < 16 loading word i of the mailbox line
+        if (threadIdx.x >= kWave) return;
+        const uint32_t lane = threadIdx.x;
+        constexpr uint32_t kWords = sizeof(fws_svc_mail) / 8;               // 16
+        constexpr uint32_t kReqW = sizeof(fws_svc_req) / 8, kTagW = offsetof(fws_svc_mail, tag) / 8;
+        const uint64_t *const src = reinterpret_cast<const uint64_t *>(mail) + (lane < kWords ? lane : 0u);
+        uint64_t *const dst = reinterpret_cast<uint64_t *>(&dv->req) + (lane >= 1u && lane <= kReqW ? lane - 1u : 0u);
         uint32_t last = seq0;
         const uint64_t t0 = wall_clock64();
         uint64_t tl = t0;
         for (;;) {
-            const uint64_t st = __hip_atomic_load(&mail->state, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+            const uint64_t wv = svc_load64(src);                            // one load instruction, 16 words
+            const uint64_t st = (uint64_t)__builtin_amdgcn_readlane((uint32_t)(wv >> 32), 0) << 32 |
+                                (uint32_t)__builtin_amdgcn_readlane((uint32_t)wv, 0);
             const uint32_t sq = (uint32_t)(st >> 1);
             if (sq != last) {
-                // the request, word by word from the coherent mailbox into device memory
-                const uint64_t *src = reinterpret_cast<const uint64_t *>(&mail->req);
-                uint64_t *dst = reinterpret_cast<uint64_t *>(&dv->req);
-                for (uint32_t i = 0; i < sizeof(fws_svc_req) / 8; ++i) dst[i] = svc_load64(src + i);
+                const uint32_t tag = (uint32_t)__builtin_amdgcn_readlane((uint32_t)wv, kTagW);
+                if (tag != sq) continue;                                    // the request's half was read first: again
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");               // system scope, after the state
+                if (lane >= 1u && lane <= kReqW) *dst = wv;                 // the request into device memory
                 last = sq;
-                if (dv->req.kind == 1u) {                      // quit: stop and tell the workers
-                    __hip_atomic_store(&mail->state, (uint64_t)sq << 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-                    __hip_atomic_store(&dv->quit, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-                    return;
+                static_assert(offsetof(fws_svc_req, kind) % 8 == 0, "kind: the low half of a word");
+                const bool quit = (uint32_t)__builtin_amdgcn_readlane(
+                                      (uint32_t)wv, 1u + (uint32_t)(offsetof(fws_svc_req, kind) / 8)) == 1u;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                if (lane == 0) {
+                    if (quit) {                                             // stop and tell the workers
+                        __hip_atomic_store(&mail->state, (uint64_t)sq << 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+                        __hip_atomic_store(&dv->quit, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                    } else {
+                        __hip_atomic_store(&dv->seq, sq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                    }
                 }
-                __hip_atomic_store(&dv->seq, sq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                if (quit) return;
                 tl = wall_clock64();
                 continue;
             }
             const uint64_t now = wall_clock64();
             if (now - tl > linger || now - t0 > life) {
-                uint64_t exp = ((uint64_t)last << 1) | 1u;
-                if (__hip_atomic_compare_exchange_strong(&mail->state, &exp, (uint64_t)last << 1, __ATOMIC_ACQ_REL,
-                                                         __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM)) {
-                    __hip_atomic_store(&dv->quit, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-                    return;
+                uint32_t stopped = 0;
+                if (lane == 0) {
+                    uint64_t exp = ((uint64_t)last << 1) | 1u;
+                    stopped = __hip_atomic_compare_exchange_strong(&mail->state, &exp, (uint64_t)last << 1,
+                                                                   __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE,
+                                                                   __HIP_MEMORY_SCOPE_SYSTEM) ? 1u : 0u;
+                    if (stopped) __hip_atomic_store(&dv->quit, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
                 }
-                continue;                                      // a request came in meanwhile
+                if (__builtin_amdgcn_readlane(stopped, 0)) return;
+                continue;                                                   // a request came in meanwhile
             }
             __builtin_amdgcn_s_sleep(2);
         }

@@ -198,9 +198,9 @@ __device__ __forceinline__ void tx_unit(uint8_t *__restrict__ out, const uint8_t
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const uint64_t a = a0 + (uint64_t)j * 1024u;
-        const bool own = a < own_end;
-        const bool inA = own && a >= z.PA && a + 16 <= z.EA;
-        const bool inB = own && two && a >= z.PB && a + 16 <= z.EB;
+        const bool own = a < own_end, whole = a + 16 <= total;   // a chunk crossing `total` is built as a seam
+        const bool inA = own && whole && a >= z.PA && a + 16 <= z.EA;
+        const bool inB = own && whole && two && a >= z.PB && a + 16 <= z.EB;
         if (inA || inB) full |= 1u << j;
         else if (own && a < total) seam |= 1u << j;
         const uintptr_t sa = (inB ? SB : SA) + (uintptr_t)a;
@@ -421,11 +421,18 @@ extern "C" __attribute__((visibility("default"))) int fws_internal_set_tx_w5(int
     return old;
 }
 
-// tuning hook: the one-launch form k_tx_one (1, the default for batches whose
-// frames average <= kTxOneMaxAvg bytes of out_cap; 2 = for every batch, tests)
-// or plan + encode (0); and the output bytes per k_tx_one workgroup (its frames
-// F = span / average frame)
-static int g_tx_one = 1;
+// tuning hook: the one-launch form k_tx_one (1: for batches whose frames
+// average <= kTxOneMaxAvg bytes of out_cap; 2 = for every batch, tests) or plan +
+// encode (0, the default); and the output bytes per k_tx_one workgroup (its
+// frames F = span / average frame). Measured on the C2 TX shape (r05,
+// profiles/r05/ab_tx.jsonl, one process, order alternated): plan + encode
+// 0.105 ms, k_tx_one 0.132 ms at 128 KiB per workgroup, 0.141 at 64 / 256 KiB,
+// 0.169 at 32 KiB. A frame-major grid has one wave per ~span / 4 workgroup
+// units: at 128 KiB spans 2,048 waves (2 per SIMD) stream the whole batch, too
+// few to keep HBM busy; smaller spans add workgroups whose look-back chains
+// (read 256 predecessors a round) grow with the grid. The unit-major kernel
+// keeps one wave per 4 KiB unit (65,668) and pays one plan launch.
+static int g_tx_one = 0;   // off: measured slower (tools/ab_tx.py, profiles/r05/ab_tx.jsonl)
 static uint64_t g_tx_one_span = 64u << 10;
 constexpr uint64_t kTxOneMaxAvg = 16u << 10;
 extern "C" __attribute__((visibility("default"))) int fws_internal_set_tx_one(int on, int span_kib) {

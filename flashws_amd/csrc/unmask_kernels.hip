@@ -383,6 +383,9 @@ __device__ __forceinline__ uint32_t utf8_chunk_err32(const u32x4 &u, uint32_t pr
 #ifndef FWS_UNMASK_PRE
 #define FWS_UNMASK_PRE 1
 #endif
+#ifndef FWS_ABL_U8
+#define FWS_ABL_U8 0
+#endif
 constexpr bool kUnmaskPre = FWS_UNMASK_PRE != 0;   // A/B: every unit's loads before its frame lookup
 
 // kPf (UTF-8 only, r05): the next unit's loads go out at the top of each unit,
@@ -1029,8 +1032,11 @@ __device__ __forceinline__ void unmask_sorted_body(uint8_t *base, const fws_fram
                     gstore16<kNT>(c0 + uint64_t(j) * 1024u, x[j]);
                 }
                 // the unit's first and last unmasked dwords for k_utf8_seam_sorted
+#if (FWS_ABL_U8 & 2) == 0          // (ablation builds only: make exp EXP_DEFS=-DFWS_ABL_U8=1|2|3)
                 if (sw && lane == 0) seam[2u * u] = x[0].x;
                 if (sw && lane == 63) seam[2u * u + 1u] = x[kUnmaskU - 1].w;
+#endif
+#if (FWS_ABL_U8 & 1) == 0
                 uint32_t err = 0, carry = 0;
 #pragma unroll
                 for (int j = 0; j < kUnmaskU; ++j) {
@@ -1041,6 +1047,7 @@ __device__ __forceinline__ void unmask_sorted_body(uint8_t *base, const fws_fram
                     err |= e0 | utf8_err(x[j].y, x[j].x) | utf8_err(x[j].z, x[j].y) | utf8_err(x[j].w, x[j].z);
                 }
                 if (__any(err != 0u) && lane == 0) ok[A] = 0;
+#endif
                 continue;
             }
         }

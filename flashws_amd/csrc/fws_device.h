@@ -35,6 +35,29 @@ __device__ __forceinline__ void gstore16(uintptr_t a, u32x4 v) {
     else *p = v;
 }
 
+// A store through a global-address-space pointer: global_store (vmcnt only),
+// where a generic pointer gives flat_store, which also counts in lgkmcnt --
+// so the next workgroup barrier's lgkmcnt(0) would wait for the store's
+// acknowledgment (a PCIe round trip when it lands in host memory).
+// (A record goes out as dwords: its type's copy assignment cannot bind to an
+// address-space-qualified object.)
+template <typename T>
+__device__ __forceinline__ void gput(T *p, const T &v) {
+    if constexpr (sizeof(T) % 4 == 0 && alignof(T) >= 4) {
+        typedef __attribute__((address_space(1))) uint32_t g_u32;
+        uint32_t w[sizeof(T) / 4];
+        __builtin_memcpy(w, &v, sizeof(T));
+#pragma unroll
+        for (uint32_t i = 0; i < sizeof(T) / 4; ++i) ((g_u32 *)(uintptr_t)p)[i] = w[i];
+    } else {
+        static_assert(sizeof(T) == 1, "gput: bytes or dword-aligned records");
+        *(__attribute__((address_space(1))) T *)(uintptr_t)p = v;
+    }
+}
+__device__ __forceinline__ uint8_t gget(const uint8_t *p) {
+    return *(const __attribute__((address_space(1))) uint8_t *)(uintptr_t)p;
+}
+
 // base/constexpr_math.h:67-82 RotateR, 32-bit.
 __device__ __forceinline__ uint32_t rotr32(uint32_t v, uint32_t b) {
     b &= 31u;

@@ -90,7 +90,8 @@ struct alignas(128) fws_svc_dev {      // device memory, zeroed before each laun
     fws_svc_req req;
 };
 int fws_launch_rx_service(fws_svc_mail *mail, fws_svc_dev *dv, uint32_t seq0, uint32_t workers, uint64_t linger_ticks,
-                          uint64_t life_ticks, hipStream_t s);
+                          uint64_t life_ticks, uint32_t trace, hipStream_t s);
+int fws_rx_service_trace_read(unsigned long long *out8);
 struct fws_rx_service;
 // the context's service (created on first use when enabled), or null: not enabled
 fws_rx_service *fws_ctx_rx_service(fws_gpu_ctx *ctx);

@@ -12,6 +12,7 @@
 // its flag before the next is published.
 #include <string.h>
 
+#include <chrono>
 #include <mutex>
 
 #include "fws_internal.h"
@@ -30,7 +31,29 @@ struct fws_rx_service {
 namespace {
 uint64_t g_linger_us = 250;            // idle time before the grid exits (tests shorten it)
 constexpr uint64_t kLifeUs = 200000;   // and its longest stay: it leaves at the next idle moment
+// phase trace (tools/lat_feed.cpp): the device's phase clocks (grids launched
+// while it is on) and the host's publish / wait times, summed in ns
+bool g_trace = false;
+uint64_t g_host_ns[3];                 // requests, entry -> published, published -> flag seen
 }  // namespace
+
+// on: trace the grids launched from now on; out: [0..7] the device sums
+// (small_kernels.hip g_svc_trace, wall-clock ticks), [8] ticks per us,
+// [9..11] the host sums; every sum is zeroed after the copy
+extern "C" __attribute__((visibility("default"))) int fws_internal_rx_service_trace(int on, int device,
+                                                                                   unsigned long long *out12) {
+    g_trace = on != 0;
+    if (!out12) return 0;
+    int r = fws_rx_service_trace_read(out12);
+    int khz = 0;
+    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) != hipSuccess) khz = 0;
+    out12[8] = (unsigned long long)khz / 1000u;
+    for (int i = 0; i < 3; ++i) {
+        out12[9 + i] = g_host_ns[i];
+        g_host_ns[i] = 0;
+    }
+    return r;
+}
 
 extern "C" __attribute__((visibility("default"))) int fws_internal_set_rx_linger_us(int us) {
     const int old = (int)g_linger_us;
@@ -93,6 +116,9 @@ int fws_rx_service_run(fws_rx_service *v, uint8_t *base, const fws_seg_desc *des
                        uint32_t flag_seq) {
     if (!v || !nseg || !flag || (!descs && !one)) return FWS_ERR_INVALID;
     std::lock_guard<std::mutex> lk(v->mu);
+    const bool tr = g_trace;
+    std::chrono::steady_clock::time_point t0, t1;
+    if (tr) t0 = std::chrono::steady_clock::now();
     fws_svc_req &q = v->mail->req;     // plain stores; the CAS / store below publishes them
     q.base = (uint64_t)(uintptr_t)base;
     q.descs = (uint64_t)(uintptr_t)descs;
@@ -123,14 +149,21 @@ int fws_rx_service_run(fws_rx_service *v, uint8_t *base, const fws_seg_desc *des
         int r = fws_hip_status(hipMemsetAsync(v->dv, 0, sizeof(fws_svc_dev), v->stream));
         if (!r)
             r = fws_launch_rx_service(v->mail, v->dv, seq0, v->workers, g_linger_us * v->ticks_per_us,
-                                      kLifeUs * v->ticks_per_us, v->stream);
+                                      kLifeUs * v->ticks_per_us, tr ? 1u : 0u, v->stream);
         if (r) {
             __atomic_store_n(&v->mail->state, (uint64_t)seq0 << 1, __ATOMIC_SEQ_CST);
             return r;
         }
         ++v->launches;
     }
-    return fws_wait_flag(flag, flag_seq, v->stream);
+    if (!tr) return fws_wait_flag(flag, flag_seq, v->stream);
+    t1 = std::chrono::steady_clock::now();
+    const int r = fws_wait_flag(flag, flag_seq, v->stream);
+    const auto t2 = std::chrono::steady_clock::now();
+    g_host_ns[0] += 1;
+    g_host_ns[1] += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count();
+    g_host_ns[2] += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t2 - t1).count();
+    return r;
 }
 
 extern "C" {

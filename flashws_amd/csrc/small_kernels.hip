@@ -30,7 +30,8 @@ constexpr uint32_t kSChunks = kSmallMax / 16;
 // The decode of one small read by the calling workgroup (kSThreads threads).
 __device__ __forceinline__ void decode_small_wg(uint8_t *__restrict__ wire, uint32_t N,
                                                 fws_frame_info *__restrict__ frames, uint32_t cap,
-                                                fws_decode_result *__restrict__ res) {
+                                                fws_decode_result *__restrict__ res,
+                                                uint64_t *tr = nullptr) {   // phase clocks (service trace)
     __shared__ u32x4 s_buf[kSChunks + 1];
     __shared__ uint32_t s_po[kSmallFrames + 1];     // payload start of path frame f
     __shared__ uint32_t s_pe[kSmallFrames + 1];     // payload end, clipped to N
@@ -58,6 +59,7 @@ __device__ __forceinline__ void decode_small_wg(uint8_t *__restrict__ wire, uint
     }
     if (tid == 0) s_buf[nch] = u32x4{0u, 0u, 0u, 0u};
     __syncthreads();
+    if (tr && tid == 0) tr[0] = wall_clock64();
     const uint8_t *sb = (const uint8_t *)s_buf;
 
     // 2. the header chain from offset 0 (one lane; the terminal walk of
@@ -85,7 +87,7 @@ __device__ __forceinline__ void decode_small_wg(uint8_t *__restrict__ wire, uint
                 fi.hdr_off = q; fi.payload_len = h.plen; fi.key = h.key; fi.opcode = (uint8_t)h.opcode;
                 fi.fin = (uint8_t)h.fin; fi.hdr_len = (uint8_t)rc;
                 fi.flags = pe > N ? (uint8_t)FWS_FRAME_TRUNCATED : (uint8_t)0;
-                frames[nf] = fi;
+                gput(frames + nf, fi);
             }
             ++nf;
             pos = pe;
@@ -107,9 +109,10 @@ __device__ __forceinline__ void decode_small_wg(uint8_t *__restrict__ wire, uint
             r.n_survivors = nf;
         }
         s_nf = nf < cap ? nf : cap;                          // the frames listed are the ones unmasked
-        *res = r;
+        gput(res, r);
     }
     __syncthreads();
+    if (tr && tid == 0) tr[1] = wall_clock64();
 
     // 3. unmask: every chunk holding payload bytes, from LDS, one store each
     const uint32_t nf = s_nf;
@@ -145,7 +148,7 @@ __device__ __forceinline__ void decode_small_wg(uint8_t *__restrict__ wire, uint
         if (hi <= N) {
             gstore16(base + lo, v);
         } else {
-            for (uint32_t j = 0; lo + j < N; ++j) wire[lo + j] = (uint8_t)(v[j >> 2] >> (8u * (j & 3u)));
+            for (uint32_t j = 0; lo + j < N; ++j) gput(wire + lo + j, (uint8_t)(v[j >> 2] >> (8u * (j & 3u))));
         }
     }
 }
@@ -163,7 +166,7 @@ __global__ __launch_bounds__(kSThreads) void k_decode_small(uint8_t *__restrict_
 // the rest of the read), decoded as above.
 __device__ __forceinline__ void decode_segment(uint8_t *__restrict__ batch, const fws_seg_desc &d,
                                                fws_frame_info *__restrict__ frames,
-                                               fws_decode_result *__restrict__ res) {
+                                               fws_decode_result *__restrict__ res, uint64_t *tr = nullptr) {
     const uint32_t tid = threadIdx.x;
     // continuation: 16-B aligned start, so every 4-byte group uses the key as is.
     // Offsets are taken modulo 2^64: a read decoded in place (registered host
@@ -176,12 +179,12 @@ __device__ __forceinline__ void decode_segment(uint8_t *__restrict__ batch, cons
             v ^= u32x4{d.key, d.key, d.key, d.key};
             gstore16(reinterpret_cast<uintptr_t>(cont + lo), v);
         } else {
-            for (uint32_t j = lo; j < d.u; ++j) cont[j] ^= (uint8_t)(d.key >> (8u * (j & 3u)));
+            for (uint32_t j = lo; j < d.u; ++j) gput(cont + j, (uint8_t)(gget(cont + j) ^ (uint8_t)(d.key >> (8u * (j & 3u)))));
         }
     }
     if (d.L)
         decode_small_wg(reinterpret_cast<uint8_t *>(reinterpret_cast<uintptr_t>(batch) + d.hs_off), d.L,
-                        frames + d.fbase, d.fcap, res);
+                        frames + d.fbase, d.fcap, res, tr);
 }
 
 // Completion for a host that polls instead of synchronizing the stream (the
@@ -206,7 +209,10 @@ __device__ __forceinline__ void host_done(uint32_t *ctr, uint32_t target, uint32
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "");
         __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
-    __hip_atomic_store(flag, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    // (a global-space store: a flat one would hold the caller's next barrier
+    // until the host acknowledged it)
+    __hip_atomic_store((__attribute__((address_space(1))) uint32_t *)(uintptr_t)flag, seq, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 __global__ __launch_bounds__(kSThreads) void k_decode_segments(uint8_t *__restrict__ batch,
@@ -230,74 +236,119 @@ __global__ __launch_bounds__(kSThreads) void k_decode_one(uint8_t *__restrict__ 
 }
 
 // ------------------------------------------------------------ persistent service
-// fws_rx_service (fws_internal.h): block 0 is the poller (one lane: a
-// system-scope load of the mailbox state per ~0.1 us), blocks 1..workers the
-// decoders. A worker takes segments w, w + workers, ... of each request; all
-// workers count in dv->ctr and the last one stores the request's flag
-// (host_done). Host memory the request names (descriptors, reads in place,
+// fws_rx_service (fws_internal.h): block 0 is the poller (wave 0: one
+// system-scope load of the whole mailbox line per poll) and decodes the
+// one-segment requests itself (a session's read: no hop through device memory,
+// no completion counter); blocks 1..workers decode the larger ones, segments
+// w, w + workers, ... each; they count in dv->ctr and the last one stores the
+// request's flag (host_done). Host memory the request names (descriptors, reads in place,
 // frame records) is read after a system-scope acquire by each worker, so no L2
 // line of an earlier request is reused; the flag follows a system-scope release.
 __device__ __forceinline__ uint64_t svc_load64(const uint64_t *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// phase clocks of the one-segment requests (fws_internal_rx_service_trace):
+// [0] requests, [1..5] summed ticks from the request's detection to the
+// acquire, the staged read, the header walk, the unmask, the flag store
+__device__ unsigned long long g_svc_trace[8];
+
 __global__ __launch_bounds__(kSThreads) void k_rx_service(fws_svc_mail *mail, fws_svc_dev *dv, uint32_t seq0,
-                                                          uint32_t workers, uint64_t linger, uint64_t life) {
+                                                          uint32_t workers, uint64_t linger, uint64_t life,
+                                                          uint32_t trace) {
+    __shared__ uint32_t s_cmd[2];
+    __shared__ fws_svc_req s_req;
     if (blockIdx.x == 0) {
-        // the poller: wave 0, every lane i < 16 loading word i of the mailbox line
-        if (threadIdx.x >= kWave) return;
-        const uint32_t lane = threadIdx.x;
+        // the poller's workgroup: wave 0 polls, every lane i < 16 loading word i
+        // of the mailbox line; a one-segment request (a session's read) is
+        // decoded here by the whole workgroup, a larger one is handed to the
+        // workers through dv
+        const uint32_t lane = threadIdx.x & (kWave - 1u);
+        const bool poller = threadIdx.x < kWave;
         constexpr uint32_t kWords = sizeof(fws_svc_mail) / 8;               // 16
         constexpr uint32_t kReqW = sizeof(fws_svc_req) / 8, kTagW = offsetof(fws_svc_mail, tag) / 8;
+        static_assert(offsetof(fws_svc_req, nseg) % 8 == 0 && offsetof(fws_svc_req, kind) % 8 == 0,
+                      "nseg / kind: the low half of a word");
         const uint64_t *const src = reinterpret_cast<const uint64_t *>(mail) + (lane < kWords ? lane : 0u);
         uint64_t *const dst = reinterpret_cast<uint64_t *>(&dv->req) + (lane >= 1u && lane <= kReqW ? lane - 1u : 0u);
+        uint64_t *const ldst = reinterpret_cast<uint64_t *>(&s_req) + (lane >= 1u && lane <= kReqW ? lane - 1u : 0u);
         uint32_t last = seq0;
         const uint64_t t0 = wall_clock64();
-        uint64_t tl = t0;
+        uint64_t tl = t0, tq[4] = {0, 0, 0, 0}, tf = 0;
         for (;;) {
-            const uint64_t wv = svc_load64(src);                            // one load instruction, 16 words
-            const uint64_t st = (uint64_t)__builtin_amdgcn_readlane((uint32_t)(wv >> 32), 0) << 32 |
-                                (uint32_t)__builtin_amdgcn_readlane((uint32_t)wv, 0);
-            const uint32_t sq = (uint32_t)(st >> 1);
-            if (sq != last) {
-                const uint32_t tag = (uint32_t)__builtin_amdgcn_readlane((uint32_t)wv, kTagW);
-                if (tag != sq) continue;                                    // the request's half was read first: again
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");               // system scope, after the state
-                if (lane >= 1u && lane <= kReqW) *dst = wv;                 // the request into device memory
-                last = sq;
-                static_assert(offsetof(fws_svc_req, kind) % 8 == 0, "kind: the low half of a word");
-                const bool quit = (uint32_t)__builtin_amdgcn_readlane(
-                                      (uint32_t)wv, 1u + (uint32_t)(offsetof(fws_svc_req, kind) / 8)) == 1u;
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-                if (lane == 0) {
-                    if (quit) {                                             // stop and tell the workers
-                        __hip_atomic_store(&mail->state, (uint64_t)sq << 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-                        __hip_atomic_store(&dv->quit, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-                    } else {
-                        __hip_atomic_store(&dv->seq, sq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            if (poller) {
+                uint32_t cmd = 1u;                                          // 0: decode s_req here, 1: exit
+                for (;;) {
+                    const uint64_t wv = svc_load64(src);                    // one load instruction, 16 words
+                    const uint32_t sq = (uint32_t)__builtin_amdgcn_readlane((uint32_t)wv, 0) >> 1 |
+                                        (uint32_t)__builtin_amdgcn_readlane((uint32_t)(wv >> 32), 0) << 31;
+                    if (sq != last) {
+                        const uint32_t tag = (uint32_t)__builtin_amdgcn_readlane((uint32_t)wv, kTagW);
+                        if (tag != sq) continue;                            // the request's half was read first: again
+                        tl = wall_clock64();
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");       // system scope, after the state
+                        if (trace) tf = wall_clock64();
+                        last = sq;
+                        const bool quit = (uint32_t)__builtin_amdgcn_readlane(
+                                              (uint32_t)wv, 1u + (uint32_t)(offsetof(fws_svc_req, kind) / 8)) == 1u;
+                        const uint32_t nseg = (uint32_t)__builtin_amdgcn_readlane(
+                            (uint32_t)wv, 1u + (uint32_t)(offsetof(fws_svc_req, nseg) / 8));
+                        if (quit) {                                         // stop and tell the workers
+                            if (lane == 0) {
+                                __hip_atomic_store(&mail->state, (uint64_t)sq << 1, __ATOMIC_RELEASE,
+                                                   __HIP_MEMORY_SCOPE_SYSTEM);
+                                __hip_atomic_store(&dv->quit, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                            }
+                            break;
+                        }
+                        if (nseg == 1u) {                                   // this workgroup decodes it
+                            if (lane >= 1u && lane <= kReqW) *ldst = wv;
+                            cmd = 0u;
+                            break;
+                        }
+                        if (lane >= 1u && lane <= kReqW) *dst = wv;         // the request into device memory
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                        if (lane == 0) __hip_atomic_store(&dv->seq, sq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                        continue;
                     }
+                    const uint64_t now = wall_clock64();
+                    if (now - tl > linger || now - t0 > life) {
+                        uint32_t stopped = 0;
+                        if (lane == 0) {
+                            uint64_t exp = ((uint64_t)last << 1) | 1u;
+                            stopped = __hip_atomic_compare_exchange_strong(&mail->state, &exp, (uint64_t)last << 1,
+                                                                           __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE,
+                                                                           __HIP_MEMORY_SCOPE_SYSTEM) ? 1u : 0u;
+                            if (stopped)
+                                __hip_atomic_store(&dv->quit, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                        }
+                        if (__builtin_amdgcn_readlane(stopped, 0)) break;
+                        continue;                                           // a request came in meanwhile
+                    }
+                    __builtin_amdgcn_s_sleep(2);
                 }
-                if (quit) return;
-                tl = wall_clock64();
-                continue;
+                if (lane == 0) s_cmd[0] = cmd;
             }
-            const uint64_t now = wall_clock64();
-            if (now - tl > linger || now - t0 > life) {
-                uint32_t stopped = 0;
-                if (lane == 0) {
-                    uint64_t exp = ((uint64_t)last << 1) | 1u;
-                    stopped = __hip_atomic_compare_exchange_strong(&mail->state, &exp, (uint64_t)last << 1,
-                                                                   __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE,
-                                                                   __HIP_MEMORY_SCOPE_SYSTEM) ? 1u : 0u;
-                    if (stopped) __hip_atomic_store(&dv->quit, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-                }
-                if (__builtin_amdgcn_readlane(stopped, 0)) return;
-                continue;                                                   // a request came in meanwhile
+            __syncthreads();
+            if (s_cmd[0]) return;
+            const fws_svc_req rq = s_req;
+            const fws_seg_desc d = rq.descs ? *reinterpret_cast<const fws_seg_desc *>(rq.descs) : rq.one;
+            decode_segment(reinterpret_cast<uint8_t *>(rq.base), d, reinterpret_cast<fws_frame_info *>(rq.frames),
+                           reinterpret_cast<fws_decode_result *>(rq.res), trace ? tq : nullptr);
+            if (trace && threadIdx.x == 0) tq[2] = wall_clock64();
+            host_done(nullptr, 0u, reinterpret_cast<uint32_t *>(rq.flag), rq.flag_seq);
+            if (trace && threadIdx.x == 0) {                               // (thread 0 detected it: tl, tf)
+                const uint64_t te = wall_clock64();
+                g_svc_trace[0] += 1u;
+                g_svc_trace[1] += tf - tl;
+                g_svc_trace[2] += tq[0] - tl;
+                g_svc_trace[3] += tq[1] - tl;
+                g_svc_trace[4] += tq[2] - tl;
+                g_svc_trace[5] += te - tl;
             }
-            __builtin_amdgcn_s_sleep(2);
+            __syncthreads();                                               // s_req / s_cmd rewritten next round
         }
     }
-    __shared__ uint32_t s_cmd[2];
     const uint32_t w = blockIdx.x - 1u;
     uint32_t wlast = seq0;
     for (;;) {
@@ -335,11 +386,21 @@ __global__ __launch_bounds__(kSThreads) void k_rx_service(fws_svc_mail *mail, fw
 }  // namespace fwsk
 
 int fws_launch_rx_service(fws_svc_mail *mail, fws_svc_dev *dv, uint32_t seq0, uint32_t workers, uint64_t linger_ticks,
-                          uint64_t life_ticks, hipStream_t s) {
+                          uint64_t life_ticks, uint32_t trace, hipStream_t s) {
     if (!workers) return FWS_ERR_INVALID;
     hipLaunchKernelGGL(fwsk::k_rx_service, dim3(workers + 1u), dim3(fwsk::kSThreads), 0, s, mail, dv, seq0, workers,
-                       linger_ticks, life_ticks);
+                       linger_ticks, life_ticks, trace);
     return fws_hip_status(hipGetLastError());
+}
+
+// the service's phase clocks (fws_rx_service's trace hook): copied out, then zeroed
+int fws_rx_service_trace_read(unsigned long long *out8) {
+    hipError_t e = hipMemcpyFromSymbol(out8, HIP_SYMBOL(fwsk::g_svc_trace), sizeof(unsigned long long) * 8);
+    if (e == hipSuccess) {
+        const unsigned long long z[8] = {};
+        e = hipMemcpyToSymbol(HIP_SYMBOL(fwsk::g_svc_trace), z, sizeof(z));
+    }
+    return fws_hip_status(e);
 }
 
 int fws_launch_decode_segments(uint8_t *batch, const fws_seg_desc *segs, uint32_t n, fws_frame_info *frames,

@@ -1482,10 +1482,11 @@ using namespace fwsk;
 // wavefront, capped per kernel family (measured on MI355X, tools/tune_c5.py):
 // the sorted unmask runs one unit per wavefront (1.39 vs 1.54 ms on C5's 4 GiB
 // at 16384 workgroups: its owner lookup and loads are not pipelined across a
-// wave's units), the UTF-8 form 16 (65536 workgroups: 1.61 vs 1.76 / 1.69 ms
-// at 16384 / 262144); the stream unmask 2 (3.04 vs 3.26 ms for the C5 stream
-// decode at 16384; C2 / C3 batches have <= 65536 units, one per wavefront either way).
-constexpr int kCapStream = 16384, kCapSorted = 1 << 20, kCapSortedUtf8 = 65536, kCapStreamUnmask = 131072;
+// wave's units), and so does the UTF-8 form since its per-prefix lookup check
+// (r05, tools/ab_c5d.py: 1.436 ms at 1<<20 vs 1.568 / 1.493 / 1.437 at 65536 /
+// 131072 / 262144 workgroups); the stream unmask 2 (3.04 vs 3.26 ms for the C5
+// stream decode at 16384; C2 / C3 batches have <= 65536 units, one per wavefront either way).
+constexpr int kCapStream = 16384, kCapSorted = 1 << 20, kCapSortedUtf8 = 1 << 20, kCapStreamUnmask = 131072;
 static int g_grid_cap = 0;  // tuning hook: max workgroups of every streaming kernel (0: the defaults above)
 extern "C" __attribute__((visibility("default"))) int fws_internal_set_grid_cap(int blocks) {
     const int old = g_grid_cap;

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """A/B of the C5 stream decode (fws_gpu_decode_stream + UTF-8 flags on one 4 GiB
 C5 batch) with and without the cross-unit prefetch of k_unmask_stream<utf8>
-(fws_internal_set_stream_utf8_pf), in one process; every timed call decodes a
+(fws_internal_set_stream_utf8_pf) and, with AB_CAPS=a,b,..., at those caps
+on every streaming kernel's grid (fws_internal_set_grid_cap), in one process; every timed call decodes a
 freshly masked copy (4 copies rotated, re-masked by a device copy between
 repetitions, outside the timed region). One JSON line per (mode, rep)."""
 import json
@@ -34,9 +35,11 @@ def main(k=4, reps=3):
     while time.perf_counter() - t0 < 0.5:                     # warm clocks (re-masked below)
         gpu.decode_stream(ctx, bufs[0], cap, frames=frames, result=res, utf8_ok=ok)
         torch.cuda.synchronize()
+    modes = [(1, 0), (0, 0)] + [(1, int(c)) for c in (os.environ.get("AB_CAPS") or "").split(",") if c]
     for rep in range(reps):
-        for pf in ((1, 0) if rep % 2 == 0 else (0, 1)):
+        for pf, gcap in (modes if rep % 2 == 0 else modes[::-1]):
             lib().fws_internal_set_stream_utf8_pf(pf)
+            lib().fws_internal_set_grid_cap(gcap)       # 0: the library's default grids
             for b in bufs:
                 b.copy_(master)
             torch.cuda.synchronize()
@@ -48,7 +51,8 @@ def main(k=4, reps=3):
             torch.cuda.synchronize()
             r = gpu.read_result(res)
             flags_ok = bool(np.array_equal(ok[:n].cpu().numpy(), np.asarray(ok5, dtype=np.uint8)[:n]))
-            print(json.dumps({"pf": pf, "rep": rep, "ms": round(e0.elapsed_time(e1) / k, 4),
+            lib().fws_internal_set_grid_cap(0)
+            print(json.dumps({"pf": pf, "grid_cap": gcap, "rep": rep, "ms": round(e0.elapsed_time(e1) / k, 4),
                               "status": int(r["status"]), "frames_ok": int(r["n_frames"]) == n,
                               "flags_ok": flags_ok}), flush=True)
     lib().fws_internal_set_stream_utf8_pf(1)

@@ -167,8 +167,8 @@ __device__ __forceinline__ void tx_store_tail(uint8_t *out, uint64_t a, uint64_t
 // skipped; no byte at or past total is written.
 template <typename DescP, typename OffP>
 __device__ __forceinline__ void tx_unit(uint8_t *__restrict__ out, const uint8_t *__restrict__ src, DescP d,
-                                        OffP obase, uint32_t flo, uint32_t fhi, const fws_tx_desc &dA,
-                                        const fws_tx_desc &dB, uint64_t OA, uint64_t OB, uint64_t a0,
+                                        OffP obase, uint32_t flo, uint32_t fhi, const fws_tx_desc dA,
+                                        const fws_tx_desc dB, uint64_t OA, uint64_t OB, uint64_t a0,
                                         uint64_t own_end, uint64_t total) {
     if (fhi - flo >= 2u) {                             // small frames: bytewise with a search
         for (int j = 0; j < 4; ++j) {
@@ -179,7 +179,7 @@ __device__ __forceinline__ void tx_unit(uint8_t *__restrict__ out, const uint8_t
         }
         return;
     }
-    // at most two frames: uniform metadata (dA, dB = d[flo], d[fhi] at OA, OB);
+    // at most two frames: uniform metadata (dA, dB = d[flo], d[fhi] at OA, OB, by value);
     // payload k of frame X covers [PX, EX)
     TxSeam z;
     z.PA = OA + tx_hdr_len(dA);
@@ -289,8 +289,10 @@ __device__ __forceinline__ void tx_encode_body(uint8_t *__restrict__ out, const 
         }
         const uint32_t flo = uf0;
         const uint32_t fhi = (u + 1 < n_units) ? uf1 : n - 1;
-        tx_unit(out, src, d, obase, flo, fhi, d[flo], d[fhi], obase[flo], obase[fhi], u * kTxUnit + (uint64_t)lane * 16u,
-                total, total);
+        // (copies: a reference into `d` would be re-read after every store to `out`)
+        const fws_tx_desc dA = d[flo], dB = d[fhi];
+        const uint64_t OA = obase[flo], OB = obase[fhi];
+        tx_unit(out, src, d, obase, flo, fhi, dA, dB, OA, OB, u * kTxUnit + (uint64_t)lane * 16u, total, total);
     }
 }
 

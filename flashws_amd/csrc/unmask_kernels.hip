@@ -1484,9 +1484,11 @@ using namespace fwsk;
 // at 16384 workgroups: its owner lookup and loads are not pipelined across a
 // wave's units), and so does the UTF-8 form since its per-prefix lookup check
 // (r05, tools/ab_c5d.py: 1.436 ms at 1<<20 vs 1.568 / 1.493 / 1.437 at 65536 /
-// 131072 / 262144 workgroups); the stream unmask 2 (3.04 vs 3.26 ms for the C5
-// stream decode at 16384; C2 / C3 batches have <= 65536 units, one per wavefront either way).
-constexpr int kCapStream = 16384, kCapSorted = 1 << 20, kCapSortedUtf8 = 1 << 20, kCapStreamUnmask = 131072;
+// 131072 / 262144 workgroups); the stream unmask too since its UTF-8 form's
+// cross-unit prefetch (r05, tools/ab_c5s.py on the 4 GiB C5 stream decode:
+// 2.807-2.837 ms at 1<<20 against 2.860-2.889 at 131072 and 2.91 / 3.01 at
+// 65536 / 32768; C2 / C3 batches have <= 65536 units, one per wavefront either way).
+constexpr int kCapStream = 16384, kCapSorted = 1 << 20, kCapSortedUtf8 = 1 << 20, kCapStreamUnmask = 1 << 20;
 static int g_grid_cap = 0;  // tuning hook: max workgroups of every streaming kernel (0: the defaults above)
 extern "C" __attribute__((visibility("default"))) int fws_internal_set_grid_cap(int blocks) {
     const int old = g_grid_cap;

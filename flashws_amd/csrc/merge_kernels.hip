@@ -53,10 +53,16 @@
 
 namespace fwsk {
 
-// tiles per super tile: kStTiles (512 KiB), halved down to kStTilesMin for a
+// tiles per super tile: kStTiles (1 MiB), halved down to kStTilesMin for a
 // stream too short to give kStTarget super tiles (the host picks it per call,
-// MergeParams::st_tiles; LDS tables are sized for kStTiles)
-constexpr uint32_t kStTiles = 256;
+// MergeParams::st_tiles; LDS tables are sized for kStTiles). Streams under
+// 512 MiB (C2 / C3: 256 MiB) get 512 KiB super tiles as before; the C5 stream
+// (4 GiB) gets 4,096 super tiles of 1 MiB instead of 8,192 of 512 KiB, so
+// k_merge's three workgroups per CU take 6 rounds of its latency chain, not 11.
+#ifndef FWS_ST_TILES
+#define FWS_ST_TILES 512                                // (A/B builds: make exp EXP_DEFS=-DFWS_ST_TILES=256)
+#endif
+constexpr uint32_t kStTiles = FWS_ST_TILES;
 #ifndef FWS_ST_TILES_MIN
 #define FWS_ST_TILES_MIN 16
 #endif
@@ -288,9 +294,11 @@ __device__ uint32_t reserve_tails(const MergeParams &P, uint32_t s, uint32_t k) 
 
 // ------------------------------------------------------------------ k_merge
 constexpr uint32_t kDenseWaves = 4;                 // k_merge wavefronts running dense_tile()
-constexpr uint32_t kMidCap = 8192;                  // big super tiles merged / emitted in LDS (else global scratch)
+constexpr uint32_t kMidCap = 6144;                  // big super tiles merged / emitted in LDS (else global scratch;
+                                                    //   6144, not 8192: k_merge keeps 3 workgroups per CU at 512 tiles)
+constexpr uint16_t kDenseTile16 = (uint16_t)kDenseTile;   // tcnt's mark (real tile counts are <= kTile)
 struct MergeLds {
-    uint32_t tcnt[kStTiles];
+    uint16_t tcnt[kStTiles];                         // (u16: three workgroups per CU at 512 tiles)
     uint32_t tsp[kStTiles];
     uint32_t tbase[kStTiles];
     union {
@@ -317,7 +325,11 @@ struct MergeLds {
     uint32_t red32[kMWaves];
     uint32_t n_tail, tail_base;
 };
-static_assert(sizeof(MergeLds) <= 160u * 1024u / 3u, "three k_merge workgroups per CU (513 super tiles of C2 / C3)");
+// (LDS is allocated in 512-B blocks: 54,576 B at kMidCap 8192 rounded to three
+// blocks too many, and C2 / C3's 513 super tiles took a second round, +4 %)
+static_assert(3u * ((sizeof(MergeLds) + 1024u + 511u) / 512u * 512u) <= 160u * 1024u,
+              "three k_merge workgroups per CU (513 super tiles of C2 / C3), with 1 KB for its other LDS");
+static_assert(kStTiles <= (uint32_t)kMThreads, "one thread per tile of a super tile");
 
 // Slot id of survivor i of ST s (tile by a search of the ST's tile prefix in LDS).
 __device__ __forceinline__ uint32_t st_sid(const MergeParams &P, const MergeLds &L, uint32_t t0, uint32_t i) {
@@ -579,19 +591,19 @@ __global__ __launch_bounds__(kMThreads) void k_merge(MergeParams P) {
         // survivors to spill runs; the counts go back to tile_count / tile_spill for k_link
         // and k_emit (find_node)
         if (tid < kStTiles) {
-            L.tcnt[tid] = c;
+            L.tcnt[tid] = (uint16_t)c;               // (kDenseTile -> kDenseTile16)
             L.tsp[tid] = sp;
         }
         __syncthreads();
         const uint32_t w = tid >> 6;
         if (w < kDenseWaves) {
             for (uint32_t i = w; i < kStTiles; i += kDenseWaves) {
-                if (L.tcnt[i] != kDenseTile) continue;           // wave-uniform
+                if (L.tcnt[i] != kDenseTile16) continue;         // wave-uniform
                 if ((tid & 63) == 0) atomicAdd(&C[kCntDenseTiles], 1u);
                 const uint64_t r = dense_tile(L.dw[w], P.wire, P.N, t0 + i, P.spill_w, C, P.s_cap);
                 const uint32_t dn = (uint32_t)r, dsp = (uint32_t)(r >> 32);
                 if ((tid & 63) == 0) {
-                    L.tcnt[i] = dn;
+                    L.tcnt[i] = (uint16_t)dn;
                     L.tsp[i] = dsp;
                     P.tile_count[t0 + i] = dn;
                     P.tile_spill[t0 + i] = dsp;
@@ -609,7 +621,7 @@ __global__ __launch_bounds__(kMThreads) void k_merge(MergeParams P) {
     const uint32_t b = block_excl<uint32_t>(c, L.red32, &n);
     if (tid == 0) P.st_n[s] = n;        // (the survivor total: summed by the path resolve, no hot atomic)
     if (tid < kStTiles) {
-        L.tcnt[tid] = c;
+        L.tcnt[tid] = (uint16_t)c;
         L.tsp[tid] = sp;
         L.tbase[tid] = b;
     }
@@ -1632,9 +1644,15 @@ using namespace fwsk;
 
 // super tiles of kStTiles tiles, halved while that gives fewer than kStTarget
 // (a short stream's resolve then spreads over more CUs), down to kStTilesMin
+static uint64_t g_st_target = kStTarget;   // test hook: 1 = the largest super tiles on any stream
+extern "C" __attribute__((visibility("default"))) int fws_internal_set_st_target(int t) {
+    const int old = (int)g_st_target;
+    g_st_target = t > 0 && (uint64_t)t <= kStTarget ? (uint64_t)t : kStTarget;   // fewer super tiles only:
+    return old;                                                                    // the workspaces stay in bounds
+}
 static uint32_t st_tiles_for(uint64_t n_tiles) {
     uint32_t t = kStTiles;
-    while (t > kStTilesMin && n_tiles < (uint64_t)t * kStTarget) t >>= 1;
+    while (t > kStTilesMin && n_tiles < (uint64_t)t * g_st_target) t >>= 1;
     return t;
 }
 uint64_t fws_merge_super_tiles(uint64_t n_tiles) {

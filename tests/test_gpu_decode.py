@@ -16,8 +16,8 @@ from wsframes import frame
 
 pytestmark = pytest.mark.gpu
 
-# mode -> fws_internal_set_resolve_mode
-RESOLVE_MODES = {"super_tile": 0, "big_st": 1, "small_read": 2}
+# mode -> (fws_internal_set_resolve_mode, fws_internal_set_st_target)
+RESOLVE_MODES = {"super_tile": (0, 512), "big_st": (1, 512), "small_read": (2, 512), "st_1mib": (0, 1)}
 CNT_FAILED = 9              # decode_common.h Counter::kCntFallback (the resolve failed)
 CNT_BIG = 12                # decode_common.h Counter::kCntBig (super tiles on the big-ST path)
 
@@ -28,12 +28,17 @@ def resolve_mode(request):
     the super-tile resolve in LDS (merge_kernels.hip) and with the big-ST path
     forced for every super tile; and the RX session's one-launch small-read
     kernel (small_kernels.hip; streams <= 128 KiB with <= 256 headers, the rest
-    fall back to the super-tile path as the session does)."""
+    fall back to the super-tile path as the session does); and the super-tile
+    path with the largest super tiles (1 MiB, r05: streams of 512 MiB and up get
+    them) on every stream (st_1mib)."""
     from flashws_amd import _lib
     L = _lib.lib()
-    old = L.fws_internal_set_resolve_mode(RESOLVE_MODES[request.param])
+    mode, target = RESOLVE_MODES[request.param]
+    old = L.fws_internal_set_resolve_mode(mode)
+    old_t = L.fws_internal_set_st_target(target)
     yield request.param
     L.fws_internal_set_resolve_mode(old)
+    L.fws_internal_set_st_target(old_t)
 
 
 def counters(ctx):
@@ -205,7 +210,7 @@ def test_false_chains_join_the_path(ctx, cuda, seed):
 
 
 @pytest.mark.parametrize("stride", [256, 1000, 2900, 4500])
-def test_many_exit_tails_per_super_tile(ctx, cuda, stride):
+def test_many_exit_tails_per_super_tile(ctx, cuda, stride, resolve_mode):
     """Planted 126-form headers of 65,000 B inside long payloads, one every
     `stride` bytes: each survives its tile and leaves its super tile, so every
     64 KiB super tile of this 2.4 MB stream has ~250, ~65, ~22 or ~14 EXIT
@@ -213,7 +218,9 @@ def test_many_exit_tails_per_super_tile(ctx, cuda, stride):
     overflow area, taken with an atomic, and k_link's loop over it), and
     within it. Bit-exact with the oracle; at ~250 per super tile the tail list
     of a workspace sized for this stream (64 per super tile + 4096) is full and
-    the decode ends with FWS_ERR_CAPACITY, nothing listed or unmasked."""
+    the decode ends with FWS_ERR_CAPACITY, nothing listed or unmasked. With
+    1 MiB super tiles (st_1mib) a planted header's exit lands in its own super
+    tile: few EXIT tails, and the decode is checked bit-exact instead."""
     rng = np.random.default_rng(stride)
     frames = []
     for i in range(40):
@@ -227,7 +234,7 @@ def test_many_exit_tails_per_super_tile(ctx, cuda, stride):
     # stream, not by the larger streams earlier tests decoded
     small = gpu.Ctx(0, max_frames=len(wire) // 6 + 16, max_stream_bytes=len(wire))
     try:
-        if stride > 256:
+        if stride > 256 or resolve_mode == "st_1mib":
             check(small, cuda, wire)
             return
         got, _, r = decode(small, wire, cuda)

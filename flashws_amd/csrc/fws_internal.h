@@ -69,7 +69,8 @@ struct fws_svc_req {
     uint64_t frames;                   // fws_frame_info*
     uint64_t res;                      // fws_decode_result[nseg]
     uint64_t flag;                     // uint32_t* in host memory: flag_seq is stored there when done
-    uint32_t nseg, flag_seq, kind, pad;   // kind 1: quit
+    uint64_t out;                      // kind 2: where the decoded bytes [0, span) of base go (host memory)
+    uint32_t nseg, flag_seq, kind, span;   // kind 1: quit; 2: a pushed read (base: device staging)
     fws_seg_desc one;
 };
 static_assert(sizeof(fws_svc_req) % 8 == 0, "8-B words");
@@ -78,19 +79,26 @@ static_assert(sizeof(fws_svc_req) % 8 == 0, "8-B words");
 // the request's seq, written with the request (a later 64-B half than the
 // state word): a read that sees the new state and the new tag saw the whole
 // request, since the host writes the request, then the tag, then CASes state.
-struct alignas(128) fws_svc_mail {     // coherent pinned host memory
+// Push mode (large-BAR devices, r05): the line the poller reads lives in
+// fine-grained device memory and the host writes it -- and a pushed read's
+// bytes, into the staging after it -- with CPU stores, an sfence before the
+// state word and one after it (write-combining buffers otherwise hold them).
+// The running bit keeps its CAS protocol on the pinned host line's state word.
+struct alignas(128) fws_svc_mail {     // coherent pinned host memory (or device memory: push mode)
     uint64_t state;
     fws_svc_req req;                   // written before the CAS that publishes its seq
     uint64_t tag;
-    uint64_t pad[2];
+    uint64_t pad[1];
 };
 static_assert(sizeof(fws_svc_mail) == 128, "one line");
 struct alignas(128) fws_svc_dev {      // device memory, zeroed before each launch
     uint32_t seq, quit, ctr, pad[29];
     fws_svc_req req;
 };
-int fws_launch_rx_service(fws_svc_mail *mail, fws_svc_dev *dv, uint32_t seq0, uint32_t workers, uint64_t linger_ticks,
-                          uint64_t life_ticks, uint32_t trace, hipStream_t s);
+// mail: the pinned line (its state word's running bit); poll: the line the
+// poller reads (mail, or the device-memory line in push mode)
+int fws_launch_rx_service(fws_svc_mail *mail, const fws_svc_mail *poll, fws_svc_dev *dv, uint32_t seq0,
+                          uint32_t workers, uint64_t linger_ticks, uint64_t life_ticks, uint32_t trace, hipStream_t s);
 int fws_rx_service_trace_read(unsigned long long *out8);
 struct fws_rx_service;
 // the context's service (created on first use when enabled), or null: not enabled
@@ -101,6 +109,16 @@ void fws_rx_service_destroy(fws_rx_service *v);
 int fws_rx_service_run(fws_rx_service *v, uint8_t *base, const fws_seg_desc *descs, const fws_seg_desc *one,
                        uint32_t nseg, fws_frame_info *frames, fws_decode_result *res, uint32_t *flag,
                        uint32_t flag_seq);
+// Push mode: can a read of `span` staged bytes be pushed (the service runs in
+// push mode and its device staging holds them)?
+bool fws_rx_service_can_push(const fws_rx_service *v, uint64_t span);
+// One pushed read, waited for: the host bytes src[0, span) are copied into the
+// service's device staging with CPU stores, decoded there as segment `d`
+// (offsets relative to the staging, 16-B aligned layout), and the decoded bytes
+// are written to out_dev[0, span) (host memory the device addresses: a
+// registered alias or pinned memory) before the flag.
+int fws_rx_service_push(fws_rx_service *v, const uint8_t *src, uint64_t span, uint8_t *out_dev, const fws_seg_desc &d,
+                        fws_frame_info *frames, fws_decode_result *res, uint32_t *flag, uint32_t flag_seq);
 
 // Device workspace for the chunk plan of one descriptor batch.
 // Descriptor batches are planned two ways in one launch (k_plan): chunk space

@@ -5,11 +5,21 @@
 // §4.5: ~6 us of a 4 KiB read's ~10 us). With the service the launch is gone
 // from the steady state: the decode grid stays resident while reads keep
 // coming (FLoop::OneStep's read loop, floop.h:661-703, hands over a read or a
-// step's batch every few us), polls a mailbox in coherent pinned memory, and
-// exits on its own after `linger` without a request -- so an idle process
-// holds no CUs and no hardware queue, and the next request relaunches it.
-// Requests are serialised per context (one mailbox); each is waited for by
-// its flag before the next is published.
+// step's batch every few us), polls a mailbox, and exits on its own after
+// `linger` without a request -- so an idle process holds no CUs and no
+// hardware queue, and the next request relaunches it. Requests are serialised
+// per context (one mailbox); each is waited for by its flag before the next
+// is published.
+//
+// Push mode (large-BAR devices): the mailbox the grid polls, and a staging
+// area for one small read, live in fine-grained device memory that the CPU
+// writes directly (write-combined stores, flushed by sfence). The grid then
+// polls local memory instead of reading host memory over PCIe per poll, and a
+// session's read arrives with its doorbell instead of being pulled by the
+// kernel: a doorbell round trip of 3.05 against 4.85 us, and 3.44 against
+// 5.99 us with 4 KiB pushed in and written back (tools/vram_probe.hip,
+// profiles/r05/vram_probe.jsonl).
+#include <stdlib.h>
 #include <string.h>
 
 #include <chrono>
@@ -22,13 +32,30 @@ struct fws_rx_service {
     uint32_t workers = 0;
     uint64_t ticks_per_us = 100;      // wall_clock64 rate (s_memrealtime, 100 MHz on gfx9)
     hipStream_t stream = nullptr;
-    fws_svc_mail *mail = nullptr;     // coherent pinned
+    fws_svc_mail *mail = nullptr;     // coherent pinned: the running bit (and the request, pull mode)
+    fws_svc_mail *vmail = nullptr;    // push mode: the polled line, in device memory (CPU-written only)
+    uint8_t *vstage = nullptr;        // push mode: a pushed read's staging, after vmail
+    bool push = false;
     fws_svc_dev *dv = nullptr;
     std::mutex mu;
-    uint64_t launches = 0, requests = 0;
+    uint64_t launches = 0, requests = 0, pushes = 0;
 };
 
 namespace {
+constexpr uint64_t kPushCap = (16u << 10) + 128u;   // a staged session read (kZcMax + pad + header bytes)
+int g_push = -1;                       // -1: FWS_RX_PUSH (default on where the device has a large BAR)
+
+// write-combined stores to device memory leave the CPU's buffers in order at a fence
+inline void wc_flush() {
+#if defined(__x86_64__) || defined(__i386__)
+    __builtin_ia32_sfence();
+#elif defined(__aarch64__)
+    __asm__ __volatile__("dsb st" ::: "memory");
+#else
+    __atomic_thread_fence(__ATOMIC_SEQ_CST);
+#endif
+}
+
 uint64_t g_linger_us = 250;            // idle time before the grid exits (tests shorten it)
 constexpr uint64_t kLifeUs = 200000;   // and its longest stay: it leaves at the next idle moment
 // phase trace (tools/lat_feed.cpp): the device's phase clocks (grids launched
@@ -61,13 +88,28 @@ extern "C" __attribute__((visibility("default"))) int fws_internal_set_rx_linger
     return old;
 }
 
-// launches and requests served by the context's service (tests)
+// launches and requests served by the context's service (tests); with a third
+// word: the pushed reads among them
 extern "C" __attribute__((visibility("default"))) int fws_internal_rx_service_stats(fws_gpu_ctx *ctx,
                                                                                    uint64_t *out2) {
     if (!ctx || !out2) return FWS_ERR_INVALID;
     out2[0] = ctx->svc ? ctx->svc->launches : 0;
     out2[1] = ctx->svc ? ctx->svc->requests : 0;
     return 0;
+}
+extern "C" __attribute__((visibility("default"))) int fws_internal_rx_service_pushes(fws_gpu_ctx *ctx,
+                                                                                    uint64_t *out1) {
+    if (!ctx || !out1) return FWS_ERR_INVALID;
+    *out1 = ctx->svc ? ctx->svc->pushes : 0;
+    return 0;
+}
+
+// push mode for services created from now on: 1 on (where the device has a
+// large BAR), 0 off, -1 the FWS_RX_PUSH environment variable (default on)
+extern "C" __attribute__((visibility("default"))) int fws_internal_set_rx_push(int on) {
+    const int old = g_push;
+    g_push = on < 0 ? -1 : (on ? 1 : 0);
+    return old;
 }
 
 fws_rx_service *fws_ctx_rx_service(fws_gpu_ctx *ctx) {
@@ -87,25 +129,128 @@ fws_rx_service *fws_ctx_rx_service(fws_gpu_ctx *ctx) {
         return nullptr;                // the per-read launch path stays in use
     }
     memset((void *)v->mail, 0, sizeof(fws_svc_mail));
+    int want = g_push;
+    if (want < 0) {
+        const char *e = getenv("FWS_RX_PUSH");
+        want = !(e && e[0] == '0');
+    }
+    int large_bar = 0;
+    if (want && hipDeviceGetAttribute(&large_bar, hipDeviceAttributeIsLargeBar, ctx->device) == hipSuccess &&
+        large_bar) {
+        void *p = nullptr;
+        if (hipExtMallocWithFlags(&p, sizeof(fws_svc_mail) + kPushCap, hipDeviceMallocFinegrained) == hipSuccess) {
+            if (hipMemset(p, 0, sizeof(fws_svc_mail)) == hipSuccess && hipDeviceSynchronize() == hipSuccess) {
+                v->vmail = static_cast<fws_svc_mail *>(p);
+                v->vstage = static_cast<uint8_t *>(p) + sizeof(fws_svc_mail);
+                v->push = true;
+            } else {
+                (void)hipFree(p);      // pull mode
+            }
+        }
+    }
     ctx->svc = v;
     return v;
 }
+
+bool fws_rx_service_can_push(const fws_rx_service *v, uint64_t span) {
+    return v && v->push && span <= kPushCap;
+}
+
+// Publishes the request written into line(v)->req as the next seq (tag, then
+// the running bit's CAS on the pinned line; push mode: then the device line's
+// state word) or launches a grid for it; the caller holds v->mu.
+namespace {
+fws_svc_mail *line(fws_rx_service *v) { return v->push ? v->vmail : v->mail; }
+
+int publish(fws_rx_service *v, bool tr) {
+    fws_svc_mail *const L = line(v);
+    uint64_t old = __atomic_load_n(&v->mail->state, __ATOMIC_ACQUIRE);
+    // the tag names the seq this request is published as (the poller reads the
+    // line in one load and trusts the request only when the tag matches)
+    if (v->push) {
+        L->tag = (old >> 1) + 1u;
+        wc_flush();                    // request, pushed bytes and tag before the state word
+    } else {
+        __atomic_store_n(&L->tag, (old >> 1) + 1u, __ATOMIC_RELEASE);
+    }
+    bool published = false;
+    if (old & 1u) {                    // a grid is running: hand it the request
+        uint64_t e = old;
+        published = __atomic_compare_exchange_n(&v->mail->state, &e, (((old >> 1) + 1u) << 1) | 1u, false,
+                                                __ATOMIC_SEQ_CST, __ATOMIC_SEQ_CST);
+        if (!published) old = e;       // it stopped in the meantime (same seq, running bit clear)
+    }
+    const uint64_t next = (((old >> 1) + 1u) << 1) | 1u;
+    if (published) {
+        if (v->push) {                 // the running grid polls the device line
+            L->state = next;
+            wc_flush();
+        }
+        return 0;
+    }
+    // no grid: publish the request as the next seq and launch one behind the
+    // previous grid's exit (stream order), its device words zeroed first
+    const uint32_t seq0 = (uint32_t)(old >> 1);
+    if (v->push) {
+        L->state = next;
+        wc_flush();
+    }
+    __atomic_store_n(&v->mail->state, next, __ATOMIC_SEQ_CST);
+    int r = fws_hip_status(hipMemsetAsync(v->dv, 0, sizeof(fws_svc_dev), v->stream));
+    if (!r)
+        r = fws_launch_rx_service(v->mail, line(v), v->dv, seq0, v->workers, g_linger_us * v->ticks_per_us,
+                                  kLifeUs * v->ticks_per_us, tr ? 1u : 0u, v->stream);
+    if (r) {
+        __atomic_store_n(&v->mail->state, (uint64_t)seq0 << 1, __ATOMIC_SEQ_CST);
+        if (v->push) {
+            L->state = (uint64_t)seq0 << 1;
+            wc_flush();
+        }
+        return r;
+    }
+    ++v->launches;
+    return 0;
+}
+
+int wait_traced(fws_rx_service *v, uint32_t *flag, uint32_t flag_seq, bool tr,
+                std::chrono::steady_clock::time_point t0) {
+    if (!tr) return fws_wait_flag(flag, flag_seq, v->stream);
+    const auto t1 = std::chrono::steady_clock::now();
+    const int r = fws_wait_flag(flag, flag_seq, v->stream);
+    const auto t2 = std::chrono::steady_clock::now();
+    g_host_ns[0] += 1;
+    g_host_ns[1] += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count();
+    g_host_ns[2] += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t2 - t1).count();
+    return r;
+}
+}  // namespace
 
 void fws_rx_service_destroy(fws_rx_service *v) {
     if (!v) return;
     if (v->mail && v->stream) {
         std::lock_guard<std::mutex> lk(v->mu);
-        uint64_t old = __atomic_load_n(&v->mail->state, __ATOMIC_ACQUIRE);
+        const uint64_t old = __atomic_load_n(&v->mail->state, __ATOMIC_ACQUIRE);
         if (old & 1u) {                // a grid is running: a quit request
-            v->mail->req.kind = 1u;
-            __atomic_store_n(&v->mail->tag, (old >> 1) + 1u, __ATOMIC_RELEASE);
+            fws_svc_mail *const L = line(v);
+            L->req.kind = 1u;
+            if (v->push) {
+                L->tag = (old >> 1) + 1u;
+                wc_flush();
+            } else {
+                __atomic_store_n(&L->tag, (old >> 1) + 1u, __ATOMIC_RELEASE);
+            }
             uint64_t e = old;
-            (void)__atomic_compare_exchange_n(&v->mail->state, &e, (((old >> 1) + 1u) << 1) | 1u, false,
-                                              __ATOMIC_SEQ_CST, __ATOMIC_SEQ_CST);   // fails: it just stopped
+            if (__atomic_compare_exchange_n(&v->mail->state, &e, (((old >> 1) + 1u) << 1) | 1u, false,
+                                            __ATOMIC_SEQ_CST, __ATOMIC_SEQ_CST) &&
+                v->push) {             // (a failed CAS: it just stopped)
+                L->state = (((old >> 1) + 1u) << 1) | 1u;
+                wc_flush();
+            }
         }
         (void)hipStreamSynchronize(v->stream);   // the grid has drained (quit or linger)
     }
     if (v->dv) (void)hipFree(v->dv);
+    if (v->vmail) (void)hipFree(v->vmail);
     if (v->mail) (void)hipHostFree(v->mail);
     if (v->stream) (void)hipStreamDestroy(v->stream);
     delete v;
@@ -117,53 +262,49 @@ int fws_rx_service_run(fws_rx_service *v, uint8_t *base, const fws_seg_desc *des
     if (!v || !nseg || !flag || (!descs && !one)) return FWS_ERR_INVALID;
     std::lock_guard<std::mutex> lk(v->mu);
     const bool tr = g_trace;
-    std::chrono::steady_clock::time_point t0, t1;
+    std::chrono::steady_clock::time_point t0;
     if (tr) t0 = std::chrono::steady_clock::now();
-    fws_svc_req &q = v->mail->req;     // plain stores; the CAS / store below publishes them
+    fws_svc_req &q = line(v)->req;     // plain stores; publish() orders them before the state word
     q.base = (uint64_t)(uintptr_t)base;
     q.descs = (uint64_t)(uintptr_t)descs;
     q.frames = (uint64_t)(uintptr_t)frames;
     q.res = (uint64_t)(uintptr_t)res;
     q.flag = (uint64_t)(uintptr_t)flag;
+    q.out = 0;
     q.nseg = nseg;
     q.flag_seq = flag_seq;
     q.kind = 0;
+    q.span = 0;
     if (!descs) q.one = *one;
-    uint64_t old = __atomic_load_n(&v->mail->state, __ATOMIC_ACQUIRE);
-    // the tag names the seq this request is published as (the poller reads the
-    // line in one load and trusts the request only when the tag matches)
-    __atomic_store_n(&v->mail->tag, (old >> 1) + 1u, __ATOMIC_RELEASE);
-    bool published = false;
-    if (old & 1u) {                    // a grid is running: hand it the request
-        uint64_t e = old;
-        published = __atomic_compare_exchange_n(&v->mail->state, &e, (((old >> 1) + 1u) << 1) | 1u, false,
-                                                __ATOMIC_SEQ_CST, __ATOMIC_SEQ_CST);
-        if (!published) old = e;       // it stopped in the meantime
-    }
     ++v->requests;
-    if (!published) {
-        // no grid: publish the request as the next seq and launch one behind the
-        // previous grid's exit (stream order), its device words zeroed first
-        const uint32_t seq0 = (uint32_t)(old >> 1);
-        __atomic_store_n(&v->mail->state, ((uint64_t)(seq0 + 1u) << 1) | 1u, __ATOMIC_SEQ_CST);
-        int r = fws_hip_status(hipMemsetAsync(v->dv, 0, sizeof(fws_svc_dev), v->stream));
-        if (!r)
-            r = fws_launch_rx_service(v->mail, v->dv, seq0, v->workers, g_linger_us * v->ticks_per_us,
-                                      kLifeUs * v->ticks_per_us, tr ? 1u : 0u, v->stream);
-        if (r) {
-            __atomic_store_n(&v->mail->state, (uint64_t)seq0 << 1, __ATOMIC_SEQ_CST);
-            return r;
-        }
-        ++v->launches;
-    }
-    if (!tr) return fws_wait_flag(flag, flag_seq, v->stream);
-    t1 = std::chrono::steady_clock::now();
-    const int r = fws_wait_flag(flag, flag_seq, v->stream);
-    const auto t2 = std::chrono::steady_clock::now();
-    g_host_ns[0] += 1;
-    g_host_ns[1] += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count();
-    g_host_ns[2] += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t2 - t1).count();
-    return r;
+    if (int r = publish(v, tr)) return r;
+    return wait_traced(v, flag, flag_seq, tr, t0);
+}
+
+int fws_rx_service_push(fws_rx_service *v, const uint8_t *src, uint64_t span, uint8_t *out_dev, const fws_seg_desc &d,
+                        fws_frame_info *frames, fws_decode_result *res, uint32_t *flag, uint32_t flag_seq) {
+    if (!fws_rx_service_can_push(v, span) || !flag || !out_dev || (span && !src)) return FWS_ERR_INVALID;
+    std::lock_guard<std::mutex> lk(v->mu);
+    const bool tr = g_trace;
+    std::chrono::steady_clock::time_point t0;
+    if (tr) t0 = std::chrono::steady_clock::now();
+    memcpy(v->vstage, src, span);      // the push: write-combined stores, flushed in publish()
+    fws_svc_req &q = v->vmail->req;
+    q.base = (uint64_t)(uintptr_t)v->vstage;
+    q.descs = 0;
+    q.frames = (uint64_t)(uintptr_t)frames;
+    q.res = (uint64_t)(uintptr_t)res;
+    q.flag = (uint64_t)(uintptr_t)flag;
+    q.out = (uint64_t)(uintptr_t)out_dev;
+    q.nseg = 1;
+    q.flag_seq = flag_seq;
+    q.kind = 2u;
+    q.span = (uint32_t)span;
+    q.one = d;
+    ++v->requests;
+    ++v->pushes;
+    if (int r = publish(v, tr)) return r;
+    return wait_traced(v, flag, flag_seq, tr, t0);
 }
 
 extern "C" {

@@ -405,7 +405,12 @@ static int feed_impl(fws_rx_session *s, uint8_t *buf, uint64_t size, uint64_t bu
         d.L = (uint32_t)(rest ? L : 0);
         d.fcap = segcap;
         const uint32_t seq = ++s->seq;
-        if (fws_rx_service *v = fws_ctx_rx_service(s->ctx)) {          // the resident grid, no launch
+        fws_rx_service *const v = fws_ctx_rx_service(s->ctx);
+        if (fws_rx_service_can_push(v, size)) {
+            // the resident grid, the read pushed into its device staging; the decoded
+            // bytes come back to the registered range itself
+            if ((r = fws_rx_service_push(v, buf, size, dev, d, s->hframes, s->hres, s->hflag, seq))) return r;
+        } else if (v) {                                                  // the resident grid, no launch
             if ((r = fws_rx_service_run(v, dev, nullptr, &d, 1, s->hframes, s->hres, s->hflag, seq))) return r;
         } else {
             if ((r = fws_launch_decode_one(dev, d, s->hframes, s->hres, st, s->hflag, seq))) return r;
@@ -442,7 +447,13 @@ static int feed_impl(fws_rx_session *s, uint8_t *buf, uint64_t size, uint64_t bu
         d.fcap = segcap;
         d.fbase = 0;
         const uint32_t seq = ++s->seq;
-        if (fws_rx_service *v = fws_ctx_rx_service(s->ctx)) {
+        fws_rx_service *const v = fws_ctx_rx_service(s->ctx);
+        const uint64_t span = rest ? hs_off + L : u;                     // the staged layout's bytes
+        if (fws_rx_service_can_push(v, span)) {
+            // pushed into the grid's device staging; the decoded bytes come back here
+            if ((r = fws_rx_service_push(v, s->hstage, span, s->hstage, d, s->hframes, s->hres, s->hflag, seq)))
+                return r;
+        } else if (v) {
             if ((r = fws_rx_service_run(v, s->hstage, nullptr, &d, 1, s->hframes, s->hres, s->hflag, seq))) return r;
         } else {
             if ((r = fws_launch_decode_one(s->hstage, d, s->hframes, s->hres, st, s->hflag, seq))) return r;

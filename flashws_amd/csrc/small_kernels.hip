@@ -31,7 +31,8 @@ constexpr uint32_t kSChunks = kSmallMax / 16;
 __device__ __forceinline__ void decode_small_wg(uint8_t *__restrict__ wire, uint32_t N,
                                                 fws_frame_info *__restrict__ frames, uint32_t cap,
                                                 fws_decode_result *__restrict__ res,
-                                                uint64_t *tr = nullptr) {   // phase clocks (service trace)
+                                                uint64_t *tr = nullptr,     // phase clocks (service trace)
+                                                uint8_t *out = nullptr) {   // else in place: every chunk to out
     __shared__ u32x4 s_buf[kSChunks + 1];
     __shared__ uint32_t s_po[kSmallFrames + 1];     // payload start of path frame f
     __shared__ uint32_t s_pe[kSmallFrames + 1];     // payload end, clipped to N
@@ -61,10 +62,14 @@ __device__ __forceinline__ void decode_small_wg(uint8_t *__restrict__ wire, uint
     __syncthreads();
     if (tr && tid == 0) tr[0] = wall_clock64();
     const uint8_t *sb = (const uint8_t *)s_buf;
+    static_assert(sizeof(s_buf) >= kSmallMax + 16u, "the header window of the last offset stays in s_buf");
 
-    // 2. the header chain from offset 0 (one lane; the terminal walk of
-    //    merge_kernels.hip resolve_path, from the stream start)
-    if (tid == 0) {
+    // 2. the header chain from offset 0 (wave 0, uniformly: each lane loads one
+    //    byte of the 16-byte header window, parse_hdr reads them by readlane --
+    //    one LDS round per header instead of a chain of dependent byte loads;
+    //    the terminal walk of merge_kernels.hip resolve_path, from the stream start)
+    if (tid < kWave) {
+        const uint32_t lane = tid;
         fws_decode_result r{};
         r.status = FWS_OK;
         uint64_t pos = 0;
@@ -73,16 +78,20 @@ __device__ __forceinline__ void decode_small_wg(uint8_t *__restrict__ wire, uint
         while (pos < N) {
             Hdr h;
             const uint32_t q = (uint32_t)pos;
-            const int rc = parse_hdr([&](int i) -> uint32_t { return sb[q + (uint32_t)i]; }, N - q, true, h);
+            const uint32_t bl = sb[q + (lane & 15u)];        // (in bounds: s_buf has a chunk past N)
+            const int rc = parse_hdr([&](int i) -> uint32_t { return (uint32_t)__builtin_amdgcn_readlane((int)bl, i); },
+                                     N - q, true, h);
             if (rc < 0) { r.status = rc; r.err_off = q; break; }
             if (rc == 0) break;                               // incomplete trailing header
             if (nf == kSmallFrames) { declined = true; break; }
             const uint64_t po = q + (uint32_t)rc;
             const uint64_t pe = po + h.plen;
-            s_po[nf] = (uint32_t)po;
-            s_pe[nf] = (uint32_t)(pe < N ? pe : N);
-            s_key[nf] = h.key;
-            if (nf < cap) {
+            if (lane == 0) {
+                s_po[nf] = (uint32_t)po;
+                s_pe[nf] = (uint32_t)(pe < N ? pe : N);
+                s_key[nf] = h.key;
+            }
+            if (nf < cap && lane == 0) {
                 fws_frame_info fi;
                 fi.hdr_off = q; fi.payload_len = h.plen; fi.key = h.key; fi.opcode = (uint8_t)h.opcode;
                 fi.fin = (uint8_t)h.fin; fi.hdr_len = (uint8_t)rc;
@@ -108,26 +117,29 @@ __device__ __forceinline__ void decode_small_wg(uint8_t *__restrict__ wire, uint
             r.n_frames = nf;
             r.n_survivors = nf;
         }
-        s_nf = nf < cap ? nf : cap;                          // the frames listed are the ones unmasked
-        gput(res, r);
+        if (lane == 0) {
+            s_nf = nf < cap ? nf : cap;                      // the frames listed are the ones unmasked
+            gput(res, r);
+        }
     }
     __syncthreads();
     if (tr && tid == 0) tr[1] = wall_clock64();
 
     // 3. unmask: every chunk holding payload bytes, from LDS, one store each
+    // (with `out`: every chunk, to out)
     const uint32_t nf = s_nf;
-    if (nf == 0) return;
+    if (nf == 0 && !out) return;
     for (uint32_t c = tid; c < nch; c += kSThreads) {
         const uint32_t lo = 16u * c, hi = lo + 16u;
         // last frame whose payload starts at or before lo (or frame 0)
-        uint32_t a = 0, b = nf - 1u;
+        uint32_t a = 0, b = nf ? nf - 1u : 0u;
         while (a < b) {
             const uint32_t m = (a + b + 1u) >> 1;
             if (s_po[m] <= lo) a = m; else b = m - 1u;
         }
         u32x4 v = s_buf[c];
         bool touched = false;
-        for (uint32_t f = a; f < nf && s_po[f] < hi; ++f) {
+        for (uint32_t f = a; f < nf && s_po[f] < hi; ++f) {   // (none when nf == 0)
             const uint32_t po = s_po[f], pe = s_pe[f];
             if (pe <= lo) continue;
             touched = true;
@@ -144,11 +156,12 @@ __device__ __forceinline__ void decode_small_wg(uint8_t *__restrict__ wire, uint
                 v[w] ^= m;
             }
         }
-        if (!touched) continue;
+        if (!touched && !out) continue;
+        uint8_t *const dst = out ? out : wire;
         if (hi <= N) {
-            gstore16(base + lo, v);
+            gstore16((uintptr_t)dst + lo, v);
         } else {
-            for (uint32_t j = 0; lo + j < N; ++j) gput(wire + lo + j, (uint8_t)(v[j >> 2] >> (8u * (j & 3u))));
+            for (uint32_t j = 0; lo + j < N; ++j) gput(dst + lo + j, (uint8_t)(v[j >> 2] >> (8u * (j & 3u))));
         }
     }
 }
@@ -166,25 +179,27 @@ __global__ __launch_bounds__(kSThreads) void k_decode_small(uint8_t *__restrict_
 // the rest of the read), decoded as above.
 __device__ __forceinline__ void decode_segment(uint8_t *__restrict__ batch, const fws_seg_desc &d,
                                                fws_frame_info *__restrict__ frames,
-                                               fws_decode_result *__restrict__ res, uint64_t *tr = nullptr) {
+                                               fws_decode_result *__restrict__ res, uint64_t *tr = nullptr,
+                                               uint8_t *out = nullptr) {   // else in place (offsets as batch's)
     const uint32_t tid = threadIdx.x;
     // continuation: 16-B aligned start, so every 4-byte group uses the key as is.
     // Offsets are taken modulo 2^64: a read decoded in place (registered host
     // memory, rx_session.cpp) is addressed relative to the batch base too.
     uint8_t *const cont = reinterpret_cast<uint8_t *>(reinterpret_cast<uintptr_t>(batch) + d.cont_off);
+    uint8_t *const ocont = out ? out + d.cont_off : cont;
     for (uint32_t c = tid; 16u * c < d.u; c += kSThreads) {
         const uint32_t lo = 16u * c;
         if (lo + 16u <= d.u) {
             u32x4 v = gload16(reinterpret_cast<uintptr_t>(cont + lo));
             v ^= u32x4{d.key, d.key, d.key, d.key};
-            gstore16(reinterpret_cast<uintptr_t>(cont + lo), v);
+            gstore16(reinterpret_cast<uintptr_t>(ocont + lo), v);
         } else {
-            for (uint32_t j = lo; j < d.u; ++j) gput(cont + j, (uint8_t)(gget(cont + j) ^ (uint8_t)(d.key >> (8u * (j & 3u)))));
+            for (uint32_t j = lo; j < d.u; ++j) gput(ocont + j, (uint8_t)(gget(cont + j) ^ (uint8_t)(d.key >> (8u * (j & 3u)))));
         }
     }
     if (d.L)
         decode_small_wg(reinterpret_cast<uint8_t *>(reinterpret_cast<uintptr_t>(batch) + d.hs_off), d.L,
-                        frames + d.fbase, d.fcap, res, tr);
+                        frames + d.fbase, d.fcap, res, tr, out ? out + d.hs_off : nullptr);
 }
 
 // Completion for a host that polls instead of synchronizing the stream (the
@@ -253,9 +268,9 @@ __device__ __forceinline__ uint64_t svc_load64(const uint64_t *p) {
 // acquire, the staged read, the header walk, the unmask, the flag store
 __device__ unsigned long long g_svc_trace[8];
 
-__global__ __launch_bounds__(kSThreads) void k_rx_service(fws_svc_mail *mail, fws_svc_dev *dv, uint32_t seq0,
-                                                          uint32_t workers, uint64_t linger, uint64_t life,
-                                                          uint32_t trace) {
+__global__ __launch_bounds__(kSThreads) void k_rx_service(fws_svc_mail *mail, const fws_svc_mail *poll,
+                                                          fws_svc_dev *dv, uint32_t seq0, uint32_t workers,
+                                                          uint64_t linger, uint64_t life, uint32_t trace) {
     __shared__ uint32_t s_cmd[2];
     __shared__ fws_svc_req s_req;
     if (blockIdx.x == 0) {
@@ -269,7 +284,7 @@ __global__ __launch_bounds__(kSThreads) void k_rx_service(fws_svc_mail *mail, fw
         constexpr uint32_t kReqW = sizeof(fws_svc_req) / 8, kTagW = offsetof(fws_svc_mail, tag) / 8;
         static_assert(offsetof(fws_svc_req, nseg) % 8 == 0 && offsetof(fws_svc_req, kind) % 8 == 0,
                       "nseg / kind: the low half of a word");
-        const uint64_t *const src = reinterpret_cast<const uint64_t *>(mail) + (lane < kWords ? lane : 0u);
+        const uint64_t *const src = reinterpret_cast<const uint64_t *>(poll) + (lane < kWords ? lane : 0u);
         uint64_t *const dst = reinterpret_cast<uint64_t *>(&dv->req) + (lane >= 1u && lane <= kReqW ? lane - 1u : 0u);
         uint64_t *const ldst = reinterpret_cast<uint64_t *>(&s_req) + (lane >= 1u && lane <= kReqW ? lane - 1u : 0u);
         uint32_t last = seq0;
@@ -278,13 +293,20 @@ __global__ __launch_bounds__(kSThreads) void k_rx_service(fws_svc_mail *mail, fw
         for (;;) {
             if (poller) {
                 uint32_t cmd = 1u;                                          // 0: decode s_req here, 1: exit
+                // two polls in flight: the next line load is issued before this one is
+                // checked (a load older than the last request it saw is ignored: seqs
+                // only grow)
+                uint64_t wv = svc_load64(src);                              // one load instruction, 16 words
                 for (;;) {
-                    const uint64_t wv = svc_load64(src);                    // one load instruction, 16 words
+                    const uint64_t wn = svc_load64(src);
                     const uint32_t sq = (uint32_t)__builtin_amdgcn_readlane((uint32_t)wv, 0) >> 1 |
                                         (uint32_t)__builtin_amdgcn_readlane((uint32_t)(wv >> 32), 0) << 31;
-                    if (sq != last) {
+                    if ((int32_t)(sq - last) > 0) {
                         const uint32_t tag = (uint32_t)__builtin_amdgcn_readlane((uint32_t)wv, kTagW);
-                        if (tag != sq) continue;                            // the request's half was read first: again
+                        if (tag != sq) {                                    // the request's half was read first: again
+                            wv = wn;
+                            continue;
+                        }
                         tl = wall_clock64();
                         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");       // system scope, after the state
                         if (trace) tf = wall_clock64();
@@ -309,6 +331,7 @@ __global__ __launch_bounds__(kSThreads) void k_rx_service(fws_svc_mail *mail, fw
                         if (lane >= 1u && lane <= kReqW) *dst = wv;         // the request into device memory
                         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
                         if (lane == 0) __hip_atomic_store(&dv->seq, sq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                        wv = wn;
                         continue;
                     }
                     const uint64_t now = wall_clock64();
@@ -323,9 +346,11 @@ __global__ __launch_bounds__(kSThreads) void k_rx_service(fws_svc_mail *mail, fw
                                 __hip_atomic_store(&dv->quit, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
                         }
                         if (__builtin_amdgcn_readlane(stopped, 0)) break;
+                        wv = wn;
                         continue;                                           // a request came in meanwhile
                     }
-                    __builtin_amdgcn_s_sleep(2);
+                    __builtin_amdgcn_s_sleep(1);
+                    wv = wn;
                 }
                 if (lane == 0) s_cmd[0] = cmd;
             }
@@ -333,8 +358,10 @@ __global__ __launch_bounds__(kSThreads) void k_rx_service(fws_svc_mail *mail, fw
             if (s_cmd[0]) return;
             const fws_svc_req rq = s_req;
             const fws_seg_desc d = rq.descs ? *reinterpret_cast<const fws_seg_desc *>(rq.descs) : rq.one;
+            // a pushed read (kind 2) is decoded in the device staging and written to rq.out
             decode_segment(reinterpret_cast<uint8_t *>(rq.base), d, reinterpret_cast<fws_frame_info *>(rq.frames),
-                           reinterpret_cast<fws_decode_result *>(rq.res), trace ? tq : nullptr);
+                           reinterpret_cast<fws_decode_result *>(rq.res), trace ? tq : nullptr,
+                           rq.kind == 2u ? reinterpret_cast<uint8_t *>(rq.out) : nullptr);
             if (trace && threadIdx.x == 0) tq[2] = wall_clock64();
             host_done(nullptr, 0u, reinterpret_cast<uint32_t *>(rq.flag), rq.flag_seq);
             if (trace && threadIdx.x == 0) {                               // (thread 0 detected it: tl, tf)
@@ -385,11 +412,11 @@ __global__ __launch_bounds__(kSThreads) void k_rx_service(fws_svc_mail *mail, fw
 
 }  // namespace fwsk
 
-int fws_launch_rx_service(fws_svc_mail *mail, fws_svc_dev *dv, uint32_t seq0, uint32_t workers, uint64_t linger_ticks,
-                          uint64_t life_ticks, uint32_t trace, hipStream_t s) {
+int fws_launch_rx_service(fws_svc_mail *mail, const fws_svc_mail *poll, fws_svc_dev *dv, uint32_t seq0,
+                          uint32_t workers, uint64_t linger_ticks, uint64_t life_ticks, uint32_t trace, hipStream_t s) {
     if (!workers) return FWS_ERR_INVALID;
-    hipLaunchKernelGGL(fwsk::k_rx_service, dim3(workers + 1u), dim3(fwsk::kSThreads), 0, s, mail, dv, seq0, workers,
-                       linger_ticks, life_ticks, trace);
+    hipLaunchKernelGGL(fwsk::k_rx_service, dim3(workers + 1u), dim3(fwsk::kSThreads), 0, s, mail, poll, dv, seq0,
+                       workers, linger_ticks, life_ticks, trace);
     return fws_hip_status(hipGetLastError());
 }
 

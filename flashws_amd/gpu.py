@@ -89,6 +89,12 @@ class Ctx:
         check("fws_internal_rx_service_stats", lib().fws_internal_rx_service_stats(self.h, out))
         return int(out[0]), int(out[1])
 
+    def rx_service_pushes(self):
+        """reads the persistent decode took pushed into device memory (push mode)"""
+        out = (C.c_uint64 * 1)()
+        check("fws_internal_rx_service_pushes", lib().fws_internal_rx_service_pushes(self.h, out))
+        return int(out[0])
+
     def close(self):
         if self.h:
             lib().fws_gpu_ctx_destroy(self.h)

@@ -18,6 +18,7 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <cstdlib>
 #include <stdexcept>
 #include <string_view>
 #include <utility>
@@ -32,13 +33,27 @@ inline int WSMaskBytesFastDevice(void *dev_src, size_t size, uint32_t mask, void
     return fws_gpu_mask(dev_src, size, mask, hip_stream);
 }
 
-// RAII device context (one per host thread / FLoop, floop.h:331-345).
+// RAII device context (one per host thread / FLoop, floop.h:331-345). Server
+// reads are decoded by the persistent receive decode by default (a resident
+// grid of kDefaultPersistent workgroups while reads keep coming, gone after
+// 250 us without one; push mode on large-BAR devices: DESIGN.md §4.5): the
+// environment variable FWS_RX_PERSISTENT=N sets the workgroups, 0 a kernel
+// launch per read; SetPersistent() changes it later.
 class GpuContext {
 public:
+    static constexpr uint32_t kDefaultPersistent = 16;
     explicit GpuContext(int device = 0, uint64_t max_frames = 0, uint64_t max_stream_bytes = 0) {
         if (fws_gpu_ctx_create(device, &ctx_) != 0) throw std::runtime_error("fws_gpu_ctx_create failed");
-        if ((max_frames || max_stream_bytes) && fws_gpu_ctx_reserve(ctx_, max_frames, max_stream_bytes) != 0)
+        if ((max_frames || max_stream_bytes) && fws_gpu_ctx_reserve(ctx_, max_frames, max_stream_bytes) != 0) {
+            fws_gpu_ctx_destroy(ctx_);
             throw std::runtime_error("fws_gpu_ctx_reserve failed");
+        }
+        const char *e = std::getenv("FWS_RX_PERSISTENT");
+        const long w = e && *e ? std::strtol(e, nullptr, 10) : (long)kDefaultPersistent;
+        if (w > 0 && fws_gpu_ctx_set_rx_persistent(ctx_, (uint32_t)(w < 1024 ? w : 1024)) != 0) {
+            fws_gpu_ctx_destroy(ctx_);
+            throw std::runtime_error("fws_gpu_ctx_set_rx_persistent failed");
+        }
     }
     ~GpuContext() { fws_gpu_ctx_destroy(ctx_); }
     GpuContext(const GpuContext &) = delete;

@@ -21,12 +21,23 @@ from test_gpu_session import _out_matches, session_view
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module")
-def sctx(cuda):
+def _set_push(on):
+    from flashws_amd._lib import lib
+    return lib().fws_internal_set_rx_push(on)
+
+
+@pytest.fixture(scope="module", params=[1, 0], ids=["push", "pull"])
+def sctx(cuda, request):
+    """A context with the service in push mode (the session's small reads
+    written into device memory by the CPU, where the device has a large BAR)
+    and in pull mode (the grid reads them over PCIe)."""
+    old = _set_push(request.param)
     c = gpu.Ctx(0, max_frames=1 << 16, max_stream_bytes=1 << 24)
     c.set_rx_persistent(16)
+    c.push_mode = request.param
     yield c
     c.close()
+    _set_push(old)
 
 
 @pytest.fixture(scope="module")
@@ -61,6 +72,11 @@ def test_service_session_kat(sctx, arena, align_off):
     launches, requests = sctx.rx_service_stats()
     assert requests - before[1] > 100                  # the reads went through the resident grid
     assert launches - before[0] < requests - before[1]  # which was not relaunched per read
+    pushes = sctx.rx_service_pushes()
+    if sctx.push_mode:
+        assert pushes > 100                            # (the MI355X boxes have a large BAR)
+    else:
+        assert pushes == 0
 
 
 def test_service_mux_kat(sctx, arena, monkeypatch):

@@ -20,8 +20,7 @@ def run(mode, clients, msgs, persistent):
     args = [DROPIN, "server", "--port", "0", "--conns", str(clients), "--max-seconds", "60"]
     if mode != "reference":
         args += ["--gpu-batch" if mode == "batched" else "--gpu", "--device", "0"]
-        if persistent:
-            args += ["--persistent", str(persistent)]
+        args += ["--persistent", str(persistent)]        # (0: a launch per read)
     p = subprocess.Popen(args, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
     line = p.stdout.readline()
     if not line.startswith("listening"):

@@ -60,7 +60,8 @@ struct Opts {
     int port = 0;
     bool gpu = false;
     bool gpu_batch = false;             // --gpu-batch: GpuRxHook::EnableBatched
-    int persistent = 0;                 // --persistent N: the context's resident decode grid (N workgroups)
+    int persistent = -1;                // --persistent N: the context's resident decode grid (N workgroups,
+                                        //   0 = a launch per read; default: GpuContext's)
     int device = 0;
     int conns = 1;
     int clients = 1;
@@ -175,7 +176,7 @@ int RunServer(const Opts &o) {
     std::unique_ptr<fws_amd::GpuRxHookT<kTls>> hook;
     if (o.gpu) {
         gpu = std::make_unique<fws_amd::GpuContext>(o.device);
-        if (o.persistent > 0) gpu->SetPersistent(uint32_t(o.persistent));
+        if (o.persistent >= 0) gpu->SetPersistent(uint32_t(o.persistent));
         hook = std::make_unique<fws_amd::GpuRxHookT<kTls>>(*gpu);
         if (o.gpu_batch) hook->EnableBatched(ws, srv.loop);   // (or: every read of a loop step in one GPU batch)
         else hook->Enable(ws);                 // the one added line

@@ -110,7 +110,11 @@ int fws_gpu_ctx_reserve(fws_gpu_ctx *ctx, uint64_t max_frames, uint64_t max_stre
  * workgroups (+ one poller) that the context launches on first use and that
  * exits by itself after ~250 us without a read -- no kernel launch per read
  * while reads keep coming. 0 (the default) = a launch per read. The grid holds
- * `workers` CUs' LDS and one hardware queue while it is resident. */
+ * `workers` CUs' LDS and one hardware queue while it is resident. On a device
+ * with a large BAR the grid polls a mailbox in device memory that the CPU
+ * writes, and a session read of <= 16 KiB is copied there by the CPU with its
+ * doorbell (push mode; FWS_RX_PUSH=0 in the environment keeps every read a
+ * device-side pull over PCIe). Results are the same either way. */
 int fws_gpu_ctx_set_rx_persistent(fws_gpu_ctx *ctx, uint32_t workers);
 
 /* seam 1 -- device twin of WSMaskBytesFast (ws_mask.h:175): XOR n bytes at

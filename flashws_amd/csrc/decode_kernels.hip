@@ -45,6 +45,14 @@ constexpr bool kScanNT = FWS_SCAN_NT != 0;   // nontemporal stream loads
 constexpr uint32_t kSets = 2;                // tiles in flight per wavefront (register sets; 3 sets
                                              //   at 6 waves per SIMD measured slower)
 constexpr uint32_t kScanBlocksPerCu = 8;     // resident k_scan workgroups per CU
+#ifndef FWS_SCAN_EARLY_PF
+#define FWS_SCAN_EARLY_PF 0                     // A/B builds: 1 = refill a set as soon as its tile is in LDS
+#endif
+// 0: a register set is refilled after its tile's stores; 1: as soon as its tile
+// is staged in LDS (its loads get the tile's work time too) -- measured slower
+// on C2 / C3 (0.1858-0.1861 vs 0.1812-0.1815 ms, two in flight 0.171-0.173 vs
+// 0.163-0.164), 1 % faster on the C5 stream (profiles/r05/ab_scan_pf.txt)
+constexpr bool kEarlyPf = FWS_SCAN_EARLY_PF != 0;
 
 #ifdef FWS_SCAN_PROF
 // phase clocks of k_scan summed over wavefronts (tools/prof_scan.py; build: make prof)
@@ -160,6 +168,7 @@ __global__ __launch_bounds__(kScanThreads) __attribute__((amdgpu_waves_per_eu(8,
             }
             wave_sync();
             SCAN_MARK(0);
+            if (kEarlyPf) prefetch(t + kSets * GW, pf, halo);   // pf is in LDS now: refill it
 #if FWS_ABL == 1      // ablation (exp builds, timing only): stage the tile, nothing else
             {
                 const uint32_t v = *reinterpret_cast<const uint32_t *>(B + L32);
@@ -354,7 +363,7 @@ __global__ __launch_bounds__(kScanThreads) __attribute__((amdgpu_waves_per_eu(8,
             *reinterpret_cast<uint64_t *>(di32 + 4) = *reinterpret_cast<const uint64_t *>(f32 + 4);
             *dc = cv;
         }
-        prefetch(t + kSets * GW, pf, halo);
+        if (!kEarlyPf || !valid) prefetch(t + kSets * GW, pf, halo);
     };
 
     auto dummy_stores = [&]() {   // same younger-op count for a set on entry as on the loop back edge

@@ -78,6 +78,10 @@ constexpr uint32_t kTailRun = 16;                   // EXIT tails of one super t
 #define FWS_LAND_WAVE 1                               // A/B: 0 = one thread per tail, stage slots only
 #endif
 constexpr uint32_t kLandCap = 256;                  // k_merge: EXIT tails whose landing survivor it looks up
+#ifndef FWS_LAND_WAVE_MAX
+#define FWS_LAND_WAVE_MAX 24                          // A/B builds: 7 = one tail per idle wave (r04)
+#endif
+constexpr uint32_t kLandWaveMax = FWS_LAND_WAVE_MAX;  // up to this many: a wavefront per tail (7 idle waves)
 constexpr uint32_t kTailCapMax = 1u << 18;          // LDS bitmap of the path pruning
 constexpr uint32_t kCompCap = 32768;                // tails that are some tail's next (+ the root's)
 constexpr uint32_t kMaxPruneRounds = 64;
@@ -740,14 +744,16 @@ __global__ __launch_bounds__(kMThreads) void k_merge(MergeParams P) {
     // is left to k_link (kNone), and so is every tail of a stream with dense
     // tiles (another k_merge workgroup may be rewriting a tile's count and
     // spill offset while this one reads them)
-    if (FWS_LAND_WAVE && L.n_tail < kMThreads / 64u) {
-        // few tails (every dense-frame super tile): one wavefront per tail, so a
-        // spilled exit tile (more than 8 survivors: frames under ~250 B) is
-        // searched too -- its lanes read the spill run's offsets, one ballot --
-        // instead of k_link's binary search over it (a chain of dependent loads)
+    if (FWS_LAND_WAVE && L.n_tail <= kLandWaveMax) {
+        // few tails (every dense-frame super tile): one wavefront per tail, waves
+        // 1..7 taking every seventh, so a spilled exit tile (more than 8
+        // survivors: frames under ~250 B) is searched too -- its lanes read the
+        // spill run's offsets, one ballot -- instead of k_link's binary search
+        // over it (a chain of dependent loads). The 200,000 x 64 B stream's
+        // super tiles have 16 EXIT tails each (false chains leave with long
+        // lengths): k_link's first phase 6.2 -> see DESIGN 4.3.
         const uint32_t wv = tid >> 6, ln = tid & 63u;
-        if (wv >= 1u && wv - 1u < L.n_tail) {
-            const uint32_t k = wv - 1u;
+        for (uint32_t k = wv - 1u; wv >= 1u && k < L.n_tail; k += (uint32_t)kMWaves - 1u) {
             uint32_t w = kNone;
             if (!no_land) {
                 const uint64_t x = L.texit[k];

@@ -92,7 +92,9 @@ struct alignas(128) fws_svc_mail {     // coherent pinned host memory (or device
 };
 static_assert(sizeof(fws_svc_mail) == 128, "one line");
 struct alignas(128) fws_svc_dev {      // device memory, zeroed before each launch
-    uint32_t seq, quit, ctr, pad[29];
+    uint64_t seqn;                     // the request's seq | its segment count << 32 (one word: a worker
+                                       //   without a segment of it needs no fence)
+    uint32_t quit, ctr, pad[28];
     fws_svc_req req;
 };
 // mail: the pinned line (its state word's running bit); poll: the line the
@@ -112,6 +114,7 @@ int fws_rx_service_run(fws_rx_service *v, uint8_t *base, const fws_seg_desc *des
 // Push mode: can a read of `span` staged bytes be pushed (the service runs in
 // push mode and its device staging holds them)?
 bool fws_rx_service_can_push(const fws_rx_service *v, uint64_t span);
+uint32_t fws_rx_service_workers(const fws_rx_service *v);   // its decode workgroups (0: none)
 // One pushed read, waited for: the host bytes src[0, span) are copied into the
 // service's device staging with CPU stores, decoded there as segment `d`
 // (offsets relative to the staging, 16-B aligned layout), and the decoded bytes

@@ -152,6 +152,8 @@ fws_rx_service *fws_ctx_rx_service(fws_gpu_ctx *ctx) {
     return v;
 }
 
+uint32_t fws_rx_service_workers(const fws_rx_service *v) { return v ? v->workers : 0u; }
+
 bool fws_rx_service_can_push(const fws_rx_service *v, uint64_t span) {
     return v && v->push && span <= kPushCap;
 }

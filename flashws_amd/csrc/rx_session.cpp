@@ -779,7 +779,12 @@ int fws_rx_mux_feed(fws_rx_mux *m, const fws_rx_read *reads, uint32_t n, fws_rx_
             fws_decode_result *hr = (fws_decode_result *)(m->hmeta + desc_bytes);
             fws_frame_info *hf = (fws_frame_info *)(m->hmeta + desc_bytes + res_bytes);
             const uint32_t seq = ++m->seq;
-            if (fws_rx_service *v = fws_ctx_rx_service(m->ctx)) {      // the resident grid, no launch
+            // the resident grid when its workers cover the round (each takes its
+            // segments one after another): 64 reads of 4 KiB took 36.3 us on 16
+            // workers against 21.4 us for a launch with a workgroup per read
+            // (tools/lat_feed.cpp, profiles/r05/lat_mux.jsonl)
+            fws_rx_service *const v = fws_ctx_rx_service(m->ctx);
+            if (v && nseg <= fws_rx_service_workers(v)) {
                 if ((r = fws_rx_service_run(v, m->hbuf, (const fws_seg_desc *)m->hmeta, nullptr, nseg, hf, hr, m->hflag,
                                             seq)))
                     return r;

@@ -107,6 +107,48 @@ int main(int argc, char **argv) {
         }
         fws_gpu_ctx_destroy(ctx);
     }
+    // mux rounds (the batched hook's call per loop step): k reads of 4 KiB, one
+    // per connection, in registered memory, decoded in place
+    const uint32_t mux_workers[] = {0, 16, 64};
+    for (uint32_t workers : mux_workers) {
+        fws_gpu_ctx *ctx = nullptr;
+        if (fws_gpu_ctx_create(0, &ctx) || fws_gpu_ctx_set_rx_persistent(ctx, workers)) return 1;
+        for (uint32_t k : {1u, 8u, 32u, 64u}) {
+            fws_rx_mux *m = nullptr;
+            if (fws_rx_mux_create(ctx, k, &m)) return 1;
+            const size_t n = make_frame(frame, 4096, 0x1B2C3D4Eu);
+            const size_t slot = 8192;
+            std::vector<fws_rx_read> rd(k);
+            std::vector<fws_rx_read_result> res(k);
+            std::vector<double> us;
+            for (int i = 0; i < iters / 4 + 100; ++i) {
+                for (uint32_t c = 0; c < k; ++c) {
+                    memcpy(reg + c * slot, frame, n);
+                    rd[c] = fws_rx_read{c, 0u, reg + c * slot, n, slot};
+                }
+                const auto t0 = std::chrono::steady_clock::now();
+                const int r = fws_rx_mux_feed(m, rd.data(), k, res.data());
+                const auto t1 = std::chrono::steady_clock::now();
+                if (r) {
+                    fprintf(stderr, "mux feed failed: %d\n", r);
+                    return 1;
+                }
+                for (uint32_t c = 0; c < k; ++c)
+                    if (res[c].ret || res[c].n_events != 1) {
+                        fprintf(stderr, "mux read %u: ret %d events %llu\n", c, res[c].ret,
+                                (unsigned long long)res[c].n_events);
+                        return 1;
+                    }
+                if (i >= 100) us.push_back(std::chrono::duration<double, std::micro>(t1 - t0).count());
+            }
+            std::sort(us.begin(), us.end());
+            printf("{\"mux\": true, \"workers\": %u, \"reads\": %u, \"p10_us\": %.2f, \"p50_us\": %.2f, "
+                   "\"p90_us\": %.2f}\n", workers, k, us[us.size() / 10], us[us.size() / 2], us[us.size() * 9 / 10]);
+            fflush(stdout);
+            fws_rx_mux_destroy(m);
+        }
+        fws_gpu_ctx_destroy(ctx);
+    }
     fws_gpu_host_unregister(reg);
     return 0;
 }

@@ -27,6 +27,65 @@ namespace fwsk {
 constexpr uint32_t kSThreads = 1024;
 constexpr uint32_t kSChunks = kSmallMax / 16;
 
+// The one-frame read (one message per read, the drop-in hook's common case):
+// the stream is one complete header whose payload reaches or passes N. Every
+// wave reads the first 16 bytes itself (one broadcast load, the same bytes, so
+// the same wave-uniform parse) and each thread unmasks its own chunks straight
+// from memory: no LDS staging, no serial walk, no workgroup barrier. Results
+// are the general path's for such a stream (one frame record, carry-out of the
+// unread payload). Returns false, having written nothing, for any other stream.
+__device__ __forceinline__ bool decode_one_frame(uint8_t *__restrict__ wire, uint32_t N,
+                                                 fws_frame_info *__restrict__ frames, uint32_t cap,
+                                                 fws_decode_result *__restrict__ res, uint8_t *out) {
+    if (N < 2u || cap == 0u) return false;
+    const uintptr_t base = (uintptr_t)wire;
+    const u32x4 hv = gload16(base);                  // (16-B aligned: never past the page of byte N - 1)
+    // (readfirstlane returns int: through uint32_t, or the low word's sign would fill the high half)
+    const uint64_t lo = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(hv.y) << 32 |
+                        (uint32_t)__builtin_amdgcn_readfirstlane(hv.x);
+    const uint64_t hi = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(hv.w) << 32 |
+                        (uint32_t)__builtin_amdgcn_readfirstlane(hv.z);
+    Hdr h;
+    const int rc = parse_hdr([&](int i) -> uint32_t {
+        return (uint32_t)((i < 8 ? lo >> (8 * i) : hi >> (8 * (i - 8))) & 0xFFu);
+    }, N, true, h);
+    if (rc <= 0) return false;                       // an incomplete header or an error: the general path
+    const uint64_t po = (uint64_t)rc, pe = po + h.plen;
+    if (pe < N) return false;                        // more headers follow
+    if (threadIdx.x == 0) {
+        fws_frame_info fi;
+        fi.hdr_off = 0; fi.payload_len = h.plen; fi.key = h.key; fi.opcode = (uint8_t)h.opcode;
+        fi.fin = (uint8_t)h.fin; fi.hdr_len = (uint8_t)rc;
+        fi.flags = pe > N ? (uint8_t)FWS_FRAME_TRUNCATED : (uint8_t)0;
+        gput(frames, fi);
+        fws_decode_result r{};
+        r.status = FWS_OK;
+        r.consumed = N;
+        r.carry_unread = pe - N;                     // 0 when the frame ends at N
+        r.n_frames = 1;
+        r.n_survivors = 1;
+        gput(res, r);
+    }
+    // the payload [po, N): full dwords take the key rotated by the payload
+    // phase of a 4-aligned address, (-po) & 3; edge dwords keep their other bytes
+    const uint32_t rk = rotr32(h.key, 8u * ((0u - (uint32_t)po) & 3u));
+    const uint32_t nch = (N + 15u) >> 4;
+    uint8_t *const dst = out ? out : wire;
+    for (uint32_t c = threadIdx.x; c < nch; c += kSThreads) {
+        const uint32_t x0 = 16u * c;
+        if (!out && x0 + 16u <= po) continue;        // header bytes only: unchanged in place
+        u32x4 v = gload16(base + x0);
+#pragma unroll
+        for (uint32_t k = 0; k < 4u; ++k) v[k] ^= rk & sel_bytes(x0 + 4u * k, po, N);
+        if (x0 + 16u <= N) {
+            gstore16((uintptr_t)dst + x0, v);
+        } else {
+            for (uint32_t j = 0; x0 + j < N; ++j) gput(dst + x0 + j, (uint8_t)(v[j >> 2] >> (8u * (j & 3u))));
+        }
+    }
+    return true;
+}
+
 // The decode of one small read by the calling workgroup (kSThreads threads).
 __device__ __forceinline__ void decode_small_wg(uint8_t *__restrict__ wire, uint32_t N,
                                                 fws_frame_info *__restrict__ frames, uint32_t cap,
@@ -41,6 +100,7 @@ __device__ __forceinline__ void decode_small_wg(uint8_t *__restrict__ wire, uint
     const uint32_t tid = threadIdx.x;
     const uint32_t nch = (N + 15u) >> 4;
     const uintptr_t base = (uintptr_t)wire;
+    if (!tr && decode_one_frame(wire, N, frames, cap, res, out)) return;   // (wave-uniform)
 
     // 1. stage: all loads of a thread in flight together (the base is 16-B
     //    aligned, so the last chunk's block never crosses a page)

@@ -307,8 +307,8 @@ __device__ __forceinline__ void tx_encode_body(uint8_t *__restrict__ out, const 
 // LDS. Every chunk has one owner (the workgroup holding its first byte), so
 // all but the batch's last chunk are full 16-B stores.
 __device__ __forceinline__ uint64_t sgpr64(uint64_t v) {   // a wave-uniform value into SGPRs
-    return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
-           __builtin_amdgcn_readfirstlane((uint32_t)v);
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
+           (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);   // (int results: no sign extension)
 }
 __device__ __forceinline__ void sgpr_copy(const fws_tx_desc &x, fws_tx_desc &y) {
     static_assert(sizeof(fws_tx_desc) == 24, "6 words");

@@ -114,6 +114,30 @@ def test_truncated_payload(ctx, cuda):
     assert int(r["carry_unread"]) == 777
 
 
+@pytest.mark.parametrize("plen", [0, 1, 3, 4, 5, 15, 16, 17, 125, 126, 127, 4095, 4096, 65535, 65536, 70001])
+def test_one_frame_streams(ctx, cuda, plen):
+    """Streams that are one frame (the small-read decode's one-frame path,
+    small_kernels.hip decode_one_frame, r05: the header parsed per wave from one
+    broadcast load, chunks unmasked straight from memory): every length form at
+    its boundaries, whole and cut -- inside the header (the general path: an
+    incomplete header), right after it, one byte into the payload, one byte
+    short of the end -- with keys whose bytes have the top bit set (a
+    sign-extension bug in the header bytes' widening showed only with those),
+    forced 16- and 64-bit length forms too, TEXT and BIN; bit-exact with the
+    oracle in every resolve mode."""
+    rng = np.random.default_rng(plen + 11)
+    payload = rng.integers(0, 256, plen, dtype=np.uint8).tobytes()
+    for key in (0x3D21FA37, 0xF1E2D3C4, 0x80808080):
+        forms = [None] + ([126] if plen <= 65535 else []) + [127]
+        for form in forms:
+            for opcode in (1, 2):
+                w = frame(opcode, payload, key=key, len_form=form)
+                hdr = len(w) - plen
+                for cut in sorted({len(w), len(w) - 1, hdr, hdr + 1, hdr - 1, 2}):
+                    if 0 < cut <= len(w):
+                        check(ctx, cuda, w[:cut])
+
+
 @pytest.mark.parametrize("cut", [1, 3, 7, 40, 97, 3001])
 def test_dense_units_cut_anywhere(ctx, cuda, cut):
     """Units that meet 3-64 frames (k_unmask_stream's register-held frames,

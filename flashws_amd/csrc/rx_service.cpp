@@ -22,6 +22,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <atomic>
 #include <chrono>
 #include <mutex>
 
@@ -43,7 +44,7 @@ struct fws_rx_service {
 
 namespace {
 constexpr uint64_t kPushCap = (16u << 10) + 128u;   // a staged session read (kZcMax + pad + header bytes)
-int g_push = -1;                       // -1: FWS_RX_PUSH (default on where the device has a large BAR)
+std::atomic<int> g_push{-1};           // -1: FWS_RX_PUSH (default on where the device has a large BAR)
 
 // write-combined stores to device memory leave the CPU's buffers in order at a fence
 inline void wc_flush() {
@@ -56,12 +57,12 @@ inline void wc_flush() {
 #endif
 }
 
-uint64_t g_linger_us = 250;            // idle time before the grid exits (tests shorten it)
+std::atomic<uint64_t> g_linger_us{250};   // idle time before the grid exits (tests shorten it)
 constexpr uint64_t kLifeUs = 200000;   // and its longest stay: it leaves at the next idle moment
 // phase trace (tools/lat_feed.cpp): the device's phase clocks (grids launched
 // while it is on) and the host's publish / wait times, summed in ns
-bool g_trace = false;
-uint64_t g_host_ns[3];                 // requests, entry -> published, published -> flag seen
+std::atomic<bool> g_trace{false};
+std::atomic<uint64_t> g_host_ns[3];    // requests, entry -> published, published -> flag seen
 }  // namespace
 
 // on: trace the grids launched from now on; out: [0..7] the device sums
@@ -75,15 +76,12 @@ extern "C" __attribute__((visibility("default"))) int fws_internal_rx_service_tr
     int khz = 0;
     if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) != hipSuccess) khz = 0;
     out12[8] = (unsigned long long)khz / 1000u;
-    for (int i = 0; i < 3; ++i) {
-        out12[9 + i] = g_host_ns[i];
-        g_host_ns[i] = 0;
-    }
+    for (int i = 0; i < 3; ++i) out12[9 + i] = g_host_ns[i].exchange(0);
     return r;
 }
 
 extern "C" __attribute__((visibility("default"))) int fws_internal_set_rx_linger_us(int us) {
-    const int old = (int)g_linger_us;
+    const int old = (int)g_linger_us.load();
     if (us > 0) g_linger_us = (uint64_t)us;
     return old;
 }
@@ -107,9 +105,7 @@ extern "C" __attribute__((visibility("default"))) int fws_internal_rx_service_pu
 // push mode for services created from now on: 1 on (where the device has a
 // large BAR), 0 off, -1 the FWS_RX_PUSH environment variable (default on)
 extern "C" __attribute__((visibility("default"))) int fws_internal_set_rx_push(int on) {
-    const int old = g_push;
-    g_push = on < 0 ? -1 : (on ? 1 : 0);
-    return old;
+    return g_push.exchange(on < 0 ? -1 : (on ? 1 : 0));
 }
 
 fws_rx_service *fws_ctx_rx_service(fws_gpu_ctx *ctx) {
@@ -220,9 +216,11 @@ int wait_traced(fws_rx_service *v, uint32_t *flag, uint32_t flag_seq, bool tr,
     const auto t1 = std::chrono::steady_clock::now();
     const int r = fws_wait_flag(flag, flag_seq, v->stream);
     const auto t2 = std::chrono::steady_clock::now();
-    g_host_ns[0] += 1;
-    g_host_ns[1] += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count();
-    g_host_ns[2] += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t2 - t1).count();
+    g_host_ns[0].fetch_add(1, std::memory_order_relaxed);
+    g_host_ns[1].fetch_add((uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count(),
+                           std::memory_order_relaxed);
+    g_host_ns[2].fetch_add((uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t2 - t1).count(),
+                           std::memory_order_relaxed);
     return r;
 }
 }  // namespace

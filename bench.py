@@ -563,8 +563,12 @@ def c1_echo_extra(device=0):
     """BASELINE config 1: loopback echo of 4 KiB masked BIN
     frames through the drop-in server -- the reference's own FLoop +
     WSServerSocket<false> (oracle/_ref/ws_dropin, tools/dropin/ws_dropin.cpp)
-    with and without the one-line GpuRxHook -- for 1 and 8 clients (window 1,
-    every echoed byte checked), goodput rx+tx and RTT p50/p99; and the
+    with and without the one-line GpuRxHook -- for 1, 8 and 64 clients (window 1,
+    every echoed byte checked; 20,000 / 12,000 / 3,000 messages per client, so a
+    case runs ~0.5-1 s: the 64-client case at 500 messages, 0.1 s, measured the
+    ramp-up -- first-touch registration of the pool's read buffers, the resident
+    grid's first launch -- as much as the steady state, 17 against 21 Gbit/s,
+    tools/echo_prof.py), goodput rx+tx and RTT p50/p99; and the
     reference's own unchanged echo client (tests/new-ws-echo/test_ws_client.cpp,
     oracle/_ref/ws_ref_client_1, 40,000 messages, its HashArr check every
     16,384th) against the hooked and the plain server. Host-memory path: every
@@ -597,7 +601,7 @@ def c1_echo_extra(device=0):
 
     out = {"workload": "C1: loopback echo, 4 KiB masked BIN frames, window 1, plain ws:// on 127.0.0.1",
            "server": "reference FLoop + WSServerSocket<false> (ws_dropin); hooked = + fws_amd::GpuRxHook::Enable"}
-    for clients, msgs in ((1, 20000), (8, 4000), (64, 500)):
+    for clients, msgs in ((1, 20000), (8, 12000), (64, 3000)):
         for mode in ("reference", "gpu_hook", "gpu_hook_batched"):
             if clients == 1 and mode == "gpu_hook_batched":
                 continue                     # one read per loop step: the per-read path's round trip

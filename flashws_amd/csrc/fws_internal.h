@@ -111,6 +111,11 @@ void fws_rx_service_destroy(fws_rx_service *v);
 int fws_rx_service_run(fws_rx_service *v, uint8_t *base, const fws_seg_desc *descs, const fws_seg_desc *one,
                        uint32_t nseg, fws_frame_info *frames, fws_decode_result *res, uint32_t *flag,
                        uint32_t flag_seq);
+// The same request published and not waited for (fws_rx_mux_submit); the next
+// request on the service, or fws_rx_service_wait(flag, flag_seq), waits for it.
+int fws_rx_service_post(fws_rx_service *v, uint8_t *base, const fws_seg_desc *descs, uint32_t nseg,
+                        fws_frame_info *frames, fws_decode_result *res, uint32_t *flag, uint32_t flag_seq);
+int fws_rx_service_wait(fws_rx_service *v, uint32_t *flag, uint32_t flag_seq);
 // Push mode: can a read of `span` staged bytes be pushed (the service runs in
 // push mode and its device staging holds them)?
 bool fws_rx_service_can_push(const fws_rx_service *v, uint64_t span);

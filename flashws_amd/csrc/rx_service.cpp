@@ -40,6 +40,10 @@ struct fws_rx_service {
     fws_svc_dev *dv = nullptr;
     std::mutex mu;
     uint64_t launches = 0, requests = 0, pushes = 0;
+    // a request published by fws_rx_service_post and not waited for yet: the
+    // next request on the service waits for it first (one request at a time)
+    uint32_t *pend_flag = nullptr;
+    uint32_t pend_seq = 0;
 };
 
 namespace {
@@ -210,6 +214,14 @@ int publish(fws_rx_service *v, bool tr) {
     return 0;
 }
 
+// the posted request, if any, done (caller holds v->mu)
+int drain(fws_rx_service *v) {
+    if (!v->pend_flag) return 0;
+    uint32_t *const f = v->pend_flag;
+    v->pend_flag = nullptr;
+    return fws_wait_flag(f, v->pend_seq, v->stream);
+}
+
 int wait_traced(fws_rx_service *v, uint32_t *flag, uint32_t flag_seq, bool tr,
                 std::chrono::steady_clock::time_point t0) {
     if (!tr) return fws_wait_flag(flag, flag_seq, v->stream);
@@ -229,6 +241,7 @@ void fws_rx_service_destroy(fws_rx_service *v) {
     if (!v) return;
     if (v->mail && v->stream) {
         std::lock_guard<std::mutex> lk(v->mu);
+        (void)drain(v);                // a posted request is served before the quit
         const uint64_t old = __atomic_load_n(&v->mail->state, __ATOMIC_ACQUIRE);
         if (old & 1u) {                // a grid is running: a quit request
             fws_svc_mail *const L = line(v);
@@ -256,14 +269,10 @@ void fws_rx_service_destroy(fws_rx_service *v) {
     delete v;
 }
 
-int fws_rx_service_run(fws_rx_service *v, uint8_t *base, const fws_seg_desc *descs, const fws_seg_desc *one,
-                       uint32_t nseg, fws_frame_info *frames, fws_decode_result *res, uint32_t *flag,
-                       uint32_t flag_seq) {
-    if (!v || !nseg || !flag || (!descs && !one)) return FWS_ERR_INVALID;
-    std::lock_guard<std::mutex> lk(v->mu);
-    const bool tr = g_trace;
-    std::chrono::steady_clock::time_point t0;
-    if (tr) t0 = std::chrono::steady_clock::now();
+namespace {
+// the request of fws_rx_service_run / _post into the polled line (caller holds v->mu)
+void fill_run(fws_rx_service *v, uint8_t *base, const fws_seg_desc *descs, const fws_seg_desc *one, uint32_t nseg,
+              fws_frame_info *frames, fws_decode_result *res, uint32_t *flag, uint32_t flag_seq) {
     fws_svc_req &q = line(v)->req;     // plain stores; publish() orders them before the state word
     q.base = (uint64_t)(uintptr_t)base;
     q.descs = (uint64_t)(uintptr_t)descs;
@@ -277,14 +286,48 @@ int fws_rx_service_run(fws_rx_service *v, uint8_t *base, const fws_seg_desc *des
     q.span = 0;
     if (!descs) q.one = *one;
     ++v->requests;
+}
+}  // namespace
+
+int fws_rx_service_run(fws_rx_service *v, uint8_t *base, const fws_seg_desc *descs, const fws_seg_desc *one,
+                       uint32_t nseg, fws_frame_info *frames, fws_decode_result *res, uint32_t *flag,
+                       uint32_t flag_seq) {
+    if (!v || !nseg || !flag || (!descs && !one)) return FWS_ERR_INVALID;
+    std::lock_guard<std::mutex> lk(v->mu);
+    if (int r = drain(v)) return r;
+    const bool tr = g_trace;
+    std::chrono::steady_clock::time_point t0;
+    if (tr) t0 = std::chrono::steady_clock::now();
+    fill_run(v, base, descs, one, nseg, frames, res, flag, flag_seq);
     if (int r = publish(v, tr)) return r;
     return wait_traced(v, flag, flag_seq, tr, t0);
+}
+
+int fws_rx_service_post(fws_rx_service *v, uint8_t *base, const fws_seg_desc *descs, uint32_t nseg,
+                        fws_frame_info *frames, fws_decode_result *res, uint32_t *flag, uint32_t flag_seq) {
+    if (!v || !nseg || !flag || !descs) return FWS_ERR_INVALID;
+    std::lock_guard<std::mutex> lk(v->mu);
+    if (int r = drain(v)) return r;
+    fill_run(v, base, descs, nullptr, nseg, frames, res, flag, flag_seq);
+    if (int r = publish(v, false)) return r;
+    v->pend_flag = flag;
+    v->pend_seq = flag_seq;
+    return 0;
+}
+
+int fws_rx_service_wait(fws_rx_service *v, uint32_t *flag, uint32_t flag_seq) {
+    if (!v || !flag) return FWS_ERR_INVALID;
+    std::lock_guard<std::mutex> lk(v->mu);
+    if (v->pend_flag == flag && v->pend_seq == flag_seq) return drain(v);
+    // drained by a later request already: its flag is set
+    return __atomic_load_n(flag, __ATOMIC_ACQUIRE) == flag_seq ? 0 : fws_wait_flag(flag, flag_seq, v->stream);
 }
 
 int fws_rx_service_push(fws_rx_service *v, const uint8_t *src, uint64_t span, uint8_t *out_dev, const fws_seg_desc &d,
                         fws_frame_info *frames, fws_decode_result *res, uint32_t *flag, uint32_t flag_seq) {
     if (!fws_rx_service_can_push(v, span) || !flag || !out_dev || (span && !src)) return FWS_ERR_INVALID;
     std::lock_guard<std::mutex> lk(v->mu);
+    if (int r = drain(v)) return r;
     const bool tr = g_trace;
     std::chrono::steady_clock::time_point t0;
     if (tr) t0 = std::chrono::steady_clock::now();

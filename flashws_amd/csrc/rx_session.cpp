@@ -590,6 +590,19 @@ struct fws_rx_mux {
     uint32_t *dctr = nullptr;         // host_done counter of the zero-copy launch (reset by its last workgroup)
     uint32_t *hflag = nullptr;        // and its flag (coherent pinned word)
     uint32_t seq = 0;
+    // the submitted batch (fws_rx_mux_submit .. fws_rx_mux_complete)
+    struct Plan {
+        uint64_t u, rest, L, cont_off, hs_off;
+        uint32_t part0, seg;                     // seg: index in the launch, or kNone (session path)
+        uint8_t *dev;                            // decoded in place (registered host memory), or null
+    };
+    enum Wait { kWaitNone, kWaitService, kWaitFlag, kWaitStream };
+    bool inflight = false;
+    Wait wait = kWaitNone;
+    std::vector<fws_rx_read> sub_reads;
+    std::vector<Plan> sub_plan;
+    uint64_t sub_desc_bytes = 0, sub_res_bytes = 0;
+    uint32_t sub_seq = 0;
 
     int ensure(uint64_t bytes, uint64_t meta) {
         hipError_t e;
@@ -660,6 +673,8 @@ int fws_rx_mux_create(fws_gpu_ctx *ctx, uint32_t n_conns, fws_rx_mux **out) {
 
 void fws_rx_mux_destroy(fws_rx_mux *m) {
     if (!m) return;
+    if (m->inflight && m->wait == fws_rx_mux::kWaitService)   // a posted request: served before the buffers go
+        (void)fws_rx_service_wait(fws_ctx_rx_service(m->ctx), m->hflag, m->sub_seq);
     if (m->stream) (void)hipStreamSynchronize(m->stream);
     for (fws_rx_session *s : m->conns) fws_rx_session_destroy(s);
     if (m->hbuf) (void)hipHostFree(m->hbuf);
@@ -688,8 +703,8 @@ int fws_rx_mux_error(const fws_rx_mux *m, uint32_t conn, uint32_t *opcode) {
     return fws_rx_session_error(m->conns[conn], opcode);
 }
 
-int fws_rx_mux_feed(fws_rx_mux *m, const fws_rx_read *reads, uint32_t n, fws_rx_read_result *results) {
-    if (!m || (n && (!reads || !results))) return FWS_ERR_INVALID;
+int fws_rx_mux_submit(fws_rx_mux *m, const fws_rx_read *reads, uint32_t n) {
+    if (!m || (n && !reads) || m->inflight) return FWS_ERR_INVALID;
     for (uint32_t i = 0; i < n; ++i) {
         const fws_rx_read &rd = reads[i];
         if (rd.conn >= m->conns.size() || (rd.size && !rd.buf) || m->seen[rd.conn]) {
@@ -703,12 +718,9 @@ int fws_rx_mux_feed(fws_rx_mux *m, const fws_rx_read *reads, uint32_t n, fws_rx_
     if ((r = fws_hip_status(hipSetDevice(m->ctx->device)))) return r;
 
     // 1. plan: per read its continuation, header stream and frame slots
-    struct Plan {
-        uint64_t u, rest, L, cont_off, hs_off;
-        uint32_t part0, seg;                     // seg: index in the launch, or kNone (session path)
-        uint8_t *dev;                            // decoded in place (registered host memory), or null
-    };
-    std::vector<Plan> plan(n);
+    using Plan = fws_rx_mux::Plan;
+    std::vector<Plan> &plan = m->sub_plan;
+    plan.resize(n);
     uint64_t bytes = 0, frames = 0;
     uint32_t nseg = 0;
     for (uint32_t i = 0; i < n; ++i) {
@@ -739,6 +751,7 @@ int fws_rx_mux_feed(fws_rx_mux *m, const fws_rx_read *reads, uint32_t n, fws_rx_
     }
     const uint64_t desc_bytes = al16((uint64_t)nseg * sizeof(fws_seg_desc));
     const uint64_t res_bytes = al16((uint64_t)nseg * sizeof(fws_decode_result));
+    fws_rx_mux::Wait wait = fws_rx_mux::kWaitNone;
     if (nseg) {
         if ((r = m->ensure(bytes ? bytes : 16, desc_bytes + res_bytes + frames * sizeof(fws_frame_info)))) return r;
         fws_seg_desc *hd = (fws_seg_desc *)m->hmeta;
@@ -771,28 +784,29 @@ int fws_rx_mux_feed(fws_rx_mux *m, const fws_rx_read *reads, uint32_t n, fws_rx_
             d.pad = 0;
             fbase += d.fcap;
         }
-        // 2. one round trip: H2D, the segments' decode, D2H -- or for a small
-        // batch the decode alone, on the pinned buffers
+        // 2. one round trip, not waited for here: H2D, the segments' decode, D2H --
+        // or for a small batch the decode alone, on the pinned buffers
         hipStream_t st = m->stream;
         hipError_t e;
         if (bytes <= m->zc_max) {
             fws_decode_result *hr = (fws_decode_result *)(m->hmeta + desc_bytes);
             fws_frame_info *hf = (fws_frame_info *)(m->hmeta + desc_bytes + res_bytes);
-            const uint32_t seq = ++m->seq;
+            m->sub_seq = ++m->seq;
             // the resident grid when its workers cover the round (each takes its
             // segments one after another): 64 reads of 4 KiB took 36.3 us on 16
             // workers against 21.4 us for a launch with a workgroup per read
             // (tools/lat_feed.cpp, profiles/r05/lat_mux.jsonl)
             fws_rx_service *const v = fws_ctx_rx_service(m->ctx);
             if (v && nseg <= fws_rx_service_workers(v)) {
-                if ((r = fws_rx_service_run(v, m->hbuf, (const fws_seg_desc *)m->hmeta, nullptr, nseg, hf, hr, m->hflag,
-                                            seq)))
+                if ((r = fws_rx_service_post(v, m->hbuf, (const fws_seg_desc *)m->hmeta, nseg, hf, hr, m->hflag,
+                                             m->sub_seq)))
                     return r;
+                wait = fws_rx_mux::kWaitService;
             } else {
                 if ((r = fws_launch_decode_segments(m->hbuf, (const fws_seg_desc *)m->hmeta, nseg, hf, hr, st, m->dctr,
-                                                    nseg, m->hflag, seq)))
+                                                    nseg, m->hflag, m->sub_seq)))
                     return r;
-                if ((r = fws_wait_flag(m->hflag, seq, st))) return r;
+                wait = fws_rx_mux::kWaitFlag;
             }
         } else {
             fws_decode_result *dres = (fws_decode_result *)(m->dmeta + desc_bytes);
@@ -805,17 +819,40 @@ int fws_rx_mux_feed(fws_rx_mux *m, const fws_rx_read *reads, uint32_t n, fws_rx_
                 (e = hipMemcpyAsync(m->hmeta + desc_bytes, m->dmeta + desc_bytes,
                                     res_bytes + frames * sizeof(fws_frame_info), hipMemcpyDeviceToHost, st)) != hipSuccess)
                 return fws_hip_status(e);
-            if ((e = hipStreamSynchronize(st)) != hipSuccess) return fws_hip_status(e);
+            wait = fws_rx_mux::kWaitStream;
         }
     }
+    m->sub_reads.assign(reads, reads + n);
+    m->sub_desc_bytes = desc_bytes;
+    m->sub_res_bytes = res_bytes;
+    m->wait = wait;
+    m->inflight = true;
+    return 0;
+}
+
+int fws_rx_mux_complete(fws_rx_mux *m, fws_rx_read_result *results) {
+    if (!m || !m->inflight || (!m->sub_reads.empty() && !results)) return FWS_ERR_INVALID;
+    m->inflight = false;
+    int r = 0;
+    switch (m->wait) {
+    case fws_rx_mux::kWaitService: r = fws_rx_service_wait(fws_ctx_rx_service(m->ctx), m->hflag, m->sub_seq); break;
+    case fws_rx_mux::kWaitFlag: r = fws_wait_flag(m->hflag, m->sub_seq, m->stream); break;
+    case fws_rx_mux::kWaitStream: r = fws_hip_status(hipStreamSynchronize(m->stream)); break;
+    case fws_rx_mux::kWaitNone: break;
+    }
+    if (r) return r;
 
     // 3. per read: the bytes back, OnRecvData's bookkeeping, the events
+    const uint32_t n = (uint32_t)m->sub_reads.size();
+    const fws_rx_read *reads = m->sub_reads.data();
+    const fws_rx_mux::Plan *plan = m->sub_plan.data();
+    const uint64_t desc_bytes = m->sub_desc_bytes, res_bytes = m->sub_res_bytes;
     const fws_seg_desc *hd = (const fws_seg_desc *)m->hmeta;
     const fws_decode_result *hres = (const fws_decode_result *)(m->hmeta + desc_bytes);
     const fws_frame_info *hfr = (const fws_frame_info *)(m->hmeta + desc_bytes + res_bytes);
     for (uint32_t i = 0; i < n; ++i) {
         const fws_rx_read &rd = reads[i];
-        const Plan &p = plan[i];
+        const fws_rx_mux::Plan &p = plan[i];
         fws_rx_session *s = m->conns[rd.conn];
         s->own = true;
         s->own_ev.clear();
@@ -845,6 +882,12 @@ int fws_rx_mux_feed(fws_rx_mux *m, const fws_rx_read *reads, uint32_t n, fws_rx_
         s->own = false;
     }
     return 0;
+}
+
+int fws_rx_mux_feed(fws_rx_mux *m, const fws_rx_read *reads, uint32_t n, fws_rx_read_result *results) {
+    if (!m || (n && (!reads || !results))) return FWS_ERR_INVALID;
+    const int r = fws_rx_mux_submit(m, reads, n);
+    return r ? r : fws_rx_mux_complete(m, results);
 }
 
 }  // extern "C"

@@ -360,18 +360,26 @@ class RxMux:
         self.h = h
         self.n = n_conns
 
-    def feed(self, reads, extra_cap=0, arena=None, align_off=None):
+    def feed(self, reads, extra_cap=0, arena=None, align_off=None, between=None):
         """reads: [(conn, bytes)]. Returns [(ret, unmasked bytes, events, ctl bytes)].
         arena: a HostArena the reads are placed in (align_off(i) -> offset past a
-        64-B boundary for read i), else fresh host copies."""
+        64-B boundary for read i), else fresh host copies. between: a callable run
+        while the batch decodes (fws_rx_mux_submit, between(), fws_rx_mux_complete)
+        instead of one fws_rx_mux_feed."""
         bufs = [arena.place(d, align_off(i) if align_off else 0) if arena is not None
                 else np.frombuffer(bytes(d), dtype=np.uint8).copy() for i, (_, d) in enumerate(reads)]
         rr = np.zeros(len(reads), dtype=_lib.RX_READ)
         for i, ((conn, _), b) in enumerate(zip(reads, bufs)):
             rr[i] = (conn, 0, b.ctypes.data if len(b) else 0, len(b), len(b) + extra_cap)
         out = np.zeros(len(reads), dtype=_lib.RX_READ_RESULT)
-        check("fws_rx_mux_feed", lib().fws_rx_mux_feed(self.h, rr.ctypes.data if len(reads) else None, len(reads),
-                                                       out.ctypes.data if len(reads) else None))
+        if between is None:
+            check("fws_rx_mux_feed", lib().fws_rx_mux_feed(self.h, rr.ctypes.data if len(reads) else None,
+                                                           len(reads), out.ctypes.data if len(reads) else None))
+        else:
+            check("fws_rx_mux_submit", lib().fws_rx_mux_submit(self.h, rr.ctypes.data if len(reads) else None,
+                                                               len(reads)))
+            between()
+            check("fws_rx_mux_complete", lib().fws_rx_mux_complete(self.h, out.ctypes.data if len(reads) else None))
         res = []
         for i, b in enumerate(bufs):
             o = out[i]
@@ -384,6 +392,14 @@ class RxMux:
                 C.memmove(ctl.ctypes.data, int(o["ctl"]), n_ctl)
             res.append((int(o["ret"]), b.copy() if arena is not None else b, ev, ctl))
         return res
+
+    def submit_raw(self, rr, n):
+        """fws_rx_mux_submit on a prepared RX_READ array (tests); returns the code"""
+        return int(lib().fws_rx_mux_submit(self.h, rr.ctypes.data if n else None, n))
+
+    def complete_raw(self, out):
+        """fws_rx_mux_complete into a prepared RX_READ_RESULT array (tests); returns the code"""
+        return int(lib().fws_rx_mux_complete(self.h, out.ctypes.data if len(out) else None))
 
     def reset(self, conn):
         check("fws_rx_mux_reset", lib().fws_rx_mux_reset(self.h, conn))

@@ -37,17 +37,23 @@
 //
 // Batched (ws:// and wss://): EnableBatched(listen, loop) makes
 // every OPEN connection's read of one FLoop::OneStep wait in a pending list
-// (the reference decodes it inside the read loop, floop.h:661-703); at the end
-// of the step -- the loop's on_event callback, floop.h:743, which the hook
-// wraps and chains to the application's -- the reads of all connections go to
-// the GPU in one fws_rx_mux_feed (one H2D, one launch, one D2H) and their
-// events are dispatched in read order. A connection with a second read in the
-// same step (a full read buffer, floop.h:670-672), whose peer closes in the
-// step (on_eof), or which the loop closes in the step (the EOF / error branch,
-// floop.h:715-730 -> on_close) has the pending batch decoded first, so each
-// connection sees its events in order and before its EOF / on_close. Per
-// connection the callbacks are the per-read path's; only their timing moves to
-// the end of the step. A read of a connection that an earlier read's callbacks
+// (the reference decodes it inside the read loop, floop.h:661-703) and sends
+// the reads of many connections to the GPU in one fws_rx_mux round trip (one
+// H2D or none, one launch or resident-grid request, one D2H). Chunks of
+// SetChunk() reads (default 16) go out as they fill, from inside the step's
+// read loop, through fws_rx_mux_submit / _complete: a chunk decodes while the
+// loop reads the next sockets, and a completed chunk's events are dispatched
+// while the following chunk decodes. The rest goes at the end of the step (the
+// loop's on_event callback, floop.h:743, which the hook wraps and chains to the
+// application's); its events are dispatched there, in read order. A connection
+// with a second read in the same step (a full read buffer, floop.h:670-672) or
+// whose previous read is still in flight, whose peer closes in the step
+// (on_eof), or which the loop closes in the step (the EOF / error branch,
+// floop.h:715-730 -> on_close) has everything pending decoded and dispatched
+// first, so each connection sees its events in order and before its EOF /
+// on_close. Per connection the callbacks are the per-read path's; only their
+// timing moves (to a chunk boundary or the end of the step). A read of a
+// connection that an earlier read's callbacks
 // closed in the same step goes to the reference's own readable callback, as on
 // the per-read path. A protocol error closes the connection as the reference
 // does and removes it from the loop (DeleteFd, as floop.h:672-674 does after a
@@ -70,7 +76,9 @@
 // GPU decodes the plaintext WebSocket stream and TLS stays in OpenSSL.
 #pragma once
 
+#include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <memory>
@@ -190,14 +198,19 @@ public:
         app_on_event_ = [app_event, lp]() mutable { app_event(*lp); };
         delete_fd_ = [lp](void *p) { (lp->*(&LA::DeleteFd))(p, false); };
         GpuRxHookT *self = this;
+        prof_on_ = std::getenv("FWS_HOOK_PROF") != nullptr;
+        if (const char *c = std::getenv("FWS_HOOK_CHUNK")) chunk_ = (uint32_t)std::strtoul(c, nullptr, 10);
         loop.SetOnEventFunc([self](Loop &) {
+            if (self->prof_on_) self->ProfStep(true);
             self->Flush();
             self->DeleteDeferred();
             self->app_on_event_();
+            if (self->prof_on_) self->ProfStep(false);
         });
     }
 
     ~GpuRxHookT() {
+        if (mux_ && fl_active_) (void)CompleteInflight();   // (its reads' buffers go with pending state)
         if (mux_) fws_rx_mux_destroy(mux_);
         for (uint8_t *p : registered_) (void)fws_gpu_host_unregister(p);
     }
@@ -208,18 +221,36 @@ public:
     // staged through pinned memory as with SetZeroCopy(false).
     void SetZeroCopy(bool on) { zero_copy_ = on; }
 
+    // Batched path: the reads of a step go to the GPU in chunks of this many as
+    // they arrive (each chunk's round trip overlaps the step's later reads and
+    // the previous chunk's dispatch); 0 = one batch at the end of the step.
+    // Default kDefaultChunk; env FWS_HOOK_CHUNK at EnableBatched.
+    void SetChunk(uint32_t reads) { chunk_ = reads; }
+
     size_t connections() const { return conns_.size(); }
     uint64_t gpu_reads() const { return gpu_reads_; }
     uint64_t gpu_batches() const { return gpu_batches_; }
     size_t zero_copy_slots() const { return registered_.size(); }   // MemPool slots decoded in place
 
+    // Step profile of the batched path (env FWS_HOOK_PROF set at EnableBatched;
+    // tools): loop steps, flushes, reads, and the wall time of the loop's own
+    // part of the steps (epoll + reads, between two end-of-step callbacks), of
+    // the mux rounds and of the event dispatch (the application's callbacks).
+    struct StepProf {
+        uint64_t steps = 0, flushes = 0, reads = 0;
+        double loop_us = 0, mux_us = 0, dispatch_us = 0, step_end_us = 0;
+    };
+    const StepProf &step_prof() const { return prof_; }
+
 private:
     static constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
+    static constexpr uint32_t kDefaultChunk = 16;
     struct Conn {
         Sock *ws;
         std::unique_ptr<GpuRxDecoder<fws::IOBuffer>> dec;   // per-read path (no mux slot)
         uint32_t slot = kNoSlot;                           // batched path: fws_rx_mux slot
         bool pending = false;                              // a read of this step waits in pending_
+        bool inflight = false;                             // a read of it is in the submitted batch
         typename U::EofFunc ref_eof;                       // the under-socket's own on_eof
     };
     struct Pending {
@@ -298,7 +329,7 @@ private:
     void Retire(Sock &w) {
         auto it = conns_.find(&w.under_socket());
         if (it == conns_.end()) return;
-        if (it->second.pending && retiring_ == nullptr) {
+        if ((it->second.pending || it->second.inflight) && retiring_ == nullptr) {
             retiring_ = static_cast<USock *>(&w.under_socket());
             Flush();
             retiring_ = nullptr;
@@ -316,41 +347,74 @@ private:
         auto it = conns_.find(&t);
         if (it == conns_.end()) return;              // retired: its socket is being torn down
         typename U::EofFunc ref = it->second.ref_eof;
-        if (it->second.pending) Flush();
+        if (it->second.pending || it->second.inflight) Flush();
         if (ref) ref(t, ud);
     }
 
-    // The step's pending reads: one fws_rx_mux_feed, then each read's events
-    // in read order (ws_server_socket.h:172-196 per read).
-    void Flush() {
-        if (pending_.empty()) return;
-        std::vector<Pending> batch;
-        batch.swap(pending_);
+    // A batch of reads on its way through the mux: submitted (fws_rx_mux_submit),
+    // then completed (results) and dispatched.
+    struct Batch {
+        std::vector<Pending> items;
         std::vector<fws_rx_read> reads;
-        std::vector<uint32_t> idx;                   // reads[k] -> batch index
-        reads.reserve(batch.size());
-        for (uint32_t i = 0; i < batch.size(); ++i) {
-            auto it = conns_.find(batch[i].u);
+        std::vector<uint32_t> idx;                   // reads[k] -> items index
+        std::vector<fws_rx_read_result> res;
+        int rc = 0;
+    };
+
+    // pending_ -> the submitted batch (none may be in flight)
+    void SubmitPending() {
+        if (pending_.empty()) return;
+        Batch &b = fl_;
+        b = Batch{};
+        b.items.swap(pending_);
+        b.reads.reserve(b.items.size());
+        for (uint32_t i = 0; i < b.items.size(); ++i) {
+            auto it = conns_.find(b.items[i].u);
             if (it == conns_.end()) continue;
             it->second.pending = false;
-            fws::IOBuffer &b = batch[i].buf;
-            reads.push_back(fws_rx_read{it->second.slot, 0u, b.data + b.start_pos, (uint64_t)b.size,
-                                        (uint64_t)(b.capacity - b.start_pos)});
-            idx.push_back(i);
+            it->second.inflight = true;
+            fws::IOBuffer &buf = b.items[i].buf;
+            b.reads.push_back(fws_rx_read{it->second.slot, 0u, buf.data + buf.start_pos, (uint64_t)buf.size,
+                                          (uint64_t)(buf.capacity - buf.start_pos)});
+            b.idx.push_back(i);
         }
-        std::vector<fws_rx_read_result> res(reads.size());
-        const int rc = reads.empty() ? 0 : fws_rx_mux_feed(mux_, reads.data(), (uint32_t)reads.size(), res.data());
-        if (!reads.empty()) ++gpu_batches_;
-        for (size_t k = 0; k < reads.size(); ++k) {
-            Pending &p = batch[idx[k]];
+        const auto t0 = prof_on_ ? Clock::now() : Clock::time_point{};
+        b.rc = b.reads.empty() ? 0 : fws_rx_mux_submit(mux_, b.reads.data(), (uint32_t)b.reads.size());
+        if (prof_on_) prof_.mux_us += std::chrono::duration<double, std::micro>(Clock::now() - t0).count();
+        if (!b.reads.empty()) ++gpu_batches_;
+        fl_active_ = true;
+    }
+
+    // the submitted batch, waited for; no batch is in flight afterwards
+    Batch CompleteInflight() {
+        Batch b = std::move(fl_);
+        fl_ = Batch{};
+        fl_active_ = false;
+        const auto t0 = prof_on_ ? Clock::now() : Clock::time_point{};
+        b.res.resize(b.reads.size());
+        if (!b.reads.empty() && b.rc == 0) b.rc = fws_rx_mux_complete(mux_, b.res.data());
+        if (prof_on_) prof_.mux_us += std::chrono::duration<double, std::micro>(Clock::now() - t0).count();
+        for (uint32_t k = 0; k < b.reads.size(); ++k) {
+            auto it = conns_.find(b.items[b.idx[k]].u);
+            if (it != conns_.end()) it->second.inflight = false;
+        }
+        return b;
+    }
+
+    // A completed batch's events, read by read in read order (ws_server_socket.h:
+    // 172-196 per read).
+    void Dispatch(Batch &b) {
+        const auto t0 = prof_on_ ? Clock::now() : Clock::time_point{};
+        for (size_t k = 0; k < b.reads.size(); ++k) {
+            Pending &p = b.items[b.idx[k]];
             auto it = conns_.find(p.u);               // an earlier read's callbacks may have closed it
             if (it == conns_.end()) continue;
             Sock &sock = *it->second.ws;
-            // closed by an earlier read's callbacks in this step (an application
-            // closing another connection): the read goes to the reference's own
-            // callback, as on the per-read path -- in a closing state it does not
-            // decode the bytes (the mux has unmasked them in place), it closes the
-            // TCP socket (ws_server_socket.h:187-194)
+            // closed by an earlier read's callbacks (an application closing another
+            // connection): the read goes to the reference's own callback, as on the
+            // per-read path -- in a closing state it does not decode the bytes (the
+            // mux has unmasked them in place), it closes the TCP socket
+            // (ws_server_socket.h:187-194)
             if ((sock.*(&A::server_status_)) != A::kOpen) {
                 if (p.u == retiring_) continue;      // inside its own Close already
                 ref_readable_(*p.u, std::move(p.buf), p.ud);
@@ -359,11 +423,12 @@ private:
             }
             ++gpu_reads_;
             const uint32_t slot = it->second.slot;
-            int ret = rc;
-            if (rc == 0) {
-                ret = res[k].ret;
+            int ret = b.rc;
+            if (b.rc == 0) {
+                ret = b.res[k].ret;
                 Sink sink{sock};
-                GpuRxDecoder<fws::IOBuffer>::DispatchEvents(p.buf, res[k].events, res[k].n_events, res[k].ctl, sink);
+                GpuRxDecoder<fws::IOBuffer>::DispatchEvents(p.buf, b.res[k].events, b.res[k].n_events, b.res[k].ctl,
+                                                            sink);
             }
             Finish(sock, *p.u, ret, [&]() {
                 uint32_t op = 0;
@@ -371,6 +436,44 @@ private:
                 return op;
             }, true);
         }
+        if (prof_on_) {
+            ++prof_.flushes;
+            prof_.reads += b.reads.size();
+            prof_.dispatch_us += std::chrono::duration<double, std::micro>(Clock::now() - t0).count();
+        }
+    }
+
+    // One step of the pipeline: the batch in flight completes, the pending reads
+    // go to the GPU, and the completed batch's events are dispatched while they
+    // decode. Connections of the two batches are disjoint (a connection's next
+    // read waits until its previous one is dispatched), so each connection
+    // still sees its events in read order.
+    void Advance() {
+        if (!fl_active_) {
+            SubmitPending();
+            return;
+        }
+        Batch c = CompleteInflight();
+        SubmitPending();
+        Dispatch(c);
+    }
+
+    // Every pending and in-flight read decoded and dispatched, in order.
+    void Flush() {
+        while (fl_active_ || !pending_.empty()) Advance();
+    }
+
+    // end-of-step callback entry (begin) and exit: the loop's own part of a step
+    // is the time from one exit to the next entry
+    void ProfStep(bool begin) {
+        const auto now = Clock::now();
+        if (begin) {
+            if (prof_.steps) prof_.loop_us += std::chrono::duration<double, std::micro>(now - prof_t_).count();
+            ++prof_.steps;
+        } else {
+            prof_.step_end_us += std::chrono::duration<double, std::micro>(now - prof_b_).count();
+        }
+        (begin ? prof_b_ : prof_t_) = now;
     }
 
     // After a read's events: a protocol error closes the connection with the
@@ -445,7 +548,7 @@ private:
         }
         EnsureRegistered(buf);
         if (it->second.slot != kNoSlot) {            // batched: decoded at the end of the step
-            if (it->second.pending) {                // a second read this step: the batch goes first
+            if (it->second.pending || it->second.inflight) {   // its previous read goes first
                 Flush();
                 it = conns_.find(&u);
                 if (it == conns_.end() || (it->second.ws->*(&A::server_status_)) != A::kOpen) {
@@ -455,6 +558,9 @@ private:
             }
             it->second.pending = true;
             pending_.push_back(Pending{&u, std::move(buf), ud});
+            // a full chunk goes to the GPU now, so its round trip overlaps the
+            // step's remaining reads (and the previous chunk's dispatch)
+            if (chunk_ && pending_.size() >= chunk_) Advance();
             return;
         }
         Sock &sock = *it->second.ws;
@@ -492,6 +598,9 @@ private:
     fws_rx_mux *mux_ = nullptr;
     std::vector<uint32_t> free_slots_;
     std::vector<Pending> pending_;
+    Batch fl_;                                         // the submitted batch
+    bool fl_active_ = false;
+    uint32_t chunk_ = kDefaultChunk;                   // reads per submitted chunk within a step (0: per step)
     std::function<void()> app_on_event_;
     std::function<void(void *)> delete_fd_;
     USock *retiring_ = nullptr;                        // Retire's flush in progress for this socket
@@ -499,6 +608,11 @@ private:
     bool zero_copy_ = true;
     std::unordered_set<uint8_t *> registered_, unregistrable_;
     std::vector<USock *> deferred_;                    // DeleteFd at the end of the step
+    // step profile (FWS_HOOK_PROF)
+    using Clock = std::chrono::steady_clock;
+    bool prof_on_ = false;
+    StepProf prof_;
+    Clock::time_point prof_t_, prof_b_;
 };
 
 using GpuRxHook = GpuRxHookT<false>;      // ws://

@@ -314,6 +314,16 @@ int fws_rx_mux_error(const fws_rx_mux *m, uint32_t conn, uint32_t *opcode);
 /* Decode n reads (distinct connections). Returns 0 (per-read codes in
  * results[i].ret) or FWS_ERR_INVALID / a HIP error for the call itself. */
 int fws_rx_mux_feed(fws_rx_mux *m, const fws_rx_read *reads, uint32_t n, fws_rx_read_result *results);
+/* fws_rx_mux_feed in two halves, so the host can go on (read more sockets,
+ * dispatch an earlier batch's events) while the GPU decodes: submit stages and
+ * starts the batch and returns; complete waits for it and fills results[0, n)
+ * exactly as feed would. One batch at a time: submit again only after
+ * complete. Until complete returns the reads' buffers belong to the mux
+ * (unmasked in place), and the connections' state is the state before the
+ * batch. Other GPU calls of the context may be made in between (a request of
+ * the context's persistent receive decode waits for the batch first). */
+int fws_rx_mux_submit(fws_rx_mux *m, const fws_rx_read *reads, uint32_t n);
+int fws_rx_mux_complete(fws_rx_mux *m, fws_rx_read_result *results);
 
 /* ---- send path: batch frame builder -------------------
  * The bytes WSocket::SendFrame (w_socket.h:832-944) writes for one frame:

@@ -141,13 +141,16 @@ def _run_all(gpu, tls=False, batch=False):
     return got, srv.finish()
 
 
-@pytest.mark.parametrize("tls,batch", [(False, False), (True, False), (False, True), (True, True)],
-                         ids=["ws", "wss", "ws_batched", "wss_batched"])
-def test_dropin_scripted_parity_with_reference_server(cuda, tls, batch):
+@pytest.mark.parametrize("tls,batch,chunk", [(False, False, None), (True, False, None), (False, True, None),
+                                             (True, True, None), (False, True, 1), (True, True, 2)],
+                         ids=["ws", "wss", "ws_batched", "wss_batched", "ws_batched_chunk1", "wss_batched_chunk2"])
+def test_dropin_scripted_parity_with_reference_server(cuda, tls, batch, chunk, monkeypatch):
     """Scripted sessions (split reads, PING, fragmented messages, protocol
     errors, CLOSE) against the reference server and the hooked one, per read
     and batched per loop step (GpuRxHook::EnableBatched): handshake replies,
     every echoed / control / close frame byte and the close log are equal."""
+    if chunk is not None:           # the batched hook's reads go to the GPU in chunks of this many
+        monkeypatch.setenv("FWS_HOOK_CHUNK", str(chunk))
     ref, ref_srv = _run_all(gpu=False, tls=tls)
     gpu, gpu_srv = _run_all(gpu=True, tls=tls, batch=batch)
     assert gpu_srv["gpu_reads"] > 0 and ref_srv["gpu_reads"] == 0
@@ -169,12 +172,14 @@ def test_dropin_scripted_parity_with_reference_server(cuda, tls, batch):
     assert sum(1 for f in fr if f[1] == 10) > 0                       # PONGs
 
 
-@pytest.mark.parametrize("clients,msg_len,tls,batch", [(1, 4096, False, False), (8, 4096, False, False),
-                                                       (4, 70000, False, False), (16, 512, False, False),
-                                                       (8, 4096, True, False), (2, 70000, True, False),
-                                                       (8, 4096, False, True), (4, 70000, False, True),
-                                                       (16, 512, False, True), (8, 4096, True, True)])
-def test_dropin_reference_client_load(cuda, clients, msg_len, tls, batch):
+@pytest.mark.parametrize("clients,msg_len,tls,batch,chunk", [
+    (1, 4096, False, False, None), (8, 4096, False, False, None), (4, 70000, False, False, None),
+    (16, 512, False, False, None), (8, 4096, True, False, None), (2, 70000, True, False, None),
+    (8, 4096, False, True, None), (4, 70000, False, True, None), (16, 512, False, True, None),
+    (8, 4096, True, True, None), (16, 512, False, True, 3), (8, 70000, False, True, 2), (8, 4096, True, True, 2)])
+def test_dropin_reference_client_load(cuda, clients, msg_len, tls, batch, chunk, monkeypatch):
+    if chunk is not None:           # the batched hook's reads go to the GPU in chunks of this many
+        monkeypatch.setenv("FWS_HOOK_CHUNK", str(chunk))
     srv = Server(True, conns=clients, tls=tls, batch=batch)
     r = subprocess.run([DROPIN, "client", "--port", str(srv.port), "--clients", str(clients), "--msgs", "600",
                         "--warmup", "20", "--msg-len", str(msg_len), "--ping-every", "50", "--max-seconds", "60"]
@@ -272,8 +277,8 @@ def test_reference_echo_server_unchanged_with_gpu_hook(cuda, n_clients, tmp_path
 
 
 @pytest.mark.parametrize("scenario", ["close_peers", "eof_with_data"])
-@pytest.mark.parametrize("mode", ["gpu", "gpu_batch"])
-def test_dropin_same_step_reads_match_reference(cuda, scenario, mode):
+@pytest.mark.parametrize("mode", ["gpu", "gpu_batch", "gpu_batch_chunk1"])
+def test_dropin_same_step_reads_match_reference(cuda, scenario, mode, monkeypatch):
     """Two reads in one FLoop step (tests/dropin_steps.py): (close_peers) A's
     on_read closes connection B while B's read of the same step is still to be
     handled -- the batched hook hands it to the reference's closing-state
@@ -284,6 +289,9 @@ def test_dropin_same_step_reads_match_reference(cuda, scenario, mode):
     the server's message count and close log equal the reference server's."""
     import dropin_steps
     ref = dropin_steps.run_scenario(DROPIN, "reference", scenario)
+    if mode == "gpu_batch_chunk1":  # every read submitted as it arrives, dispatched at the next one
+        monkeypatch.setenv("FWS_HOOK_CHUNK", "1")
+        mode = "gpu_batch"
     got = dropin_steps.run_scenario(DROPIN, mode, scenario)
     assert got["server"]["gpu_reads"] > 0
     if mode == "gpu_batch":

@@ -12,7 +12,9 @@ own carried state (staged header bytes, unread payload, rotated key).
 * 64 connections with random frame streams cut at random read sizes, some
   reads over the mux's segment limits (the per-connection session path):
   each connection's results equal a standalone fws_rx_session fed the same
-  reads.
+  reads;
+* fws_rx_mux_submit / _complete (the batched hook's pipeline): one batch at a
+  time, and the result of a split call equals fws_rx_mux_feed.
 """
 import gzip
 import json
@@ -87,8 +89,9 @@ def _random_stream(rng, n_frames):
     return b"".join(out)
 
 
+@pytest.mark.parametrize("split", [False, True], ids=["feed", "submit_complete"])
 @pytest.mark.parametrize("seed", range(2))
-def test_mux_matches_per_connection_sessions(mctx, seed, zc_mode):
+def test_mux_matches_per_connection_sessions(mctx, seed, zc_mode, split):
     rng = np.random.default_rng(900 + seed)
     n_conns = 64
     streams = [_random_stream(rng, int(rng.integers(5, 60))) for _ in range(n_conns)]
@@ -105,7 +108,7 @@ def test_mux_matches_per_connection_sessions(mctx, seed, zc_mode):
     for r in range(max(len(c) for c in cuts)):
         live = [ci for ci in range(n_conns) if r < len(cuts[ci])]
         reads = [(ci, streams[ci][cuts[ci][r][0]:cuts[ci][r][1]]) for ci in live]
-        got = mux.feed(reads)
+        got = mux.feed(reads, between=(lambda: None) if split else None)
         for (ci, data), (ret, buf, ev, ctl) in zip(reads, got):
             rret, rbuf, rev, rctl = ref[ci].feed(data)
             assert ret == rret, (ci, r)
@@ -131,4 +134,18 @@ def test_mux_reset_and_invalid_calls(mctx):
     with pytest.raises(Exception):
         mux.feed([(2, masked)])                        # no such slot
     assert mux.feed([]) == []
+    # submit / complete: one batch at a time, complete only after a submit
+    from flashws_amd import _lib
+    rr = np.zeros(1, dtype=_lib.RX_READ)
+    buf = np.frombuffer(masked, dtype=np.uint8).copy()
+    rr[0] = (1, 0, buf.ctypes.data, len(buf), len(buf))
+    out = np.zeros(1, dtype=_lib.RX_READ_RESULT)
+    assert mux.complete_raw(out) != 0                  # nothing submitted
+    assert mux.submit_raw(rr, 1) == 0
+    assert mux.submit_raw(rr, 1) != 0                  # a batch is in flight
+    assert mux.complete_raw(out) == 0 and int(out[0]["ret"]) == 0
+    assert bytes(buf[8:]) == b"x" * 300                # unmasked in place (8-B header: 16-bit length)
+    assert mux.complete_raw(out) != 0
+    assert mux.submit_raw(rr, 0) == 0 and mux.complete_raw(out[:0]) == 0   # an empty batch
+    assert mux.submit_raw(rr, 1) == 0                  # left in flight: destroy waits for it
     mux.close()

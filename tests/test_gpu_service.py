@@ -132,6 +132,72 @@ def test_service_mux_random_vs_sessions(sctx, plain_ctx, arena):
         s.close()
 
 
+def test_service_mux_split_interleaved(sctx, plain_ctx, arena):
+    """fws_rx_mux_submit / _complete with other requests of the same context in
+    between (the batched hook's pipeline): chunks of at most 12 reads go to the
+    resident grid (posted, not waited for), chunks of 20-24 to a launch; while
+    a chunk decodes, another connection's session read on the same context
+    (which waits for the posted chunk first) and a second mux's whole batch
+    run. Every read equals a standalone session on a context without the
+    service."""
+    rng = np.random.default_rng(707)
+    n = 40
+    streams = [_random_stream(rng, int(rng.integers(5, 30))) for _ in range(n + 1)]
+    cuts = []
+    for st in streams:
+        pos, c = 0, []
+        while pos < len(st):
+            k = int(rng.choice([1, 9, 300, 4096, 6000]))
+            c.append(st[pos:pos + k])
+            pos += k
+        cuts.append(c)
+    mux, mux2 = gpu.RxMux(sctx, n), gpu.RxMux(sctx, 1)
+    side = gpu.RxSession(sctx)                          # connection n: fed between submit and complete
+    ref = [gpu.RxSession(plain_ctx) for _ in range(n + 2)]
+    side_r, dead = [0], set()
+    extra = _random_stream(rng, 40)
+    extra_cuts = [extra[i:i + 777] for i in range(0, len(extra), 777)]
+    extra_r = [0]
+
+    def between():
+        i = side_r[0]
+        if i < len(cuts[n]) and n not in dead:
+            ret, buf, ev, ctl = side.feed(cuts[n][i], arena=arena, align_off=0)
+            eret, ebuf, eev, ectl = ref[n].feed(cuts[n][i])
+            assert (ret, bytes(buf), session_view(ev, ctl)) == (eret, bytes(ebuf), session_view(eev, ectl))
+            if ret < 0:
+                dead.add(n)
+            side_r[0] += 1
+        j = extra_r[0]
+        if j < len(extra_cuts):                        # a whole second mux batch in between
+            (ret, buf, ev, ctl), = mux2.feed([(0, extra_cuts[j])], arena=arena)
+            eret, ebuf, eev, ectl = ref[n + 1].feed(extra_cuts[j])
+            assert (ret, bytes(buf), session_view(ev, ctl)) == (eret, bytes(ebuf), session_view(eev, ectl))
+            extra_r[0] += 1
+
+    chunks = 0
+    for r in range(max(len(c) for c in cuts[:n])):
+        live = [i for i in range(n) if r < len(cuts[i]) and i not in dead]
+        while live:
+            k = int(rng.choice([3, 12, 20, 24]))
+            part, live = live[:k], live[k:]
+            got = mux.feed([(i, cuts[i][r]) for i in part], arena=arena, between=between)
+            chunks += 1
+            for i, (ret, buf, ev, ctl) in zip(part, got):
+                eret, ebuf, eev, ectl = ref[i].feed(cuts[i][r])
+                assert ret == eret, (i, r)
+                assert bytes(buf) == bytes(ebuf), (i, r)
+                assert session_view(ev, ctl) == session_view(eev, ectl), (i, r)
+                if ret < 0:
+                    dead.add(i)
+    assert chunks > 20
+    mux.close()
+    mux2.close()
+    side.close()
+    for s in ref:
+        s.close()
+
+
 def test_service_declined_small_read(sctx, plain_ctx, arena):
     rng = np.random.default_rng(606)
     reads = _declined_reads(rng, 700)

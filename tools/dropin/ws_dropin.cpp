@@ -205,6 +205,13 @@ int RunServer(const Opts &o) {
         log += (i ? ", " : "") + std::string("[") + std::to_string(srv.close_log[i].first) + ", \"" + r + "\"]";
     }
     log += "]";
+    if (hook && std::getenv("FWS_HOOK_PROF")) {
+        const auto &pf = hook->step_prof();
+        std::printf("{\"hook_prof\": {\"steps\": %llu, \"flushes\": %llu, \"reads\": %llu, \"loop_us\": %.1f, "
+                    "\"mux_us\": %.1f, \"dispatch_us\": %.1f, \"step_end_us\": %.1f}}\n",
+                    (unsigned long long)pf.steps, (unsigned long long)pf.flushes, (unsigned long long)pf.reads, pf.loop_us,
+                    pf.mux_us, pf.dispatch_us, pf.step_end_us);
+    }
     std::printf("{\"mode\": \"server\", \"tls\": %s, \"gpu\": %s, \"msgs\": %llu, \"bytes\": %llu, \"closes\": %d, "
                 "\"close_log_hex\": %s, \"gpu_reads\": %llu, \"gpu_batches\": %llu, \"zc_slots\": %llu}\n",
                 kTls ? "true" : "false", o.gpu ? "true" : "false", (unsigned long long)srv.msgs, (unsigned long long)srv.bytes, srv.closes,

@@ -814,11 +814,16 @@ int fws_rx_mux_submit(fws_rx_mux *m, const fws_rx_read *reads, uint32_t n) {
             if ((e = hipMemcpyAsync(m->dbuf, m->hbuf, bytes, hipMemcpyHostToDevice, st)) != hipSuccess ||
                 (e = hipMemcpyAsync(m->dmeta, m->hmeta, desc_bytes, hipMemcpyHostToDevice, st)) != hipSuccess)
                 return fws_hip_status(e);
-            if ((r = fws_launch_decode_segments(m->dbuf, (const fws_seg_desc *)m->dmeta, nseg, dfr, dres, st))) return r;
+            if ((r = fws_launch_decode_segments(m->dbuf, (const fws_seg_desc *)m->dmeta, nseg, dfr, dres, st))) {
+                (void)hipStreamSynchronize(st);  // nothing of this batch may still write the staging
+                return r;
+            }
             if ((e = hipMemcpyAsync(m->hbuf, m->dbuf, bytes, hipMemcpyDeviceToHost, st)) != hipSuccess ||
                 (e = hipMemcpyAsync(m->hmeta + desc_bytes, m->dmeta + desc_bytes,
-                                    res_bytes + frames * sizeof(fws_frame_info), hipMemcpyDeviceToHost, st)) != hipSuccess)
+                                    res_bytes + frames * sizeof(fws_frame_info), hipMemcpyDeviceToHost, st)) != hipSuccess) {
+                (void)hipStreamSynchronize(st);
                 return fws_hip_status(e);
+            }
             wait = fws_rx_mux::kWaitStream;
         }
     }

@@ -7,7 +7,7 @@ closed loop), and the server hook's step profile (FWS_HOOK_CHUNK: reads per subm
 the loop's own part of the steps (epoll + recv), the mux rounds and the event
 dispatch (application callbacks: the echo sends), per step.
 
-usage: python tools/echo_prof.py [reps] [msgs_per_client]"""
+usage: python tools/echo_prof.py [reps] [msgs_per_client] [chunk|prefetch]"""
 import json
 import os
 import subprocess
@@ -24,8 +24,8 @@ def wait_rusage(p):
     return ru.ru_utime + ru.ru_stime
 
 
-def run(mode, clients, msgs, persistent, chunk=None):
-    env = dict(os.environ, FWS_HOOK_PROF="1")
+def run(mode, clients, msgs, persistent, chunk=None, extra_env=None):
+    env = dict(os.environ, FWS_HOOK_PROF="1", **(extra_env or {}))
     if chunk is not None:
         env["FWS_HOOK_CHUNK"] = str(chunk)       # reads per submitted chunk (0: one batch per step)
     args = [DROPIN, "server", "--port", "0", "--conns", str(clients), "--max-seconds", "60"]
@@ -67,12 +67,19 @@ def run(mode, clients, msgs, persistent, chunk=None):
 def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 1
     msgs = int(sys.argv[2]) if len(sys.argv) > 2 else 3000
-    cases = [("reference", 64, 0, None)] + [("batched", 64, 16, c) for c in (0, 8, 16, 32)] + \
-            [("reference", 8, 0, None), ("batched", 8, 16, 0), ("batched", 8, 16, 4)]
+    which = sys.argv[3] if len(sys.argv) > 3 else "chunk"
+    if which == "prefetch":      # the dispatch's prefetch of the next read (FWS_HOOK_PREFETCH)
+        cases = [("reference", 64, 0, None, None)] + \
+                [("batched", c, 16, 16, {"FWS_HOOK_PREFETCH": p}) for c in (64, 8) for p in ("1", "0")]
+    else:
+        cases = [("reference", 64, 0, None, None)] + [("batched", 64, 16, c, None) for c in (0, 8, 16, 32)] + \
+                [("reference", 8, 0, None, None), ("batched", 8, 16, 0, None), ("batched", 8, 16, 4, None)]
     for rep in range(reps):
-        for mode, clients, pers, chunk in (cases if rep % 2 == 0 else cases[::-1]):
-            rec = run(mode, clients, msgs if clients > 8 else 4 * msgs, pers, chunk)
+        for mode, clients, pers, chunk, env in (cases if rep % 2 == 0 else cases[::-1]):
+            rec = run(mode, clients, msgs if clients > 8 else 4 * msgs, pers, chunk, env)
             rec["rep"] = rep
+            if env:
+                rec["env"] = env
             print(json.dumps(rec), flush=True)
 
 

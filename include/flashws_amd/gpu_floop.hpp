@@ -547,7 +547,7 @@ private:
             return;
         }
         EnsureRegistered(buf);
-        if (it->second.slot != kNoSlot) {            // batched: decoded at the end of the step
+        if (it->second.slot != kNoSlot) {            // batched: decoded with its chunk or at the end of the step
             if (it->second.pending || it->second.inflight) {   // its previous read goes first
                 Flush();
                 it = conns_.find(&u);

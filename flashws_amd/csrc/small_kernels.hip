@@ -52,7 +52,31 @@ __device__ __forceinline__ bool decode_one_frame(uint8_t *__restrict__ wire, uin
     if (rc <= 0) return false;                       // an incomplete header or an error: the general path
     const uint64_t po = (uint64_t)rc, pe = po + h.plen;
     if (pe < N) return false;                        // more headers follow
-    if (threadIdx.x == 0) {
+    // the payload [po, N): full dwords take the key rotated by the payload
+    // phase of a 4-aligned address, (-po) & 3; edge dwords keep their other bytes.
+    // Chunks start at wave 1: wave 0 (the resident decode's poller, its last poll
+    // load still in flight) has none below ~15 KiB, and the frame record and
+    // result are stored by the last thread, idle then too -- a wave's loads and
+    // stores retire in issue order (vmcnt), so a chunk load issued behind those
+    // host-memory stores waited for their PCIe acknowledgements
+    const uint32_t rk = rotr32(h.key, 8u * ((0u - (uint32_t)po) & 3u));
+    const uint32_t nch = (N + 15u) >> 4;
+    uint8_t *const dst = out ? out : wire;
+    for (uint32_t c = (threadIdx.x + kSThreads - kWave) % kSThreads; c < nch; c += kSThreads) {
+        const uint32_t x0 = 16u * c;
+        if (!out && x0 + 16u <= po) continue;        // header bytes only: unchanged in place
+        u32x4 v = gload16(base + x0);
+#pragma unroll
+        for (uint32_t k = 0; k < 4u; ++k) v[k] ^= rk & sel_bytes(x0 + 4u * k, po, N);
+        if (x0 + 16u <= N) {
+            gstore16((uintptr_t)dst + x0, v);
+        } else {                                     // the last chunk: whole dwords, then bytes
+            uint32_t j = 0;
+            for (; x0 + j + 4u <= N; j += 4u) gput(reinterpret_cast<uint32_t *>(dst + x0 + j), v[j >> 2]);
+            for (; x0 + j < N; ++j) gput(dst + x0 + j, (uint8_t)(v[j >> 2] >> (8u * (j & 3u))));
+        }
+    }
+    if (threadIdx.x == kSThreads - 1u) {
         fws_frame_info fi;
         fi.hdr_off = 0; fi.payload_len = h.plen; fi.key = h.key; fi.opcode = (uint8_t)h.opcode;
         fi.fin = (uint8_t)h.fin; fi.hdr_len = (uint8_t)rc;
@@ -65,23 +89,6 @@ __device__ __forceinline__ bool decode_one_frame(uint8_t *__restrict__ wire, uin
         r.n_frames = 1;
         r.n_survivors = 1;
         gput(res, r);
-    }
-    // the payload [po, N): full dwords take the key rotated by the payload
-    // phase of a 4-aligned address, (-po) & 3; edge dwords keep their other bytes
-    const uint32_t rk = rotr32(h.key, 8u * ((0u - (uint32_t)po) & 3u));
-    const uint32_t nch = (N + 15u) >> 4;
-    uint8_t *const dst = out ? out : wire;
-    for (uint32_t c = threadIdx.x; c < nch; c += kSThreads) {
-        const uint32_t x0 = 16u * c;
-        if (!out && x0 + 16u <= po) continue;        // header bytes only: unchanged in place
-        u32x4 v = gload16(base + x0);
-#pragma unroll
-        for (uint32_t k = 0; k < 4u; ++k) v[k] ^= rk & sel_bytes(x0 + 4u * k, po, N);
-        if (x0 + 16u <= N) {
-            gstore16((uintptr_t)dst + x0, v);
-        } else {
-            for (uint32_t j = 0; x0 + j < N; ++j) gput(dst + x0 + j, (uint8_t)(v[j >> 2] >> (8u * (j & 3u))));
-        }
     }
     return true;
 }
@@ -100,7 +107,10 @@ __device__ __forceinline__ void decode_small_wg(uint8_t *__restrict__ wire, uint
     const uint32_t tid = threadIdx.x;
     const uint32_t nch = (N + 15u) >> 4;
     const uintptr_t base = (uintptr_t)wire;
-    if (!tr && decode_one_frame(wire, N, frames, cap, res, out)) return;   // (wave-uniform)
+    if (decode_one_frame(wire, N, frames, cap, res, out)) {               // (wave-uniform)
+        if (tr && tid == 0) tr[0] = tr[1] = wall_clock64();              // (its own chunks done)
+        return;
+    }
 
     // 1. stage: all loads of a thread in flight together (the base is 16-B
     //    aligned, so the last chunk's block never crosses a page)
@@ -325,7 +335,8 @@ __device__ __forceinline__ uint64_t svc_load64(const uint64_t *p) {
 
 // phase clocks of the one-segment requests (fws_internal_rx_service_trace):
 // [0] requests, [1..5] summed ticks from the request's detection to the
-// acquire, the staged read, the header walk, the unmask, the flag store
+// acquire, the staged read, the header walk, the unmask, the flag store;
+// [6] to every wave's stores drained (before the completion's release)
 __device__ unsigned long long g_svc_trace[8];
 
 __global__ __launch_bounds__(kSThreads) void k_rx_service(fws_svc_mail *mail, const fws_svc_mail *poll,
@@ -425,6 +436,11 @@ __global__ __launch_bounds__(kSThreads) void k_rx_service(fws_svc_mail *mail, co
                            reinterpret_cast<fws_decode_result *>(rq.res), trace ? tq : nullptr,
                            rq.kind == 2u ? reinterpret_cast<uint8_t *>(rq.out) : nullptr);
             if (trace && threadIdx.x == 0) tq[2] = wall_clock64();
+            if (trace) {                                                   // host_done's steps, clocked
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();
+                if (threadIdx.x == 0) tq[3] = wall_clock64();              // every wave's stores done
+            }
             host_done(nullptr, 0u, reinterpret_cast<uint32_t *>(rq.flag), rq.flag_seq);
             if (trace && threadIdx.x == 0) {                               // (thread 0 detected it: tl, tf)
                 const uint64_t te = wall_clock64();
@@ -434,6 +450,7 @@ __global__ __launch_bounds__(kSThreads) void k_rx_service(fws_svc_mail *mail, co
                 g_svc_trace[3] += tq[1] - tl;
                 g_svc_trace[4] += tq[2] - tl;
                 g_svc_trace[5] += te - tl;
+                g_svc_trace[6] += tq[3] - tl;
             }
             __syncthreads();                                               // s_req / s_cmd rewritten next round
         }

@@ -96,9 +96,10 @@ int main(int argc, char **argv) {
                     const double hn = tr[9] ? (double)tr[9] : 1.0;
                     printf("{\"trace\": true, \"payload\": %zu, \"buffer\": \"%s\", \"gpu_requests\": %llu, "
                            "\"acquire_us\": %.2f, \"staged_us\": %.2f, \"walked_us\": %.2f, \"unmasked_us\": %.2f, "
-                           "\"flag_stored_us\": %.2f, \"host_publish_us\": %.2f, \"host_wait_us\": %.2f}\n",
+                           "\"stores_drained_us\": %.2f, \"flag_stored_us\": %.2f, \"host_publish_us\": %.2f, "
+                           "\"host_wait_us\": %.2f}\n",
                            pl, registered ? "registered" : "plain", tr[0], tr[1] / n / tpu, tr[2] / n / tpu,
-                           tr[3] / n / tpu, tr[4] / n / tpu, tr[5] / n / tpu, tr[10] / hn / 1000.0,
+                           tr[3] / n / tpu, tr[4] / n / tpu, tr[6] / n / tpu, tr[5] / n / tpu, tr[10] / hn / 1000.0,
                            tr[11] / hn / 1000.0);
                 }
                 fflush(stdout);

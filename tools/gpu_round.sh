@@ -14,6 +14,7 @@
 #   prof_decode  rocprofv3 kernel trace + stats of the C2/C3/dense/C5 stream decodes
 #   prof_extra   rocprofv3 kernel trace + stats of C4 gather, TX encode, C5 descriptor mode
 #   pmc_decode   FETCH_SIZE / WRITE_SIZE passes of the C3 decode (tools/run_decode.py c3)
+#   pmc_extra    FETCH_SIZE / WRITE_SIZE passes of C4 (tools/run_c4.py) and TX (tools/run_tx.py)
 #   sq_decode    SQ counters of the C3 decode kernels
 #   trace        phase clocks of k_scan and per-workgroup timelines of the resolve kernels
 #                (FWS_SCAN_PROF build: make -C flashws_amd/csrc prof, built beforehand)
@@ -66,6 +67,11 @@ for step in "$@"; do
     pmc_decode)
         prof pmc_dec_fetch 120 --pmc FETCH_SIZE -f csv -d "$O/pmc_dec_fetch" -o run -- python3 "$R/tools/run_decode.py" c3
         prof pmc_dec_write 120 --pmc WRITE_SIZE -f csv -d "$O/pmc_dec_write" -o run -- python3 "$R/tools/run_decode.py" c3 ;;
+    pmc_extra)
+        for c in c4 tx; do
+            prof "pmc_${c}_fetch" 150 --pmc FETCH_SIZE -f csv -d "$O/pmc_${c}_fetch" -o run -- python3 "$R/tools/run_$c.py"
+            prof "pmc_${c}_write" 150 --pmc WRITE_SIZE -f csv -d "$O/pmc_${c}_write" -o run -- python3 "$R/tools/run_$c.py"
+        done ;;
     sq_decode)
         prof sq_dec 120 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_VMEM -f csv -d "$O/sq_dec" -o run -- python3 "$R/tools/run_decode.py" c3 ;;
     trace)

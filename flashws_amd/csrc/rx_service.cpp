@@ -25,6 +25,7 @@
 #include <atomic>
 #include <chrono>
 #include <mutex>
+#include <thread>
 
 #include "fws_internal.h"
 
@@ -62,6 +63,14 @@ inline void wc_flush() {
 }
 
 std::atomic<uint64_t> g_linger_us{250};   // idle time before the grid exits (tests shorten it)
+// the service stream's hardware queue: 1 (default) a queue of
+// its own -- a stream with a CU mask (every CU) is never given a pooled queue,
+// so no other stream of the process shares the queue the resident grid sits on
+// (with GPU_MAX_HW_QUEUES = 4, the 5th pooled stream shares one, and a shared
+// queue runs its packets in order: work queued there behind the grid would wait
+// until the grid leaves); 0 a plain non-blocking stream from the pool (r05)
+std::atomic<int> g_svc_queue{1};
+std::mutex g_create_mu;                   // ctx->svc is created once under it
 constexpr uint64_t kLifeUs = 200000;   // and its longest stay: it leaves at the next idle moment
 // phase trace (tools/lat_feed.cpp): the device's phase clocks (grids launched
 // while it is on) and the host's publish / wait times, summed in ns
@@ -82,6 +91,10 @@ extern "C" __attribute__((visibility("default"))) int fws_internal_rx_service_tr
     out12[8] = (unsigned long long)khz / 1000u;
     for (int i = 0; i < 3; ++i) out12[9 + i] = g_host_ns[i].exchange(0);
     return r;
+}
+
+extern "C" __attribute__((visibility("default"))) int fws_internal_set_rx_service_queue(int mode) {
+    return g_svc_queue.exchange(mode ? 1 : 0);
 }
 
 extern "C" __attribute__((visibility("default"))) int fws_internal_set_rx_linger_us(int us) {
@@ -112,8 +125,30 @@ extern "C" __attribute__((visibility("default"))) int fws_internal_set_rx_push(i
     return g_push.exchange(on < 0 ? -1 : (on ? 1 : 0));
 }
 
+namespace {
+// the service stream: with a queue of its own (g_svc_queue 1), else pooled
+bool create_service_stream(fws_rx_service *v) {
+    if (g_svc_queue.load() == 1) {
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, v->device) == hipSuccess && cus > 0) {
+            uint32_t mask[64] = {};
+            const uint32_t words = ((uint32_t)cus + 31u) / 32u;
+            if (words <= 64u) {
+                for (int i = 0; i < cus; ++i) mask[i / 32] |= 1u << (i % 32);
+                if (hipExtStreamCreateWithCUMask(&v->stream, words, mask) == hipSuccess) return true;
+            }
+        }
+    }
+    v->stream = nullptr;
+    return hipStreamCreateWithFlags(&v->stream, hipStreamNonBlocking) == hipSuccess;
+}
+}  // namespace
+
 fws_rx_service *fws_ctx_rx_service(fws_gpu_ctx *ctx) {
     if (!ctx || !ctx->svc_workers) return nullptr;
+    if (fws_rx_service *v = __atomic_load_n(&ctx->svc, __ATOMIC_ACQUIRE)) return v;
+    // first use: created once (two threads feeding one context race here only)
+    std::lock_guard<std::mutex> lk(g_create_mu);
     if (ctx->svc) return ctx->svc;
     fws_rx_service *v = new fws_rx_service();
     v->device = ctx->device;
@@ -121,7 +156,7 @@ fws_rx_service *fws_ctx_rx_service(fws_gpu_ctx *ctx) {
     int khz = 0;
     bool ok = hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, ctx->device) == hipSuccess && khz > 0;
     if (ok) v->ticks_per_us = (uint64_t)khz / 1000u ? (uint64_t)khz / 1000u : 1u;
-    ok = ok && hipStreamCreateWithFlags(&v->stream, hipStreamNonBlocking) == hipSuccess;
+    ok = ok && create_service_stream(v);
     ok = ok && hipHostMalloc((void **)&v->mail, sizeof(fws_svc_mail), hipHostMallocCoherent) == hipSuccess;
     ok = ok && hipMalloc((void **)&v->dv, sizeof(fws_svc_dev)) == hipSuccess;
     if (!ok) {
@@ -139,7 +174,10 @@ fws_rx_service *fws_ctx_rx_service(fws_gpu_ctx *ctx) {
         large_bar) {
         void *p = nullptr;
         if (hipExtMallocWithFlags(&p, sizeof(fws_svc_mail) + kPushCap, hipDeviceMallocFinegrained) == hipSuccess) {
-            if (hipMemset(p, 0, sizeof(fws_svc_mail)) == hipSuccess && hipDeviceSynchronize() == hipSuccess) {
+            // on the service's own stream: a device-wide synchronise would also wait for
+            // every other stream, another context's resident grid included
+            if (hipMemsetAsync(p, 0, sizeof(fws_svc_mail), v->stream) == hipSuccess &&
+                hipStreamSynchronize(v->stream) == hipSuccess) {
                 v->vmail = static_cast<fws_svc_mail *>(p);
                 v->vstage = static_cast<uint8_t *>(p) + sizeof(fws_svc_mail);
                 v->push = true;
@@ -148,7 +186,7 @@ fws_rx_service *fws_ctx_rx_service(fws_gpu_ctx *ctx) {
             }
         }
     }
-    ctx->svc = v;
+    __atomic_store_n(&ctx->svc, v, __ATOMIC_RELEASE);
     return v;
 }
 
@@ -214,19 +252,43 @@ int publish(fws_rx_service *v, bool tr) {
     return 0;
 }
 
+// A request's flag. Not fws_wait_flag: its fallback after 200 us blocks on
+// the stream, and the service stream stays busy while the grid lingers (up
+// to kLifeUs), so a long request would be seen done only when the grid left.
+// Here the spin turns into a polling sleep, and the stream is only queried:
+// idle with the flag unset means the grid died or never ran (an error).
+int wait_flag_svc(fws_rx_service *v, const uint32_t *flag, uint32_t seq) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t i = 0;; ++i) {
+        if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == seq) return 0;
+        if ((i & 255u) == 255u && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(200)) break;
+#if defined(__x86_64__) || defined(__i386__)
+        __builtin_ia32_pause();
+#endif
+    }
+    for (;;) {
+        if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == seq) return 0;
+        const hipError_t q = hipStreamQuery(v->stream);
+        if (q == hipSuccess)                // the grid has left
+            return __atomic_load_n(flag, __ATOMIC_ACQUIRE) == seq ? 0 : FWS_ERR_INTERNAL;
+        if (q != hipErrorNotReady) return fws_hip_status(q);
+        std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+}
+
 // the posted request, if any, done (caller holds v->mu)
 int drain(fws_rx_service *v) {
     if (!v->pend_flag) return 0;
     uint32_t *const f = v->pend_flag;
     v->pend_flag = nullptr;
-    return fws_wait_flag(f, v->pend_seq, v->stream);
+    return wait_flag_svc(v, f, v->pend_seq);
 }
 
 int wait_traced(fws_rx_service *v, uint32_t *flag, uint32_t flag_seq, bool tr,
                 std::chrono::steady_clock::time_point t0) {
-    if (!tr) return fws_wait_flag(flag, flag_seq, v->stream);
+    if (!tr) return wait_flag_svc(v, flag, flag_seq);
     const auto t1 = std::chrono::steady_clock::now();
-    const int r = fws_wait_flag(flag, flag_seq, v->stream);
+    const int r = wait_flag_svc(v, flag, flag_seq);
     const auto t2 = std::chrono::steady_clock::now();
     g_host_ns[0].fetch_add(1, std::memory_order_relaxed);
     g_host_ns[1].fetch_add((uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count(),
@@ -320,7 +382,7 @@ int fws_rx_service_wait(fws_rx_service *v, uint32_t *flag, uint32_t flag_seq) {
     std::lock_guard<std::mutex> lk(v->mu);
     if (v->pend_flag == flag && v->pend_seq == flag_seq) return drain(v);
     // drained by a later request already: its flag is set
-    return __atomic_load_n(flag, __ATOMIC_ACQUIRE) == flag_seq ? 0 : fws_wait_flag(flag, flag_seq, v->stream);
+    return __atomic_load_n(flag, __ATOMIC_ACQUIRE) == flag_seq ? 0 : wait_flag_svc(v, flag, flag_seq);
 }
 
 int fws_rx_service_push(fws_rx_service *v, const uint8_t *src, uint64_t span, uint8_t *out_dev, const fws_seg_desc &d,

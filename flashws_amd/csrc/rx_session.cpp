@@ -603,6 +603,7 @@ struct fws_rx_mux {
     std::vector<Plan> sub_plan;
     uint64_t sub_desc_bytes = 0, sub_res_bytes = 0;
     uint32_t sub_seq = 0;
+    fws_rx_service *sub_svc = nullptr;           // the service a kWaitService chunk was posted to
 
     int ensure(uint64_t bytes, uint64_t meta) {
         hipError_t e;
@@ -671,10 +672,20 @@ int fws_rx_mux_create(fws_gpu_ctx *ctx, uint32_t n_conns, fws_rx_mux **out) {
     return 0;
 }
 
+// A chunk posted to the context's service, done. If that service is gone
+// (fws_gpu_ctx_set_rx_persistent between submit and complete), its teardown
+// drained the grid, which served the request and set the flag: the flag
+// alone tells.
+static int mux_wait_service(fws_rx_mux *m) {
+    fws_rx_service *v = m->ctx->svc;
+    if (v && v == m->sub_svc) return fws_rx_service_wait(v, m->hflag, m->sub_seq);
+    return __atomic_load_n(m->hflag, __ATOMIC_ACQUIRE) == m->sub_seq ? 0 : fws_wait_flag(m->hflag, m->sub_seq, m->stream);
+}
+
 void fws_rx_mux_destroy(fws_rx_mux *m) {
     if (!m) return;
     if (m->inflight && m->wait == fws_rx_mux::kWaitService)   // a posted request: served before the buffers go
-        (void)fws_rx_service_wait(fws_ctx_rx_service(m->ctx), m->hflag, m->sub_seq);
+        (void)mux_wait_service(m);
     if (m->stream) (void)hipStreamSynchronize(m->stream);
     for (fws_rx_session *s : m->conns) fws_rx_session_destroy(s);
     if (m->hbuf) (void)hipHostFree(m->hbuf);
@@ -802,6 +813,7 @@ int fws_rx_mux_submit(fws_rx_mux *m, const fws_rx_read *reads, uint32_t n) {
                                              m->sub_seq)))
                     return r;
                 wait = fws_rx_mux::kWaitService;
+                m->sub_svc = v;
             } else {
                 if ((r = fws_launch_decode_segments(m->hbuf, (const fws_seg_desc *)m->hmeta, nseg, hf, hr, st, m->dctr,
                                                     nseg, m->hflag, m->sub_seq)))
@@ -840,7 +852,7 @@ int fws_rx_mux_complete(fws_rx_mux *m, fws_rx_read_result *results) {
     m->inflight = false;
     int r = 0;
     switch (m->wait) {
-    case fws_rx_mux::kWaitService: r = fws_rx_service_wait(fws_ctx_rx_service(m->ctx), m->hflag, m->sub_seq); break;
+    case fws_rx_mux::kWaitService: r = mux_wait_service(m); break;
     case fws_rx_mux::kWaitFlag: r = fws_wait_flag(m->hflag, m->sub_seq, m->stream); break;
     case fws_rx_mux::kWaitStream: r = fws_hip_status(hipStreamSynchronize(m->stream)); break;
     case fws_rx_mux::kWaitNone: break;

@@ -12,6 +12,7 @@ import time
 
 import numpy as np
 import pytest
+import torch
 
 from flashws_amd import gpu
 from test_gpu_inplace import CASES, _declined_reads, _state
@@ -252,3 +253,99 @@ def test_service_teardown_while_resident(cuda, arena):
         t0 = time.perf_counter()
         c.close()                                            # the grid is still lingering
         assert time.perf_counter() - t0 < 1.0
+
+
+@pytest.mark.parametrize("queue", [1, 0], ids=["own_queue", "pooled"])
+def test_service_grid_beside_other_streams(cuda, arena, queue):
+    """The resident grid's hardware queue. The box runs
+    GPU_MAX_HW_QUEUES=4; torch's stream plus 7 non-blocking HIP streams are
+    more than that, so pooled streams share queues, and a shared queue runs
+    its packets in order. With the grid resident (a 300 ms linger), a small
+    unmask on every one of those streams must finish in far less than the
+    linger, and the grid must still be the one that was launched (no
+    relaunch: nothing forced it out). The default service stream has a queue
+    of its own (a CU-masked stream is never pooled); the r05 pooled stream is
+    measured too: the test records, for each stream, whether its work waited
+    for the grid, and requires that none did only for the default."""
+    from flashws_amd._lib import lib
+    old_q = lib().fws_internal_set_rx_service_queue(queue)
+    old_l = lib().fws_internal_set_rx_linger_us(300000)
+    c = gpu.Ctx(0)
+    streams = [gpu.hip_stream() for _ in range(7)]
+    try:
+        c.set_rx_persistent(8)
+        wire, descs, _ = gpu.config_c2(seed=5, n_frames=256)
+        dev = torch.from_numpy(wire).to(cuda)
+        dd = gpu.descs_to_device(descs, cuda)
+        every = [torch.cuda.current_stream()] + streams
+
+        def one(st):
+            t0 = time.perf_counter()
+            gpu.unmask_sorted(c, dev, dd, len(descs), stream=st)
+            st.synchronize()
+            return time.perf_counter() - t0
+
+        for st in every:                                   # warm, no grid yet
+            one(st)
+        s = gpu.RxSession(c)
+        reads = [bytes.fromhex(r) for r in CASES[sorted(CASES)[0]]["reads"]]
+        got = s.feed(reads[0], arena=arena)
+        launches0, _ = c.rx_service_stats()
+        assert launches0 == 1
+        times = [one(st) for st in every]
+        s2 = gpu.RxSession(c)
+        s2.feed(reads[0], arena=arena)                    # the same grid serves it
+        launches1, _ = c.rx_service_stats()
+        waited = [t > 0.05 for t in times]
+        print(f"queue={queue} per-stream ms {[round(t * 1e3, 2) for t in times]} waited {waited} "
+              f"launches {launches0}->{launches1}")
+        if queue == 1:
+            assert not any(waited), times
+            assert launches1 == launches0
+        assert torch.equal(dev.cpu(), torch.from_numpy(wire))   # 16 unmasks: an even count
+        s.close()
+        s2.close()
+        del got
+    finally:
+        c.close()
+        for st in streams:
+            st.close()
+        lib().fws_internal_set_rx_linger_us(old_l)
+        lib().fws_internal_set_rx_service_queue(old_q)
+
+
+def test_service_mux_complete_after_persistent_off(cuda, arena):
+    """fws_rx_mux_submit posts a chunk to the resident grid; the service is
+    switched off (fws_gpu_ctx_set_rx_persistent(ctx, 0), whose teardown drains
+    the grid) before fws_rx_mux_complete. The chunk's results still come back,
+    equal to a context without the service, and later chunks use launches."""
+    rng = np.random.default_rng(808)
+    n = 6
+    streams = [_random_stream(rng, 12) for _ in range(n)]
+    c, plain = gpu.Ctx(0), gpu.Ctx(0)
+    try:
+        c.set_rx_persistent(16)
+        mux = gpu.RxMux(c, n)
+        ref = [gpu.RxSession(plain) for _ in range(n)]
+        cuts = [[st[i:i + 700] for i in range(0, len(st), 700)] for st in streams]
+        toggled = [False]
+
+        def between():
+            if not toggled[0]:
+                c.set_rx_persistent(0)
+                toggled[0] = True
+
+        for r in range(max(len(x) for x in cuts)):
+            part = [i for i in range(n) if r < len(cuts[i])]
+            got = mux.feed([(i, cuts[i][r]) for i in part], arena=arena, between=between)
+            for i, (ret, buf, ev, ctl) in zip(part, got):
+                eret, ebuf, eev, ectl = ref[i].feed(cuts[i][r])
+                assert (ret, bytes(buf)) == (eret, bytes(ebuf)), (i, r)
+                assert session_view(ev, ctl) == session_view(eev, ectl), (i, r)
+        assert toggled[0]
+        mux.close()
+        for s in ref:
+            s.close()
+    finally:
+        c.close()
+        plain.close()

@@ -40,6 +40,17 @@ def batch_path(request):
     L.fws_internal_set_unmask_any(old)
 
 
+@pytest.fixture(params=[0, 2], ids=["lookup_first", "loads_first"])
+def sorted_kernel(request):
+    """fws_gpu_unmask_sorted's two one-launch forms: k_unmask_sorted (owner
+    lookup, then the unit's loads) and k_unmask_sorted_ld (loads first, slow
+    units deferred past the unit loop, the first parked in LDS)."""
+    L = _lib.lib()
+    old = L.fws_internal_set_sorted_early(request.param)
+    yield request.param
+    L.fws_internal_set_sorted_early(old)
+
+
 @pytest.fixture
 def planned():
     """The planned form only (the tests that read the plan's mode)."""
@@ -277,7 +288,7 @@ def run_sorted(ctx, host, descs, cuda, base_shift=0):
 
 
 @pytest.mark.parametrize("n_frames", [1, 2, 7, 4096, 65536])
-def test_sorted_c2_shape(ctx, cuda, n_frames):
+def test_sorted_c2_shape(ctx, cuda, sorted_kernel, n_frames):
     """BASELINE C2 layout (65 536 at full size): interpolation guesses hit."""
     wire, descs, _ = gpu.config_c2(seed=17, n_frames=n_frames)
     got = run_sorted(ctx, wire, descs, cuda)
@@ -288,7 +299,7 @@ def test_sorted_c2_shape(ctx, cuda, n_frames):
 
 
 @pytest.mark.parametrize("shift", [1, 3, 8, 15])
-def test_sorted_unaligned_base(ctx, cuda, shift):
+def test_sorted_unaligned_base(ctx, cuda, sorted_kernel, shift):
     wire, descs, _ = gpu.config_c2(seed=19, n_frames=300)
     got = run_sorted(ctx, wire, descs, cuda, base_shift=shift)
     exp = wire.copy()
@@ -296,7 +307,7 @@ def test_sorted_unaligned_base(ctx, cuda, shift):
     assert np.array_equal(got, exp)
 
 
-def test_sorted_mixed_c3(ctx, cuda):
+def test_sorted_mixed_c3(ctx, cuda, sorted_kernel):
     """C3-shaped 64 B-64 KiB frames: guesses miss, binary search finds owners."""
     wire, descs, _ = gpu.config_c3(seed=23, target=16 << 20)
     got = run_sorted(ctx, wire, descs, cuda)
@@ -306,7 +317,7 @@ def test_sorted_mixed_c3(ctx, cuda):
     assert np.array_equal(got, exp)
 
 
-def test_sorted_alignment_sweep(ctx, cuda):
+def test_sorted_alignment_sweep(ctx, cuda, sorted_kernel):
     rng = np.random.default_rng(29)
     regions, pos = [], 0
     for ln in range(0, 601):
@@ -322,7 +333,7 @@ def test_sorted_alignment_sweep(ctx, cuda):
 
 @pytest.mark.parametrize("n,max_len,max_gap", [(1, 5, 0), (3, 20, 3), (1025, 64, 2), (70000, 30, 3),
                                                 (300000, 12, 1), (5000, 0, 2)])
-def test_sorted_tiny_frames(ctx, cuda, n, max_len, max_gap):
+def test_sorted_tiny_frames(ctx, cuda, sorted_kernel, n, max_len, max_gap):
     """Many frames per 4 KiB unit (slow-kind units), zero-length frames."""
     rng = np.random.default_rng(n + 7)
     regions, pos = _rand_regions(rng, n, max_len, max_gap)
@@ -332,7 +343,7 @@ def test_sorted_tiny_frames(ctx, cuda, n, max_len, max_gap):
     assert np.array_equal(run_sorted(ctx, host, descs, cuda), oracle_unmask_regions(host, descs))
 
 
-def test_sorted_large_and_sparse(ctx, cuda):
+def test_sorted_large_and_sparse(ctx, cuda, sorted_kernel):
     """A 16 MiB frame among tiny ones (guesses miss), then a sparse batch
     (64 B every 1 MiB: gap units skipped)."""
     rng = np.random.default_rng(37)
@@ -352,7 +363,7 @@ def test_sorted_large_and_sparse(ctx, cuda):
     assert np.array_equal(run_sorted(ctx, host, descs, cuda), oracle_unmask_regions(host, descs))
 
 
-def test_sorted_matches_batch_and_involution(ctx, cuda, batch_path):
+def test_sorted_matches_batch_and_involution(ctx, cuda, sorted_kernel, batch_path):
     """Full C2 size: _sorted and _batch agree, and two _sorted passes restore the input."""
     wire, descs, _ = gpu.config_c2(seed=43)
     dev = torch.from_numpy(wire).to(cuda)
@@ -401,6 +412,29 @@ def test_sorted_early_variant(ctx, cuda):
         assert np.array_equal(run_sorted(ctx, host, descs, cuda), oracle_unmask_regions(host, descs))
     finally:
         lib().fws_internal_set_sorted_early(old)
+
+
+@pytest.mark.parametrize("cap", [1, 3, 64])
+def test_sorted_ld_grid_stride(ctx, cuda, cap):
+    """k_unmask_sorted_ld on grids far smaller than the unit count: each wave
+    walks many units, so its deferred slow units take every route (the first
+    parked in LDS, the next 64 strides by bit, the rest by the far rescan)."""
+    L = _lib.lib()
+    old_v, old_cap = L.fws_internal_set_sorted_early(2), L.fws_internal_set_grid_cap(cap)
+    try:
+        rng = np.random.default_rng(67 + cap)
+        regions, pos = _rand_regions(rng, 30000, 40, 3)
+        host = aligned_host(pos + 32)
+        host[:] = rng.integers(0, 256, len(host), dtype=np.uint8)
+        descs = np.array(regions, dtype=gpu.FRAME_DESC)
+        assert np.array_equal(run_sorted(ctx, host, descs, cuda), oracle_unmask_regions(host, descs))
+        wire, descs, _ = gpu.config_c3(seed=71 + cap, target=2 << 20)
+        exp = wire.copy()
+        orc.orc_decode_stream(exp)
+        assert np.array_equal(run_sorted(ctx, wire, descs, cuda), exp)
+    finally:
+        L.fws_internal_set_grid_cap(old_cap)
+        L.fws_internal_set_sorted_early(old_v)
 
 
 def test_check_sorted_contract(ctx, cuda):

@@ -63,12 +63,16 @@ inline void wc_flush() {
 }
 
 std::atomic<uint64_t> g_linger_us{250};   // idle time before the grid exits (tests shorten it)
-// the service stream's hardware queue: 1 (default) a queue of
-// its own -- a stream with a CU mask (every CU) is never given a pooled queue,
-// so no other stream of the process shares the queue the resident grid sits on
-// (with GPU_MAX_HW_QUEUES = 4, the 5th pooled stream shares one, and a shared
-// queue runs its packets in order: work queued there behind the grid would wait
-// until the grid leaves); 0 a plain non-blocking stream from the pool (r05)
+// the service stream's hardware queue. ROCclr keeps a pool of
+// hardware queues per stream priority (GPU_MAX_HW_QUEUES each, 4 on the box)
+// and maps streams onto them round robin; a queue shared by two streams runs
+// its packets in order, so work queued there behind the resident grid would
+// wait until the grid leaves (up to kLifeUs). 1 (default): a non-blocking
+// stream of the highest priority -- a pool of its own, which the process's
+// normal-priority streams (torch's, the pipes', the engine's) never share;
+// 0: a plain non-blocking stream from the normal pool (r05); 2: a CU-masked
+// stream (every CU: never pooled, but created blocking, so the legacy null
+// stream waits for the lingering grid -- measured, not used).
 std::atomic<int> g_svc_queue{1};
 std::mutex g_create_mu;                   // ctx->svc is created once under it
 constexpr uint64_t kLifeUs = 200000;   // and its longest stay: it leaves at the next idle moment
@@ -94,7 +98,7 @@ extern "C" __attribute__((visibility("default"))) int fws_internal_rx_service_tr
 }
 
 extern "C" __attribute__((visibility("default"))) int fws_internal_set_rx_service_queue(int mode) {
-    return g_svc_queue.exchange(mode ? 1 : 0);
+    return g_svc_queue.exchange(mode >= 0 && mode <= 2 ? mode : 1);
 }
 
 extern "C" __attribute__((visibility("default"))) int fws_internal_set_rx_linger_us(int us) {
@@ -126,9 +130,15 @@ extern "C" __attribute__((visibility("default"))) int fws_internal_set_rx_push(i
 }
 
 namespace {
-// the service stream: with a queue of its own (g_svc_queue 1), else pooled
+// the service stream (g_svc_queue: 1 highest priority, 2 CU-masked, 0 pooled)
 bool create_service_stream(fws_rx_service *v) {
-    if (g_svc_queue.load() == 1) {
+    const int mode = g_svc_queue.load();
+    if (mode == 1) {
+        int least = 0, greatest = 0;
+        if (hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess &&
+            hipStreamCreateWithPriority(&v->stream, hipStreamNonBlocking, greatest) == hipSuccess)
+            return true;
+    } else if (mode == 2) {
         int cus = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, v->device) == hipSuccess && cus > 0) {
             uint32_t mask[64] = {};

@@ -255,7 +255,7 @@ def test_service_teardown_while_resident(cuda, arena):
         assert time.perf_counter() - t0 < 1.0
 
 
-@pytest.mark.parametrize("queue", [1, 0], ids=["own_queue", "pooled"])
+@pytest.mark.parametrize("queue", [1, 0, 2], ids=["high_priority", "pooled", "cu_masked"])
 def test_service_grid_beside_other_streams(cuda, arena, queue):
     """The resident grid's hardware queue. The box runs
     GPU_MAX_HW_QUEUES=4; torch's stream plus 7 non-blocking HIP streams are
@@ -263,10 +263,12 @@ def test_service_grid_beside_other_streams(cuda, arena, queue):
     its packets in order. With the grid resident (a 300 ms linger), a small
     unmask on every one of those streams must finish in far less than the
     linger, and the grid must still be the one that was launched (no
-    relaunch: nothing forced it out). The default service stream has a queue
-    of its own (a CU-masked stream is never pooled); the r05 pooled stream is
-    measured too: the test records, for each stream, whether its work waited
-    for the grid, and requires that none did only for the default."""
+    relaunch: nothing forced it out). The default service stream is a
+    non-blocking stream of the highest priority, whose queue pool no
+    normal-priority stream shares; the r05 pooled stream and a CU-masked one
+    (never pooled, but blocking: the legacy null stream waits for it) are
+    measured too. The test prints, per stream, whether its work waited for
+    the grid, and requires that none did for the default."""
     from flashws_amd._lib import lib
     old_q = lib().fws_internal_set_rx_service_queue(queue)
     old_l = lib().fws_internal_set_rx_linger_us(300000)

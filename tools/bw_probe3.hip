@@ -1,0 +1,91 @@
+// tools/bw_probe3.hip -- r06 HBM ceiling probe (not part of the library): the
+// in-place 16-B XOR of bw_probe2 (C2's 269 MB wire, 4 rotating buffers,
+// nontemporal loads and stores) at 1, 2 and 4 units of 4 KiB per wave (all
+// loads of a wave issued before its first store), and the 1-unit form with
+// a dependent scalar load ahead of the data loads (the latency a descriptor
+// lookup puts in front of a unit).
+//   hipcc --offload-arch=gfx950 -O3 -o tools/bin/bw_probe3 tools/bw_probe3.hip && tools/bin/bw_probe3
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdint.h>
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) u32x4 g_u32x4;
+
+#define CK(x) do { if ((x) != hipSuccess) { printf("HIP error %s line %d\n", #x, __LINE__); return 1; } } while (0)
+
+// U units of 4 KiB per wave; DEP: 0 none, 1 one scalar load (a per-unit word) before the data loads
+template <int U, int DEP>
+__global__ __launch_bounds__(256) void k_xor(u32x4 *__restrict__ buf, uint64_t n16, uint32_t key,
+                                             const uint32_t *__restrict__ words) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t wave = (uint64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t base = wave * 256 * U;
+    uint32_t k = key;
+    if (DEP) k ^= words[wave & 1023];
+    g_u32x4 *p = (g_u32x4 *)buf;
+    u32x4 v[4 * U];
+#pragma unroll
+    for (int j = 0; j < 4 * U; ++j) {
+        const uint64_t i = base + j * 64 + lane;
+        v[j] = __builtin_nontemporal_load(p + (i < n16 ? i : 0));
+    }
+#pragma unroll
+    for (int j = 0; j < 4 * U; ++j) {
+        const uint64_t i = base + j * 64 + lane;
+        if (i < n16) __builtin_nontemporal_store(v[j] ^ k, p + i);
+    }
+}
+
+static hipEvent_t e0, e1;
+
+template <typename F>
+static void timeit(const char *name, F launch, double bytes) {
+    for (int i = 0; i < 8; ++i) launch(i & 3);
+    hipError_t err = hipDeviceSynchronize();
+    if (err == hipSuccess) err = hipGetLastError();
+    if (err != hipSuccess) {
+        printf("%-36s error %s\n", name, hipGetErrorString(err));
+        return;
+    }
+    const int steps = 100;
+    float t[5] = {};
+    for (int r = 0; r < 5; ++r) {
+        if (hipEventRecord(e0, 0) != hipSuccess) printf("record e0 failed\n");
+        for (int i = 0; i < steps; ++i) launch(i & 3);
+        if (hipEventRecord(e1, 0) != hipSuccess) printf("record e1 failed\n");
+        if (hipEventSynchronize(e1) != hipSuccess) printf("sync failed\n");
+        const hipError_t q = hipEventElapsedTime(&t[r], e0, e1);
+        if (q != hipSuccess) printf("elapsed failed: %s\n", hipGetErrorString(q));
+    }
+    float best = t[0], sum = 0;
+    for (int r = 0; r < 5; ++r) { best = t[r] < best ? t[r] : best; sum += t[r]; }
+    printf("%-36s best %7.2f us  mean %7.2f us  %7.1f GB/s (best)\n", name, best * 1e3 / steps, sum / 5 * 1e3 / steps,
+           bytes / (best * 1e3 / steps) / 1e3);
+    fflush(stdout);
+}
+
+int main() {
+    const uint64_t bytes = 268959744ull;
+    const uint64_t n16 = bytes / 16;
+    u32x4 *bufs[4];
+    uint32_t *words;
+    for (int i = 0; i < 4; ++i) { CK(hipMalloc(&bufs[i], bytes)); CK(hipMemset(bufs[i], i, bytes)); }
+    CK(hipMalloc(&words, 4096));
+    CK(hipMemset(words, 0, 4096));
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    const double rw = 2.0 * bytes;
+    for (int rep = 0; rep < 2; ++rep) {
+#define X(U, DEP, NAME)                                                                                        \
+        timeit(NAME, [&](int i) {                                                                              \
+            const uint64_t waves = (n16 + 256 * U - 1) / (256 * U);                                            \
+            k_xor<U, DEP><<<(unsigned)((waves + 3) / 4), 256>>>(bufs[i], n16, 0x12345678u, words);            \
+        }, rw)
+        X(1, 0, "xor 1 unit/wave");
+        X(2, 0, "xor 2 units/wave");
+        X(4, 0, "xor 4 units/wave");
+        X(1, 1, "xor 1 unit/wave, scalar dep first");
+    }
+    return 0;
+}

@@ -9,5 +9,7 @@ timeout -k 10 300 python -u tools/ab_sorted.py 9 200 0,2 > $O/ab_sorted.jsonl 2>
 tail -2 $O/ab_sorted.jsonl
 timeout -k 10 120 tools/bin/bw_probe2 > $O/bw_probe2.txt 2>&1 || exit 1
 head -3 $O/bw_probe2.txt
+timeout -k 10 120 tools/bin/bw_probe3 > $O/bw_probe3.txt 2>&1 || exit 1
+cat $O/bw_probe3.txt
 timeout -k 10 400 python -u -m pytest tests/test_gpu_service.py -x -v -s --timeout 120 --timeout-method thread > $O/t_service.log 2>&1 || { tail -30 $O/t_service.log; exit 1; }
 grep "queue=" $O/t_service.log; tail -2 $O/t_service.log

@@ -350,10 +350,10 @@ void fws_tx_next(uint32_t frame_type, int last_frame_if_possible, uint8_t *last_
 
 /* dev_out (16-B aligned) = the frames of dev_descs[0..n) back to back;
  * *dev_out_len (device u64) = their total size, or ~0 if it exceeds out_cap.
- * No byte at or past out_cap is ever written; when the total exceeds out_cap
- * the bytes below it are unspecified (the one-launch form writes the frames
- * that fit). One launch (k_tx_one) when the frames average <= 16 KiB of
- * out_cap, else plan + encode. */
+ * The default form (plan + encode: k_out_plan, k_tx_encode_w5) writes nothing
+ * when the total exceeds out_cap. The opt-in one-launch tuning form (k_tx_one,
+ * fws_internal_set_tx_one; measured slower) never writes a
+ * byte at or past out_cap, but writes the frames that fit below it. */
 int fws_gpu_encode_frames(fws_gpu_ctx *ctx, void *dev_out, uint64_t out_cap, const void *dev_src,
                           const fws_tx_desc *dev_descs, uint32_t n, uint64_t *dev_out_len, void *stream);
 

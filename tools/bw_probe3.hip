@@ -14,8 +14,18 @@ typedef __attribute__((address_space(1))) u32x4 g_u32x4;
 
 #define CK(x) do { if ((x) != hipSuccess) { printf("HIP error %s line %d\n", #x, __LINE__); return 1; } } while (0)
 
-// U units of 4 KiB per wave; DEP: 0 none, 1 one scalar load (a per-unit word) before the data loads
-template <int U, int DEP>
+// a 16-B store with an explicit cache policy (ST: 1 sc1, 2 sc0 sc1, 3 sc1 nt); the
+// trailing s_nop covers the store-data hazard (the compiler pads nothing in asm)
+template <int ST>
+__device__ __forceinline__ void store_pol(g_u32x4 *p, u32x4 v) {
+    if constexpr (ST == 1) asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" :: "v"(p), "v"(v) : "memory");
+    else if constexpr (ST == 2) asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1" :: "v"(p), "v"(v) : "memory");
+    else asm volatile("global_store_dwordx4 %0, %1, off sc1 nt\n\ts_nop 1" :: "v"(p), "v"(v) : "memory");
+}
+
+// U units of 4 KiB per wave; DEP: 0 none, 1 one scalar load (a per-unit word) before
+// the data loads; ST: 0 nontemporal stores, else store_pol<ST>
+template <int U, int DEP, int ST = 0>
 __global__ __launch_bounds__(256) void k_xor(u32x4 *__restrict__ buf, uint64_t n16, uint32_t key,
                                              const uint32_t *__restrict__ words) {
     const uint32_t lane = threadIdx.x & 63;
@@ -33,7 +43,10 @@ __global__ __launch_bounds__(256) void k_xor(u32x4 *__restrict__ buf, uint64_t n
 #pragma unroll
     for (int j = 0; j < 4 * U; ++j) {
         const uint64_t i = base + j * 64 + lane;
-        if (i < n16) __builtin_nontemporal_store(v[j] ^ k, p + i);
+        if (i < n16) {
+            if constexpr (ST == 0) __builtin_nontemporal_store(v[j] ^ k, p + i);
+            else store_pol<ST>(p + i, v[j] ^ k);
+        }
     }
 }
 
@@ -65,7 +78,8 @@ static void timeit(const char *name, F launch, double bytes) {
     fflush(stdout);
 }
 
-int main() {
+int main(int argc, char **argv) {
+    const bool quick = argc > 1;   // one variant, one repetition (counter passes)
     const uint64_t bytes = 268959744ull;
     const uint64_t n16 = bytes / 16;
     u32x4 *bufs[4];
@@ -76,16 +90,20 @@ int main() {
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     const double rw = 2.0 * bytes;
-    for (int rep = 0; rep < 2; ++rep) {
-#define X(U, DEP, NAME)                                                                                        \
+    for (int rep = 0; rep < (quick ? 1 : 2); ++rep) {
+#define X(U, DEP, ST, NAME)                                                                                    \
         timeit(NAME, [&](int i) {                                                                              \
             const uint64_t waves = (n16 + 256 * U - 1) / (256 * U);                                            \
-            k_xor<U, DEP><<<(unsigned)((waves + 3) / 4), 256>>>(bufs[i], n16, 0x12345678u, words);            \
+            k_xor<U, DEP, ST><<<(unsigned)((waves + 3) / 4), 256>>>(bufs[i & 3], n16, 0x12345678u, words);    \
         }, rw)
-        X(1, 0, "xor 1 unit/wave");
-        X(2, 0, "xor 2 units/wave");
-        X(4, 0, "xor 4 units/wave");
-        X(1, 1, "xor 1 unit/wave, scalar dep first");
+        X(1, 0, 0, "xor 1 unit/wave");
+        if (quick) break;
+        X(2, 0, 0, "xor 2 units/wave");
+        X(4, 0, 0, "xor 4 units/wave");
+        X(1, 1, 0, "xor 1 unit/wave, scalar dep first");
+        X(1, 0, 1, "xor 1 unit/wave, sc1 stores");
+        X(1, 0, 2, "xor 1 unit/wave, sc0 sc1 stores");
+        X(1, 0, 3, "xor 1 unit/wave, sc1 nt stores");
     }
     return 0;
 }

@@ -35,6 +35,22 @@ __device__ __forceinline__ void gstore16(uintptr_t a, u32x4 v) {
     else *p = v;
 }
 
+// A 16-B store with cache policy `sc1 nt`: write-through, the line not kept in
+// the XCD's L2. On the in-place XOR stream it beats the plain nontemporal
+// store (tools/bw_probe3.hip, profiles/r06/bw_probe3.txt: 82.35 against
+// 83.0-83.1 us per 269 MB; `sc1` alone or `sc0 sc1`: 84.2), and the C2 headline
+// went 85.1 -> 83.0-83.4 us with it; on the out-of-place kernels (C4 gather,
+// TX encode) it measured slower, so they keep gstore16<true>
+// (profiles/r06/ab_wt_stores.jsonl). hipcc has no builtin for the policy: one
+// asm store, whose trailing s_nop covers the store-data hazard (the compiler
+// pads nothing inside asm). Its completion is outside the compiler's vmcnt
+// bookkeeping; that stays correct because vector memory operations complete
+// in issue order (a later compiler wait can only wait longer).
+__device__ __forceinline__ void gstore16_wt(uintptr_t a, u32x4 v) {
+    g_u32x4 *p = (g_u32x4 *)a;
+    asm volatile("global_store_dwordx4 %0, %1, off sc1 nt\n\ts_nop 1" : : "v"(p), "v"(v) : "memory");
+}
+
 // A store through a global-address-space pointer: global_store (vmcnt only),
 // where a generic pointer gives flat_store, which also counts in lgkmcnt --
 // so the next workgroup barrier's lgkmcnt(0) would wait for the store's

@@ -16,6 +16,22 @@
 
 namespace fwsk {
 
+// The unmask kernels' streaming stores: write-through nontemporal (`sc1 nt`,
+// fws_device.h gstore16_wt) unless kWT is false or the build sets
+// FWS_UNMASK_WT=0 (the r05 nontemporal stores, A/B). Measured in one process
+// per build, alternating (profiles/r06/ab_wt_stores.jsonl): C2 84.6-84.7 ->
+// 83.25-83.4 us, C3 decode 0.181 -> 0.1805 ms, C5 stream 2.659 -> 2.636 ms;
+// the sorted UTF-8 kernel (C5 descriptor) 1.430 -> 1.532 ms, so it keeps the
+// nontemporal stores (kWT false).
+#ifndef FWS_UNMASK_WT
+#define FWS_UNMASK_WT 1
+#endif
+template <bool kNT, bool kWT = true>
+__device__ __forceinline__ void ustore16(uintptr_t a, u32x4 v) {
+    if constexpr (kNT && kWT && FWS_UNMASK_WT != 0) gstore16_wt(a, v);
+    else gstore16<kNT>(a, v);
+}
+
 // ---------------------------------------------------------------- plan
 constexpr int kPlanItems = 1;                        // frames per thread (k_plan)
 constexpr int kPlanTile = kBlock * kPlanItems;       // frames per block
@@ -493,7 +509,7 @@ __global__ __launch_bounds__(kBlock) void k_unmask_stream(uint8_t *base, uint64_
 #pragma unroll
             for (int j = 0; j < kUnmaskU; ++j) {
                 const uint64_t c = c0 + uint64_t(j) * 1024u;
-                if (c < N && (m[j].x | m[j].y | m[j].z | m[j].w)) gstore16<kNT>(b0 + c, v[j] ^ m[j]);
+                if (c < N && (m[j].x | m[j].y | m[j].z | m[j].w)) ustore16<kNT>(b0 + c, v[j] ^ m[j]);
             }
             continue;
         }
@@ -517,7 +533,7 @@ __global__ __launch_bounds__(kBlock) void k_unmask_stream(uint8_t *base, uint64_
                 u32x4 v{0u, 0u, 0u, 0u};
                 const bool touched = c < N && (m.x | m.y | m.z | m.w);
                 if (kUtf8 ? c < N : touched) v = gload16<kNT>(b0 + c);
-                if (touched) gstore16<kNT>(b0 + c, v ^ m);
+                if (touched) ustore16<kNT>(b0 + c, v ^ m);
                 if constexpr (kUtf8) {
                     const u32x4 x = v ^ m;
                     uint32_t prev = __shfl_up(x.w, 1, 64);
@@ -552,7 +568,7 @@ __global__ __launch_bounds__(kBlock) void k_unmask_stream(uint8_t *base, uint64_
 #pragma unroll
                 for (int j = 0; j < kUnmaskU; ++j) {
                     x[j] = pre[j] ^ u32x4{rk, rk, rk, rk};
-                    gstore16<kNT>(b0 + c0 + uint64_t(j) * 1024u, x[j]);
+                    ustore16<kNT>(b0 + c0 + uint64_t(j) * 1024u, x[j]);
                 }
                 if (lane == 0) seam[2u * u] = x[0].x;
                 if (lane == 63) seam[2u * u + 1u] = x[kUnmaskU - 1].w;
@@ -596,7 +612,7 @@ __global__ __launch_bounds__(kBlock) void k_unmask_stream(uint8_t *base, uint64_
         }
 #pragma unroll
         for (int j = 0; j < kUnmaskU; ++j)
-            if (live[j]) gstore16<kNT>(ca[j], v[j] ^ mk[j]);
+            if (live[j]) ustore16<kNT>(ca[j], v[j] ^ mk[j]);
         if constexpr (kUtf8) {
             if (A.text || (two && B.text)) {
                 bool badA = false, badB = false;
@@ -748,7 +764,7 @@ __device__ __forceinline__ void slow_unit_masks(const fws_frame_desc *__restrict
 
 // XOR and store of a slow-kind unit's chunks (loaded from c0 + 1024 j, clamped
 // into the span): chunks reaching outside [E0, E1) are stored byte-exact.
-template <bool kNT>
+template <bool kNT, bool kWT = true>
 __device__ __forceinline__ void slow_unit_store(uint64_t c0, uint64_t E0, uint64_t E1, const u32x4 (&v)[kUnmaskU],
                                                 const u32x4 (&m)[kUnmaskU]) {
 #pragma unroll
@@ -756,7 +772,7 @@ __device__ __forceinline__ void slow_unit_store(uint64_t c0, uint64_t E0, uint64
         const uint64_t c = c0 + uint64_t(j) * 1024u;
         if (c >= E1 || !(m[j].x | m[j].y | m[j].z | m[j].w)) continue;
         const u32x4 x = v[j] ^ m[j];
-        if (c >= E0 && c + 16u <= E1) gstore16<kNT>(c, x);
+        if (c >= E0 && c + 16u <= E1) ustore16<kNT, kWT>(c, x);
         else store_bytes(c, x, E0, E1);
     }
 }
@@ -820,7 +836,7 @@ __device__ __forceinline__ void byte_space_unit(uint8_t *base, const fws_frame_d
     for (int j = 0; j < kUnmaskU; ++j) v[j] = gload16<kNT>(c0 + uint64_t(j) * 1024u);
 #pragma unroll
     for (int j = 0; j < kUnmaskU; ++j)
-        if (mk[j].x | mk[j].y | mk[j].z | mk[j].w) gstore16<kNT>(c0 + uint64_t(j) * 1024u, v[j] ^ mk[j]);
+        if (mk[j].x | mk[j].y | mk[j].z | mk[j].w) ustore16<kNT>(c0 + uint64_t(j) * 1024u, v[j] ^ mk[j]);
 }
 
 
@@ -868,7 +884,7 @@ __device__ __forceinline__ void chunk_space_unit(uint8_t *base, const fws_frame_
         if (!live[j]) continue;
         const uintptr_t lo = s1[j] ? a1 : a0, hi = s1[j] ? a1 + d1.payload_len : a0 + d0.payload_len;
         const uint32_t rk = s1[j] ? R1 : R0;
-        if (ca[j] >= lo && ca[j] + 16u <= hi) gstore16<kNT>(ca[j], v[j] ^ rk);
+        if (ca[j] >= lo && ca[j] + 16u <= hi) ustore16<kNT>(ca[j], v[j] ^ rk);
         else store_partial(ca[j], v[j], rk, lo, hi);
     }
 }
@@ -1029,7 +1045,7 @@ __device__ __forceinline__ void unmask_sorted_body(uint8_t *base, const fws_fram
 #pragma unroll
                 for (int j = 0; j < kUnmaskU; ++j) {
                     x[j] = x[j] ^ u32x4{rk, rk, rk, rk};
-                    gstore16<kNT>(c0 + uint64_t(j) * 1024u, x[j]);
+                    ustore16<kNT, !kUtf8>(c0 + uint64_t(j) * 1024u, x[j]);
                 }
                 // the unit's first and last unmasked dwords for k_utf8_seam_sorted
 #if (FWS_ABL_U8 & 2) == 0          // (ablation builds only: make exp EXP_DEFS=-DFWS_ABL_U8=1|2|3)
@@ -1075,7 +1091,7 @@ __device__ __forceinline__ void unmask_sorted_body(uint8_t *base, const fws_fram
                 v[j] = v[j] ^ m[j];
                 const uint64_t c = c0 + uint64_t(j) * 1024u;
                 if (!t || (slow && c >= E1)) continue;
-                if (!slow || (c >= E0 && c + 16u <= E1)) gstore16<kNT>(c, v[j]);
+                if (!slow || (c >= E0 && c + 16u <= E1)) ustore16<kNT, !kUtf8>(c, v[j]);
                 else store_bytes(c, v[j], E0, E1);
             }
         } else if (slow) {
@@ -1083,7 +1099,7 @@ __device__ __forceinline__ void unmask_sorted_body(uint8_t *base, const fws_fram
         } else {
 #pragma unroll
             for (int j = 0; j < kUnmaskU; ++j)      // fast kind: every chunk lies inside [E0, E1)
-                if (m[j].x | m[j].y | m[j].z | m[j].w) gstore16<kNT>(c0 + uint64_t(j) * 1024u, v[j] ^ m[j]);
+                if (m[j].x | m[j].y | m[j].z | m[j].w) ustore16<kNT, !kUtf8>(c0 + uint64_t(j) * 1024u, v[j] ^ m[j]);
         }
         if constexpr (kUtf8) {
             // the unmasked chunks, still in registers; a chunk's left context is the previous
@@ -1301,7 +1317,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) voi
                            (rec.x & byte_sel32(o + 8u, a0, a1)) | (rec.y & byte_sel32(o + 8u, e0, e1)),
                            (rec.x & byte_sel32(o + 12u, a0, a1)) | (rec.y & byte_sel32(o + 12u, e0, e1))};
             }
-            if (mk.x | mk.y | mk.z | mk.w) gstore16<kNT>(c0 + uint64_t(j) * 1024u, v[j] ^ mk);
+            if (mk.x | mk.y | mk.z | mk.w) ustore16<kNT>(c0 + uint64_t(j) * 1024u, v[j] ^ mk);
         }
     }
     if (parked != ~uint64_t(0)) {                     // lane-private LDS cells: no barrier needed
@@ -1409,18 +1425,18 @@ __device__ __forceinline__ void unmask_sorted_utf8_pipe(uint8_t *base, const fws
 #pragma unroll
             for (int j = 0; j < kUnmaskU; ++j) {
                 x[j] = v[j] ^ u32x4{rk, rk, rk, rk};
-                gstore16<kNT>(c0 + uint64_t(j) * 1024u, x[j]);
+                ustore16<kNT, false>(c0 + uint64_t(j) * 1024u, x[j]);
             }
         } else if (!cur.gap) {
             u32x4 m[kUnmaskU];
             if (cur.slow) slow_unit_masks(d, n, cur.A, b0, cur.U0, lane, m);
             else fast_unit_masks(cur.rec, lane, m);
             if (cur.slow) {
-                slow_unit_store<kNT>(c0, E0, E1, v, m);
+                slow_unit_store<kNT, false>(c0, E0, E1, v, m);
             } else {
 #pragma unroll
                 for (int j = 0; j < kUnmaskU; ++j)
-                    if (m[j].x | m[j].y | m[j].z | m[j].w) gstore16<kNT>(c0 + uint64_t(j) * 1024u, v[j] ^ m[j]);
+                    if (m[j].x | m[j].y | m[j].z | m[j].w) ustore16<kNT, false>(c0 + uint64_t(j) * 1024u, v[j] ^ m[j]);
             }
 #pragma unroll
             for (int j = 0; j < kUnmaskU; ++j) x[j] = v[j] ^ m[j];
@@ -1532,7 +1548,7 @@ __device__ __forceinline__ void unmask_range(uintptr_t po, uint32_t key, uint32_
             const uintptr_t c = cs + (uintptr_t)j * 1024u + (uintptr_t)lane * 16u;
             const uint32_t rk = rotr32(key, 8u * ((uint32_t)(c - po + phase) & 3u));
             v[j] = v[j] ^ u32x4{rk, rk, rk, rk};
-            if (c >= lo && c + 16u <= hi) gstore16<kNT>(c, v[j]);
+            if (c >= lo && c + 16u <= hi) ustore16<kNT>(c, v[j]);
             else if (c < hi) part |= 1u << j;
         }
         // the range's partial chunks (at most its first and last), byte stores

@@ -988,7 +988,21 @@ __device__ __forceinline__ void utf8_slow_chunk(const fws_frame_desc *__restrict
     }
 }
 
-template <bool kNT, bool kEarly, bool kUtf8 = false>
+// Workgroup -> unit order with each XCD on runs of 8 consecutive workgroups
+// (32 units): workgroups are dealt round robin over the 8 XCDs, so in the
+// plain order every 16 KiB of units changes XCD and the descriptor lines at
+// the seams are fetched by two XCDs' L2s. Within each group of 64 workgroups,
+// dispatch slot r = 8 k + x becomes workgroup 8 x + k. A speed choice only
+// (dispatch order and placement are not promised); the last partial group
+// keeps the plain order, so the map is a bijection on any grid.
+__device__ __forceinline__ uint32_t xcd_run_block(uint32_t b, uint32_t nb) {
+    const uint32_t g = b >> 6;
+    if ((g << 6) + 64u > nb) return b;
+    const uint32_t r = b & 63u;
+    return (g << 6) | ((r & 7u) << 3) | (r >> 3);
+}
+
+template <bool kNT, bool kEarly, bool kUtf8 = false, bool kXcdRun = false>
 __device__ __forceinline__ void unmask_sorted_body(uint8_t *base, const fws_frame_desc *__restrict__ d, uint32_t n,
                                                    uint8_t *__restrict__ ok = nullptr,
                                                    uint32_t *__restrict__ seam = nullptr,
@@ -997,7 +1011,8 @@ __device__ __forceinline__ void unmask_sorted_body(uint8_t *base, const fws_fram
     const int lane = threadIdx.x & (kWave - 1);
     const uintptr_t b0 = (uintptr_t)base;
     const uint64_t nwaves = uint64_t(gridDim.x) * (kBlock / kWave);
-    const uint64_t u0 = uint64_t(blockIdx.x) * (kBlock / kWave) + __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const uint32_t blk = kXcdRun ? xcd_run_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    const uint64_t u0 = uint64_t(blk) * (kBlock / kWave) + __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const uint64_t po0 = d[0].payload_off;
     const fws_frame_desc dl = d[n - 1];
     const uint64_t last_pe = dl.payload_off + dl.payload_len;
@@ -1209,10 +1224,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FWS_SORT
     unmask_sorted_body<kNT, true>(base, d, n);
 }
 
-template <bool kNT>
+template <bool kNT, bool kXcdRun = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) void k_unmask_sorted(
     uint8_t *base, const fws_frame_desc *__restrict__ d, uint32_t n) {
-    unmask_sorted_body<kNT, false>(base, d, n);
+    unmask_sorted_body<kNT, false, false, kXcdRun>(base, d, n);
 }
 
 // k_unmask_sorted_ld: the unit's four 16-B loads are issued first -- their
@@ -1645,10 +1660,12 @@ extern "C" __attribute__((visibility("default"))) int fws_internal_set_grid_cap(
     return old;
 }
 
-static int g_sorted_early = 0;  // tuning hook: 0 = k_unmask_sorted, 1 = k_unmask_sorted_early, 2 = k_unmask_sorted_ld
+// tuning hook: 0 = k_unmask_sorted, 1 = k_unmask_sorted_early, 2 = k_unmask_sorted_ld,
+// 3 = k_unmask_sorted with XCD runs (xcd_run_block)
+static int g_sorted_early = 0;
 extern "C" __attribute__((visibility("default"))) int fws_internal_set_sorted_early(int on) {
     const int old = g_sorted_early;
-    g_sorted_early = on >= 0 && on <= 2 ? on : 0;
+    g_sorted_early = on >= 0 && on <= 3 ? on : 0;
     return old;
 }
 
@@ -1734,7 +1751,9 @@ int fws_launch_unmask_sorted(uint8_t *base, const fws_frame_desc *d, uint32_t n,
                              hipStream_t s) {
     if (n == 0) return 0;
     const uint64_t units = max_span / 4096u + 2u;
-    if (g_sorted_early == 2)
+    if (g_sorted_early == 3)
+        hipLaunchKernelGGL((k_unmask_sorted<true, true>), dim3(grid_for_units(units, kCapSorted)), dim3(kBlock), 0, s, base, d, n);
+    else if (g_sorted_early == 2)
         hipLaunchKernelGGL((k_unmask_sorted_ld<true>), dim3(grid_for_units(units, kCapSorted)), dim3(kBlock), 0, s, base, d, n);
     else if (g_sorted_early)
         hipLaunchKernelGGL(k_unmask_sorted_early<true>, dim3(grid_for_units(units, kCapSorted)), dim3(kBlock), 0, s, base, d, n);

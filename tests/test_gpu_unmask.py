@@ -40,11 +40,13 @@ def batch_path(request):
     L.fws_internal_set_unmask_any(old)
 
 
-@pytest.fixture(params=[0, 2], ids=["lookup_first", "loads_first"])
+@pytest.fixture(params=[0, 2, 3], ids=["lookup_first", "loads_first", "xcd_runs"])
 def sorted_kernel(request):
-    """fws_gpu_unmask_sorted's two one-launch forms: k_unmask_sorted (owner
-    lookup, then the unit's loads) and k_unmask_sorted_ld (loads first, slow
-    units deferred past the unit loop, the first parked in LDS)."""
+    """fws_gpu_unmask_sorted's one-launch forms: k_unmask_sorted (owner
+    lookup, then the unit's loads), k_unmask_sorted_ld (loads first, slow
+    units deferred past the unit loop, the first parked in LDS) and
+    k_unmask_sorted with the XCD-run workgroup order (a bijection on any grid:
+    the C2 shape covers full groups of 64 workgroups and a partial last one)."""
     L = _lib.lib()
     old = L.fws_internal_set_sorted_early(request.param)
     yield request.param

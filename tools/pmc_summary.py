@@ -11,6 +11,16 @@ Both counters are in KiB. Per MI355X_MICROARCH.md (HBM section), FETCH_SIZE
 reports exactly half the bytes of a 16-B-per-lane streaming read on gfx950,
 so it is doubled; WRITE_SIZE is exact for 16-B-per-lane stores.
 
+r06: with --rdreq DIR (a third pass, --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum
+TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum) the read bytes are counted per
+request size instead: 32 x RDREQ_32B + 64 x RDREQ_64B + 128 x RDREQ_128B.
+FETCH_SIZE's expression counts every request that is not 32 B as 64 B
+(its 128-B term is TCC_BUBBLE, zero on gfx950), which is where the "half" of a
+streaming read comes from; the doubling then also doubles the 64-B requests
+(scalar descriptor loads). Calibration (profiles/r06/pmc_rq_calibration.json):
+on the plain in-place XOR probe the sized count is the wire's 268,959,744 B
+plus 12 KiB.
+
 usage: python tools/pmc_summary.py --fetch DIR --write DIR --kernel k_unmask_fast \
            --alg-bytes 537395200 --out profiles/pmc_unmask.json
 """
@@ -42,6 +52,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--fetch", required=True)
     ap.add_argument("--write", required=True)
+    ap.add_argument("--rdreq", default="", help="a pass of the four TCC_EA0_RDREQ*_sum counters: sized read bytes")
     ap.add_argument("--kernel", required=True)
     ap.add_argument("--alg-bytes", type=int, required=True)
     ap.add_argument("--out", required=True)
@@ -65,6 +76,16 @@ def main():
     fk, wk = statistics.median(f), statistics.median(w)
     read_b = 2.0 * fk * 1024.0          # gfx950: FETCH_SIZE counts half of a wide streaming read
     write_b = wk * 1024.0
+    sized = None
+    if a.rdreq:
+        n32 = statistics.median(per_dispatch(a.rdreq, "TCC_EA0_RDREQ_32B_sum", a.kernel))
+        n64 = statistics.median(per_dispatch(a.rdreq, "TCC_EA0_RDREQ_64B_sum", a.kernel))
+        n128 = statistics.median(per_dispatch(a.rdreq, "TCC_EA0_RDREQ_128B_sum", a.kernel))
+        nall = statistics.median(per_dispatch(a.rdreq, "TCC_EA0_RDREQ_sum", a.kernel))
+        sized = {"RDREQ": nall, "RDREQ_32B": n32, "RDREQ_64B": n64, "RDREQ_128B": n128,
+                 "read_bytes": round(32 * n32 + 64 * n64 + 128 * n128),
+                 "fetch_x2_read_bytes": round(read_b)}
+        read_b = float(sized["read_bytes"])
     out = {
         "kernel": a.kernel,
         "dispatches": {"fetch_pass": len(f), "write_pass": len(w)},
@@ -75,8 +96,11 @@ def main():
         "hbm_bytes_per_launch": round(read_b + write_b),
         "alg_bytes_per_launch": a.alg_bytes,
         "traffic_over_alg": round((read_b + write_b) / a.alg_bytes, 4),
-        "correction": "read = 2 x FETCH_SIZE (gfx950 half-count of 16-B/lane streaming reads, "
-                      "MI355X_MICROARCH.md HBM); write = WRITE_SIZE; KiB = 1024 B",
+        "correction": ("read = 32 x RDREQ_32B + 64 x RDREQ_64B + 128 x RDREQ_128B (sized requests; "
+                       "2 x FETCH_SIZE kept as fetch_x2_read_bytes)" if sized else
+                       "read = 2 x FETCH_SIZE (gfx950 half-count of 16-B/lane streaming reads, "
+                       "MI355X_MICROARCH.md HBM)") + "; write = WRITE_SIZE; KiB = 1024 B",
+        "sized_reads": sized,
         "kernel_source": a.source,
         "kernel_source_sha16": src_sha,
         "commit": commit,

@@ -1,0 +1,58 @@
+#!/usr/bin/env python3
+"""Interleaved A/B of k_gather_one forms on BASELINE C4 (one 256 MiB message in
+1 427 fragments, 4 rotating destinations, HIP events around back-to-back
+fws_gpu_unmask_gather calls): 0 = two loads per chunk (r05), 1 = one load per
+chunk + the neighbour lane's block by DPP, 2 = k_gather_one_w8 (8 waves per
+SIMD) (fws_internal_set_gather_dpp), at 512 or 256 threads per workgroup. Every round times each form once.
+usage: python tools/ab_c4.py [rounds] [steps] [dpp:threads:mult,...]"""
+import json
+import os
+import statistics
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from flashws_amd import _lib, gpu  # noqa: E402
+
+
+def main():
+    rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 7
+    steps = int(sys.argv[2]) if len(sys.argv) > 2 else 100
+    L = _lib.lib()
+    dev = torch.device("cuda:0")
+    w4, d4, _ = gpu.config_c4()
+    c = gpu.Ctx(0, max_frames=len(d4) + 8, max_stream_bytes=len(w4))
+    src = torch.from_numpy(w4).to(dev)
+    total = int(d4["payload_len"].sum())
+    alg = len(w4) + total
+    dsts = [torch.empty(total + 64, dtype=torch.uint8, device=dev) for _ in range(4)]
+    dd = gpu.descs_to_device(d4, dev)
+    forms = [tuple(int(x) for x in f.split(":")) for f in sys.argv[3].split(",")] if len(sys.argv) > 3 else \
+        [(0, 512, 4), (2, 512, 4), (2, 256, 4), (1, 512, 4)]
+    times = {f: [] for f in forms}
+    for r in range(rounds):
+        for f in (forms if r % 2 == 0 else forms[::-1]):
+            L.fws_internal_set_gather_dpp(f[0])
+            L.fws_internal_set_gather_shape(f[1], f[2])
+            for i in range(10):
+                gpu.unmask_gather(c, dsts[i % 4], src, dd, len(d4))
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda.synchronize()
+            e0.record()
+            for i in range(steps):
+                gpu.unmask_gather(c, dsts[i % 4], src, dd, len(d4))
+            e1.record()
+            torch.cuda.synchronize()
+            times[f].append(e0.elapsed_time(e1) * 1e3 / steps)
+    L.fws_internal_set_gather_dpp(0)
+    L.fws_internal_set_gather_shape(0, 0)
+    for f in forms:
+        med = statistics.median(times[f])
+        print(json.dumps({"dpp": f[0], "threads": f[1], "mult": f[2], "us_median": round(med, 2), "us_min": round(min(times[f]), 2),
+                          "frac_median": round(alg / med / 8e6, 4), "runs": [round(t, 2) for t in times[f]]}))
+    c.close()
+
+
+if __name__ == "__main__":
+    main()

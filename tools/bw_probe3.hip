@@ -50,6 +50,67 @@ __global__ __launch_bounds__(256) void k_xor(u32x4 *__restrict__ buf, uint64_t n
     }
 }
 
+// Out of place with the source 8 B off the destination's 16-B grid (C4's and
+// TX's shifted windows): dst chunk a = src bytes [a + 8, a + 24) ^ key.
+// SH 0: two aligned default-policy loads per chunk (v1 of lane L = v0 of lane
+// L + 1, served by the cache: k_gather_one's form); SH 1: one nontemporal load
+// per chunk and v1 from the next lane by a DPP wave shift (lane 63: lane 0 of
+// the next chunk, the unit's last one loaded); SH 2: SH 1 with default-policy loads.
+__device__ __forceinline__ u32x4 shl_lane(const u32x4 &v) {   // lane L gets lane L + 1's value (wave_shl:1)
+    return u32x4{(uint32_t)__builtin_amdgcn_update_dpp(0, (int)v.x, 0x130, 0xF, 0xF, false),
+                 (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v.y, 0x130, 0xF, 0xF, false),
+                 (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v.z, 0x130, 0xF, 0xF, false),
+                 (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v.w, 0x130, 0xF, 0xF, false)};
+}
+__device__ __forceinline__ u32x4 bcast0(const u32x4 &v) {
+    return u32x4{(uint32_t)__builtin_amdgcn_readlane((int)v.x, 0), (uint32_t)__builtin_amdgcn_readlane((int)v.y, 0),
+                 (uint32_t)__builtin_amdgcn_readlane((int)v.z, 0), (uint32_t)__builtin_amdgcn_readlane((int)v.w, 0)};
+}
+template <int SH>
+__global__ __launch_bounds__(256) void k_shift(const u32x4 *__restrict__ src, u32x4 *__restrict__ dst, uint64_t n16,
+                                               uint32_t key) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t wave = (uint64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t base = wave * 256;                 // in 16-B blocks; src has n16 + 1 blocks
+    const g_u32x4 *s = (const g_u32x4 *)src;
+    g_u32x4 *d = (g_u32x4 *)dst;
+    u32x4 v0[4], v1[4];
+    if (SH == 0) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint64_t i = base + j * 64 + lane;
+            const uint64_t ii = i < n16 ? i : 0;
+            uint64_t i1 = ii + 1;
+            asm volatile("" : "+v"(i1));
+            v0[j] = s[ii];
+            v1[j] = s[i1];
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint64_t i = base + j * 64 + lane;
+            v0[j] = SH == 1 ? __builtin_nontemporal_load(s + (i < n16 ? i : 0)) : s[i < n16 ? i : 0];
+        }
+        u32x4 last = u32x4{0u, 0u, 0u, 0u};
+        if (lane == 63) {
+            const uint64_t i = base + 256;
+            last = SH == 1 ? __builtin_nontemporal_load(s + (i <= n16 ? i : 0)) : s[i <= n16 ? i : 0];
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            v1[j] = shl_lane(v0[j]);
+            const u32x4 nx = j < 3 ? bcast0(v0[j < 3 ? j + 1 : 0]) : last;
+            if (lane == 63) v1[j] = nx;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint64_t i = base + j * 64 + lane;
+        const u32x4 w = u32x4{v0[j].z, v0[j].w, v1[j].x, v1[j].y} ^ key;   // bytes 8..23
+        if (i < n16) __builtin_nontemporal_store(w, d + i);
+    }
+}
+
 static hipEvent_t e0, e1;
 
 template <typename F>
@@ -104,6 +165,24 @@ int main(int argc, char **argv) {
         X(1, 0, 1, "xor 1 unit/wave, sc1 stores");
         X(1, 0, 2, "xor 1 unit/wave, sc0 sc1 stores");
         X(1, 0, 3, "xor 1 unit/wave, sc1 nt stores");
+    }
+    // shifted out-of-place copy: src 269 MB + 16 B, 4 rotating destinations
+    if (!quick) {
+        u32x4 *src;
+        CK(hipMalloc(&src, bytes + 64));
+        CK(hipMemset(src, 7, bytes + 64));
+        const double cb = 2.0 * bytes;
+        for (int rep = 0; rep < 2; ++rep) {
+            timeit("shift copy, 2 loads/chunk (cached)", [&](int i) {
+                k_shift<0><<<(unsigned)((n16 / 256 + 1 + 3) / 4), 256>>>(src, bufs[i & 3], n16, 0x12345678u);
+            }, cb);
+            timeit("shift copy, 1 nt load + DPP shift", [&](int i) {
+                k_shift<1><<<(unsigned)((n16 / 256 + 1 + 3) / 4), 256>>>(src, bufs[i & 3], n16, 0x12345678u);
+            }, cb);
+            timeit("shift copy, 1 cached load + DPP shift", [&](int i) {
+                k_shift<2><<<(unsigned)((n16 / 256 + 1 + 3) / 4), 256>>>(src, bufs[i & 3], n16, 0x12345678u);
+            }, cb);
+        }
     }
     return 0;
 }

@@ -345,7 +345,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     uint64_t rel = inc - sz;                           // offset of frame t from O0
 #pragma unroll
     for (int i = 0; i < kBlock / kWave; ++i) rel += i < w ? s_wsum[i] : 0;
-    if (threadIdx.x <= nl) s_ob[threadIdx.x] = rel;    // t = nl: the end of the loaded frames
+    // s_ob[t] = frame t's offset from O0; s_ob[nl] = the end of the loaded frames,
+    // written by the thread of the last loaded frame (nl can be kBlock: there is
+    // no thread nl then -- r05 read that entry unwritten, a flaky k_tx_one)
+    if (threadIdx.x < nl) s_ob[threadIdx.x] = rel;
+    if (threadIdx.x + 1u == nl) s_ob[nl] = rel + sz;
     __syncthreads();
     const uint64_t agg = sgpr64(s_ob[nf]);             // the span's own bytes
     bool unused;
@@ -354,7 +358,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     const bool last = fb + nf >= n;
     if (last && threadIdx.x == 0) *out_len = O1 <= out_cap ? O1 : ~0ull;
     __syncthreads();                                   // every thread read s_ob[nf], s_ob[nl]
-    if (threadIdx.x <= nl) s_ob[threadIdx.x] += O0;
+    if (threadIdx.x < nl) s_ob[threadIdx.x] += O0;
+    if (threadIdx.x + 1u == nl) s_ob[nl] += O0;
     __syncthreads();
     // bytes past the batch (Lend = O1 for the last span) and past out_cap are never written
     const uint64_t clip = Lend < out_cap ? Lend : out_cap;

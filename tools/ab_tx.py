@@ -37,7 +37,7 @@ def main():
     outs = [torch.empty(total, dtype=torch.uint8, device=dev) for _ in range(4)]
     olen = torch.empty(1, dtype=torch.int64, device=dev)
     ref = None
-    modes = [("plan", 0, 0)] + [(f"one_span{k}k", 1, k) for k in (32, 64, 128, 256)]
+    modes = [("plan", 0, 0, 1)] + [(f"one_span{k}k", 1, k, 1) for k in (32, 64, 128, 256)]
     if len(sys.argv) > 2:
         modes = [m for m in modes if m[0] in sys.argv[2].split(",")]
     # warm the clocks before the first timed mode (tools/c4_thermal_probe.py)
@@ -47,8 +47,9 @@ def main():
         gpu.encode_frames(c, outs[0], tsrc, tdd, n, out_len=olen)
         torch.cuda.synchronize()
     for rep in range(3):
-        for name, one, span in (modes if rep % 2 == 0 else modes[::-1]):
+        for name, one, span, w in (modes if rep % 2 == 0 else modes[::-1]):
             L.fws_internal_set_tx_one(one, span)
+            L.fws_internal_set_tx_w5(w)
             for i in range(4):
                 gpu.encode_frames(c, outs[i % 4], tsrc, tdd, n, out_len=olen)
             torch.cuda.synchronize()
@@ -63,10 +64,11 @@ def main():
             if ref is None:
                 ref = got.clone()
             same = bool(torch.equal(ref, got))
-            print(json.dumps({"mode": name, "rep": rep, "ms": round(ms, 4),
+            print(json.dumps({"lib": os.path.basename(_lib.LIB_PATH), "mode": name, "rep": rep, "ms": round(ms, 4),
                               "frac": round((n * pl + total) / ms / 1e-3 / 8e12, 4), "same_output": same}), flush=True)
             assert same
-    L.fws_internal_set_tx_one(1, 64)
+    L.fws_internal_set_tx_one(0, 64)
+    L.fws_internal_set_tx_w5(1)
     c.close()
 
 

@@ -10,6 +10,7 @@
 #   bench_quick  python bench.py --no-extra --no-cpu
 #   share2       bench.py --gpus 2 --share-device (two ranks on device 0, gloo): the N-rank path on HIP
 #   pmc          FETCH_SIZE / WRITE_SIZE passes of the headline kernel (separate runs)
+#   pmc_rq       the TCC_EA0_RDREQ 32/64/128-B request counts of the headline kernel (sized reads)
 #   prof_main    rocprofv3 kernel trace + stats of the headline bench
 #   prof_decode  rocprofv3 kernel trace + stats of the C2/C3/dense/C5 stream decodes
 #   prof_extra   rocprofv3 kernel trace + stats of C4 gather, TX encode, C5 descriptor mode
@@ -19,7 +20,7 @@
 #   trace        phase clocks of k_scan and per-workgroup timelines of the resolve kernels
 #                (FWS_SCAN_PROF build: make -C flashws_amd/csrc prof, built beforehand)
 set -o pipefail
-ROUND=${ROUND:-r05}
+ROUND=${ROUND:-r06}
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 O=$R/gpurun_out/$ROUND
 mkdir -p "$O"
@@ -54,6 +55,8 @@ for step in "$@"; do
     pmc)
         prof pmc_fetch 120 --pmc FETCH_SIZE -f csv -d "$O/pmc_fetch" -o run -- python3 "$R/bench.py" --no-extra --no-cpu --no-batch-extra --steps 10 --warmup 2
         prof pmc_write 120 --pmc WRITE_SIZE -f csv -d "$O/pmc_write" -o run -- python3 "$R/bench.py" --no-extra --no-cpu --no-batch-extra --steps 10 --warmup 2 ;;
+    pmc_rq)      # sized read requests of the headline kernel (tools/pmc_summary.py --rdreq)
+        prof pmc_rq 120 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum -f csv -d "$O/pmc_rq" -o run -- python3 "$R/bench.py" --no-extra --no-cpu --no-batch-extra --steps 10 --warmup 2 ;;
     prof_main)
         prof prof_main 300 --kernel-trace --stats -f csv -d "$O/prof_main" -o run -- python3 "$R/bench.py" --no-extra --no-cpu ;;
     prof_decode)

@@ -1162,7 +1162,7 @@ __device__ __forceinline__ void unmask_sorted_body(uint8_t *base, const fws_fram
     }
 }
 
-// The first 3 bytes of every unit u in [1, n_units) of a sorted batch, whose
+// The first 3 bytes of every unit u in [0, n_units) of a sorted batch, whose
 // left context lies in unit u - 1 (k_unmask_sorted_utf8 skipped them), for
 // every non-empty region meeting them as payload or 3-byte tail. One thread
 // per unit seam; reads the already unmasked bytes. The owner of the seam is
@@ -1178,10 +1178,17 @@ __global__ __launch_bounds__(kBlock) void k_utf8_seam_sorted(const uint8_t *base
     const uint64_t Sa = E0 & ~uint64_t(15);
     const uint64_t nus = E1 > Sa ? (E1 - Sa + 4095u) / 4096u : 0;
     const float rate = (float)n / (float)(E1 > E0 ? E1 - E0 : 1u);
-    for (uint64_t u = uint64_t(blockIdx.x) * kBlock + threadIdx.x + 1u; u < nus; u += uint64_t(gridDim.x) * kBlock) {
+    // unit 0 too (r06): its bytes 0..2 are payload when the first region starts
+    // within 2 bytes past a 16-B boundary, and the unmask skips them in every unit
+#ifndef FWS_SEAM_U0
+#define FWS_SEAM_U0 1                                // 0: the r05 loop from unit 1 (A/B of the test only)
+#endif
+    for (uint64_t u = uint64_t(blockIdx.x) * kBlock + threadIdx.x + (FWS_SEAM_U0 ? 0u : 1u); u < nus;
+         u += uint64_t(gridDim.x) * kBlock) {
     const uint64_t P = Sa + 4096u * u;               // P < E1: the dwords at P - 4 and P are in the span's chunks
+    if (u == 0 && E0 >= P + 3u) continue;            // no region byte among unit 0's first 3
     // last region with po < P + 3: guess from the span, bracket check, else binary search
-    uint64_t g = (uint64_t)((float)(P - E0) * rate);
+    uint64_t g = P > E0 ? (uint64_t)((float)(P - E0) * rate) : 0u;
     g = g >= 1u ? g - 1u : 0u;
     if (g > n - 1u) g = n - 1u;
     uint32_t L;
@@ -1201,8 +1208,18 @@ __global__ __launch_bounds__(kBlock) void k_utf8_seam_sorted(const uint8_t *base
     // the unmask's per-unit record (two adjacent words per thread) rather than two
     // stream lines 4 KiB apart; the software-pipelined unmask writes none (seam null)
     const bool sw = seam && u < seam_units;          // else the unmask wrote no words for u
-    const uint32_t cur = sw ? seam[2u * u] : *(const uint32_t *)(base + (P - b0));
-    const uint32_t prev = sw ? seam[2u * u - 1u] : *(const uint32_t *)(base + (P - 4u - b0));
+    uint32_t cur = 0, prev = 0;                      // unit 0: no region byte lies before it
+    if (u == 0) {
+        if (sw) {
+            cur = seam[0];
+        } else {                                     // the bytes at or past E0 (>= base) only
+            for (uint32_t k = 0; k < 4u; ++k)
+                if (P + k >= E0) cur |= (uint32_t)gget(base + (P + k - b0)) << (8u * k);
+        }
+    } else {
+        cur = sw ? seam[2u * u] : *(const uint32_t *)(base + (P - b0));
+        prev = sw ? seam[2u * u - 1u] : *(const uint32_t *)(base + (P - 4u - b0));
+    }
     for (uint32_t f = L + 1u; f-- > 0;) {
         const fws_frame_desc fd = d[f];
         const uint64_t po = b0 + fd.payload_off, pe = po + fd.payload_len;

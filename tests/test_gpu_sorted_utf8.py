@@ -197,3 +197,28 @@ def test_sorted_utf8_invalid_bytes_at_seams(ctx, cuda):
     exp = np.array([_valid(c) for c in cases])
     assert not exp.any()
     assert np.array_equal(ok.astype(bool), exp), np.nonzero(ok.astype(bool) != exp)[0][:10]
+
+
+@pytest.mark.parametrize("lead", [0, 1, 2, 3, 17])
+@pytest.mark.parametrize("first", [b"\x80abc", b"\xc0\x80", b"\xbf" * 5, b"ok\xff"])
+def test_sorted_utf8_first_bytes_of_batch(ctx, cuda, lead, first):
+    """The batch's first region starting 0-2 bytes past a 16-B boundary: its
+    first bytes are unit 0's bytes 0..2, whose error flags the unmask kernel
+    leaves to the seam pass (they have no left context in the unit). An
+    invalid byte there must still clear the region's flag."""
+    rng = np.random.default_rng(lead * 7 + len(first))
+    cases = [first, "héllo".encode(), b"\x80", b"fine"]
+    regions, pos, parts = [], lead, [bytes(lead)]
+    for c in cases:
+        regions.append((pos, len(c), int(rng.integers(0, 2**32)), int(rng.integers(0, 4))))
+        parts.append(c)
+        pos += len(c) + 3
+        parts.append(b"\x00\x00\x00")
+    plain = aligned_host(pos + 32)
+    plain[:] = np.frombuffer(b"".join(parts) + bytes(32), dtype=np.uint8)[:len(plain)]
+    descs = np.array(regions, dtype=gpu.FRAME_DESC)
+    masked = oracle_unmask_regions(plain, descs)
+    got, ok = _run(ctx, cuda, masked, descs)
+    assert np.array_equal(got, plain)
+    exp = np.array([_valid(c) for c in cases])
+    assert np.array_equal(ok.astype(bool), exp), (ok, exp)

@@ -44,7 +44,13 @@ namespace fwsk {
 constexpr bool kScanNT = FWS_SCAN_NT != 0;   // nontemporal stream loads
 constexpr uint32_t kSets = 2;                // tiles in flight per wavefront (register sets; 3 sets
                                              //   at 6 waves per SIMD measured slower)
-constexpr uint32_t kScanBlocksPerCu = 8;     // resident k_scan workgroups per CU
+#ifndef FWS_SCAN_DMA
+#define FWS_SCAN_DMA 0                           // A/B build (make exp): tiles staged by LDS-DMA
+#endif
+// FWS_SCAN_DMA: the next tiles land in LDS by global_load_lds_dwordx4 (two LDS
+// tile buffers per wave instead of two register sets; 5.8 KB of LDS per wave,
+// so 6 workgroups per CU fit, or the first-hop tables would have to shrink)
+constexpr uint32_t kScanBlocksPerCu = FWS_SCAN_DMA ? 6 : 8;   // resident k_scan workgroups per CU
 #ifndef FWS_SCAN_EARLY_PF
 #define FWS_SCAN_EARLY_PF 0                     // A/B builds: 1 = refill a set as soon as its tile is in LDS
 #endif
@@ -72,6 +78,9 @@ __device__ unsigned long long g_scan_prof[16];
 // LDS of one k_scan wavefront
 struct ScanLds {
     uint8_t bytes[kTile + kHaloX];
+#if FWS_SCAN_DMA
+    uint8_t bytes2[kTile + kHaloX];          // the other register set's tile (LDS-DMA)
+#endif
     uint32_t cm[64];                         // candidate bits of lane L's 32 offsets
     uint32_t lm[64];                         // live bits of lane L's 32 offsets
     uint32_t lpre[64];                       // node index of lane L's first live offset (first
@@ -105,7 +114,11 @@ __global__ __launch_bounds__(kScanThreads) __attribute__((amdgpu_waves_per_eu(8,
     __shared__ __attribute__((aligned(16))) ScanLds lds_w[kScanWaves];
     const uint32_t lane = threadIdx.x & 63;
     ScanLds &W = lds_w[threadIdx.x >> 6];
+#if FWS_SCAN_DMA
+    uint8_t *B = W.bytes;                    // the buffer of the set in hand
+#else
     uint8_t *const B = W.bytes;
+#endif
     // wave-uniform: readfirstlane keeps the tile index and every tile-level
     // address in SGPRs (threadIdx.x >> 6 alone is a VGPR to the compiler)
     const uint32_t gw = __builtin_amdgcn_readfirstlane(blockIdx.x * kScanWaves + (threadIdx.x >> 6));
@@ -126,6 +139,27 @@ __global__ __launch_bounds__(kScanThreads) __attribute__((amdgpu_waves_per_eu(8,
     auto prefetch = [&](uint32_t tt, u32x4 (&pf)[2], u32x4 &halo) {
         if (!kPipe) return;
         const uint64_t o = uint64_t(tt < last_inner ? tt : last_inner) * kTile;
+#if FWS_SCAN_DMA
+        // into B (this set's buffer: its tile is done with it): lane L's 16 B land at
+        // M0 + 16 L; three DMA instructions, the halo on lanes 0..8 only
+        (void)pf;
+        (void)halo;
+        const uint32_t lb =
+            __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t *)B);
+        const uint8_t *g0 = wire + o + L16;
+        uint32_t keep;
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
+                     "s_mov_b32 m0, %0"
+                     : "=&s"(keep) : "v"(g0), "s"(lb) : "memory");
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
+                     "s_mov_b32 m0, %0"
+                     : "=&s"(keep) : "v"(g0 + 1024u), "s"(lb + 1024u) : "memory");
+        if (L16 < kHaloX)
+            asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
+                         "s_mov_b32 m0, %0"
+                         : "=&s"(keep) : "v"(g0 + kTile), "s"(lb + kTile) : "memory");
+        return;
+#endif
         // coalesced: each load instruction reads 1 KiB contiguous (lane L: 16 B at 16L)
         pf[0] = gload16<kScanNT>(reinterpret_cast<uintptr_t>(wire + o + L16));
         pf[1] = gload16<kScanNT>(reinterpret_cast<uintptr_t>(wire + o + 1024u + L16));
@@ -151,10 +185,19 @@ __global__ __launch_bounds__(kScanThreads) __attribute__((amdgpu_waves_per_eu(8,
         if (valid) {
             const bool inner = kPipe && t <= last_inner;
             W.lm[lane] = 0u;
+#if FWS_SCAN_DMA
+            // this set's DMA into B has landed: after its three instructions came the
+            // other set's step, 3 stores and 3 DMA instructions (in-order completion;
+            // also before the bounds-checked path below writes B itself)
+            if (kPipe) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+#endif
             if (inner) {
+#if FWS_SCAN_DMA
+#else
                 *reinterpret_cast<u32x4 *>(B + L16) = pf[0];
                 *reinterpret_cast<u32x4 *>(B + 1024u + L16) = pf[1];
                 if (L16 < kHaloX) *reinterpret_cast<u32x4 *>(B + kTile + L16) = halo;
+#endif
             } else {
                 for (uint32_t i = lane * 16u; i < kTile + kHaloX; i += 64u * 16u) {
                     const uint64_t q = t0 + i;
@@ -375,6 +418,19 @@ __global__ __launch_bounds__(kScanThreads) __attribute__((amdgpu_waves_per_eu(8,
         asm volatile("" ::: "memory");
     };
     u32x4 pa[2], pah, pb[2], pbh;
+#if FWS_SCAN_DMA
+    B = W.bytes;
+    prefetch(gw, pa, pah);
+    dummy_stores();
+    B = W.bytes2;
+    prefetch(gw + GW, pb, pbh);
+    for (uint32_t t = gw; t < n_tiles; t += 2u * GW) {
+        B = W.bytes;
+        tile(t, pa, pah);
+        B = W.bytes2;
+        tile(t + GW, pb, pbh);
+    }
+#else
     prefetch(gw, pa, pah);
     dummy_stores();
     prefetch(gw + GW, pb, pbh);
@@ -382,6 +438,7 @@ __global__ __launch_bounds__(kScanThreads) __attribute__((amdgpu_waves_per_eu(8,
         tile(t, pa, pah);
         tile(t + GW, pb, pbh);
     }
+#endif
 #ifdef FWS_SCAN_PROF
     if (lane == 0) {
         for (int i = 0; i < 8; ++i) atomicAdd(&g_scan_prof[i], (unsigned long long)prof_acc[i]);

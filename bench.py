@@ -48,11 +48,12 @@ DENSE_FRAMES, DENSE_PAYLOAD = 200000, 64   # SURVEY §6 dense small-frame worklo
 EXTRA_WARMUP = 10
 ENGINE_JOBS = 16               # batches per fws_decode_engine run (distinct buffers)
 EXTRA_WARM_S = 0.05            # and at least this long (s) of untimed calls before each extra config
+HEAD_WARM_S = 0.25             # the headline's warmup: at least W calls and this long (s) of them
 EXTRA_CONFIGS = ("c2s", "c3", "dense", "c4", "tx", "c5s", "c5d", "e2e", "c1", "batch")
 C5_STREAM_STEPS = 16           # timed C5 stream calls, each on its own freshly masked 4 GiB buffer
 # rocprofv3 kernel stats of each extra config, captured warm (bench.py --only <cfg> under
 # rocprofv3 --kernel-trace --stats; tools/gpu_round.sh prof_extras)
-PROFILE_DIR = "profiles/r05"
+PROFILE_DIR = "profiles/r06"
 
 
 def parse():
@@ -414,10 +415,12 @@ def main():
     dd = gpu.descs_to_device(descs, dev)
     stream = torch.cuda.current_stream()
 
-    # a packed batch is sorted by construction: the one-launch fws_gpu_unmask_sorted
-    for i in range(args.warmup):
-        gpu.unmask_sorted(ctx, bufs[i % args.nbuf], dd, n)
-    torch.cuda.synchronize()
+    # a packed batch is sorted by construction: the one-launch fws_gpu_unmask_sorted.
+    # Warmup: at least W untimed steps and at least HEAD_WARM_S seconds of them (the
+    # host-side CPU baseline and setup before it leave the GPU idle for tens of
+    # seconds; the first ~100 launches after that run 1-5 % slower while the clocks
+    # ramp up, profiles/r06/ab_*.jsonl first rounds)
+    _warm(lambda i: gpu.unmask_sorted(ctx, bufs[i % args.nbuf], dd, n), args.warmup, HEAD_WARM_S)
 
     # ---- timed region: K whole steps. The dominant kernel (k_unmask_sorted, the
     # step's only launch) is timed by HIP events on its stream (the current
@@ -472,6 +475,7 @@ def main():
                    "frames_per_gpu": n, "payload_bytes_per_frame": args.payload,
                    "wire_bytes_per_gpu": wire_bytes, "rotating_buffers": args.nbuf,
                    "parallelism": f"batch split x{world} (no collective)"},
+        "warmup_policy": f"at least {args.warmup} untimed steps and at least {HEAD_WARM_S} s of them",
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "traffic_source": traffic_src,

@@ -1247,139 +1247,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) voi
     unmask_sorted_body<kNT, false, false, kXcdRun>(base, d, n);
 }
 
-// k_unmask_sorted_ld: the unit's four 16-B loads are issued first -- their
-// addresses need only the span ([E0, E1) from d[0] and d[n-1], one L2-hot
-// scalar round shared by every wave) -- and the owner lookup's scalar rounds
-// run while they are in flight, as in a plain XOR stream. The fast kind (<= 2
-// frames, no outer edge: every C2 unit but the two edge ones) forms its masks
-// chunk by chunk from the record and stores. A slow-kind unit is deferred
-// past the loop so the frame walk's registers never meet the data's (inlined
-// into the loop, the walk made the allocator spill the loaded chunks):
-// the wave's first slow unit parks its loaded chunks in the wave's 4 KiB LDS
-// slot, later ones (grid-stride iterations: spans above 16 GiB) are reloaded.
-// 8 waves per SIMD, where k_unmask_sorted_early (data live across a
-// 16-register mask array) needed 80 VGPRs and 6 waves. A gap unit (no payload
-// byte: a sparse batch) has spent its loads and stores nothing.
-template <bool kNT, bool kLds>
-__device__ __forceinline__ void sorted_slow_unit(uint8_t *base, const fws_frame_desc *__restrict__ d, uint32_t n,
-                                                 uint32_t A, uint64_t E0, uint64_t E1, uint64_t U0, int lane,
-                                                 const u32x4 *slot) {
-    const uint64_t c0 = U0 + uint64_t(lane) * 16u;
-    const uint64_t safe = (E1 - 1u) & ~uint64_t(15);
-    u32x4 m[kUnmaskU];
-    slow_unit_masks(d, n, A, (uintptr_t)base, U0, lane, m);
-    u32x4 v[kUnmaskU];
-#pragma unroll
-    for (int j = 0; j < kUnmaskU; ++j) {
-        const uint64_t c = c0 + uint64_t(j) * 1024u;
-        v[j] = kLds ? slot[j * kWave + lane] : gload16<kNT>(c < E1 ? c : safe);
-    }
-    slow_unit_store<kNT>(c0, E0, E1, v, m);
-}
-
-template <bool kNT>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) void k_unmask_sorted_ld(
-    uint8_t *base, const fws_frame_desc *__restrict__ d, uint32_t n) {
-    __shared__ u32x4 s_slow[kBlock / kWave][kUnmaskU * kWave];   // 4 KiB per wave: 16 KiB, 8 workgroups per CU fit
-    if (n == 0) return;
-    const int lane = threadIdx.x & (kWave - 1);
-    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-    const uintptr_t b0 = (uintptr_t)base;
-    const uint64_t nwaves = uint64_t(gridDim.x) * (kBlock / kWave);
-    const uint64_t u0 = uint64_t(blockIdx.x) * (kBlock / kWave) + wv;
-    const uint64_t po0 = d[0].payload_off;
-    const fws_frame_desc dl = d[n - 1];
-    const uint64_t E0 = b0 + po0, E1 = b0 + dl.payload_off + dl.payload_len;
-    const uint64_t Sa = E0 & ~uint64_t(15);
-    const uint64_t nus = E1 > Sa ? (E1 - Sa + 4095u) / 4096u : 0;
-    const uint64_t safe = (E1 - 1u) & ~uint64_t(15);
-    const float rate = (float)n * 4096.0f / (float)(E1 > E0 ? E1 - E0 : 1u);
-    // deferred slow units (wave-uniform): the parked one, the next 64 iterations
-    // by bit, and whether any lies further out
-    uint64_t parked = ~uint64_t(0), later = 0;
-    bool far = false;
-    uint32_t k = 0;
-    for (uint64_t u = u0; u < nus; u += nwaves, ++k) {
-        const uint64_t U0 = Sa + 4096u * u;
-        const uint64_t c0 = U0 + uint64_t(lane) * 16u;
-        u32x4 v[kUnmaskU];
-#pragma unroll
-        for (int j = 0; j < kUnmaskU; ++j) {
-            const uint64_t c = c0 + uint64_t(j) * 1024u;
-            v[j] = gload16<kNT>(c < E1 ? c : safe);
-        }
-        const uint32_t A = sorted_owner(d, n, b0, U0, E0, u, rate);
-        const bool hasB = A + 1u < n, hasC = A + 2u < n;
-        const fws_frame_desc fa = d[A];
-        fws_frame_desc fb{0, 0, 0, 0};
-        if (hasB) fb = d[A + 1u];
-        const uint64_t poC = hasC ? b0 + d[A + 2u].payload_off : 0;
-        const uint64_t poA = b0 + fa.payload_off, peA = poA + fa.payload_len;
-        const uint64_t poB = b0 + fb.payload_off, peB = poB + fb.payload_len;
-        const u32x4 rec = unit_record(U0, E0, E1, A, poA, peA, aligned_key(fa.key, fa.phase, poA), hasB, poB, peB,
-                                      aligned_key(fb.key, fb.phase, poB), hasC, poC);
-        if (rec.z & kRecSlow) {
-            if (parked == ~uint64_t(0)) {
-#pragma unroll
-                for (int j = 0; j < kUnmaskU; ++j) s_slow[wv][j * kWave + lane] = v[j];
-                parked = u;
-            } else if (k < 64u) {
-                later |= uint64_t(1) << k;
-            } else {
-                far = true;
-            }
-            continue;
-        }
-        const uint32_t a0 = rec.z & 0x1FFFu, a1 = (rec.z >> 13) & 0x1FFFu;
-        const uint32_t e0 = rec.w & 0x1FFFu, e1 = (rec.w >> 13) & 0x1FFFu;
-        if (a1 <= a0 && e1 <= e0) continue;
-        uint32_t o0 = (uint32_t)lane * 16u;
-        asm volatile("" : "+v"(o0));
-#pragma unroll
-        for (int j = 0; j < kUnmaskU; ++j) {
-            const uint32_t o = o0 + (uint32_t)j * 1024u;
-            const bool inA = o >= a0 && o + 16u <= a1, inB = o >= e0 && o + 16u <= e1;
-            u32x4 mk;
-            if (inA || inB) {
-                const uint32_t rk = inA ? rec.x : rec.y;
-                mk = u32x4{rk, rk, rk, rk};
-            } else {
-                mk = u32x4{(rec.x & byte_sel32(o, a0, a1)) | (rec.y & byte_sel32(o, e0, e1)),
-                           (rec.x & byte_sel32(o + 4u, a0, a1)) | (rec.y & byte_sel32(o + 4u, e0, e1)),
-                           (rec.x & byte_sel32(o + 8u, a0, a1)) | (rec.y & byte_sel32(o + 8u, e0, e1)),
-                           (rec.x & byte_sel32(o + 12u, a0, a1)) | (rec.y & byte_sel32(o + 12u, e0, e1))};
-            }
-            if (mk.x | mk.y | mk.z | mk.w) ustore16<kNT>(c0 + uint64_t(j) * 1024u, v[j] ^ mk);
-        }
-    }
-    if (parked != ~uint64_t(0)) {                     // lane-private LDS cells: no barrier needed
-        const uint64_t U0 = Sa + 4096u * parked;
-        sorted_slow_unit<kNT, true>(base, d, n, sorted_owner(d, n, b0, U0, E0, parked, rate), E0, E1, U0, lane,
-                                    s_slow[wv]);
-    }
-    while (later) {
-        const uint32_t kk = (uint32_t)__builtin_ctzll(later);
-        later &= later - 1u;
-        const uint64_t u = u0 + uint64_t(kk) * nwaves, U0 = Sa + 4096u * u;
-        sorted_slow_unit<kNT, false>(base, d, n, sorted_owner(d, n, b0, U0, E0, u, rate), E0, E1, U0, lane, nullptr);
-    }
-    if (far) {                                        // spans beyond 64 grid strides (> 1 TiB at the grid cap)
-        for (uint64_t u = u0 + 64u * nwaves; u < nus; u += nwaves) {
-            const uint64_t U0 = Sa + 4096u * u;
-            const uint32_t A = sorted_owner(d, n, b0, U0, E0, u, rate);
-            const bool hasB = A + 1u < n, hasC = A + 2u < n;
-            const fws_frame_desc fa = d[A];
-            fws_frame_desc fb{0, 0, 0, 0};
-            if (hasB) fb = d[A + 1u];
-            const uint64_t poC = hasC ? b0 + d[A + 2u].payload_off : 0;
-            const uint64_t poA = b0 + fa.payload_off, poB = b0 + fb.payload_off;
-            const u32x4 rec = unit_record(U0, E0, E1, A, poA, poA + fa.payload_len, 0u, hasB, poB,
-                                          poB + fb.payload_len, 0u, hasC, poC);
-            if (rec.z & kRecSlow) sorted_slow_unit<kNT, false>(base, d, n, A, E0, E1, U0, lane, nullptr);
-        }
-    }
-}
-
 // Software-pipelined form of unmask_sorted_body<.., kUtf8 = true>: a wave's
 // grid-stride units (16 per wave on C5) are processed so that the next unit's
 // owner lookup and data loads are issued before the current unit's UTF-8
@@ -1677,12 +1544,14 @@ extern "C" __attribute__((visibility("default"))) int fws_internal_set_grid_cap(
     return old;
 }
 
-// tuning hook: 0 = k_unmask_sorted, 1 = k_unmask_sorted_early, 2 = k_unmask_sorted_ld,
-// 3 = k_unmask_sorted with XCD runs (xcd_run_block)
+// tuning hook: 0 = k_unmask_sorted, 1 = k_unmask_sorted_early, 3 = k_unmask_sorted
+// with XCD runs (xcd_run_block). (2 was r06's loads-first k_unmask_sorted_ld with
+// the slow units deferred past the unit loop: 83.27 against 83.02 us, removed;
+// DESIGN.md §4.1b, profiles/r06/ab_sorted_ld.jsonl.)
 static int g_sorted_early = 0;
 extern "C" __attribute__((visibility("default"))) int fws_internal_set_sorted_early(int on) {
     const int old = g_sorted_early;
-    g_sorted_early = on >= 0 && on <= 3 ? on : 0;
+    g_sorted_early = on == 1 || on == 3 ? on : 0;
     return old;
 }
 
@@ -1770,8 +1639,6 @@ int fws_launch_unmask_sorted(uint8_t *base, const fws_frame_desc *d, uint32_t n,
     const uint64_t units = max_span / 4096u + 2u;
     if (g_sorted_early == 3)
         hipLaunchKernelGGL((k_unmask_sorted<true, true>), dim3(grid_for_units(units, kCapSorted)), dim3(kBlock), 0, s, base, d, n);
-    else if (g_sorted_early == 2)
-        hipLaunchKernelGGL((k_unmask_sorted_ld<true>), dim3(grid_for_units(units, kCapSorted)), dim3(kBlock), 0, s, base, d, n);
     else if (g_sorted_early)
         hipLaunchKernelGGL(k_unmask_sorted_early<true>, dim3(grid_for_units(units, kCapSorted)), dim3(kBlock), 0, s, base, d, n);
     else

@@ -40,13 +40,12 @@ def batch_path(request):
     L.fws_internal_set_unmask_any(old)
 
 
-@pytest.fixture(params=[0, 2, 3], ids=["lookup_first", "loads_first", "xcd_runs"])
+@pytest.fixture(params=[0, 3], ids=["lookup_first", "xcd_runs"])
 def sorted_kernel(request):
     """fws_gpu_unmask_sorted's one-launch forms: k_unmask_sorted (owner
-    lookup, then the unit's loads), k_unmask_sorted_ld (loads first, slow
-    units deferred past the unit loop, the first parked in LDS) and
-    k_unmask_sorted with the XCD-run workgroup order (a bijection on any grid:
-    the C2 shape covers full groups of 64 workgroups and a partial last one)."""
+    lookup, then the unit's loads) and the same kernel with the XCD-run
+    workgroup order (a bijection on any grid: the C2 shape covers full groups
+    of 64 workgroups and a partial last one)."""
     L = _lib.lib()
     old = L.fws_internal_set_sorted_early(request.param)
     yield request.param
@@ -414,29 +413,6 @@ def test_sorted_early_variant(ctx, cuda):
         assert np.array_equal(run_sorted(ctx, host, descs, cuda), oracle_unmask_regions(host, descs))
     finally:
         lib().fws_internal_set_sorted_early(old)
-
-
-@pytest.mark.parametrize("cap", [1, 3, 64])
-def test_sorted_ld_grid_stride(ctx, cuda, cap):
-    """k_unmask_sorted_ld on grids far smaller than the unit count: each wave
-    walks many units, so its deferred slow units take every route (the first
-    parked in LDS, the next 64 strides by bit, the rest by the far rescan)."""
-    L = _lib.lib()
-    old_v, old_cap = L.fws_internal_set_sorted_early(2), L.fws_internal_set_grid_cap(cap)
-    try:
-        rng = np.random.default_rng(67 + cap)
-        regions, pos = _rand_regions(rng, 30000, 40, 3)
-        host = aligned_host(pos + 32)
-        host[:] = rng.integers(0, 256, len(host), dtype=np.uint8)
-        descs = np.array(regions, dtype=gpu.FRAME_DESC)
-        assert np.array_equal(run_sorted(ctx, host, descs, cuda), oracle_unmask_regions(host, descs))
-        wire, descs, _ = gpu.config_c3(seed=71 + cap, target=2 << 20)
-        exp = wire.copy()
-        orc.orc_decode_stream(exp)
-        assert np.array_equal(run_sorted(ctx, wire, descs, cuda), exp)
-    finally:
-        L.fws_internal_set_grid_cap(old_cap)
-        L.fws_internal_set_sorted_early(old_v)
 
 
 def test_check_sorted_contract(ctx, cuda):

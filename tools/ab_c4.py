@@ -1,9 +1,9 @@
 #!/usr/bin/env python3
 """Interleaved A/B of k_gather_one forms on BASELINE C4 (one 256 MiB message in
 1 427 fragments, 4 rotating destinations, HIP events around back-to-back
-fws_gpu_unmask_gather calls): 0 = two loads per chunk (r05), 1 = one load per
-chunk + the neighbour lane's block by DPP, 2 = k_gather_one_w8 (8 waves per
-SIMD) (fws_internal_set_gather_dpp), at 512 or 256 threads per workgroup. Every round times each form once.
+fws_gpu_unmask_gather calls): 0 = k_gather_one (r05), 2 = k_gather_one_w8
+(8 waves per SIMD) (fws_internal_set_gather_dpp), at 512 or 256 threads per
+workgroup. Every round times each form once.
 usage: python tools/ab_c4.py [rounds] [steps] [dpp:threads:mult,...]"""
 import json
 import os
@@ -29,7 +29,7 @@ def main():
     dsts = [torch.empty(total + 64, dtype=torch.uint8, device=dev) for _ in range(4)]
     dd = gpu.descs_to_device(d4, dev)
     forms = [tuple(int(x) for x in f.split(":")) for f in sys.argv[3].split(",")] if len(sys.argv) > 3 else \
-        [(0, 512, 4), (2, 512, 4), (2, 256, 4), (1, 512, 4)]
+        [(0, 512, 4), (2, 512, 4), (2, 256, 4)]
     times = {f: [] for f in forms}
     for r in range(rounds):
         for f in (forms if r % 2 == 0 else forms[::-1]):
@@ -45,7 +45,7 @@ def main():
             e1.record()
             torch.cuda.synchronize()
             times[f].append(e0.elapsed_time(e1) * 1e3 / steps)
-    L.fws_internal_set_gather_dpp(0)
+    L.fws_internal_set_gather_dpp(2)
     L.fws_internal_set_gather_shape(0, 0)
     for f in forms:
         med = statistics.median(times[f])

@@ -4,7 +4,7 @@ rotating buffers, HIP events around back-to-back calls): every round times
 each variant once, so box drift hits all of them alike. Prints one JSON line
 per variant with the median / min per-launch time and the HBM fraction.
 usage: python tools/ab_sorted.py [rounds] [steps] [variants, comma-separated]
-  variant 0 = k_unmask_sorted (lookup first), 1 = _early, 2 = _ld (loads first)"""
+  variant 0 = k_unmask_sorted (lookup first), 1 = _early, 3 = XCD-run order"""
 import json
 import os
 import statistics
@@ -21,7 +21,7 @@ ALG = 537_395_200
 def main():
     rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 7
     steps = int(sys.argv[2]) if len(sys.argv) > 2 else 200
-    variants = [int(x) for x in sys.argv[3].split(",")] if len(sys.argv) > 3 else [0, 2]
+    variants = [int(x) for x in sys.argv[3].split(",")] if len(sys.argv) > 3 else [0, 3]
     L = _lib.lib()
     dev = torch.device("cuda:0")
     wire, descs, _ = gpu.config_c2()

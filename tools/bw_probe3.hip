@@ -23,6 +23,47 @@ __device__ __forceinline__ void store_pol(g_u32x4 *p, u32x4 v) {
     else asm volatile("global_store_dwordx4 %0, %1, off sc1 nt\n\ts_nop 1" :: "v"(p), "v"(v) : "memory");
 }
 
+// One unit's four 16-B loads with an explicit cache policy, issued and waited in
+// one asm statement (the compiler does not count asm loads): LD 1 sc1 nt, 2 sc0
+// nt, 3 sc0 sc1 nt, 4 sc1.
+template <int LD>
+__device__ __forceinline__ void load4_pol(const g_u32x4 *p0, const g_u32x4 *p1, const g_u32x4 *p2, const g_u32x4 *p3,
+                                          u32x4 (&v)[4]) {
+#define LD4(POL)                                                                                              \
+    asm volatile("global_load_dwordx4 %0, %4, off " POL "\n\tglobal_load_dwordx4 %1, %5, off " POL           \
+                 "\n\tglobal_load_dwordx4 %2, %6, off " POL "\n\tglobal_load_dwordx4 %3, %7, off " POL       \
+                 "\n\ts_waitcnt vmcnt(0)"                                                                   \
+                 : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3])                                      \
+                 : "v"(p0), "v"(p1), "v"(p2), "v"(p3)                                                      \
+                 : "memory")
+    if constexpr (LD == 1) LD4("sc1 nt");
+    else if constexpr (LD == 2) LD4("sc0 nt");
+    else if constexpr (LD == 3) LD4("sc0 sc1 nt");
+    else LD4("sc1");
+#undef LD4
+}
+
+template <int LD>
+__global__ __launch_bounds__(256) void k_xor_ld(u32x4 *__restrict__ buf, uint64_t n16, uint32_t key) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t wave = (uint64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t base = wave * 256;
+    g_u32x4 *p = (g_u32x4 *)buf;
+    uint64_t ii[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint64_t i = base + j * 64 + lane;
+        ii[j] = i < n16 ? i : 0;
+    }
+    u32x4 v[4];
+    load4_pol<LD>(p + ii[0], p + ii[1], p + ii[2], p + ii[3], v);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint64_t i = base + j * 64 + lane;
+        if (i < n16) store_pol<3>(p + i, v[j] ^ key);
+    }
+}
+
 // U units of 4 KiB per wave; DEP: 0 none, 1 one scalar load (a per-unit word) before
 // the data loads; ST: 0 nontemporal stores, else store_pol<ST>
 template <int U, int DEP, int ST = 0>
@@ -165,6 +206,14 @@ int main(int argc, char **argv) {
         X(1, 0, 1, "xor 1 unit/wave, sc1 stores");
         X(1, 0, 2, "xor 1 unit/wave, sc0 sc1 stores");
         X(1, 0, 3, "xor 1 unit/wave, sc1 nt stores");
+#define XL(LD, NAME)                                                                                           \
+        timeit(NAME, [&](int i) {                                                                              \
+            k_xor_ld<LD><<<(unsigned)(((n16 + 255) / 256 + 3) / 4), 256>>>(bufs[i & 3], n16, 0x12345678u);       \
+        }, rw)
+        XL(1, "sc1 nt loads, sc1 nt stores");
+        XL(2, "sc0 nt loads, sc1 nt stores");
+        XL(3, "sc0 sc1 nt loads, sc1 nt stores");
+        XL(4, "sc1 loads, sc1 nt stores");
     }
     // shifted out-of-place copy: src 269 MB + 16 B, 4 rotating destinations
     if (!quick) {

@@ -47,6 +47,7 @@ DENSE_FRAMES, DENSE_PAYLOAD = 200000, 64   # SURVEY §6 dense small-frame worklo
 # the next 10 (tools/c5_warmup_probe.py, profiles/r03/c5_warmup.txt)
 EXTRA_WARMUP = 10
 ENGINE_JOBS = 16               # batches per fws_decode_engine run (distinct buffers)
+SRC_COPIES = 4                 # C4 / TX: rotating sources (>= 1 GiB with the outputs, past the 256 MB MALL)
 EXTRA_WARM_S = 0.05            # and at least this long (s) of untimed calls before each extra config
 HEAD_WARM_S = 0.25             # the headline's warmup: at least W calls and this long (s) of them
 EXTRA_CONFIGS = ("c2s", "c3", "dense", "c4", "tx", "c5s", "c5d", "e2e", "c1", "batch")
@@ -881,21 +882,26 @@ def stream_decode_extra(ctx, wire_c2, dev, args):
 
 
 def c4_extra(dev, steps, stream):
-    """C4: one 256 MiB fragmented message, unmask + reassemble out of place"""
+    """C4: one 256 MiB fragmented message, unmask + reassemble out of place. The
+    source rotates over SRC_COPIES copies (1 GiB with the destinations' 1 GiB):
+    one source re-read every step is partly served by the 256 MB Infinity Cache
+    (r06: 0.084 against 0.100 ms, profiles/r06/ab_mall.jsonl)."""
     out = {}
     w4, d4, _ = gpu.config_c4()
     c = gpu.Ctx(dev.index or 0, max_frames=len(d4) + 8, max_stream_bytes=len(w4))
-    src = torch.from_numpy(w4).to(dev)
+    srcs = [torch.from_numpy(w4).to(dev) for _ in range(SRC_COPIES)]
     total = int(d4["payload_len"].sum())
     dsts = [torch.empty(total + 64, dtype=torch.uint8, device=dev) for _ in range(4)]
     dd4 = gpu.descs_to_device(d4, dev)
-    t = _time(lambda i: gpu.unmask_gather(c, dsts[i % 4], src, dd4, len(d4)), steps, stream, warmup=EXTRA_WARMUP)
+    t = _time(lambda i: gpu.unmask_gather(c, dsts[i % 4], srcs[i % SRC_COPIES], dd4, len(d4)), steps, stream,
+              warmup=EXTRA_WARMUP)
     out["C4_fragmented_reassemble"] = {"GiB_per_s": round(total / t / GIB, 1), "ms_per_step": round(t * 1e3, 4),
                                        "fragments": len(d4), "alg_GB_per_s": round((len(w4) + total) / t / 1e9, 1),
+                                       "rotating_sources": SRC_COPIES,
                                        "roofline": _step_roofline(len(w4) + total, t, "whole fws_gpu_unmask_gather step: wire read + payload written out of place")}
     _profile(out["C4_fragmented_reassemble"], "c4")
     c.close()
-    del src, dsts, w4
+    del srcs, dsts, w4
     return out
 
 
@@ -913,22 +919,27 @@ def tx_extra(dev, args, steps, stream):
     txd["opcode"] = 2
     txd["fin"] = 1
     txd["masked"] = 1
-    tsrc = torch.from_numpy(rng.integers(0, 256, n * pl, dtype=np.uint8)).to(dev)
+    payload = rng.integers(0, 256, n * pl, dtype=np.uint8)
+    # the payloads rotate over SRC_COPIES copies (see c4_extra: 0.091 against 0.103 ms
+    # with one source re-read every step, profiles/r06/ab_mall.jsonl)
+    tsrcs = [torch.from_numpy(payload).to(dev) for _ in range(SRC_COPIES)]
     tdd = torch.from_numpy(txd.view(np.uint8).copy()).to(dev)
     hdr = 2 + 4 + (0 if pl < 126 else 2 if pl < 65536 else 8)
     tx_total = n * (pl + hdr)
     c = gpu.Ctx(dev.index or 0, max_frames=n, max_stream_bytes=tx_total)
     touts = [torch.empty(tx_total, dtype=torch.uint8, device=dev) for _ in range(4)]
     olen = torch.empty(1, dtype=torch.int64, device=dev)
-    t = _time(lambda i: gpu.encode_frames(c, touts[i % 4], tsrc, tdd, n, out_len=olen), steps, stream, warmup=EXTRA_WARMUP)
+    t = _time(lambda i: gpu.encode_frames(c, touts[i % 4], tsrcs[i % SRC_COPIES], tdd, n, out_len=olen), steps, stream,
+              warmup=EXTRA_WARMUP)
     assert int(olen.item()) == tx_total
     out["C2_tx_encode"] = {"GiB_per_s": round(n * pl / t / GIB, 1), "ms_per_step": round(t * 1e3, 4),
                            "frames": n, "alg_GB_per_s": round((n * pl + tx_total) / t / 1e9, 1),
+                           "rotating_sources": SRC_COPIES,
                            "path": "fws_gpu_encode_frames: client frames (header + key + masked payload)",
                            "roofline": _step_roofline(n * pl + tx_total, t, "whole fws_gpu_encode_frames step: payload read + frames written")}
     _profile(out["C2_tx_encode"], "tx")
     c.close()
-    del touts, tsrc
+    del touts, tsrcs
     return out
 
 

@@ -51,6 +51,30 @@ __device__ __forceinline__ void gstore16_wt(uintptr_t a, u32x4 v) {
     asm volatile("global_store_dwordx4 %0, %1, off sc1 nt\n\ts_nop 1" : : "v"(p), "v"(v) : "memory");
 }
 
+// Lane L gets lane L + 1's value (DPP wave_shl:1; lane 63 gets 0), and lane
+// 0's value in every lane: the 16-B window of a lane whose aligned source
+// block is its neighbour's minus 16 is its own block and the neighbour's,
+// so one load per chunk serves two windows (tools/bw_probe3.hip, shifted
+// copy: 78.2 us with one default-policy load + the shift against 79.1 us with
+// two loads per chunk).
+__device__ __forceinline__ uint32_t wave_shl1(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xF, 0xF, false);
+}
+__device__ __forceinline__ u32x4 wave_shl1(const u32x4 &v) {
+    return u32x4{wave_shl1(v.x), wave_shl1(v.y), wave_shl1(v.z), wave_shl1(v.w)};
+}
+__device__ __forceinline__ uint64_t wave_shl1_64(uint64_t v) {
+    return (uint64_t)wave_shl1((uint32_t)v) | ((uint64_t)wave_shl1((uint32_t)(v >> 32)) << 32);
+}
+__device__ __forceinline__ u32x4 lane0_of(const u32x4 &v) {
+    return u32x4{(uint32_t)__builtin_amdgcn_readlane((int)v.x, 0), (uint32_t)__builtin_amdgcn_readlane((int)v.y, 0),
+                 (uint32_t)__builtin_amdgcn_readlane((int)v.z, 0), (uint32_t)__builtin_amdgcn_readlane((int)v.w, 0)};
+}
+__device__ __forceinline__ uint64_t lane0_of64(uint64_t v) {
+    return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, 0) |
+           ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), 0) << 32);
+}
+
 // A store through a global-address-space pointer: global_store (vmcnt only),
 // where a generic pointer gives flat_store, which also counts in lgkmcnt --
 // so the next workgroup barrier's lgkmcnt(0) would wait for the store's

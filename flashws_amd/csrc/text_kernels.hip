@@ -229,7 +229,7 @@ __device__ __forceinline__ uint32_t lds_search(const uint64_t *base, uint32_t n,
 // Requires dst 16-B aligned and 1 <= n <= kGatherLdsMax. 74 VGPRs, 6 waves per
 // SIMD; forced to 7 (72 VGPRs, 2 spilled on the probe path only) it measured
 // 0.096-0.101 against 0.085-0.089 ms on C4 (profiles/r04/ab_gather_shapes.jsonl).
-template <uint32_t kT, bool kLate>
+template <uint32_t kT, bool kDpp, bool kLate>
 __device__ __forceinline__ void gather_one_body(uint8_t *__restrict__ dst, const uint8_t *__restrict__ src,
                                                 const fws_frame_desc *__restrict__ d, uint32_t n) {
     constexpr uint32_t kGatherPer = kGatherLdsMax / kT;   // regions per thread in the block scan
@@ -341,6 +341,42 @@ __device__ __forceinline__ void gather_one_body(uint8_t *__restrict__ dst, const
             const uint32_t ph = in1 ? (uint32_t)(a - B1) + d1.phase : (uint32_t)(a - B0) + d0.phase;
             rk[j] = rotr32(in1 ? d1.key : d0.key, 8u * (ph & 3u));
         }
+        if constexpr (kDpp) {
+            // one nontemporal load per chunk: a lane's second block is lane L + 1's
+            // first when that lane's block is the next one (same region and shift);
+            // lane 63's is lane 0's of the next chunk, or for the last chunk a load
+            // of its own. A full chunk whose neighbour block is another (a region
+            // seam) goes bytewise with the seam / tail chunks.
+            u32x4 v0[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v0[j] = gload16<true>(sb[j]);
+            u32x4 last = u32x4{0u, 0u, 0u, 0u};
+            if (lane == 63) last = gload16<true>(full[3] && sh[3] ? sb[3] + 16u : sb[3]);
+            uint32_t pend = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint64_t a = a0 + (uint64_t)j * 1024u;
+                uint64_t nsb = wave_shl1_64(sb[j]);
+                u32x4 v1 = wave_shl1(v0[j]);
+                if (j < 3) {
+                    const uint64_t nsb0 = lane0_of64(sb[j < 3 ? j + 1 : 0]);
+                    const u32x4 nv0 = lane0_of(v0[j < 3 ? j + 1 : 0]);
+                    if (lane == 63) {
+                        nsb = nsb0;
+                        v1 = nv0;
+                    }
+                } else if (lane == 63) {
+                    nsb = sb[3] + 16u;
+                    v1 = last;
+                }
+                const bool ok = sh[j] == 0u || nsb == sb[j] + 16u;
+                if (full[j] && ok) gstore16<true>((uintptr_t)(dst + a), shr_bytes(v0[j], v1, sh[j]) ^ rk[j]);
+                else if (a < total) pend |= 1u << j;
+            }
+            for (; pend; pend &= pend - 1u)
+                gather_bytes(dst, src, d, s_base, flo, a0 + (uint64_t)__builtin_ctz(pend) * 1024u, total);
+            continue;
+        }
         u32x4 v0[4], v1[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -370,18 +406,18 @@ __device__ __forceinline__ void gather_one_body(uint8_t *__restrict__ dst, const
     }
 }
 
-template <uint32_t kT>
+template <uint32_t kT, bool kDpp = false>
 __global__ __launch_bounds__(kT) void k_gather_one(uint8_t *__restrict__ dst, const uint8_t *__restrict__ src,
                                                    const fws_frame_desc *__restrict__ d, uint32_t n) {
-    gather_one_body<kT, false>(dst, src, d, n);
+    gather_one_body<kT, kDpp, false>(dst, src, d, n);
 }
 
 // The same at 8 waves per SIMD (62 VGPRs, no spill): the seam / tail chunks'
 // byte loop runs after the unit's full chunks (kLate), not inline with them.
-template <uint32_t kT>
+template <uint32_t kT, bool kDpp = false>
 __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(8))) void k_gather_one_w8(
     uint8_t *__restrict__ dst, const uint8_t *__restrict__ src, const fws_frame_desc *__restrict__ d, uint32_t n) {
-    gather_one_body<kT, true>(dst, src, d, n);
+    gather_one_body<kT, kDpp, true>(dst, src, d, n);
 }
 
 }  // namespace fwsk
@@ -423,14 +459,13 @@ int fws_launch_utf8_descs(const uint8_t *base, const fws_frame_desc *descs, uint
 // (profiles/r04/ab_gather_shapes.jsonl; on a 64 MiB message 256 threads is
 // ~1 us faster). Tuning hook below.
 static int g_gather_threads = 512, g_gather_mult = 4;
-// tuning hook: 0 = k_gather_one (r05); 2 = k_gather_one_w8 (8 waves per SIMD),
-// the default: 83.8 against 85.1 us (tools/ab_c4.py, profiles/r06/ab_c4.jsonl,
-// one process, order alternated). (1 was one load per chunk plus the neighbour
-// lane's block by DPP: 86.3 against 85.1 us, removed.)
+// tuning hook: 0 = k_gather_one (r05); 1 = k_gather_one<.., true> (one
+// nontemporal load per chunk + the neighbour's block by DPP); 2 =
+// k_gather_one_w8 (8 waves per SIMD), the default; 3 = k_gather_one_w8<.., true>
 static int g_gather_dpp = 2;
 extern "C" __attribute__((visibility("default"))) int fws_internal_set_gather_dpp(int on) {
     const int old = g_gather_dpp;
-    g_gather_dpp = on == 2 ? 2 : 0;
+    g_gather_dpp = on >= 0 && on <= 3 ? on : 0;
     return old;
 }
 // threads 256 or 512 (0: the default), mult > 0 (0: the default)
@@ -441,22 +476,31 @@ extern "C" __attribute__((visibility("default"))) int fws_internal_set_gather_sh
     return 0;
 }
 
+// the k_gather_one form of the hooks: (k_gather_dpp, 512 threads) -> kernel
+static const void *gather_one_kernel(int mode, bool t512) {
+    switch (mode * 2 + (t512 ? 1 : 0)) {
+    case 0: return (const void *)k_gather_one<256>;
+    case 1: return (const void *)k_gather_one<512>;
+    case 2: return (const void *)k_gather_one<256, true>;
+    case 3: return (const void *)k_gather_one<512, true>;
+    case 4: return (const void *)k_gather_one_w8<256>;
+    case 5: return (const void *)k_gather_one_w8<512>;
+    case 6: return (const void *)k_gather_one_w8<256, true>;
+    default: return (const void *)k_gather_one_w8<512, true>;
+    }
+}
+
 static int gather_one_grid(uint64_t max_bytes, uint64_t *out) {
-    static int resident[4][64] = {};               // [w8 * 2 + (512 threads)][device]
+    static int resident[8][64] = {};               // [mode * 2 + (512 threads)][device]
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return FWS_ERR_INVALID;
-    const int v = (g_gather_dpp == 2 ? 2 : 0) + (g_gather_threads == 512 ? 1 : 0);
+    const int v = g_gather_dpp * 2 + (g_gather_threads == 512 ? 1 : 0);
     if (!resident[v][dev]) {
         int cus = 0, per = 0;
         hipError_t e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        if (e == hipSuccess) {
-            switch (v) {
-            case 0: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_gather_one<256>, 256, 0); break;
-            case 1: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_gather_one<512>, 512, 0); break;
-            case 2: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_gather_one_w8<256>, 256, 0); break;
-            default: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_gather_one_w8<512>, 512, 0); break;
-            }
-        }
+        if (e == hipSuccess)
+            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, gather_one_kernel(g_gather_dpp, v & 1),
+                                                             g_gather_threads, 0);
         if (e != hipSuccess) return FWS_ERR_NO_DEVICE;
         resident[v][dev] = cus * (per > 0 ? per : 1);
     }
@@ -482,14 +526,10 @@ int fws_launch_gather(uint8_t *dst, const uint8_t *src, const fws_frame_desc *d,
         uint64_t blocks = 0;
         const int r = gather_one_grid(max_bytes, &blocks);
         if (r != 0) return r;
-        if (g_gather_dpp == 2 && g_gather_threads == 512)
-            hipLaunchKernelGGL(k_gather_one_w8<512>, dim3((unsigned)blocks), dim3(512), 0, s, dst, src, d, n);
-        else if (g_gather_dpp == 2)
-            hipLaunchKernelGGL(k_gather_one_w8<256>, dim3((unsigned)blocks), dim3(256), 0, s, dst, src, d, n);
-        else if (g_gather_threads == 512)
-            hipLaunchKernelGGL(k_gather_one<512>, dim3((unsigned)blocks), dim3(512), 0, s, dst, src, d, n);
-        else
-            hipLaunchKernelGGL(k_gather_one<256>, dim3((unsigned)blocks), dim3(256), 0, s, dst, src, d, n);
+        const void *k = gather_one_kernel(g_gather_dpp, g_gather_threads == 512);
+        void *args[] = {&dst, &src, &d, &n};
+        const hipError_t e = hipLaunchKernel(k, dim3((unsigned)blocks), dim3((unsigned)g_gather_threads), args, 0, s);
+        if (e != hipSuccess) return fws_hip_status(e);
         return fws_hip_status(hipGetLastError());
     }
     int r = fws_launch_gather_plan(d, n, ws, s);

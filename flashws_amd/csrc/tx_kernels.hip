@@ -165,7 +165,12 @@ __device__ __forceinline__ void tx_store_tail(uint8_t *out, uint64_t a, uint64_t
 // .. fhi (indices into d / obase, which may be global or a workgroup's LDS copy)
 // cover the unit; chunks at or past own_end belong to another unit owner and are
 // skipped; no byte at or past total is written.
-template <typename DescP, typename OffP>
+// kDpp (r06): one nontemporal load per full chunk; the window's second block is
+// the next lane's first (DPP wave shift; lane 63: lane 0's of the next chunk,
+// or for the last chunk a load of its own) or the next lane's A-window seam
+// block (the left neighbour of a seam chunk). A full chunk with neither (rare:
+// the chunk before the batch's last) is built by the seam path afterwards.
+template <bool kDpp = false, typename DescP, typename OffP>
 __device__ __forceinline__ void tx_unit(uint8_t *__restrict__ out, const uint8_t *__restrict__ src, DescP d,
                                         OffP obase, uint32_t flo, uint32_t fhi, const fws_tx_desc dA,
                                         const fws_tx_desc dB, uint64_t OA, uint64_t OB, uint64_t a0,
@@ -220,7 +225,61 @@ __device__ __forceinline__ void tx_unit(uint8_t *__restrict__ out, const uint8_t
     uint32_t sha, shb;
     tx_seam_blocks(as, SA, sA0, dA.len, safe16, qa0, qa1, sha);
     tx_seam_blocks(as, SB, sB0, two ? dB.len : 0, safe16, qb0, qb1, shb);
-    if (any_pay) {
+    uint32_t late = 0;
+    if constexpr (kDpp) {
+        const int lane = threadIdx.x & 63;
+        u32x4 last = u32x4{0u, 0u, 0u, 0u};
+        if (any_pay) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v0[j] = gload16<true>(sb[j]);
+            if (lane == 63) last = gload16<true>(((full >> 3) & 1u) && sh[3] ? sb[3] + 16u : sb[3]);
+            sa0 = gload16<false>(qa0);
+            sa1 = gload16<false>(qa1);
+            sb0 = gload16<false>(qb0);
+            sb1 = gload16<false>(qb1);
+            __builtin_amdgcn_sched_barrier(0);      // keep every load ahead of the first use
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v0[j] = u32x4{0u, 0u, 0u, 0u};
+            sa0 = sa1 = sb0 = sb1 = u32x4{0u, 0u, 0u, 0u};
+        }
+        // the next lane's A-window seam block (lane 63: lane 0's)
+        uint64_t nq = wave_shl1_64(qa0);
+        u32x4 wq = wave_shl1(sa0);
+        const uint64_t q0 = lane0_of64(qa0);
+        const u32x4 w0 = lane0_of(sa0);
+        if (lane == 63) {
+            nq = q0;
+            wq = w0;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            uint64_t nsb = wave_shl1_64(sb[j]);
+            u32x4 w1 = wave_shl1(v0[j]);
+            if (j < 3) {
+                const uint64_t n0 = lane0_of64(sb[j < 3 ? j + 1 : 0]);
+                const u32x4 x0 = lane0_of(v0[j < 3 ? j + 1 : 0]);
+                if (lane == 63) {
+                    nsb = n0;
+                    w1 = x0;
+                }
+            } else if (lane == 63) {
+                nsb = sb[3] + 16u;
+                w1 = last;
+            }
+            // lane 63's seam candidate for chunk j is lane 0's block of chunk j + 1
+            const uint64_t need = sb[j] + 16u;
+            if (nsb != need && nq == need) w1 = wq;
+            if ((full >> j) & 1u) {                  // stored here: v0[j] and w1 die
+                if (sh[j] == 0u || nsb == need || nq == need)
+                    gstore16<true>((uintptr_t)(out + a0 + (uint64_t)j * 1024u),
+                                   tx_shr_bytes(v0[j], w1, sh[j]) ^ rk[j]);
+                else
+                    late |= 1u << j;
+            }
+        }
+        full = 0;
+    } else if (any_pay) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             // default-policy loads: the second block of lane L is the first of lane
@@ -257,6 +316,7 @@ __device__ __forceinline__ void tx_unit(uint8_t *__restrict__ out, const uint8_t
         seam_chunk(as, sa0, sa1, sha, sb0, sb1, shb);
         seam &= seam - 1u;
     }
+    seam |= late;                                      // kDpp: full chunks without a neighbour block
     if (!__any(seam)) return;                          // a lane with a second seam chunk (rare)
 #pragma unroll 1
     for (int j = 0; j < 4; ++j) {
@@ -268,6 +328,7 @@ __device__ __forceinline__ void tx_unit(uint8_t *__restrict__ out, const uint8_t
     }
 }
 
+template <bool kDpp = false>
 __device__ __forceinline__ void tx_encode_body(uint8_t *__restrict__ out, const uint8_t *__restrict__ src,
                                                       const fws_tx_desc *__restrict__ d, uint32_t n,
                                                       const uint64_t *__restrict__ obase,
@@ -292,7 +353,8 @@ __device__ __forceinline__ void tx_encode_body(uint8_t *__restrict__ out, const 
         // (copies: a reference into `d` would be re-read after every store to `out`)
         const fws_tx_desc dA = d[flo], dB = d[fhi];
         const uint64_t OA = obase[flo], OB = obase[fhi];
-        tx_unit(out, src, d, obase, flo, fhi, dA, dB, OA, OB, u * kTxUnit + (uint64_t)lane * 16u, total, total);
+        tx_unit<kDpp>(out, src, d, obase, flo, fhi, dA, dB, OA, OB, u * kTxUnit + (uint64_t)lane * 16u, total,
+                      total);
     }
 }
 
@@ -408,6 +470,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     const uint64_t *__restrict__ total_ptr) {
     tx_encode_body(out, src, d, n, obase, unit_first, unit_cap, total_ptr);
 }
+// r06: one nontemporal load per full chunk (tx_unit<true>), at kW waves per SIMD
+template <int kW>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kW))) void k_tx_encode_dpp(
+    uint8_t *__restrict__ out, const uint8_t *__restrict__ src, const fws_tx_desc *__restrict__ d, uint32_t n,
+    const uint64_t *__restrict__ obase, const uint32_t *__restrict__ unit_first, uint64_t unit_cap,
+    const uint64_t *__restrict__ total_ptr) {
+    tx_encode_body<true>(out, src, d, n, obase, unit_first, unit_cap, total_ptr);
+}
 
 }  // namespace fwsk
 
@@ -421,10 +491,12 @@ extern "C" __attribute__((visibility("default"))) int fws_internal_set_tx_blocks
     return old;
 }
 
-static int g_tx_w5 = 1;  // tuning hook: 1 = k_tx_encode_w5 (default), 0 = the compiler's 4 waves
+// tuning hook: 1 = k_tx_encode_w5 (default), 0 = the compiler's 4 waves;
+// k_tx_encode_dpp at 5 / 6 / 8 waves per SIMD: 2 / 3 / 4
+static int g_tx_w5 = 1;
 extern "C" __attribute__((visibility("default"))) int fws_internal_set_tx_w5(int on) {
     const int old = g_tx_w5;
-    g_tx_w5 = on != 0;
+    g_tx_w5 = on >= 0 && on <= 4 ? on : 1;
     return old;
 }
 
@@ -500,12 +572,15 @@ int fws_gpu_encode_frames(fws_gpu_ctx *ctx, void *dev_out, uint64_t out_cap, con
     // TX batch's last 129 units to a second round of a few waves)
     if (blocks > (1u << 30)) blocks = 1u << 30;
     if (g_tx_blocks && blocks > (uint64_t)g_tx_blocks) blocks = (uint64_t)g_tx_blocks;
-    if (g_tx_w5)
-        hipLaunchKernelGGL(k_tx_encode_w5, dim3((unsigned)blocks), dim3(kBlock), 0, s, (uint8_t *)dev_out,
-                           (const uint8_t *)dev_src, dev_descs, n, ws.cbase, ws.unit_first, ws.unit_cap, ws.total);
-    else
-        hipLaunchKernelGGL(k_tx_encode, dim3((unsigned)blocks), dim3(kBlock), 0, s, (uint8_t *)dev_out,
-                           (const uint8_t *)dev_src, dev_descs, n, ws.cbase, ws.unit_first, ws.unit_cap, ws.total);
+    const void *k = g_tx_w5 == 0   ? (const void *)k_tx_encode
+                    : g_tx_w5 == 2 ? (const void *)k_tx_encode_dpp<5>
+                    : g_tx_w5 == 3 ? (const void *)k_tx_encode_dpp<6>
+                    : g_tx_w5 == 4 ? (const void *)k_tx_encode_dpp<8>
+                                   : (const void *)k_tx_encode_w5;
+    uint8_t *o = (uint8_t *)dev_out;
+    const uint8_t *sp = (const uint8_t *)dev_src;
+    void *args[] = {&o, &sp, &dev_descs, &n, &ws.cbase, &ws.unit_first, &ws.unit_cap, &ws.total};
+    if ((r = fws_hip_status(hipLaunchKernel(k, dim3((unsigned)blocks), dim3(kBlock), args, 0, s)))) return r;
     return fws_hip_status(hipGetLastError());
 }
 

@@ -14,13 +14,14 @@ from flashws_amd import _lib, gpu
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=["one", "plan", "one_w8"])
+@pytest.fixture(params=["one", "plan", "one_dpp", "one_w8", "one_w8_dpp"])
 def gather_mode(request):
-    """k_gather_one, plan + k_gather_fast, and k_gather_one_w8 (8 waves per
-    SIMD, seam chunks after the full ones) (fws_internal_set_gather_dpp)."""
+    """k_gather_one, plan + k_gather_fast, k_gather_one with one load per
+    chunk and the neighbour lane's block by DPP, and k_gather_one_w8 (8 waves
+    per SIMD, seam chunks after the full ones) (fws_internal_set_gather_dpp)."""
     L = _lib.lib()
     old = L.fws_internal_set_gather_one(0 if request.param == "plan" else 1)
-    old_dpp = L.fws_internal_set_gather_dpp(2 if request.param == "one_w8" else 0)
+    old_dpp = L.fws_internal_set_gather_dpp({"one_dpp": 1, "one_w8": 2, "one_w8_dpp": 3}.get(request.param, 0))
     yield request.param
     L.fws_internal_set_gather_one(old)
     L.fws_internal_set_gather_dpp(old_dpp)

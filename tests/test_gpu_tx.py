@@ -22,14 +22,18 @@ from test_tx_cpu import SESSIONS, frame_matches, tx_payload
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True, params=["one", "plan"])
+@pytest.fixture(autouse=True, params=["one", "plan", "plan_dpp"])
 def tx_form(request):
-    """every test runs on both forms of fws_gpu_encode_frames: one launch
-    (k_tx_one, forced for every batch) and k_out_plan + k_tx_encode"""
+    """every test runs on each form of fws_gpu_encode_frames: one launch
+    (k_tx_one, forced for every batch), k_out_plan + k_tx_encode_w5 (two
+    aligned loads per chunk) and k_out_plan + k_tx_encode_dpp (one nontemporal
+    load per chunk, the second block from the next lane)"""
     from flashws_amd._lib import lib
     old = lib().fws_internal_set_tx_one(2 if request.param == "one" else 0, 0)
+    old_w = lib().fws_internal_set_tx_w5(2 if request.param == "plan_dpp" else 1)
     yield request.param
     lib().fws_internal_set_tx_one(old, 0)
+    lib().fws_internal_set_tx_w5(old_w)
 
 
 def build_batch(payloads, metas, rng, gap_max=40):

@@ -1,9 +1,12 @@
 #!/usr/bin/env python3
 """Interleaved A/B of k_gather_one forms on BASELINE C4 (one 256 MiB message in
 1 427 fragments, 4 rotating destinations, HIP events around back-to-back
-fws_gpu_unmask_gather calls): 0 = k_gather_one (r05), 2 = k_gather_one_w8
-(8 waves per SIMD) (fws_internal_set_gather_dpp), at 512 or 256 threads per
-workgroup. Every round times each form once.
+fws_gpu_unmask_gather calls): 0 = two loads per chunk (r05), 1 = one
+nontemporal load per chunk + the neighbour lane's block by DPP, 2 =
+k_gather_one_w8 (8 waves per SIMD), 3 = 2 with 1's loads
+(fws_internal_set_gather_dpp), at 512 or 256 threads per workgroup. Every
+round times each form once. The source rotates over 4 copies (1 GiB, past the
+256 MB Infinity Cache) unless FWS_AB_ONE_SRC=1.
 usage: python tools/ab_c4.py [rounds] [steps] [dpp:threads:mult,...]"""
 import json
 import os
@@ -23,25 +26,25 @@ def main():
     dev = torch.device("cuda:0")
     w4, d4, _ = gpu.config_c4()
     c = gpu.Ctx(0, max_frames=len(d4) + 8, max_stream_bytes=len(w4))
-    src = torch.from_numpy(w4).to(dev)
+    srcs = [torch.from_numpy(w4).to(dev) for _ in range(1 if os.environ.get("FWS_AB_ONE_SRC") == "1" else 4)]
     total = int(d4["payload_len"].sum())
     alg = len(w4) + total
     dsts = [torch.empty(total + 64, dtype=torch.uint8, device=dev) for _ in range(4)]
     dd = gpu.descs_to_device(d4, dev)
     forms = [tuple(int(x) for x in f.split(":")) for f in sys.argv[3].split(",")] if len(sys.argv) > 3 else \
-        [(0, 512, 4), (2, 512, 4), (2, 256, 4)]
+        [(2, 512, 4), (3, 512, 4), (1, 512, 4), (3, 256, 4)]
     times = {f: [] for f in forms}
     for r in range(rounds):
         for f in (forms if r % 2 == 0 else forms[::-1]):
             L.fws_internal_set_gather_dpp(f[0])
             L.fws_internal_set_gather_shape(f[1], f[2])
             for i in range(10):
-                gpu.unmask_gather(c, dsts[i % 4], src, dd, len(d4))
+                gpu.unmask_gather(c, dsts[i % 4], srcs[i % len(srcs)], dd, len(d4))
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             torch.cuda.synchronize()
             e0.record()
             for i in range(steps):
-                gpu.unmask_gather(c, dsts[i % 4], src, dd, len(d4))
+                gpu.unmask_gather(c, dsts[i % 4], srcs[i % len(srcs)], dd, len(d4))
             e1.record()
             torch.cuda.synchronize()
             times[f].append(e0.elapsed_time(e1) * 1e3 / steps)

@@ -5,7 +5,10 @@ against the one-launch k_tx_one at several output spans per workgroup
 (fws_internal_set_tx_one), HIP events over back-to-back calls rotating four
 outputs, modes alternated in one process (order reversed every other
 repetition); outputs compared across modes. One JSON line per (mode, rep).
-(r04 used it for k_tx_encode grid caps, profiles/r04/ab_tx.jsonl.)
+(r04 used it for k_tx_encode grid caps, profiles/r04/ab_tx.jsonl.) r06: the
+source rotates over 4 copies (1 GiB, past the 256 MB Infinity Cache; one
+source re-read every step was served partly from it) unless FWS_AB_ONE_SRC=1;
+modes dpp5 / dpp6 / dpp8 = k_tx_encode_dpp at 5 / 6 / 8 waves per SIMD.
 
 usage: python tools/ab_tx.py [reps] [mode,mode,...]"""
 import json
@@ -30,33 +33,35 @@ def main():
     txd["len"] = pl
     txd["key"] = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
     txd["opcode"], txd["fin"], txd["masked"] = 2, 1, 1
-    tsrc = torch.from_numpy(rng.integers(0, 256, n * pl, dtype=np.uint8)).to(dev)
+    payload = rng.integers(0, 256, n * pl, dtype=np.uint8)
+    tsrcs = [torch.from_numpy(payload).to(dev) for _ in range(1 if os.environ.get("FWS_AB_ONE_SRC") == "1" else 4)]
     tdd = torch.from_numpy(txd.view(np.uint8).copy()).to(dev)
     total = n * (pl + 8)
     c = gpu.Ctx(0, max_frames=n, max_stream_bytes=total)
     outs = [torch.empty(total, dtype=torch.uint8, device=dev) for _ in range(4)]
     olen = torch.empty(1, dtype=torch.int64, device=dev)
     ref = None
-    modes = [("plan", 0, 0, 1)] + [(f"one_span{k}k", 1, k, 1) for k in (32, 64, 128, 256)]
+    modes = [("plan", 0, 0, 1), ("dpp5", 0, 0, 2), ("dpp6", 0, 0, 3), ("dpp8", 0, 0, 4), ("w4", 0, 0, 0)] + \
+        [(f"one_span{k}k", 1, k, 1) for k in (32, 64, 128, 256)]
     if len(sys.argv) > 2:
         modes = [m for m in modes if m[0] in sys.argv[2].split(",")]
     # warm the clocks before the first timed mode (tools/c4_thermal_probe.py)
     import time
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < 0.5:
-        gpu.encode_frames(c, outs[0], tsrc, tdd, n, out_len=olen)
+        gpu.encode_frames(c, outs[0], tsrcs[0], tdd, n, out_len=olen)
         torch.cuda.synchronize()
     for rep in range(3):
         for name, one, span, w in (modes if rep % 2 == 0 else modes[::-1]):
             L.fws_internal_set_tx_one(one, span)
             L.fws_internal_set_tx_w5(w)
             for i in range(4):
-                gpu.encode_frames(c, outs[i % 4], tsrc, tdd, n, out_len=olen)
+                gpu.encode_frames(c, outs[i % 4], tsrcs[i % len(tsrcs)], tdd, n, out_len=olen)
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for i in range(reps):
-                gpu.encode_frames(c, outs[i % 4], tsrc, tdd, n, out_len=olen)
+                gpu.encode_frames(c, outs[i % 4], tsrcs[i % len(tsrcs)], tdd, n, out_len=olen)
             e1.record()
             torch.cuda.synchronize()
             ms = e0.elapsed_time(e1) / reps

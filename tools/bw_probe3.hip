@@ -180,8 +180,50 @@ static void timeit(const char *name, F launch, double bytes) {
     fflush(stdout);
 }
 
+// Out of place, no shift: dst block i = src block i ^ key (nontemporal both ways)
+__global__ __launch_bounds__(256) void k_copy_xor(const u32x4 *__restrict__ src, u32x4 *__restrict__ dst, uint64_t n16,
+                                                  uint32_t key) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t wave = (uint64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t base = wave * 256;
+    u32x4 v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint64_t i = base + j * 64 + lane;
+        v[j] = __builtin_nontemporal_load((const g_u32x4 *)src + (i < n16 ? i : 0));
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint64_t i = base + j * 64 + lane;
+        if (i < n16) __builtin_nontemporal_store(v[j] ^ key, (g_u32x4 *)dst + i);
+    }
+}
+
+// r06 "oop" mode: the out-of-place forms with ONE source (re-read every step, as
+// bench.py's C4 / TX did up to r06) against FOUR rotating sources (1 GiB, past
+// the 256 MB Infinity Cache), beside the in-place XOR
+static int oop_mode(u32x4 **bufs, uint64_t bytes, uint64_t n16) {
+    u32x4 *srcs[4];
+    for (int i = 0; i < 4; ++i) { CK(hipMalloc(&srcs[i], bytes + 64)); CK(hipMemset(srcs[i], 7 + i, bytes + 64)); }
+    const double cb = 2.0 * bytes;
+    const unsigned g1 = (unsigned)((n16 / 256 + 1 + 3) / 4);
+    for (int rep = 0; rep < 2; ++rep) {
+        timeit("in-place xor (4 buffers)", [&](int i) {
+            k_xor<1, 0, 0><<<(unsigned)(((n16 + 255) / 256 + 3) / 4), 256>>>(bufs[i & 3], n16, 0x12345678u, nullptr);
+        }, cb);
+        timeit("copy xor, 1 src", [&](int i) { k_copy_xor<<<g1, 256>>>(srcs[0], bufs[i & 3], n16, 1u); }, cb);
+        timeit("copy xor, 4 src", [&](int i) { k_copy_xor<<<g1, 256>>>(srcs[i & 3], bufs[i & 3], n16, 1u); }, cb);
+        timeit("shift, 2 loads (cached), 1 src", [&](int i) { k_shift<0><<<g1, 256>>>(srcs[0], bufs[i & 3], n16, 1u); }, cb);
+        timeit("shift, 2 loads (cached), 4 src", [&](int i) { k_shift<0><<<g1, 256>>>(srcs[i & 3], bufs[i & 3], n16, 1u); }, cb);
+        timeit("shift, 1 nt load + DPP, 4 src", [&](int i) { k_shift<1><<<g1, 256>>>(srcs[i & 3], bufs[i & 3], n16, 1u); }, cb);
+        timeit("shift, 1 cached load + DPP, 4 src", [&](int i) { k_shift<2><<<g1, 256>>>(srcs[i & 3], bufs[i & 3], n16, 1u); }, cb);
+    }
+    return 0;
+}
+
 int main(int argc, char **argv) {
-    const bool quick = argc > 1;   // one variant, one repetition (counter passes)
+    const bool oop = argc > 1 && argv[1][0] == 'o';
+    const bool quick = argc > 1 && !oop;   // one variant, one repetition (counter passes)
     const uint64_t bytes = 268959744ull;
     const uint64_t n16 = bytes / 16;
     u32x4 *bufs[4];
@@ -191,6 +233,7 @@ int main(int argc, char **argv) {
     CK(hipMemset(words, 0, 4096));
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
+    if (oop) return oop_mode(bufs, bytes, n16);
     const double rw = 2.0 * bytes;
     for (int rep = 0; rep < (quick ? 1 : 2); ++rep) {
 #define X(U, DEP, ST, NAME)                                                                                    \

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """BASELINE C4 (one 256 MiB fragmented message) through fws_gpu_unmask_gather,
-repeatedly, for rocprofv3 kernel traces."""
+repeatedly, for rocprofv3 kernel traces; the source rotates over 4 copies as in
+bench.py (past the 256 MB Infinity Cache)."""
 import os
 import sys
 
@@ -14,12 +15,12 @@ def main(steps=20):
     dev = torch.device("cuda:0")
     w4, d4, _ = gpu.config_c4()
     c = gpu.Ctx(0, max_frames=len(d4) + 8, max_stream_bytes=len(w4))
-    src = torch.from_numpy(w4).to(dev)
+    srcs = [torch.from_numpy(w4).to(dev) for _ in range(4)]
     total = int(d4["payload_len"].sum())
     dsts = [torch.empty(total + 64, dtype=torch.uint8, device=dev) for _ in range(4)]
     dd = gpu.descs_to_device(d4, dev)
     for i in range(steps):
-        gpu.unmask_gather(c, dsts[i % 4], src, dd, len(d4))
+        gpu.unmask_gather(c, dsts[i % 4], srcs[i % 4], dd, len(d4))
     torch.cuda.synchronize()
     c.close()
 

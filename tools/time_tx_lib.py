@@ -18,7 +18,8 @@ from flashws_amd import gpu  # noqa: E402
 
 
 def main():
-    ctx, outs, src, dd, n, total = run_tx.setup()
+    ctx, outs, srcs, dd, n, total = run_tx.setup()
+    src = srcs[0]   # (r06: setup returns 4 rotating copies; this tool times one)
     out = {"lib": os.environ.get("FWS_LIB_VARIANT", "default")}
     for shift in (0, 3):
         d = dd.view(n, -1).clone()

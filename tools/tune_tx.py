@@ -18,7 +18,8 @@ import run_tx  # noqa: E402
 
 
 def main(steps=100):
-    ctx, outs, src, dd, n, total = run_tx.setup()
+    ctx, outs, srcs, dd, n, total = run_tx.setup()
+    src = srcs[0]   # (r06: setup returns 4 rotating copies; this tool times one)
     res, ref = {}, None
     for w5 in ((1, 0, 1, 0, 1, 0) if "--rev" in sys.argv else (0, 1, 0, 1)):
         lib().fws_internal_set_tx_w5(w5)

@@ -110,6 +110,7 @@ SIGNATURES = [
     ("fws_rx_mux_feed", _I, [_P, _P, _U32, _P]),
     ("fws_rx_mux_submit", _I, [_P, _P, _U32]),
     ("fws_rx_mux_complete", _I, [_P, _P]),
+    ("fws_rx_mux_ready", _I, [_P]),
     ("fws_gen_batch", _I, [C.POINTER(GenParams), _P, _U64, _PU64, _P, _U64, _PU64, _P]),
     ("fws_tx_next", None, [_U32, _I, C.POINTER(C.c_uint8), C.POINTER(C.c_uint8), C.POINTER(C.c_uint8)]),
     ("fws_gpu_encode_frames", _I, [_P, _P, _U64, _P, _P, _U32, _P, _P]),

@@ -847,6 +847,21 @@ int fws_rx_mux_submit(fws_rx_mux *m, const fws_rx_read *reads, uint32_t n) {
     return 0;
 }
 
+int fws_rx_mux_ready(fws_rx_mux *m) {
+    if (!m) return FWS_ERR_INVALID;
+    if (!m->inflight) return 1;
+    switch (m->wait) {
+    case fws_rx_mux::kWaitService:                   // the grid (or its teardown) sets the flag last
+    case fws_rx_mux::kWaitFlag: return __atomic_load_n(m->hflag, __ATOMIC_ACQUIRE) == m->sub_seq ? 1 : 0;
+    case fws_rx_mux::kWaitStream: {
+        const hipError_t e = hipStreamQuery(m->stream);
+        return e == hipSuccess ? 1 : (e == hipErrorNotReady ? 0 : fws_hip_status(e));
+    }
+    case fws_rx_mux::kWaitNone: break;
+    }
+    return 1;
+}
+
 int fws_rx_mux_complete(fws_rx_mux *m, fws_rx_read_result *results) {
     if (!m || !m->inflight || (!m->sub_reads.empty() && !results)) return FWS_ERR_INVALID;
     m->inflight = false;

@@ -112,6 +112,7 @@ template <class Loop>
 struct LoopAccess : Loop {
     using Loop::on_event_;
     using Loop::DeleteFd;
+    using Loop::fq_;
 };
 
 // the under-socket's readable callback member (the one InitUnderOnReadImp sets)
@@ -200,9 +201,20 @@ public:
         GpuRxHookT *self = this;
         prof_on_ = std::getenv("FWS_HOOK_PROF") != nullptr;
         if (const char *c = std::getenv("FWS_HOOK_CHUNK")) chunk_ = (uint32_t)std::strtoul(c, nullptr, 10);
+        if (const char *c = std::getenv("FWS_HOOK_DEFER")) defer_ = std::strtoul(c, nullptr, 10) != 0;
+#ifndef FWS_ENABLE_FSTACK
+        // "does the loop have events waiting?": a zero-timeout wait on the loop's own
+        // queue. epoll and poll are level-triggered here (fevent.h: no EPOLLET), so
+        // the events it sees are reported again to the next OneStep.
+        loop_ready_ = [lp]() {
+            fws::FEvent ev[1];
+            const timespec ts{0, 0};
+            return fws::FEventWait(lp->*(&LA::fq_), nullptr, 0, ev, 1, &ts) > 0;
+        };
+#endif
         loop.SetOnEventFunc([self](Loop &) {
             if (self->prof_on_) self->ProfStep(true);
-            self->Flush();
+            self->StepEnd();
             self->DeleteDeferred();
             self->app_on_event_();
             if (self->prof_on_) self->ProfStep(false);
@@ -226,6 +238,21 @@ public:
     // the previous chunk's dispatch); 0 = one batch at the end of the step.
     // Default kDefaultChunk; env FWS_HOOK_CHUNK at EnableBatched.
     void SetChunk(uint32_t reads) { chunk_ = reads; }
+
+    // Batched path, opt-in (env FWS_HOOK_DEFER=1 at EnableBatched): at the end of
+    // a step the last chunk goes to the GPU and, while it decodes, the hook asks
+    // the loop's queue for events (a zero-timeout wait); if some are waiting it
+    // returns and the chunk's events are dispatched in the next step (at its
+    // first full chunk, a read of one of its connections, or its end), so its
+    // round trip overlaps that step's reads. With nothing waiting it polls the
+    // chunk to completion and dispatches it at once, so a deferred chunk never
+    // waits on a blocking epoll. Per connection the order of events is the
+    // per-read path's; what moves is the step in which the last chunk's
+    // callbacks run (after the application's end-of-step callback of the step
+    // that read them). Not available on F-stack (the whole step is flushed).
+    void SetDeferLastChunk(bool on) { defer_ = on; }
+    bool defer_last_chunk() const { return defer_; }
+    uint64_t deferred_chunks() const { return deferred_chunks_; }
 
     size_t connections() const { return conns_.size(); }
     uint64_t gpu_reads() const { return gpu_reads_; }
@@ -463,6 +490,28 @@ private:
         while (fl_active_ || !pending_.empty()) Advance();
     }
 
+    // The end of a loop step: Flush, or (SetDeferLastChunk) the step's last
+    // chunk submitted and left in flight while the loop has events waiting.
+    void StepEnd() {
+        if (!defer_ || !loop_ready_) {
+            Flush();
+            return;
+        }
+        if (!pending_.empty()) Advance();            // the chunk before it completes and dispatches first
+        while (fl_active_) {
+            const int rd = fws_rx_mux_ready(mux_);
+            if (rd != 0) {                           // decoded (or an error, which complete reports)
+                Batch c = CompleteInflight();
+                Dispatch(c);
+                return;
+            }
+            if (loop_ready_()) {                     // reads are waiting: the next step dispatches it
+                ++deferred_chunks_;
+                return;
+            }
+        }
+    }
+
     // end-of-step callback entry (begin) and exit: the loop's own part of a step
     // is the time from one exit to the next entry
     void ProfStep(bool begin) {
@@ -601,6 +650,9 @@ private:
     Batch fl_;                                         // the submitted batch
     bool fl_active_ = false;
     uint32_t chunk_ = kDefaultChunk;                   // reads per submitted chunk within a step (0: per step)
+    bool defer_ = false;                               // SetDeferLastChunk
+    uint64_t deferred_chunks_ = 0;                     // step ends that left their last chunk in flight
+    std::function<bool()> loop_ready_;                 // the loop's queue has events (zero-timeout wait)
     std::function<void()> app_on_event_;
     std::function<void(void *)> delete_fd_;
     USock *retiring_ = nullptr;                        // Retire's flush in progress for this socket

@@ -324,6 +324,10 @@ int fws_rx_mux_feed(fws_rx_mux *m, const fws_rx_read *reads, uint32_t n, fws_rx_
  * the context's persistent receive decode waits for the batch first). */
 int fws_rx_mux_submit(fws_rx_mux *m, const fws_rx_read *reads, uint32_t n);
 int fws_rx_mux_complete(fws_rx_mux *m, fws_rx_read_result *results);
+/* Non-blocking: 1 when fws_rx_mux_complete would not wait (the submitted
+ * batch has decoded, or none is in flight), 0 while it decodes, < 0 on a HIP
+ * error. The batched hook's deferred completion polls it (gpu_floop.hpp). */
+int fws_rx_mux_ready(fws_rx_mux *m);
 
 /* ---- send path: batch frame builder -------------------
  * The bytes WSocket::SendFrame (w_socket.h:832-944) writes for one frame:

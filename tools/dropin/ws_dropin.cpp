@@ -213,11 +213,12 @@ int RunServer(const Opts &o) {
                     pf.mux_us, pf.dispatch_us, pf.step_end_us);
     }
     std::printf("{\"mode\": \"server\", \"tls\": %s, \"gpu\": %s, \"msgs\": %llu, \"bytes\": %llu, \"closes\": %d, "
-                "\"close_log_hex\": %s, \"gpu_reads\": %llu, \"gpu_batches\": %llu, \"zc_slots\": %llu}\n",
+                "\"close_log_hex\": %s, \"gpu_reads\": %llu, \"gpu_batches\": %llu, \"zc_slots\": %llu, \"deferred_chunks\": %llu}\n",
                 kTls ? "true" : "false", o.gpu ? "true" : "false", (unsigned long long)srv.msgs, (unsigned long long)srv.bytes, srv.closes,
                 log.c_str(), (unsigned long long)(hook ? hook->gpu_reads() : 0),
                 (unsigned long long)(hook ? hook->gpu_batches() : 0),
-                (unsigned long long)(hook ? hook->zero_copy_slots() : 0));
+                (unsigned long long)(hook ? hook->zero_copy_slots() : 0),
+                (unsigned long long)(hook ? hook->deferred_chunks() : 0));
     std::fflush(stdout);
     if constexpr (kTls) std::_Exit(0);        // see RunClient: no static TLS teardown
     return 0;

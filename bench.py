@@ -579,9 +579,11 @@ def c1_echo_extra(device=0):
     16,384th) against the hooked and the plain server. Host-memory path: every
     read crosses PCIe twice when hooked. `gpu_hook_batched`:
     GpuRxHook::EnableBatched, the reads of all connections of one loop step in
-    one GPU round trip. `gpu_hook_batched_deferred`: the same
-    with SetDeferLastChunk (env FWS_HOOK_DEFER=1): a step's last chunk is
-    dispatched in the next step when the loop has events waiting."""
+    one GPU round trip; since r06 a step's last chunk is
+    dispatched in the next step when the loop has events waiting
+    (SetDeferLastChunk, the default). `gpu_hook_batched_flush`: the same with
+    SetDeferLastChunk(false) (env FWS_HOOK_DEFER=0), every step's chunks
+    dispatched at its end (the r05 hook)."""
     import subprocess
     import tempfile
     dropin = os.path.join(ROOT, "oracle", "_ref", "ws_dropin")
@@ -594,8 +596,8 @@ def c1_echo_extra(device=0):
         if mode != "reference":
             args += ["--gpu-batch" if mode.startswith("gpu_hook_batched") else "--gpu", "--device", str(device)]
         env = dict(os.environ)
-        if mode == "gpu_hook_batched_deferred":
-            env["FWS_HOOK_DEFER"] = "1"          # GpuRxHook::SetDeferLastChunk (gpu_floop.hpp)
+        if mode == "gpu_hook_batched_flush":
+            env["FWS_HOOK_DEFER"] = "0"          # GpuRxHook::SetDeferLastChunk(false): every step flushed (r05)
         p = subprocess.Popen(args, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env)
         line = p.stdout.readline()
         if not line.startswith("listening"):
@@ -612,7 +614,7 @@ def c1_echo_extra(device=0):
     out = {"workload": "C1: loopback echo, 4 KiB masked BIN frames, window 1, plain ws:// on 127.0.0.1",
            "server": "reference FLoop + WSServerSocket<false> (ws_dropin); hooked = + fws_amd::GpuRxHook::Enable"}
     for clients, msgs in ((1, 20000), (8, 12000), (64, 3000)):
-        for mode in ("reference", "gpu_hook", "gpu_hook_batched", "gpu_hook_batched_deferred"):
+        for mode in ("reference", "gpu_hook", "gpu_hook_batched", "gpu_hook_batched_flush"):
             if clients == 1 and mode.startswith("gpu_hook_batched"):
                 continue                     # one read per loop step: the per-read path's round trip
             p, port = server(mode, clients)
@@ -625,7 +627,7 @@ def c1_echo_extra(device=0):
                 "goodput_rx_tx_mbps": rec.get("goodput_rx_tx_mbps"), "rtt_us": rec.get("rtt_us"),
                 "msgs_per_s": rec.get("msgs_per_s"), "verified": bool(rec.get("verified")) and r.returncode == 0,
                 "gpu_reads": st.get("gpu_reads"), "gpu_batches": st.get("gpu_batches"),
-                **({"deferred_chunks": st.get("deferred_chunks")} if mode == "gpu_hook_batched_deferred" else {})}
+                "deferred_chunks": st.get("deferred_chunks")}
     if os.path.exists(refcli):
         for hooked in (False, True):
             p, port = server("gpu_hook" if hooked else "reference", 1, port=58600)   # the reference client's port

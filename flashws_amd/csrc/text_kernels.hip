@@ -109,12 +109,31 @@ __device__ __forceinline__ void gather_bytes(uint8_t *dst, const uint8_t *src, c
     }
 }
 
+// kFlat (r06): the metadata in two scalar rounds (the total with the unit map,
+// then both regions' offsets and descriptors together -- the compiler had given
+// each its own dependent round, five per unit) and one nontemporal load per
+// chunk with the neighbour lane's block by DPP (the second block of a shifted
+// window re-read through the cache costs a second L2 request per line when the
+// source comes from HBM); region seams and the tail bytewise after the unit's
+// full chunks. tools/bw_probe3 (4 rotating sources, past the 256 MB MALL): the
+// DPP form of a shifted copy 84.0-84.6 us against 89.6-90.3 us for two loads.
+__device__ __forceinline__ fws_frame_desc frame_desc_of(const uint32_t (&w)[6]) {
+    fws_frame_desc x;
+    x.payload_off = w[0] | ((uint64_t)w[1] << 32);
+    x.payload_len = w[2] | ((uint64_t)w[3] << 32);
+    x.key = w[4];
+    x.phase = w[5];
+    return x;
+}
+
 // Requires dst 16-B aligned.
+template <bool kFlat>
 __global__ __launch_bounds__(kBlock) void k_gather_fast(uint8_t *__restrict__ dst, const uint8_t *__restrict__ src,
                                                         const fws_frame_desc *__restrict__ d, uint32_t n,
                                                         const uint64_t *__restrict__ dbase,
                                                         const uint32_t *__restrict__ unit_first, uint64_t unit_cap,
                                                         const uint64_t *__restrict__ total_ptr) {
+    static_assert(sizeof(fws_frame_desc) == 24, "6 words");
     const int lane = threadIdx.x & 63;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t nw = (uint64_t)gridDim.x * (kBlock / 64);
@@ -123,6 +142,7 @@ __global__ __launch_bounds__(kBlock) void k_gather_fast(uint8_t *__restrict__ ds
     const uint64_t uc = ufirst + 1 < unit_cap ? ufirst : (unit_cap >= 2 ? unit_cap - 2 : 0);
     uint32_t uf0 = unit_first[uc], uf1 = unit_first[uc + 1];
     const uint64_t total = *total_ptr;
+    if (kFlat) asm volatile("" ::"s"(uf0), "s"(uf1), "s"((uint32_t)total));
     const uint64_t n_units = (total + kGatherUnit - 1) / kGatherUnit;
     for (uint64_t u = ufirst; u < n_units; u += nw) {
         if (u != ufirst || u + 1 >= unit_cap) {       // past the map's capacity: searched (dbase)
@@ -153,9 +173,32 @@ __global__ __launch_bounds__(kBlock) void k_gather_fast(uint8_t *__restrict__ ds
             continue;
         }
         // at most two regions: uniform metadata
-        const uint64_t B0 = dbase[flo], B1 = dbase[flo + 1];
-        const uint64_t B2 = fhi > flo ? dbase[flo + 2] : B1;
-        const fws_frame_desc d0 = d[flo], d1 = d[fhi];
+        uint64_t B0, B1, B2;
+        fws_frame_desc d0, d1;
+        if constexpr (kFlat) {
+            const uint32_t *w0 = reinterpret_cast<const uint32_t *>(d + flo);
+            const uint32_t *w1 = reinterpret_cast<const uint32_t *>(d + fhi);
+            uint32_t r0[6], r1[6];
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                r0[i] = w0[i];
+                r1[i] = w1[i];
+            }
+            B0 = dbase[flo];
+            B1 = dbase[flo + 1];
+            const uint64_t b2 = dbase[fhi > flo ? flo + 2 : flo + 1];   // (dbase has n + 1 entries)
+            asm volatile("" ::"s"(r0[0]), "s"(r0[5]), "s"(r1[0]), "s"(r1[5]), "s"((uint32_t)B0), "s"((uint32_t)B1),
+                         "s"((uint32_t)b2));
+            B2 = b2;
+            d0 = frame_desc_of(r0);
+            d1 = frame_desc_of(r1);
+        } else {
+            B0 = dbase[flo];
+            B1 = dbase[flo + 1];
+            B2 = fhi > flo ? dbase[flo + 2] : B1;
+            d0 = d[flo];
+            d1 = d[fhi];
+        }
         const uintptr_t S0 = (uintptr_t)(src + d0.payload_off) - (uintptr_t)B0;   // src of dst byte a: S + a
         const uintptr_t S1 = (uintptr_t)(src + d1.payload_off) - (uintptr_t)B1;
         uintptr_t sb[4];
@@ -172,6 +215,41 @@ __global__ __launch_bounds__(kBlock) void k_gather_fast(uint8_t *__restrict__ ds
             sh[j] = (uint32_t)(sa & 15u);
             const uint32_t ph = in1 ? (uint32_t)(a - B1) + d1.phase : (uint32_t)(a - B0) + d0.phase;
             rk[j] = rotr32(in1 ? d1.key : d0.key, 8u * (ph & 3u));
+        }
+        if constexpr (kFlat) {
+            // one nontemporal load per chunk; the window's second block is lane L + 1's
+            // first when that is the next block (lane 63: lane 0's of the next chunk,
+            // or for the last chunk a load of its own); a full chunk without it, a
+            // region seam and the tail go bytewise after the full chunks
+            u32x4 w0[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) w0[j] = gload16<true>(sb[j]);
+            u32x4 last = u32x4{0u, 0u, 0u, 0u};
+            if (lane == 63) last = gload16<true>(full[3] && sh[3] ? sb[3] + 16u : sb[3]);
+            uint32_t pend = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint64_t a = a0 + (uint64_t)j * 1024u;
+                uint64_t nsb = wave_shl1_64(sb[j]);
+                u32x4 w1 = wave_shl1(w0[j]);
+                if (j < 3) {
+                    const uint64_t nsb0 = lane0_of64(sb[j < 3 ? j + 1 : 0]);
+                    const u32x4 nv0 = lane0_of(w0[j < 3 ? j + 1 : 0]);
+                    if (lane == 63) {
+                        nsb = nsb0;
+                        w1 = nv0;
+                    }
+                } else if (lane == 63) {
+                    nsb = sb[3] + 16u;
+                    w1 = last;
+                }
+                const bool ok = sh[j] == 0u || nsb == sb[j] + 16u;
+                if (full[j] && ok) gstore16<true>((uintptr_t)(dst + a), shr_bytes(w0[j], w1, sh[j]) ^ rk[j]);
+                else if (a < total) pend |= 1u << j;
+            }
+            for (; pend; pend &= pend - 1u)
+                gather_bytes(dst, src, d, dbase, flo, a0 + (uint64_t)__builtin_ctz(pend) * 1024u, total);
+            continue;
         }
         u32x4 v0[4], v1[4];
 #pragma unroll
@@ -427,6 +505,14 @@ using namespace fwsk;
 // tuning / test hook: 1 = k_gather_one for batches of <= kGatherLdsMax regions
 // (default), 0 = always the plan launch + k_gather_fast
 static int g_gather_one = 1;
+// tuning hook: the plan path's kernel, k_gather_fast<true> (r06 kFlat, the
+// default) or <false> (two loads per chunk, r05)
+static int g_gather_flat = 1;
+extern "C" __attribute__((visibility("default"))) int fws_internal_set_gather_flat(int on) {
+    const int old = g_gather_flat;
+    g_gather_flat = on != 0;
+    return old;
+}
 static int g_gather_blocks = 0;        // tuning: k_gather_one grid cap (0 = 4 x resident workgroups)
 extern "C" __attribute__((visibility("default"))) int fws_internal_set_gather_blocks(int blocks) {
     const int old = g_gather_blocks;
@@ -541,7 +627,8 @@ int fws_launch_gather(uint8_t *dst, const uint8_t *src, const fws_frame_desc *d,
     // TX batch's last 129 units to a second round of a few waves)
     if (blocks > (1u << 30)) blocks = 1u << 30;
     if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL(k_gather_fast, dim3((unsigned)blocks), dim3(kBlock), 0, s, dst, src, d, n, ws.cbase,
+    hipLaunchKernelGGL(g_gather_flat ? k_gather_fast<true> : k_gather_fast<false>, dim3((unsigned)blocks),
+                       dim3(kBlock), 0, s, dst, src, d, n, ws.cbase,
                        ws.unit_first, ws.unit_cap, ws.total);
     return fws_hip_status(hipGetLastError());
 }

@@ -328,6 +328,19 @@ __device__ __forceinline__ void tx_unit(uint8_t *__restrict__ out, const uint8_t
     }
 }
 
+// fws_tx_desc from its six words (include/fws_gpu.h layout)
+__device__ __forceinline__ fws_tx_desc tx_desc_of(const uint32_t (&w)[6]) {
+    fws_tx_desc x;
+    x.src_off = w[0] | ((uint64_t)w[1] << 32);
+    x.len = w[2] | ((uint64_t)w[3] << 32);
+    x.key = w[4];
+    x.opcode = (uint8_t)w[5];
+    x.fin = (uint8_t)(w[5] >> 8);
+    x.masked = (uint8_t)(w[5] >> 16);
+    x.pad = (uint8_t)(w[5] >> 24);
+    return x;
+}
+
 template <bool kDpp = false>
 __device__ __forceinline__ void tx_encode_body(uint8_t *__restrict__ out, const uint8_t *__restrict__ src,
                                                       const fws_tx_desc *__restrict__ d, uint32_t n,
@@ -342,6 +355,9 @@ __device__ __forceinline__ void tx_encode_body(uint8_t *__restrict__ out, const 
     const uint64_t uc = ufirst + 1 < unit_cap ? ufirst : (unit_cap >= 2 ? unit_cap - 2 : 0);
     uint32_t uf0 = unit_first[uc], uf1 = unit_first[uc + 1];
     const uint64_t total = *total_ptr;
+    // (issued together, one wait: the loop test on total had the map loads wait
+    // for it in a round of their own)
+    asm volatile("" ::"s"(uf0), "s"(uf1), "s"((uint32_t)total));
     const uint64_t n_units = (total + kTxUnit - 1) / kTxUnit;
     for (uint64_t u = ufirst; u < n_units; u += nw) {
         if (u != ufirst || u + 1 >= unit_cap) {       // past the map's capacity: searched (obase)
@@ -351,8 +367,23 @@ __device__ __forceinline__ void tx_encode_body(uint8_t *__restrict__ out, const 
         const uint32_t flo = uf0;
         const uint32_t fhi = (u + 1 < n_units) ? uf1 : n - 1;
         // (copies: a reference into `d` would be re-read after every store to `out`)
-        const fws_tx_desc dA = d[flo], dB = d[fhi];
+        // r06: both descriptors and both offsets as raw words in one scalar round,
+        // fields unpacked after it -- loaded as structs, the byte-field unpacking of
+        // d[flo] was scheduled before d[fhi]'s loads and the offsets', three
+        // dependent rounds per unit, each a full memory latency while HBM is busy
+        const uint32_t *wa = reinterpret_cast<const uint32_t *>(d + flo);
+        const uint32_t *wb = reinterpret_cast<const uint32_t *>(d + fhi);
+        uint32_t ra[6], rb[6];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            ra[i] = wa[i];
+            rb[i] = wb[i];
+        }
         const uint64_t OA = obase[flo], OB = obase[fhi];
+        // (all four issued, then one wait: an empty asm that takes a word of each --
+        // a sched_barrier alone left the loads sunk into the two-frame branch)
+        asm volatile("" ::"s"(ra[0]), "s"(ra[5]), "s"(rb[0]), "s"(rb[5]), "s"((uint32_t)OA), "s"((uint32_t)OB));
+        const fws_tx_desc dA = tx_desc_of(ra), dB = tx_desc_of(rb);
         tx_unit<kDpp>(out, src, d, obase, flo, fhi, dA, dB, OA, OB, u * kTxUnit + (uint64_t)lane * 16u, total,
                       total);
     }

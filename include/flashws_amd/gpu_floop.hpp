@@ -239,7 +239,8 @@ public:
     // Default kDefaultChunk; env FWS_HOOK_CHUNK at EnableBatched.
     void SetChunk(uint32_t reads) { chunk_ = reads; }
 
-    // Batched path, opt-in (env FWS_HOOK_DEFER=1 at EnableBatched): at the end of
+    // Batched path, on by default (off: SetDeferLastChunk(false) or env
+    // FWS_HOOK_DEFER=0 at EnableBatched): at the end of
     // a step the last chunk goes to the GPU and, while it decodes, the hook asks
     // the loop's queue for events (a zero-timeout wait); if some are waiting it
     // returns and the chunk's events are dispatched in the next step (at its
@@ -650,7 +651,7 @@ private:
     Batch fl_;                                         // the submitted batch
     bool fl_active_ = false;
     uint32_t chunk_ = kDefaultChunk;                   // reads per submitted chunk within a step (0: per step)
-    bool defer_ = false;                               // SetDeferLastChunk
+    bool defer_ = true;                                // SetDeferLastChunk
     uint64_t deferred_chunks_ = 0;                     // step ends that left their last chunk in flight
     std::function<bool()> loop_ready_;                 // the loop's queue has events (zero-timeout wait)
     std::function<void()> app_on_event_;

@@ -142,21 +142,22 @@ def _run_all(gpu, tls=False, batch=False):
 
 
 def _hook_env(chunk, monkeypatch):
-    """chunk: None (default chunks), an int (FWS_HOOK_CHUNK: the batched hook's
-    reads go to the GPU in chunks of this many) or "defer" (FWS_HOOK_DEFER:
-    SetDeferLastChunk, a step's last chunk dispatched in the next step while the
-    loop has events waiting)"""
-    if chunk == "defer":
-        monkeypatch.setenv("FWS_HOOK_DEFER", "1")
+    """chunk: None (default chunks; the step's last chunk deferred to the next
+    step while the loop has events waiting, SetDeferLastChunk's default), an int
+    (FWS_HOOK_CHUNK: the batched hook's reads go to the GPU in chunks of this
+    many) or "flush" (FWS_HOOK_DEFER=0: every step's chunks dispatched at its
+    end, the r05 hook)"""
+    if chunk == "flush":
+        monkeypatch.setenv("FWS_HOOK_DEFER", "0")
     elif chunk is not None:
         monkeypatch.setenv("FWS_HOOK_CHUNK", str(chunk))
 
 
 @pytest.mark.parametrize("tls,batch,chunk", [(False, False, None), (True, False, None), (False, True, None),
                                              (True, True, None), (False, True, 1), (True, True, 2),
-                                             (False, True, "defer"), (True, True, "defer")],
+                                             (False, True, "flush"), (True, True, "flush")],
                          ids=["ws", "wss", "ws_batched", "wss_batched", "ws_batched_chunk1", "wss_batched_chunk2",
-                              "ws_batched_defer", "wss_batched_defer"])
+                              "ws_batched_flush", "wss_batched_flush"])
 def test_dropin_scripted_parity_with_reference_server(cuda, tls, batch, chunk, monkeypatch):
     """Scripted sessions (split reads, PING, fragmented messages, protocol
     errors, CLOSE) against the reference server and the hooked one, per read
@@ -189,8 +190,8 @@ def test_dropin_scripted_parity_with_reference_server(cuda, tls, batch, chunk, m
     (16, 512, False, False, None), (8, 4096, True, False, None), (2, 70000, True, False, None),
     (8, 4096, False, True, None), (4, 70000, False, True, None), (16, 512, False, True, None),
     (8, 4096, True, True, None), (16, 512, False, True, 3), (8, 70000, False, True, 2), (8, 4096, True, True, 2),
-    (8, 4096, False, True, "defer"), (16, 512, False, True, "defer"), (4, 70000, False, True, "defer"),
-    (8, 4096, True, True, "defer")])
+    (8, 4096, False, True, "flush"), (16, 512, False, True, "flush"), (4, 70000, False, True, "flush"),
+    (8, 4096, True, True, "flush")])
 def test_dropin_reference_client_load(cuda, clients, msg_len, tls, batch, chunk, monkeypatch):
     _hook_env(chunk, monkeypatch)
     srv = Server(True, conns=clients, tls=tls, batch=batch)
@@ -207,8 +208,8 @@ def test_dropin_reference_client_load(cuda, clients, msg_len, tls, batch, chunk,
     assert all(c == [1000, b"bye".hex()] for c in st["close_log_hex"][:clients])
     if batch:                       # the step's reads went to the GPU together
         assert 0 < st["gpu_batches"] <= st["gpu_reads"]
-    if chunk == "defer":            # (how many step ends deferred depends on timing; counted, not asserted)
-        assert st["deferred_chunks"] >= 0
+    if chunk == "flush":            # SetDeferLastChunk(false): no step end leaves a chunk in flight
+        assert st["deferred_chunks"] == 0
 
 
 REF_CLIENTS = {n: os.path.join(ROOT, "oracle", "_ref", f"ws_ref_client_{n}") for n in (1, 8)}
@@ -292,7 +293,7 @@ def test_reference_echo_server_unchanged_with_gpu_hook(cuda, n_clients, tmp_path
 
 
 @pytest.mark.parametrize("scenario", ["close_peers", "eof_with_data"])
-@pytest.mark.parametrize("mode", ["gpu", "gpu_batch", "gpu_batch_chunk1", "gpu_batch_defer"])
+@pytest.mark.parametrize("mode", ["gpu", "gpu_batch", "gpu_batch_chunk1", "gpu_batch_flush"])
 def test_dropin_same_step_reads_match_reference(cuda, scenario, mode, monkeypatch):
     """Two reads in one FLoop step (tests/dropin_steps.py): (close_peers) A's
     on_read closes connection B while B's read of the same step is still to be
@@ -307,8 +308,8 @@ def test_dropin_same_step_reads_match_reference(cuda, scenario, mode, monkeypatc
     if mode == "gpu_batch_chunk1":  # every read submitted as it arrives, dispatched at the next one
         monkeypatch.setenv("FWS_HOOK_CHUNK", "1")
         mode = "gpu_batch"
-    elif mode == "gpu_batch_defer":  # the step's last chunk dispatched in the next step (SetDeferLastChunk)
-        monkeypatch.setenv("FWS_HOOK_DEFER", "1")
+    elif mode == "gpu_batch_flush":  # every step flushed at its end (SetDeferLastChunk(false))
+        monkeypatch.setenv("FWS_HOOK_DEFER", "0")
         mode = "gpu_batch"
     got = dropin_steps.run_scenario(DROPIN, mode, scenario)
     assert got["server"]["gpu_reads"] > 0

@@ -14,16 +14,19 @@ from flashws_amd import _lib, gpu
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=["one", "plan", "one_dpp", "one_w8", "one_w8_dpp"])
+@pytest.fixture(params=["one", "plan", "plan_r05", "one_dpp", "one_w8", "one_w8_dpp"])
 def gather_mode(request):
-    """k_gather_one, plan + k_gather_fast, k_gather_one with one load per
-    chunk and the neighbour lane's block by DPP, and k_gather_one_w8 (8 waves
+    """k_gather_one, plan + k_gather_fast (r06 kFlat: one load per chunk and
+    the neighbour lane's block by DPP; plan_r05: two loads per chunk),
+    k_gather_one with one load per chunk + DPP, and k_gather_one_w8 (8 waves
     per SIMD, seam chunks after the full ones) (fws_internal_set_gather_dpp)."""
     L = _lib.lib()
-    old = L.fws_internal_set_gather_one(0 if request.param == "plan" else 1)
+    old = L.fws_internal_set_gather_one(0 if request.param.startswith("plan") else 1)
+    old_flat = L.fws_internal_set_gather_flat(0 if request.param == "plan_r05" else 1)
     old_dpp = L.fws_internal_set_gather_dpp({"one_dpp": 1, "one_w8": 2, "one_w8_dpp": 3}.get(request.param, 0))
     yield request.param
     L.fws_internal_set_gather_one(old)
+    L.fws_internal_set_gather_flat(old_flat)
     L.fws_internal_set_gather_dpp(old_dpp)
 
 

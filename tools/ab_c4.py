@@ -4,7 +4,9 @@
 fws_gpu_unmask_gather calls): 0 = two loads per chunk (r05), 1 = one
 nontemporal load per chunk + the neighbour lane's block by DPP, 2 =
 k_gather_one_w8 (8 waves per SIMD), 3 = 2 with 1's loads
-(fws_internal_set_gather_dpp), at 512 or 256 threads per workgroup. Every
+(fws_internal_set_gather_dpp), at 512 or 256 threads per workgroup; -1 =
+the plan launch + k_gather_fast<kFlat> (one wave per unit, fws_internal_set_gather_one(0));
+-2 = the same with k_gather_fast's two-load form (fws_internal_set_gather_flat(0)). Every
 round times each form once. The source rotates over 4 copies (1 GiB, past the
 256 MB Infinity Cache) unless FWS_AB_ONE_SRC=1.
 usage: python tools/ab_c4.py [rounds] [steps] [dpp:threads:mult,...]"""
@@ -36,7 +38,9 @@ def main():
     times = {f: [] for f in forms}
     for r in range(rounds):
         for f in (forms if r % 2 == 0 else forms[::-1]):
-            L.fws_internal_set_gather_dpp(f[0])
+            L.fws_internal_set_gather_one(0 if f[0] < 0 else 1)   # dpp -1: plan launch + k_gather_fast
+            L.fws_internal_set_gather_flat(0 if f[0] == -2 else 1)   # -2: its r05 two-load form
+            L.fws_internal_set_gather_dpp(max(f[0], 0))
             L.fws_internal_set_gather_shape(f[1], f[2])
             for i in range(10):
                 gpu.unmask_gather(c, dsts[i % 4], srcs[i % len(srcs)], dd, len(d4))
@@ -48,6 +52,8 @@ def main():
             e1.record()
             torch.cuda.synchronize()
             times[f].append(e0.elapsed_time(e1) * 1e3 / steps)
+    L.fws_internal_set_gather_one(1)
+    L.fws_internal_set_gather_flat(1)
     L.fws_internal_set_gather_dpp(2)
     L.fws_internal_set_gather_shape(0, 0)
     for f in forms:

@@ -109,6 +109,64 @@ __device__ __forceinline__ void gather_bytes(uint8_t *dst, const uint8_t *src, c
     }
 }
 
+// Byte-select mask of the chunk's bytes [lo, hi) (offsets 0..16) for dword i
+__device__ __forceinline__ uint32_t chunk_sel(uint32_t lo, uint32_t hi, int i) {
+    const uint32_t o = 4u * (uint32_t)i;
+    if (hi <= o || lo >= o + 4u) return 0u;
+    const uint32_t s = lo > o ? lo - o : 0u, e = hi < o + 4u ? o + 4u - hi : 0u;
+    return (0xFFFFFFFFu << (8u * s)) & (0xFFFFFFFFu >> (8u * e));
+}
+__device__ __forceinline__ uint32_t chunk_rel(uint64_t x, uint64_t a) {   // x clipped to [a, a + 16), from a
+    return x <= a ? 0u : (x >= a + 16u ? 16u : (uint32_t)(x - a));
+}
+
+// dst chunk [a, min(a + 16, total)) of a unit whose regions flo (dst [B0, B1)) and
+// fhi (from B1 to B2; two = fhi > flo) cover it, in registers (r06): each
+// region's keyed 16-B source window (two aligned loads, a block outside the
+// region's source bytes replaced by the region's first block), bytes selected
+// per region. The chunks at region seams and the output's end took a
+// per-byte loop with three dependent loads per byte (gather_bytes: ~48 round
+// trips on the one lane of the wave that had one). Returns false (nothing
+// written) when a third region meets the chunk.
+__device__ __forceinline__ bool gather_seam(uint8_t *dst, const uint8_t *src, uint64_t a, uint64_t total,
+                                            const fws_frame_desc &d0, const fws_frame_desc &d1, uint64_t B0,
+                                            uint64_t B1, uint64_t B2, bool two) {
+    const uint64_t end = two ? B2 : B1;
+    if ((a + 16u < total ? a + 16u : total) > end) return false;
+    u32x4 w[2];
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+        const fws_frame_desc &fd = r ? d1 : d0;
+        const uint64_t Br = r ? B1 : B0;
+        const uintptr_t s0 = (uintptr_t)(src + fd.payload_off);
+        const uintptr_t sa = s0 + (uintptr_t)(a - Br);   // (a < Br: wraps like the offsets it mirrors)
+        const uintptr_t safe = s0 & ~uintptr_t(15);
+        uintptr_t b0 = sa & ~uintptr_t(15), b1 = b0 + 16u;
+        const bool use = fd.payload_len != 0 && (r == 0 || two);
+        if (!use || b0 + 16u <= s0 || b0 >= s0 + fd.payload_len) b0 = safe;
+        if (!use || b1 + 16u <= s0 || b1 >= s0 + fd.payload_len) b1 = safe;
+        u32x4 v0{0u, 0u, 0u, 0u}, v1{0u, 0u, 0u, 0u};
+        if (use) {
+            v0 = gload16<true>(b0);
+            v1 = gload16<true>(b1);
+        }
+        const uint32_t rk = rotr32(fd.key, 8u * ((uint32_t)(a - Br + fd.phase) & 3u));
+        w[r] = shr_bytes(v0, v1, (uint32_t)(sa & 15u)) ^ rk;
+    }
+    const uint32_t t = chunk_rel(total, a), e0 = chunk_rel(B1, a), e1 = chunk_rel(end, a);
+    const uint32_t wa[4] = {w[0].x, w[0].y, w[0].z, w[0].w}, wb[4] = {w[1].x, w[1].y, w[1].z, w[1].w};
+    uint32_t x[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        x[i] = chunk_sel(0u, t, i) & ((wa[i] & chunk_sel(0u, e0, i)) | (two ? wb[i] & chunk_sel(e0, e1, i) : 0u));
+    if (a + 16u <= total) {
+        gstore16<true>((uintptr_t)(dst + a), u32x4{x[0], x[1], x[2], x[3]});
+    } else {
+        for (uint64_t b = a; b < total; ++b) dst[b] = (uint8_t)(x[(b - a) >> 2] >> (8u * ((b - a) & 3u)));
+    }
+    return true;
+}
+
 // kFlat (r06): the metadata in two scalar rounds (the total with the unit map,
 // then both regions' offsets and descriptors together -- the compiler had given
 // each its own dependent round, five per unit) and one nontemporal load per
@@ -247,8 +305,11 @@ __global__ __launch_bounds__(kBlock) void k_gather_fast(uint8_t *__restrict__ ds
                 if (full[j] && ok) gstore16<true>((uintptr_t)(dst + a), shr_bytes(w0[j], w1, sh[j]) ^ rk[j]);
                 else if (a < total) pend |= 1u << j;
             }
-            for (; pend; pend &= pend - 1u)
-                gather_bytes(dst, src, d, dbase, flo, a0 + (uint64_t)__builtin_ctz(pend) * 1024u, total);
+            for (; pend; pend &= pend - 1u) {
+                const uint64_t a = a0 + (uint64_t)__builtin_ctz(pend) * 1024u;
+                if (!gather_seam(dst, src, a, total, d0, d1, B0, B1, B2, fhi > flo))
+                    gather_bytes(dst, src, d, dbase, flo, a, total);
+            }
             continue;
         }
         u32x4 v0[4], v1[4];
@@ -502,9 +563,14 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(8))) void k_
 
 using namespace fwsk;
 
-// tuning / test hook: 1 = k_gather_one for batches of <= kGatherLdsMax regions
-// (default), 0 = always the plan launch + k_gather_fast
-static int g_gather_one = 1;
+// tuning / test hook: 1 = k_gather_one for batches of <= kGatherLdsMax regions,
+// 0 = always the plan launch + k_gather_fast (the default since r06: with the
+// source past the 256 MB MALL, plan + k_gather_fast<kFlat> 93.4-93.6 us on C4
+// against 99.7-99.9 us for k_gather_one_w8, whose grid-stride loop waits for a
+// unit's stores before the next unit's loads -- the compiler's vmcnt(0) at the
+// loop head -- profiles/r06/ab_c4_flat_seam.jsonl; r04-r05 measured the
+// opposite order with one source re-read every step, partly from the MALL)
+static int g_gather_one = 0;
 // tuning hook: the plan path's kernel, k_gather_fast<true> (r06 kFlat, the
 // default) or <false> (two loads per chunk, r05)
 static int g_gather_flat = 1;

@@ -170,7 +170,17 @@ __device__ __forceinline__ void tx_store_tail(uint8_t *out, uint64_t a, uint64_t
 // or for the last chunk a load of its own) or the next lane's A-window seam
 // block (the left neighbour of a seam chunk). A full chunk with neither (rare:
 // the chunk before the batch's last) is built by the seam path afterwards.
-template <bool kDpp = false, typename DescP, typename OffP>
+// kLate (r06, with kDpp): no seam window preloaded with the full chunks -- every
+// seam chunk (and a full chunk whose neighbour block belongs to a seam lane)
+// loads its windows after the unit's full chunks are stored, when their data
+// registers are dead: fewer live registers (8 waves per SIMD) for a second load
+// round on the seam lanes only.
+// kSeamsOut (r06): the unit writes its full chunks only; every chunk that meets
+// a frame header or the output's end (the seam chunks) is k_tx_seams's, one
+// lane per frame after this kernel (a unit's seam chunk cost the whole wave the
+// window loads and the byte-select VALU: 30 M of the kernel's 51 M VALU
+// instructions on the C2 TX shape, profiles/r06/pmc_tx_c4_4src.txt).
+template <bool kDpp = false, bool kLate = false, bool kSeamsOut = false, typename DescP, typename OffP>
 __device__ __forceinline__ void tx_unit(uint8_t *__restrict__ out, const uint8_t *__restrict__ src, DescP d,
                                         OffP obase, uint32_t flo, uint32_t fhi, const fws_tx_desc dA,
                                         const fws_tx_desc dB, uint64_t OA, uint64_t OB, uint64_t a0,
@@ -207,7 +217,7 @@ __device__ __forceinline__ void tx_unit(uint8_t *__restrict__ out, const uint8_t
         const bool inA = own && whole && a >= z.PA && a + 16 <= z.EA;
         const bool inB = own && whole && two && a >= z.PB && a + 16 <= z.EB;
         if (inA || inB) full |= 1u << j;
-        else if (own && a < total) seam |= 1u << j;
+        else if (!kSeamsOut && own && a < total) seam |= 1u << j;
         const uintptr_t sa = (inB ? SB : SA) + (uintptr_t)a;
         sb[j] = (inA || inB) ? (sa & ~uintptr_t(15)) : safe16;
         sh[j] = (uint32_t)(sa & 15u);
@@ -233,10 +243,15 @@ __device__ __forceinline__ void tx_unit(uint8_t *__restrict__ out, const uint8_t
 #pragma unroll
             for (int j = 0; j < 4; ++j) v0[j] = gload16<true>(sb[j]);
             if (lane == 63) last = gload16<true>(((full >> 3) & 1u) && sh[3] ? sb[3] + 16u : sb[3]);
-            sa0 = gload16<false>(qa0);
-            sa1 = gload16<false>(qa1);
-            sb0 = gload16<false>(qb0);
-            sb1 = gload16<false>(qb1);
+            if constexpr (kLate || kSeamsOut) {
+                sa0 = sa1 = sb0 = sb1 = u32x4{0u, 0u, 0u, 0u};
+                qa0 = 1;                               // no lane's block: the A-window hand-over is off
+            } else {
+                sa0 = gload16<false>(qa0);
+                sa1 = gload16<false>(qa1);
+                sb0 = gload16<false>(qb0);
+                sb1 = gload16<false>(qb1);
+            }
             __builtin_amdgcn_sched_barrier(0);      // keep every load ahead of the first use
         } else {
 #pragma unroll
@@ -289,10 +304,14 @@ __device__ __forceinline__ void tx_unit(uint8_t *__restrict__ out, const uint8_t
             v0[j] = gload16<false>(sb[j]);          // (a copy would wait for the load)
             v1[j] = gload16<false>(s1);
         }
-        sa0 = gload16<false>(qa0);
-        sa1 = gload16<false>(qa1);
-        sb0 = gload16<false>(qb0);
-        sb1 = gload16<false>(qb1);
+        if constexpr (kSeamsOut) {
+            sa0 = sa1 = sb0 = sb1 = u32x4{0u, 0u, 0u, 0u};
+        } else {
+            sa0 = gload16<false>(qa0);
+            sa1 = gload16<false>(qa1);
+            sb0 = gload16<false>(qb0);
+            sb1 = gload16<false>(qb1);
+        }
         __builtin_amdgcn_sched_barrier(0);          // keep every load ahead of the first use
     } else {
 #pragma unroll
@@ -312,7 +331,10 @@ __device__ __forceinline__ void tx_unit(uint8_t *__restrict__ out, const uint8_t
         if (a + 16u <= total) gstore16<true>((uintptr_t)(out + a), x);
         else tx_store_tail(out, a, total, x);
     };
-    if (seam) {
+#ifdef FWS_TX_ABL_SEAM
+    return;                                            // ablation build only: no seam chunks (wrong bytes)
+#endif
+    if (!kLate && seam) {
         seam_chunk(as, sa0, sa1, sha, sb0, sb1, shb);
         seam &= seam - 1u;
     }
@@ -341,7 +363,7 @@ __device__ __forceinline__ fws_tx_desc tx_desc_of(const uint32_t (&w)[6]) {
     return x;
 }
 
-template <bool kDpp = false>
+template <bool kDpp = false, bool kLate = false, bool kSeamsOut = false>
 __device__ __forceinline__ void tx_encode_body(uint8_t *__restrict__ out, const uint8_t *__restrict__ src,
                                                       const fws_tx_desc *__restrict__ d, uint32_t n,
                                                       const uint64_t *__restrict__ obase,
@@ -384,7 +406,7 @@ __device__ __forceinline__ void tx_encode_body(uint8_t *__restrict__ out, const 
         // a sched_barrier alone left the loads sunk into the two-frame branch)
         asm volatile("" ::"s"(ra[0]), "s"(ra[5]), "s"(rb[0]), "s"(rb[5]), "s"((uint32_t)OA), "s"((uint32_t)OB));
         const fws_tx_desc dA = tx_desc_of(ra), dB = tx_desc_of(rb);
-        tx_unit<kDpp>(out, src, d, obase, flo, fhi, dA, dB, OA, OB, u * kTxUnit + (uint64_t)lane * 16u, total,
+        tx_unit<kDpp, kLate, kSeamsOut>(out, src, d, obase, flo, fhi, dA, dB, OA, OB, u * kTxUnit + (uint64_t)lane * 16u, total,
                       total);
     }
 }
@@ -509,6 +531,102 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kW))) vo
     const uint64_t *__restrict__ total_ptr) {
     tx_encode_body<true>(out, src, d, n, obase, unit_first, unit_cap, total_ptr);
 }
+// r06: the DPP form with late seam windows (tx_unit<true, true>) at kW waves per SIMD
+template <int kW>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kW))) void k_tx_encode_late(
+    uint8_t *__restrict__ out, const uint8_t *__restrict__ src, const fws_tx_desc *__restrict__ d, uint32_t n,
+    const uint64_t *__restrict__ obase, const uint32_t *__restrict__ unit_first, uint64_t unit_cap,
+    const uint64_t *__restrict__ total_ptr) {
+    tx_encode_body<true, true>(out, src, d, n, obase, unit_first, unit_cap, total_ptr);
+}
+// r06: full chunks only (kSeamsOut; the seam chunks are k_tx_seams's), the
+// two-load form (kDpp false) or one load + DPP, at kW waves per SIMD
+template <bool kDpp, int kW>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kW))) void k_tx_encode_so(
+    uint8_t *__restrict__ out, const uint8_t *__restrict__ src, const fws_tx_desc *__restrict__ d, uint32_t n,
+    const uint64_t *__restrict__ obase, const uint32_t *__restrict__ unit_first, uint64_t unit_cap,
+    const uint64_t *__restrict__ total_ptr) {
+    tx_encode_body<kDpp, false, true>(out, src, d, n, obase, unit_first, unit_cap, total_ptr);
+}
+
+// The seam chunks of a batch (k_tx_encode_so wrote the rest): one thread per
+// frame f builds the 16-B output chunks that meet its header [OB, OB + hB) and
+// that no earlier frame's header meets (so every chunk has one writer), from
+// frame f - 1's payload tail, the header and frame f's payload head -- its
+// keyed source windows loaded once, bytes selected in registers (the
+// tx_seam_combine of the unit walk); a chunk reaching past frame f's payload
+// into frame f + 1 (frames under 16 B) goes bytewise. The last frame's thread
+// also writes the output's last chunk when it ends inside a payload. Nothing
+// is written when the plan's total is 0 (the batch exceeds out_cap).
+__global__ __launch_bounds__(kBlock) void k_tx_seams(uint8_t *__restrict__ out, const uint8_t *__restrict__ src,
+                                                     const fws_tx_desc *__restrict__ d, uint32_t n,
+                                                     const uint64_t *__restrict__ obase,
+                                                     const uint64_t *__restrict__ total_ptr) {
+    const uint32_t f = blockIdx.x * kBlock + threadIdx.x;
+    const uint64_t total = *total_ptr;
+    if (f >= n || total == 0) return;
+    const bool hasA = f > 0;
+    const fws_tx_desc dB = d[f];
+    const uint64_t OB = obase[f];
+    fws_tx_desc dA = dB;
+    uint64_t OA = OB;
+    if (hasA) {
+        dA = d[f - 1];
+        OA = obase[f - 1];
+    }
+    const uint32_t hA = tx_hdr_len(dA), hB = tx_hdr_len(dB);
+    TxSeam z;
+    z.PA = OA + hA;
+    z.EA = z.PA + dA.len;
+    z.PB = OB + hB;
+    z.EB = z.PB + dB.len;
+    const uintptr_t sA0 = (uintptr_t)(src + dA.src_off), sB0 = (uintptr_t)(src + dB.src_off);
+    const uintptr_t SA = sA0 - (uintptr_t)z.PA, SB = sB0 - (uintptr_t)z.PB;
+    const bool payA = hasA && dA.len != 0, payB = dB.len != 0;
+    const uintptr_t safe16 = (payB ? sB0 : sA0) & ~uintptr_t(15);
+    auto chunk = [&](uint64_t c) {
+        const uint64_t ce = c + 16u < total ? c + 16u : total;
+        if (ce > z.EB) {                               // meets frame f + 1 too: bytewise
+            tx_bytes(out, src, d, obase, c < OB ? f - 1u : f, c, total);
+            return;
+        }
+        u32x4 pA{0u, 0u, 0u, 0u}, pB{0u, 0u, 0u, 0u};
+        uintptr_t b0, b1;
+        uint32_t sh;
+        if (payA && c < z.EA) {
+            tx_seam_blocks(c, SA, sA0, dA.len, safe16, b0, b1, sh);
+            const uint32_t rk = dA.masked ? rotr32(dA.key, 8u * ((uint32_t)(c - z.PA) & 3u)) : 0u;
+            pA = tx_shr_bytes(gload16<true>(b0), gload16<true>(b1), sh) ^ rk;
+        }
+        if (payB && ce > z.PB) {
+            tx_seam_blocks(c, SB, sB0, dB.len, safe16, b0, b1, sh);
+            const uint32_t rk = dB.masked ? rotr32(dB.key, 8u * ((uint32_t)(c - z.PB) & 3u)) : 0u;
+            pB = tx_shr_bytes(gload16<true>(b0), gload16<true>(b1), sh) ^ rk;
+        }
+        // (frame 0: A is B itself, one frame)
+        const u32x4 x = hasA ? tx_seam_combine(c, dA, OA, dB, OB, true, z, total, pA, pB)
+                             : tx_seam_combine(c, dB, OB, dB, OB, false, TxSeam{z.PB, z.EB, z.PB, z.EB}, total, pB,
+                                               pB);
+        if (c + 16u <= total) gstore16<true>((uintptr_t)(out + c), x);
+        else tx_store_tail(out, c, total, x);
+    };
+    const uint64_t c0 = OB & ~uint64_t(15), c1 = (OB + hB - 1u) & ~uint64_t(15);
+    for (uint64_t c = c0; c <= c1 && c < total; c += 16u)
+        if (!hasA || OA + hA <= c) chunk(c);           // else frame f - 1's header meets it: its chunk
+    if (f == n - 1u && (total & 15u) != 0u) {          // the output's last chunk, when no header meets it
+        const uint64_t ct = (total - 1u) & ~uint64_t(15);
+        if (ct > c1) chunk(ct);
+    }
+}
+
+// r06: the two-load form at kW waves per SIMD (A/B)
+template <int kW>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kW))) void k_tx_encode_wn(
+    uint8_t *__restrict__ out, const uint8_t *__restrict__ src, const fws_tx_desc *__restrict__ d, uint32_t n,
+    const uint64_t *__restrict__ obase, const uint32_t *__restrict__ unit_first, uint64_t unit_cap,
+    const uint64_t *__restrict__ total_ptr) {
+    tx_encode_body<false>(out, src, d, n, obase, unit_first, unit_cap, total_ptr);
+}
 
 }  // namespace fwsk
 
@@ -523,11 +641,14 @@ extern "C" __attribute__((visibility("default"))) int fws_internal_set_tx_blocks
 }
 
 // tuning hook: 1 = k_tx_encode_w5 (default), 0 = the compiler's 4 waves;
-// k_tx_encode_dpp at 5 / 6 / 8 waves per SIMD: 2 / 3 / 4
+// k_tx_encode_dpp at 5 / 6 / 8 waves per SIMD: 2 / 3 / 4; the two-load form
+// at 6 / 7 waves: 5 / 6; k_tx_encode_dpp at 7: 7; k_tx_encode_late at 8 / 6: 8 / 9;
+// full chunks only + k_tx_seams (k_tx_encode_so): two loads at 5 / 6 / 8 waves 10 / 11 / 12,
+// one load + DPP at 5 / 6 / 8 waves 13 / 14 / 15
 static int g_tx_w5 = 1;
 extern "C" __attribute__((visibility("default"))) int fws_internal_set_tx_w5(int on) {
     const int old = g_tx_w5;
-    g_tx_w5 = on >= 0 && on <= 4 ? on : 1;
+    g_tx_w5 = on >= 0 && on <= 15 ? on : 1;
     return old;
 }
 
@@ -607,11 +728,25 @@ int fws_gpu_encode_frames(fws_gpu_ctx *ctx, void *dev_out, uint64_t out_cap, con
                     : g_tx_w5 == 2 ? (const void *)k_tx_encode_dpp<5>
                     : g_tx_w5 == 3 ? (const void *)k_tx_encode_dpp<6>
                     : g_tx_w5 == 4 ? (const void *)k_tx_encode_dpp<8>
+                    : g_tx_w5 == 5 ? (const void *)k_tx_encode_wn<6>
+                    : g_tx_w5 == 6 ? (const void *)k_tx_encode_wn<7>
+                    : g_tx_w5 == 7 ? (const void *)k_tx_encode_dpp<7>
+                    : g_tx_w5 == 8 ? (const void *)k_tx_encode_late<8>
+                    : g_tx_w5 == 9 ? (const void *)k_tx_encode_late<6>
+                    : g_tx_w5 == 10 ? (const void *)k_tx_encode_so<false, 5>
+                    : g_tx_w5 == 11 ? (const void *)k_tx_encode_so<false, 6>
+                    : g_tx_w5 == 12 ? (const void *)k_tx_encode_so<false, 8>
+                    : g_tx_w5 == 13 ? (const void *)k_tx_encode_so<true, 5>
+                    : g_tx_w5 == 14 ? (const void *)k_tx_encode_so<true, 6>
+                    : g_tx_w5 == 15 ? (const void *)k_tx_encode_so<true, 8>
                                    : (const void *)k_tx_encode_w5;
     uint8_t *o = (uint8_t *)dev_out;
     const uint8_t *sp = (const uint8_t *)dev_src;
     void *args[] = {&o, &sp, &dev_descs, &n, &ws.cbase, &ws.unit_first, &ws.unit_cap, &ws.total};
     if ((r = fws_hip_status(hipLaunchKernel(k, dim3((unsigned)blocks), dim3(kBlock), args, 0, s)))) return r;
+    if (g_tx_w5 >= 10)                                 // the seam chunks the encode left
+        hipLaunchKernelGGL(k_tx_seams, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, o, sp, dev_descs, n,
+                           (const uint64_t *)ws.cbase, (const uint64_t *)ws.total);
     return fws_hip_status(hipGetLastError());
 }
 

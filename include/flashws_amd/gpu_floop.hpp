@@ -45,7 +45,9 @@
 // loop reads the next sockets, and a completed chunk's events are dispatched
 // while the following chunk decodes. The rest goes at the end of the step (the
 // loop's on_event callback, floop.h:743, which the hook wraps and chains to the
-// application's); its events are dispatched there, in read order. A connection
+// application's); its events are dispatched there, in read order -- or, while
+// the loop has events waiting, in the next step (SetDeferLastChunk, the
+// default since r06; see there). A connection
 // with a second read in the same step (a full read buffer, floop.h:670-672) or
 // whose previous read is still in flight, whose peer closes in the step
 // (on_eof), or which the loop closes in the step (the EOF / error branch,

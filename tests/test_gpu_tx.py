@@ -22,15 +22,20 @@ from test_tx_cpu import SESSIONS, frame_matches, tx_payload
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True, params=["one", "plan", "plan_dpp"])
+TX_FORMS = {"one": 1, "plan": 1, "plan_dpp": 2, "plan_so": 10, "plan_sod": 13}
+
+
+@pytest.fixture(autouse=True, params=list(TX_FORMS))
 def tx_form(request):
     """every test runs on each form of fws_gpu_encode_frames: one launch
     (k_tx_one, forced for every batch), k_out_plan + k_tx_encode_w5 (two
-    aligned loads per chunk) and k_out_plan + k_tx_encode_dpp (one nontemporal
-    load per chunk, the second block from the next lane)"""
+    aligned loads per chunk), k_out_plan + k_tx_encode_dpp (one nontemporal
+    load per chunk, the second block from the next lane), and k_out_plan +
+    k_tx_encode_so (full chunks only, two loads / DPP) + k_tx_seams (the seam
+    chunks, one thread per frame)"""
     from flashws_amd._lib import lib
     old = lib().fws_internal_set_tx_one(2 if request.param == "one" else 0, 0)
-    old_w = lib().fws_internal_set_tx_w5(2 if request.param == "plan_dpp" else 1)
+    old_w = lib().fws_internal_set_tx_w5(TX_FORMS[request.param])
     yield request.param
     lib().fws_internal_set_tx_one(old, 0)
     lib().fws_internal_set_tx_w5(old_w)
@@ -135,7 +140,7 @@ def test_encode_overflow_and_empty(ctx, cuda, tx_form):
     for cap in (4 * 5000, 5007, 17):                                           # 32 bytes short .. one frame
         out, got, total = encode(ctx, cuda, src, d, out_cap=cap)
         assert got == -1                                                       # ~0 as int64
-        if tx_form == "plan":
+        if tx_form.startswith("plan"):                                         # plan + encode (any form)
             assert out == b"\xEE" * len(out)                                   # nothing written at all
         else:                                                                  # the frames that fit, exact
             exp = b"".join(oracle_frames(payloads, metas))

@@ -41,7 +41,10 @@ def main():
     outs = [torch.empty(total, dtype=torch.uint8, device=dev) for _ in range(4)]
     olen = torch.empty(1, dtype=torch.int64, device=dev)
     ref = None
-    modes = [("plan", 0, 0, 1), ("dpp5", 0, 0, 2), ("dpp6", 0, 0, 3), ("dpp8", 0, 0, 4), ("w4", 0, 0, 0)] + \
+    modes = [("plan", 0, 0, 1), ("dpp5", 0, 0, 2), ("dpp6", 0, 0, 3), ("dpp8", 0, 0, 4), ("w4", 0, 0, 0),
+             ("w6", 0, 0, 5), ("w7", 0, 0, 6), ("dpp7", 0, 0, 7), ("late8", 0, 0, 8), ("late6", 0, 0, 9),
+             ("so5", 0, 0, 10), ("so6", 0, 0, 11), ("so8", 0, 0, 12), ("sod5", 0, 0, 13), ("sod6", 0, 0, 14),
+             ("sod8", 0, 0, 15)] + \
         [(f"one_span{k}k", 1, k, 1) for k in (32, 64, 128, 256)]
     if len(sys.argv) > 2:
         modes = [m for m in modes if m[0] in sys.argv[2].split(",")]

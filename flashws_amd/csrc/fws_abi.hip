@@ -29,6 +29,7 @@ void free_plan(fws_plan_ws &w) {
     dev_free(w.status);
     dev_free(w.ticket);
     dev_free(w.mode);
+    dev_free(w.tx_seam);
 }
 
 }  // namespace
@@ -47,6 +48,7 @@ int fws_ctx_ensure_plan(fws_gpu_ctx *ctx, uint64_t frames, uint64_t units) {
     if ((r = dev_alloc(&ctx->plan.status, frames / 8 + 2))) return r;
     if ((r = dev_alloc(&ctx->plan.ticket, 2))) return r;
     if ((r = dev_alloc(&ctx->plan.mode, sizeof(fws_plan_mode) / 8))) return r;
+    if ((r = dev_alloc(&ctx->plan.tx_seam, 4 * (2 * frames + 2)))) return r;
     if ((r = fws_hip_status(hipMemset(ctx->plan.status, 0, (frames / 8 + 2) * 8)))) return r;
     if ((r = fws_hip_status(hipMemset(ctx->plan.ticket, 0, 8)))) return r;
     if ((r = fws_hip_status(hipMemset(ctx->plan.mode, 0, sizeof(fws_plan_mode))))) return r;

@@ -142,6 +142,7 @@ struct fws_plan_ws {
     uint64_t *status = nullptr;       // ceil(n / 1024): k_plan look-back words (epoch-tagged)
     uint32_t *ticket = nullptr;       // k_plan's ordered block ticket (reset by its last block)
     uint64_t *mode = nullptr;         // kPlanModeWords: fws_plan_mode
+    uint32_t *tx_seam = nullptr;      // TX seam chunks built by the plan: 2 per frame + the tail, 4 words each
     uint64_t status_cap = 0;
     uint32_t epoch = 0;               // tag of the last k_plan's status words (1..0xFFFF)
     uint64_t unit_cap = 0;            // capacity of unit_first / unit_first_s (writes are clamped)

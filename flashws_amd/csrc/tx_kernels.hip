@@ -180,11 +180,13 @@ __device__ __forceinline__ void tx_store_tail(uint8_t *out, uint64_t a, uint64_t
 // lane per frame after this kernel (a unit's seam chunk cost the whole wave the
 // window loads and the byte-select VALU: 30 M of the kernel's 51 M VALU
 // instructions on the C2 TX shape, profiles/r06/pmc_tx_c4_4src.txt).
-template <bool kDpp = false, bool kLate = false, bool kSeamsOut = false, typename DescP, typename OffP>
+template <bool kDpp = false, bool kLate = false, bool kSeamsOut = false, bool kSeamRec = false, typename DescP,
+          typename OffP>
 __device__ __forceinline__ void tx_unit(uint8_t *__restrict__ out, const uint8_t *__restrict__ src, DescP d,
                                         OffP obase, uint32_t flo, uint32_t fhi, const fws_tx_desc dA,
                                         const fws_tx_desc dB, uint64_t OA, uint64_t OB, uint64_t a0,
-                                        uint64_t own_end, uint64_t total) {
+                                        uint64_t own_end, uint64_t total, const uint32_t *__restrict__ rec = nullptr,
+                                        uint32_t n_frames = 0) {
     if (fhi - flo >= 2u) {                             // small frames: bytewise with a search
         for (int j = 0; j < 4; ++j) {
             const uint64_t a = a0 + (uint64_t)j * 1024u;
@@ -236,6 +238,26 @@ __device__ __forceinline__ void tx_unit(uint8_t *__restrict__ out, const uint8_t
     tx_seam_blocks(as, SA, sA0, dA.len, safe16, qa0, qa1, sha);
     tx_seam_blocks(as, SB, sB0, two ? dB.len : 0, safe16, qb0, qb1, shb);
     uint32_t late = 0;
+    // kSeamRec: this lane's first seam chunk from the plan's record (tx_seam_records:
+    // the owner is the first frame whose header meets the chunk; a record exists
+    // when the chunk's bytes end within that frame's payload or at the output's end)
+    uint32_t rslot = ~0u;
+    if constexpr (kSeamRec) {
+        if (seam) {
+            const uint32_t hA = tx_hdr_len(dA), hB = tx_hdr_len(dB);
+            const bool mA = OA + hA > as && OA < as + 16u;
+            const bool mB = two && OB + hB > as && OB < as + 16u;
+            if (mA || mB) {
+                const uint32_t g = mA ? flo : fhi;
+                const uint64_t Og = mA ? OA : OB, Eg = mA ? z.EA : z.EB;
+                if (as + 16u <= Eg || g + 1u == n_frames) rslot = 2u * g + (as != (Og & ~uint64_t(15)) ? 1u : 0u);
+            } else {
+                rslot = 2u * n_frames;                 // the output's last chunk
+            }
+        }
+    }
+    u32x4 rv{0u, 0u, 0u, 0u};
+    if constexpr (kSeamRec) rv = gload16<false>((uintptr_t)(rec + 4u * (rslot != ~0u ? rslot : 0u)));
     if constexpr (kDpp) {
         const int lane = threadIdx.x & 63;
         u32x4 last = u32x4{0u, 0u, 0u, 0u};
@@ -304,7 +326,7 @@ __device__ __forceinline__ void tx_unit(uint8_t *__restrict__ out, const uint8_t
             v0[j] = gload16<false>(sb[j]);          // (a copy would wait for the load)
             v1[j] = gload16<false>(s1);
         }
-        if constexpr (kSeamsOut) {
+        if constexpr (kSeamsOut || kSeamRec) {
             sa0 = sa1 = sb0 = sb1 = u32x4{0u, 0u, 0u, 0u};
         } else {
             sa0 = gload16<false>(qa0);
@@ -334,7 +356,13 @@ __device__ __forceinline__ void tx_unit(uint8_t *__restrict__ out, const uint8_t
 #ifdef FWS_TX_ABL_SEAM
     return;                                            // ablation build only: no seam chunks (wrong bytes)
 #endif
-    if (!kLate && seam) {
+    if constexpr (kSeamRec) {
+        if (seam && rslot != ~0u) {
+            if (as + 16u <= total) gstore16<true>((uintptr_t)(out + as), rv);
+            else tx_store_tail(out, as, total, rv);
+            seam &= seam - 1u;
+        }
+    } else if (!kLate && seam) {
         seam_chunk(as, sa0, sa1, sha, sb0, sb1, shb);
         seam &= seam - 1u;
     }
@@ -363,12 +391,13 @@ __device__ __forceinline__ fws_tx_desc tx_desc_of(const uint32_t (&w)[6]) {
     return x;
 }
 
-template <bool kDpp = false, bool kLate = false, bool kSeamsOut = false>
+template <bool kDpp = false, bool kLate = false, bool kSeamsOut = false, bool kSeamRec = false>
 __device__ __forceinline__ void tx_encode_body(uint8_t *__restrict__ out, const uint8_t *__restrict__ src,
                                                       const fws_tx_desc *__restrict__ d, uint32_t n,
                                                       const uint64_t *__restrict__ obase,
                                                       const uint32_t *__restrict__ unit_first, uint64_t unit_cap,
-                                                      const uint64_t *__restrict__ total_ptr) {
+                                                      const uint64_t *__restrict__ total_ptr,
+                                                      const uint32_t *__restrict__ rec = nullptr) {
     const int lane = threadIdx.x & 63;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t nw = (uint64_t)gridDim.x * (kBlock / 64);
@@ -406,8 +435,8 @@ __device__ __forceinline__ void tx_encode_body(uint8_t *__restrict__ out, const 
         // a sched_barrier alone left the loads sunk into the two-frame branch)
         asm volatile("" ::"s"(ra[0]), "s"(ra[5]), "s"(rb[0]), "s"(rb[5]), "s"((uint32_t)OA), "s"((uint32_t)OB));
         const fws_tx_desc dA = tx_desc_of(ra), dB = tx_desc_of(rb);
-        tx_unit<kDpp, kLate, kSeamsOut>(out, src, d, obase, flo, fhi, dA, dB, OA, OB, u * kTxUnit + (uint64_t)lane * 16u, total,
-                      total);
+        tx_unit<kDpp, kLate, kSeamsOut, kSeamRec>(out, src, d, obase, flo, fhi, dA, dB, OA, OB,
+                                                   u * kTxUnit + (uint64_t)lane * 16u, total, total, rec, n);
     }
 }
 
@@ -619,6 +648,83 @@ __global__ __launch_bounds__(kBlock) void k_tx_seams(uint8_t *__restrict__ out, 
     }
 }
 
+// ------------------------------------------------- seam chunks from the plan
+// r06 (kSeamRec): the plan launch builds every seam chunk -- the 16-B output
+// chunks meeting a frame header, and the output's last chunk when it ends inside
+// a payload -- into a side buffer (never into `out`, so nothing is written when
+// the batch exceeds out_cap), one thread per frame, the windows and the byte
+// select amortized over a wave of frames; the encode's seam lane copies its
+// record. rec[2 f + k]: chunk k (0: the one holding the header's first byte, 1:
+// its last byte's when another) of frame f, written when frame f owns it (no
+// earlier header meets it) and its bytes end within frame f's payload (or the
+// output); rec[2 n]: the last chunk. The encode tests the same two conditions.
+__device__ __forceinline__ void tx_seam_records(const uint8_t *__restrict__ src, const fws_tx_desc *__restrict__ d,
+                                                uint32_t n, uint32_t f, uint64_t OB, uint32_t *__restrict__ rec) {
+    const bool hasA = f > 0, last = f + 1u == n;
+    const fws_tx_desc dB = d[f];
+    const fws_tx_desc dA = hasA ? d[f - 1u] : dB;
+    const uint32_t hB = tx_hdr_len(dB), hA = tx_hdr_len(dA);
+    const uint64_t OA = hasA ? OB - out_size(dA) : OB;
+    TxSeam z;
+    z.PA = OA + hA;
+    z.EA = z.PA + dA.len;
+    z.PB = OB + hB;
+    z.EB = z.PB + dB.len;
+    const uint64_t total = last ? z.EB : ~0ull;         // only the last frame's chunks can reach the end
+    const uintptr_t sA0 = (uintptr_t)(src + dA.src_off), sB0 = (uintptr_t)(src + dB.src_off);
+    const uintptr_t SA = sA0 - (uintptr_t)z.PA, SB = sB0 - (uintptr_t)z.PB;
+    const bool payA = hasA && dA.len != 0, payB = dB.len != 0;
+    const uintptr_t safe16 = (payB ? sB0 : sA0) & ~uintptr_t(15);
+    auto build = [&](uint64_t c, uint32_t slot) {
+        u32x4 pA{0u, 0u, 0u, 0u}, pB{0u, 0u, 0u, 0u};
+        uintptr_t b0, b1;
+        uint32_t sh;
+        if (payA && c < z.EA) {
+            tx_seam_blocks(c, SA, sA0, dA.len, safe16, b0, b1, sh);
+            const uint32_t rk = dA.masked ? rotr32(dA.key, 8u * ((uint32_t)(c - z.PA) & 3u)) : 0u;
+            pA = tx_shr_bytes(gload16<true>(b0), gload16<true>(b1), sh) ^ rk;
+        }
+        if (payB && c + 16u > z.PB) {
+            tx_seam_blocks(c, SB, sB0, dB.len, safe16, b0, b1, sh);
+            const uint32_t rk = dB.masked ? rotr32(dB.key, 8u * ((uint32_t)(c - z.PB) & 3u)) : 0u;
+            pB = tx_shr_bytes(gload16<true>(b0), gload16<true>(b1), sh) ^ rk;
+        }
+        const u32x4 x = hasA ? tx_seam_combine(c, dA, OA, dB, OB, true, z, total, pA, pB)
+                             : tx_seam_combine(c, dB, OB, dB, OB, false, TxSeam{z.PB, z.EB, z.PB, z.EB}, total, pB,
+                                               pB);
+        gstore16<false>((uintptr_t)(rec + 4u * slot), x);
+    };
+    const uint64_t c0 = OB & ~uint64_t(15), c1 = (OB + hB - 1u) & ~uint64_t(15);
+    for (uint64_t c = c0; c <= c1; c += 16u)
+        if ((!hasA || OA + hA <= c) && (c + 16u <= z.EB || last)) build(c, 2u * f + (c != c0 ? 1u : 0u));
+    if (last && (z.EB & 15u) != 0u) {                  // the output's last chunk, when no header meets it
+        const uint64_t ct = (z.EB - 1u) & ~uint64_t(15);
+        if (ct > c1) build(ct, 2u * n);
+    }
+}
+
+// the TX plan (out_plan_block) and the seam records of its frames, one launch
+template <int kF>
+__global__ __launch_bounds__(kBlock) void k_tx_plan_seams(const fws_tx_desc *__restrict__ d, uint32_t n,
+                                                          OutPlanArgs a, const uint8_t *__restrict__ src,
+                                                          uint32_t *__restrict__ rec) {
+    const uint32_t blk = plan_block_order(a.ticket);
+    out_plan_block<fws_tx_desc, kF>(d, n, a, blk);
+    const uint64_t f = uint64_t(blk) * kF + threadIdx.x;
+    if (threadIdx.x < (uint32_t)kF && f < n)            // base[f]: this thread's own store in out_plan_block
+        tx_seam_records(src, d, n, (uint32_t)f, a.base[f], rec);
+}
+
+// r06: full chunks from the source, seam chunks from the plan's records
+// (kSeamRec), two loads per chunk, at kW waves per SIMD
+template <int kW>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kW))) void k_tx_encode_sr(
+    uint8_t *__restrict__ out, const uint8_t *__restrict__ src, const fws_tx_desc *__restrict__ d, uint32_t n,
+    const uint64_t *__restrict__ obase, const uint32_t *__restrict__ unit_first, uint64_t unit_cap,
+    const uint64_t *__restrict__ total_ptr, const uint32_t *__restrict__ rec) {
+    tx_encode_body<false, false, false, true>(out, src, d, n, obase, unit_first, unit_cap, total_ptr, rec);
+}
+
 // r06: the two-load form at kW waves per SIMD (A/B)
 template <int kW>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kW))) void k_tx_encode_wn(
@@ -644,11 +750,12 @@ extern "C" __attribute__((visibility("default"))) int fws_internal_set_tx_blocks
 // k_tx_encode_dpp at 5 / 6 / 8 waves per SIMD: 2 / 3 / 4; the two-load form
 // at 6 / 7 waves: 5 / 6; k_tx_encode_dpp at 7: 7; k_tx_encode_late at 8 / 6: 8 / 9;
 // full chunks only + k_tx_seams (k_tx_encode_so): two loads at 5 / 6 / 8 waves 10 / 11 / 12,
-// one load + DPP at 5 / 6 / 8 waves 13 / 14 / 15
+// one load + DPP at 5 / 6 / 8 waves 13 / 14 / 15; seam chunks built by the plan
+// (k_tx_plan_seams + k_tx_encode_sr) at 5 / 8 waves: 16 / 17
 static int g_tx_w5 = 1;
 extern "C" __attribute__((visibility("default"))) int fws_internal_set_tx_w5(int on) {
     const int old = g_tx_w5;
-    g_tx_w5 = on >= 0 && on <= 15 ? on : 1;
+    g_tx_w5 = on >= 0 && on <= 17 ? on : 1;
     return old;
 }
 
@@ -717,7 +824,24 @@ int fws_gpu_encode_frames(fws_gpu_ctx *ctx, void *dev_out, uint64_t out_cap, con
     }
     if ((r = fws_ctx_ensure_plan(ctx, n, units))) return r;
     fws_plan_ws &ws = ctx->plan;
-    if ((r = fws_launch_tx_plan(dev_descs, n, ws, out_cap, dev_out_len, s))) return r;
+    const bool seam_rec = g_tx_w5 >= 16;
+    if (seam_rec) {                                    // the plan with the seam chunks (outplan_kernels.hip's shape)
+        const bool small = n <= 16384u;
+        const uint32_t nb = small ? (n + 63u) / 64u : (n + kBlock - 1) / kBlock;
+        if (nb > ws.status_cap) return FWS_ERR_CAPACITY;
+        if ((r = fws_plan_next_epoch(ws, s))) return r;
+        OutPlanArgs pa{ws.cbase, ws.unit_first, ws.unit_cap, ws.total, dev_out_len, out_cap, ws.status, ws.ticket,
+                       ws.epoch};
+        if (small)
+            hipLaunchKernelGGL((k_tx_plan_seams<64>), dim3(nb), dim3(kBlock), 0, s, dev_descs, n, pa,
+                               (const uint8_t *)dev_src, ws.tx_seam);
+        else
+            hipLaunchKernelGGL((k_tx_plan_seams<kBlock>), dim3(nb), dim3(kBlock), 0, s, dev_descs, n, pa,
+                               (const uint8_t *)dev_src, ws.tx_seam);
+        if ((r = fws_hip_status(hipGetLastError()))) return r;
+    } else if ((r = fws_launch_tx_plan(dev_descs, n, ws, out_cap, dev_out_len, s))) {
+        return r;
+    }
     uint64_t u = units < ws.unit_cap ? units : ws.unit_cap;
     uint64_t blocks = (u + 3) / 4;
     // one wave per unit in one pass (a cap at 16 384 workgroups left a C2-shaped
@@ -739,11 +863,16 @@ int fws_gpu_encode_frames(fws_gpu_ctx *ctx, void *dev_out, uint64_t out_cap, con
                     : g_tx_w5 == 13 ? (const void *)k_tx_encode_so<true, 5>
                     : g_tx_w5 == 14 ? (const void *)k_tx_encode_so<true, 6>
                     : g_tx_w5 == 15 ? (const void *)k_tx_encode_so<true, 8>
+                    : g_tx_w5 == 16 ? (const void *)k_tx_encode_sr<5>
+                    : g_tx_w5 == 17 ? (const void *)k_tx_encode_sr<8>
                                    : (const void *)k_tx_encode_w5;
     uint8_t *o = (uint8_t *)dev_out;
     const uint8_t *sp = (const uint8_t *)dev_src;
-    void *args[] = {&o, &sp, &dev_descs, &n, &ws.cbase, &ws.unit_first, &ws.unit_cap, &ws.total};
-    if ((r = fws_hip_status(hipLaunchKernel(k, dim3((unsigned)blocks), dim3(kBlock), args, 0, s)))) return r;
+    const uint32_t *rec = ws.tx_seam;
+    void *args[] = {&o, &sp, &dev_descs, &n, &ws.cbase, &ws.unit_first, &ws.unit_cap, &ws.total, &rec};
+    void *args8[] = {&o, &sp, &dev_descs, &n, &ws.cbase, &ws.unit_first, &ws.unit_cap, &ws.total};
+    if ((r = fws_hip_status(hipLaunchKernel(k, dim3((unsigned)blocks), dim3(kBlock), seam_rec ? args : args8, 0, s))))
+        return r;
     if (g_tx_w5 >= 10)                                 // the seam chunks the encode left
         hipLaunchKernelGGL(k_tx_seams, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, o, sp, dev_descs, n,
                            (const uint64_t *)ws.cbase, (const uint64_t *)ws.total);

@@ -10,6 +10,8 @@ SendFrame bytes (net/w_socket.h:832-944), bit-exact.
   nothing at all), the empty batch; both forms (one launch, plan + encode);
 * round trip: client frames encoded here, decoded by fws_gpu_decode_stream.
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -23,6 +25,8 @@ pytestmark = pytest.mark.gpu
 
 
 TX_FORMS = {"one": 1, "plan": 1, "plan_dpp": 2, "plan_so": 10, "plan_sod": 13}
+if os.environ.get("FWS_TEST_TX_SR") == "1":          # (the plan-built seam records, under test)
+    TX_FORMS.update({"plan_sr": 16, "plan_sr8": 17})
 
 
 @pytest.fixture(autouse=True, params=list(TX_FORMS))
@@ -32,7 +36,8 @@ def tx_form(request):
     aligned loads per chunk), k_out_plan + k_tx_encode_dpp (one nontemporal
     load per chunk, the second block from the next lane), and k_out_plan +
     k_tx_encode_so (full chunks only, two loads / DPP) + k_tx_seams (the seam
-    chunks, one thread per frame)"""
+    chunks, one thread per frame), and k_tx_plan_seams (the plan building the
+    seam chunks into records) + k_tx_encode_sr (at 5 / 8 waves)"""
     from flashws_amd._lib import lib
     old = lib().fws_internal_set_tx_one(2 if request.param == "one" else 0, 0)
     old_w = lib().fws_internal_set_tx_w5(TX_FORMS[request.param])

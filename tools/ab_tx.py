@@ -44,7 +44,7 @@ def main():
     modes = [("plan", 0, 0, 1), ("dpp5", 0, 0, 2), ("dpp6", 0, 0, 3), ("dpp8", 0, 0, 4), ("w4", 0, 0, 0),
              ("w6", 0, 0, 5), ("w7", 0, 0, 6), ("dpp7", 0, 0, 7), ("late8", 0, 0, 8), ("late6", 0, 0, 9),
              ("so5", 0, 0, 10), ("so6", 0, 0, 11), ("so8", 0, 0, 12), ("sod5", 0, 0, 13), ("sod6", 0, 0, 14),
-             ("sod8", 0, 0, 15)] + \
+             ("sod8", 0, 0, 15), ("sr5", 0, 0, 16), ("sr8", 0, 0, 17)] + \
         [(f"one_span{k}k", 1, k, 1) for k in (32, 64, 128, 256)]
     if len(sys.argv) > 2:
         modes = [m for m in modes if m[0] in sys.argv[2].split(",")]

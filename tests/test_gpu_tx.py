@@ -10,8 +10,6 @@ SendFrame bytes (net/w_socket.h:832-944), bit-exact.
   nothing at all), the empty batch; both forms (one launch, plan + encode);
 * round trip: client frames encoded here, decoded by fws_gpu_decode_stream.
 """
-import os
-
 import numpy as np
 import pytest
 import torch
@@ -24,9 +22,7 @@ from test_tx_cpu import SESSIONS, frame_matches, tx_payload
 pytestmark = pytest.mark.gpu
 
 
-TX_FORMS = {"one": 1, "plan": 1, "plan_dpp": 2, "plan_so": 10, "plan_sod": 13}
-if os.environ.get("FWS_TEST_TX_SR") == "1":          # (the plan-built seam records, under test)
-    TX_FORMS.update({"plan_sr": 16, "plan_sr8": 17})
+TX_FORMS = {"one": 1, "plan": 1, "plan_dpp": 2, "plan_so": 10, "plan_sod": 13, "plan_sr": 16, "plan_sr8": 17}
 
 
 @pytest.fixture(autouse=True, params=list(TX_FORMS))

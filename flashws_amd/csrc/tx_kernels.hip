@@ -170,17 +170,7 @@ __device__ __forceinline__ void tx_store_tail(uint8_t *out, uint64_t a, uint64_t
 // or for the last chunk a load of its own) or the next lane's A-window seam
 // block (the left neighbour of a seam chunk). A full chunk with neither (rare:
 // the chunk before the batch's last) is built by the seam path afterwards.
-// kLate (r06, with kDpp): no seam window preloaded with the full chunks -- every
-// seam chunk (and a full chunk whose neighbour block belongs to a seam lane)
-// loads its windows after the unit's full chunks are stored, when their data
-// registers are dead: fewer live registers (8 waves per SIMD) for a second load
-// round on the seam lanes only.
-// kSeamsOut (r06): the unit writes its full chunks only; every chunk that meets
-// a frame header or the output's end (the seam chunks) is k_tx_seams's, one
-// lane per frame after this kernel (a unit's seam chunk cost the whole wave the
-// window loads and the byte-select VALU: 30 M of the kernel's 51 M VALU
-// instructions on the C2 TX shape, profiles/r06/pmc_tx_c4_4src.txt).
-template <bool kDpp = false, bool kLate = false, bool kSeamsOut = false, bool kSeamRec = false, typename DescP,
+template <bool kDpp = false, bool kSeamsOut = false, bool kSeamRec = false, typename DescP,
           typename OffP>
 __device__ __forceinline__ void tx_unit(uint8_t *__restrict__ out, const uint8_t *__restrict__ src, DescP d,
                                         OffP obase, uint32_t flo, uint32_t fhi, const fws_tx_desc dA,
@@ -265,7 +255,7 @@ __device__ __forceinline__ void tx_unit(uint8_t *__restrict__ out, const uint8_t
 #pragma unroll
             for (int j = 0; j < 4; ++j) v0[j] = gload16<true>(sb[j]);
             if (lane == 63) last = gload16<true>(((full >> 3) & 1u) && sh[3] ? sb[3] + 16u : sb[3]);
-            if constexpr (kLate || kSeamsOut) {
+            if constexpr (kSeamsOut) {
                 sa0 = sa1 = sb0 = sb1 = u32x4{0u, 0u, 0u, 0u};
                 qa0 = 1;                               // no lane's block: the A-window hand-over is off
             } else {
@@ -362,7 +352,7 @@ __device__ __forceinline__ void tx_unit(uint8_t *__restrict__ out, const uint8_t
             else tx_store_tail(out, as, total, rv);
             seam &= seam - 1u;
         }
-    } else if (!kLate && seam) {
+    } else if (seam) {
         seam_chunk(as, sa0, sa1, sha, sb0, sb1, shb);
         seam &= seam - 1u;
     }
@@ -391,7 +381,7 @@ __device__ __forceinline__ fws_tx_desc tx_desc_of(const uint32_t (&w)[6]) {
     return x;
 }
 
-template <bool kDpp = false, bool kLate = false, bool kSeamsOut = false, bool kSeamRec = false>
+template <bool kDpp = false, bool kSeamsOut = false, bool kSeamRec = false>
 __device__ __forceinline__ void tx_encode_body(uint8_t *__restrict__ out, const uint8_t *__restrict__ src,
                                                       const fws_tx_desc *__restrict__ d, uint32_t n,
                                                       const uint64_t *__restrict__ obase,
@@ -435,7 +425,7 @@ __device__ __forceinline__ void tx_encode_body(uint8_t *__restrict__ out, const 
         // a sched_barrier alone left the loads sunk into the two-frame branch)
         asm volatile("" ::"s"(ra[0]), "s"(ra[5]), "s"(rb[0]), "s"(rb[5]), "s"((uint32_t)OA), "s"((uint32_t)OB));
         const fws_tx_desc dA = tx_desc_of(ra), dB = tx_desc_of(rb);
-        tx_unit<kDpp, kLate, kSeamsOut, kSeamRec>(out, src, d, obase, flo, fhi, dA, dB, OA, OB,
+        tx_unit<kDpp, kSeamsOut, kSeamRec>(out, src, d, obase, flo, fhi, dA, dB, OA, OB,
                                                    u * kTxUnit + (uint64_t)lane * 16u, total, total, rec, n);
     }
 }
@@ -560,14 +550,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kW))) vo
     const uint64_t *__restrict__ total_ptr) {
     tx_encode_body<true>(out, src, d, n, obase, unit_first, unit_cap, total_ptr);
 }
-// r06: the DPP form with late seam windows (tx_unit<true, true>) at kW waves per SIMD
-template <int kW>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kW))) void k_tx_encode_late(
-    uint8_t *__restrict__ out, const uint8_t *__restrict__ src, const fws_tx_desc *__restrict__ d, uint32_t n,
-    const uint64_t *__restrict__ obase, const uint32_t *__restrict__ unit_first, uint64_t unit_cap,
-    const uint64_t *__restrict__ total_ptr) {
-    tx_encode_body<true, true>(out, src, d, n, obase, unit_first, unit_cap, total_ptr);
-}
 // r06: full chunks only (kSeamsOut; the seam chunks are k_tx_seams's), the
 // two-load form (kDpp false) or one load + DPP, at kW waves per SIMD
 template <bool kDpp, int kW>
@@ -575,7 +557,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kW))) vo
     uint8_t *__restrict__ out, const uint8_t *__restrict__ src, const fws_tx_desc *__restrict__ d, uint32_t n,
     const uint64_t *__restrict__ obase, const uint32_t *__restrict__ unit_first, uint64_t unit_cap,
     const uint64_t *__restrict__ total_ptr) {
-    tx_encode_body<kDpp, false, true>(out, src, d, n, obase, unit_first, unit_cap, total_ptr);
+    tx_encode_body<kDpp, true>(out, src, d, n, obase, unit_first, unit_cap, total_ptr);
 }
 
 // The seam chunks of a batch (k_tx_encode_so wrote the rest): one thread per
@@ -722,17 +704,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kW))) vo
     uint8_t *__restrict__ out, const uint8_t *__restrict__ src, const fws_tx_desc *__restrict__ d, uint32_t n,
     const uint64_t *__restrict__ obase, const uint32_t *__restrict__ unit_first, uint64_t unit_cap,
     const uint64_t *__restrict__ total_ptr, const uint32_t *__restrict__ rec) {
-    tx_encode_body<false, false, false, true>(out, src, d, n, obase, unit_first, unit_cap, total_ptr, rec);
+    tx_encode_body<false, false, true>(out, src, d, n, obase, unit_first, unit_cap, total_ptr, rec);
 }
 
-// r06: the two-load form at kW waves per SIMD (A/B)
-template <int kW>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kW))) void k_tx_encode_wn(
-    uint8_t *__restrict__ out, const uint8_t *__restrict__ src, const fws_tx_desc *__restrict__ d, uint32_t n,
-    const uint64_t *__restrict__ obase, const uint32_t *__restrict__ unit_first, uint64_t unit_cap,
-    const uint64_t *__restrict__ total_ptr) {
-    tx_encode_body<false>(out, src, d, n, obase, unit_first, unit_cap, total_ptr);
-}
 
 }  // namespace fwsk
 
@@ -746,16 +720,17 @@ extern "C" __attribute__((visibility("default"))) int fws_internal_set_tx_blocks
     return old;
 }
 
-// tuning hook: 1 = k_tx_encode_w5 (default), 0 = the compiler's 4 waves;
-// k_tx_encode_dpp at 5 / 6 / 8 waves per SIMD: 2 / 3 / 4; the two-load form
-// at 6 / 7 waves: 5 / 6; k_tx_encode_dpp at 7: 7; k_tx_encode_late at 8 / 6: 8 / 9;
-// full chunks only + k_tx_seams (k_tx_encode_so): two loads at 5 / 6 / 8 waves 10 / 11 / 12,
-// one load + DPP at 5 / 6 / 8 waves 13 / 14 / 15; seam chunks built by the plan
-// (k_tx_plan_seams + k_tx_encode_sr) at 5 / 8 waves: 16 / 17
+// tuning hook: 1 = k_tx_encode_w5 (default), 0 = the compiler's 4 waves,
+// 2 = k_tx_encode_dpp<5> (one load + DPP), 3 / 4 = k_tx_encode_so two loads / DPP
+// (full chunks only) + k_tx_seams, 5 = k_tx_plan_seams + k_tx_encode_sr<5> (seam
+// chunks built by the plan). r06, four rotating sources: none beat 1 (DESIGN
+// §4.6); measured and removed: DPP at 6 / 7 / 8 waves and the two-load form at 6
+// / 7 (spills, 0.140-0.250 ms), late seam windows at 6 / 8 waves (0.105 / 0.122),
+// the so / sr forms at 6 / 8 waves (0.102-0.149).
 static int g_tx_w5 = 1;
 extern "C" __attribute__((visibility("default"))) int fws_internal_set_tx_w5(int on) {
     const int old = g_tx_w5;
-    g_tx_w5 = on >= 0 && on <= 17 ? on : 1;
+    g_tx_w5 = on >= 0 && on <= 5 ? on : 1;
     return old;
 }
 
@@ -824,7 +799,7 @@ int fws_gpu_encode_frames(fws_gpu_ctx *ctx, void *dev_out, uint64_t out_cap, con
     }
     if ((r = fws_ctx_ensure_plan(ctx, n, units))) return r;
     fws_plan_ws &ws = ctx->plan;
-    const bool seam_rec = g_tx_w5 >= 16;
+    const bool seam_rec = g_tx_w5 == 5;
     if (seam_rec) {                                    // the plan with the seam chunks (outplan_kernels.hip's shape)
         const bool small = n <= 16384u;
         const uint32_t nb = small ? (n + 63u) / 64u : (n + kBlock - 1) / kBlock;
@@ -850,21 +825,9 @@ int fws_gpu_encode_frames(fws_gpu_ctx *ctx, void *dev_out, uint64_t out_cap, con
     if (g_tx_blocks && blocks > (uint64_t)g_tx_blocks) blocks = (uint64_t)g_tx_blocks;
     const void *k = g_tx_w5 == 0   ? (const void *)k_tx_encode
                     : g_tx_w5 == 2 ? (const void *)k_tx_encode_dpp<5>
-                    : g_tx_w5 == 3 ? (const void *)k_tx_encode_dpp<6>
-                    : g_tx_w5 == 4 ? (const void *)k_tx_encode_dpp<8>
-                    : g_tx_w5 == 5 ? (const void *)k_tx_encode_wn<6>
-                    : g_tx_w5 == 6 ? (const void *)k_tx_encode_wn<7>
-                    : g_tx_w5 == 7 ? (const void *)k_tx_encode_dpp<7>
-                    : g_tx_w5 == 8 ? (const void *)k_tx_encode_late<8>
-                    : g_tx_w5 == 9 ? (const void *)k_tx_encode_late<6>
-                    : g_tx_w5 == 10 ? (const void *)k_tx_encode_so<false, 5>
-                    : g_tx_w5 == 11 ? (const void *)k_tx_encode_so<false, 6>
-                    : g_tx_w5 == 12 ? (const void *)k_tx_encode_so<false, 8>
-                    : g_tx_w5 == 13 ? (const void *)k_tx_encode_so<true, 5>
-                    : g_tx_w5 == 14 ? (const void *)k_tx_encode_so<true, 6>
-                    : g_tx_w5 == 15 ? (const void *)k_tx_encode_so<true, 8>
-                    : g_tx_w5 == 16 ? (const void *)k_tx_encode_sr<5>
-                    : g_tx_w5 == 17 ? (const void *)k_tx_encode_sr<8>
+                    : g_tx_w5 == 3 ? (const void *)k_tx_encode_so<false, 5>
+                    : g_tx_w5 == 4 ? (const void *)k_tx_encode_so<true, 5>
+                    : g_tx_w5 == 5 ? (const void *)k_tx_encode_sr<5>
                                    : (const void *)k_tx_encode_w5;
     uint8_t *o = (uint8_t *)dev_out;
     const uint8_t *sp = (const uint8_t *)dev_src;
@@ -873,7 +836,7 @@ int fws_gpu_encode_frames(fws_gpu_ctx *ctx, void *dev_out, uint64_t out_cap, con
     void *args8[] = {&o, &sp, &dev_descs, &n, &ws.cbase, &ws.unit_first, &ws.unit_cap, &ws.total};
     if ((r = fws_hip_status(hipLaunchKernel(k, dim3((unsigned)blocks), dim3(kBlock), seam_rec ? args : args8, 0, s))))
         return r;
-    if (g_tx_w5 >= 10)                                 // the seam chunks the encode left
+    if (g_tx_w5 == 3 || g_tx_w5 == 4)                  // the seam chunks the encode left
         hipLaunchKernelGGL(k_tx_seams, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, o, sp, dev_descs, n,
                            (const uint64_t *)ws.cbase, (const uint64_t *)ws.total);
     return fws_hip_status(hipGetLastError());

@@ -22,7 +22,7 @@ from test_tx_cpu import SESSIONS, frame_matches, tx_payload
 pytestmark = pytest.mark.gpu
 
 
-TX_FORMS = {"one": 1, "plan": 1, "plan_dpp": 2, "plan_so": 10, "plan_sod": 13, "plan_sr": 16, "plan_sr8": 17}
+TX_FORMS = {"one": 1, "plan": 1, "plan_dpp": 2, "plan_so": 3, "plan_sod": 4, "plan_sr": 5}
 
 
 @pytest.fixture(autouse=True, params=list(TX_FORMS))
@@ -33,7 +33,7 @@ def tx_form(request):
     load per chunk, the second block from the next lane), and k_out_plan +
     k_tx_encode_so (full chunks only, two loads / DPP) + k_tx_seams (the seam
     chunks, one thread per frame), and k_tx_plan_seams (the plan building the
-    seam chunks into records) + k_tx_encode_sr (at 5 / 8 waves)"""
+    seam chunks into records) + k_tx_encode_sr"""
     from flashws_amd._lib import lib
     old = lib().fws_internal_set_tx_one(2 if request.param == "one" else 0, 0)
     old_w = lib().fws_internal_set_tx_w5(TX_FORMS[request.param])

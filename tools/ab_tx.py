@@ -8,7 +8,8 @@ repetition); outputs compared across modes. One JSON line per (mode, rep).
 (r04 used it for k_tx_encode grid caps, profiles/r04/ab_tx.jsonl.) r06: the
 source rotates over 4 copies (1 GiB, past the 256 MB Infinity Cache; one
 source re-read every step was served partly from it) unless FWS_AB_ONE_SRC=1;
-modes dpp5 / dpp6 / dpp8 = k_tx_encode_dpp at 5 / 6 / 8 waves per SIMD.
+modes (fws_internal_set_tx_w5): w4, dpp5 (one load + DPP), so / sod (full
+chunks only, two loads / DPP, + k_tx_seams), sr (seam chunks built by the plan).
 
 usage: python tools/ab_tx.py [reps] [mode,mode,...]"""
 import json
@@ -41,10 +42,8 @@ def main():
     outs = [torch.empty(total, dtype=torch.uint8, device=dev) for _ in range(4)]
     olen = torch.empty(1, dtype=torch.int64, device=dev)
     ref = None
-    modes = [("plan", 0, 0, 1), ("dpp5", 0, 0, 2), ("dpp6", 0, 0, 3), ("dpp8", 0, 0, 4), ("w4", 0, 0, 0),
-             ("w6", 0, 0, 5), ("w7", 0, 0, 6), ("dpp7", 0, 0, 7), ("late8", 0, 0, 8), ("late6", 0, 0, 9),
-             ("so5", 0, 0, 10), ("so6", 0, 0, 11), ("so8", 0, 0, 12), ("sod5", 0, 0, 13), ("sod6", 0, 0, 14),
-             ("sod8", 0, 0, 15), ("sr5", 0, 0, 16), ("sr8", 0, 0, 17)] + \
+    modes = [("plan", 0, 0, 1), ("dpp5", 0, 0, 2), ("w4", 0, 0, 0), ("so", 0, 0, 3), ("sod", 0, 0, 4),
+             ("sr", 0, 0, 5)] + \
         [(f"one_span{k}k", 1, k, 1) for k in (32, 64, 128, 256)]
     if len(sys.argv) > 2:
         modes = [m for m in modes if m[0] in sys.argv[2].split(",")]

@@ -33,7 +33,7 @@ def setup(n=65536, pl=4096):
 
 def main(steps=20):
     ctx, outs, srcs, dd, n, _ = setup()
-    if os.environ.get("FWS_TX_FORM"):          # fws_internal_set_tx_w5: 0 w4, 1 w5, 2-4 dpp5 / 6 / 8
+    if os.environ.get("FWS_TX_FORM"):          # fws_internal_set_tx_w5: 0 w4, 1 w5, 2 dpp5, 3 so, 4 sod, 5 sr
         from flashws_amd import _lib
         _lib.lib().fws_internal_set_tx_w5(int(os.environ["FWS_TX_FORM"]))
     for i in range(steps):

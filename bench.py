@@ -906,6 +906,11 @@ def c4_extra(dev, steps, stream):
     out["C4_fragmented_reassemble"] = {"GiB_per_s": round(total / t / GIB, 1), "ms_per_step": round(t * 1e3, 4),
                                        "fragments": len(d4), "alg_GB_per_s": round((len(w4) + total) / t / 1e9, 1),
                                        "rotating_sources": SRC_COPIES,
+                           "note": "r06: sources rotate past the 256 MB MALL; r05 and earlier re-read one source "
+                                   "(91.0 against 103.5 us, profiles/r06/ab_mall.jsonl)",
+                                       "note": "r06: sources rotate past the 256 MB MALL; r05 and earlier re-read one "
+                                               "source (one source: 84.4 us, four: 99.9 us before r06's plan + "
+                                               "k_gather_fast<kFlat> default, profiles/r06/ab_mall.jsonl)",
                                        "roofline": _step_roofline(len(w4) + total, t, "whole fws_gpu_unmask_gather step: wire read + payload written out of place")}
     _profile(out["C4_fragmented_reassemble"], "c4")
     c.close()

@@ -1047,7 +1047,7 @@ __device__ __forceinline__ void unmask_sorted_body(uint8_t *base, const fws_fram
         // unit past it (a batch wider than the reservation) leaves its two dwords to
         // k_utf8_seam_sorted's stream reads
         const bool sw = u < seam_units;
-        if constexpr (kUtf8 && !kEarly) {
+        if constexpr (kUtf8) {
             if (rec.z == (4096u << 13) && ((rec.w >> 13) & 0x1FFFu) <= (rec.w & 0x1FFFu)) {
                 // the unit lies wholly inside A's payload and B has no byte in it (the
                 // common unit of large frames): one key, no per-chunk region tests;
@@ -1055,7 +1055,7 @@ __device__ __forceinline__ void unmask_sorted_body(uint8_t *base, const fws_fram
                 // chunk before, bound_ctrl off keeps the carried value)
                 u32x4 x[kUnmaskU];
 #pragma unroll
-                for (int j = 0; j < kUnmaskU; ++j) x[j] = gload16<kNT>(c0 + uint64_t(j) * 1024u);
+                for (int j = 0; j < kUnmaskU; ++j) x[j] = kEarly ? v[j] : gload16<kNT>(c0 + uint64_t(j) * 1024u);
                 const uint32_t rk = rec.x;
 #pragma unroll
                 for (int j = 0; j < kUnmaskU; ++j) {
@@ -1082,7 +1082,7 @@ __device__ __forceinline__ void unmask_sorted_body(uint8_t *base, const fws_fram
                 continue;
             }
         }
-        if (!kEarly && !slow) {
+        if ((!kEarly || kUtf8) && !slow) {
             const uint32_t a0 = rec.z & 0x1FFFu, a1 = (rec.z >> 13) & 0x1FFFu;
             const uint32_t e0 = rec.w & 0x1FFFu, e1 = (rec.w >> 13) & 0x1FFFu;
             // a gap between payloads (a tail of A reaches at most bytes 0..2: the seam kernel's)
@@ -1398,12 +1398,19 @@ __device__ __forceinline__ void unmask_sorted_utf8_pipe(uint8_t *base, const fws
 #ifndef FWS_UTF8_WPE
 #define FWS_UTF8_WPE 1
 #endif
-template <bool kNT, bool kPipe>
+// kForm 0: lookup, then the unit's loads; 1: software-pipelined over a wave's
+// units; 2: the unit's loads before its lookup (kEarly: one unit per wave on
+// C5, so the owner lookup's scalar rounds overlap the HBM latency, as
+// k_unmask_stream's kPf does for the stream form; the default: 1.439-1.447
+// against 1.447-1.457 ms on C5, 86 VGPRs, 5 waves per SIMD). Measured slower
+// and removed: 2 with write-through stores (1.53 ms) and 2 held to 6 waves per
+// SIMD (1.466 ms, 80 VGPRs and scratch), profiles/r06/ab_c5d_early.jsonl.
+template <bool kNT, int kForm>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FWS_UTF8_WPE))) void k_unmask_sorted_utf8(uint8_t *base, const fws_frame_desc *__restrict__ d,
                                                                uint32_t n, uint8_t *__restrict__ ok,
                                                                uint32_t *__restrict__ seam, uint64_t seam_units) {
-    if (kPipe) unmask_sorted_utf8_pipe<kNT>(base, d, n, ok, seam, seam_units);
-    else unmask_sorted_body<kNT, false, true>(base, d, n, ok, seam, seam_units);
+    if (kForm == 1) unmask_sorted_utf8_pipe<kNT>(base, d, n, ok, seam, seam_units);
+    else unmask_sorted_body<kNT, kForm == 2, true>(base, d, n, ok, seam, seam_units);
 }
 
 // ------------------------------------------------------------ one launch, any order
@@ -1555,10 +1562,13 @@ extern "C" __attribute__((visibility("default"))) int fws_internal_set_sorted_ea
     return old;
 }
 
-static int g_sorted_utf8_pipe = 0;  // tuning hook: k_unmask_sorted_utf8 software-pipelined (1; measured slower, 2.12 vs 1.89 ms on C5: 90 VGPRs) or plain (0)
+// tuning hook: k_unmask_sorted_utf8 form -- 0 lookup first (r02-r06 default),
+// 1 software-pipelined (measured slower, 2.12 vs 1.89 ms on C5: 90 VGPRs),
+// 2 loads before the lookup (default)
+static int g_sorted_utf8_pipe = 2;
 extern "C" __attribute__((visibility("default"))) int fws_internal_set_sorted_utf8_pipe(int on) {
     const int old = g_sorted_utf8_pipe;
-    g_sorted_utf8_pipe = on != 0;
+    g_sorted_utf8_pipe = on >= 0 && on <= 2 ? on : 2;
     return old;
 }
 
@@ -1653,12 +1663,14 @@ int fws_launch_unmask_sorted_utf8(uint8_t *base, const fws_frame_desc *d, uint32
     int r = fws_hip_status(hipMemsetAsync(ok, 1, n, s));
     if (r) return r;
     const uint64_t units = max_span / 4096u + 2u;
-    if (g_sorted_utf8_pipe)
-        hipLaunchKernelGGL((k_unmask_sorted_utf8<true, true>), dim3(grid_for_units(units, kCapSortedUtf8)), dim3(kBlock), 0, s, base, d,
-                           n, ok, seam, seam_units);
+    const dim3 grid(grid_for_units(units, kCapSortedUtf8));
+    if (g_sorted_utf8_pipe == 1)
+        hipLaunchKernelGGL((k_unmask_sorted_utf8<true, 1>), grid, dim3(kBlock), 0, s, base, d, n, ok, seam, seam_units);
+    else if (g_sorted_utf8_pipe == 2)
+        hipLaunchKernelGGL((k_unmask_sorted_utf8<true, 2>), grid, dim3(kBlock), 0, s, base, d, n, ok, seam, seam_units);
+
     else
-        hipLaunchKernelGGL((k_unmask_sorted_utf8<true, false>), dim3(grid_for_units(units, kCapSortedUtf8)), dim3(kBlock), 0, s, base,
-                           d, n, ok, seam, seam_units);
+        hipLaunchKernelGGL((k_unmask_sorted_utf8<true, 0>), grid, dim3(kBlock), 0, s, base, d, n, ok, seam, seam_units);
     const uint64_t seam_blocks = (units + kBlock - 1) / kBlock;   // grid-stride: any span is covered
     hipLaunchKernelGGL(k_utf8_seam_sorted, dim3((unsigned)(seam_blocks < 4096u ? seam_blocks : 4096u)), dim3(kBlock), 0, s,
                        (const uint8_t *)base, d, n, ok, seam, seam_units);

@@ -14,9 +14,10 @@ from test_gpu_unmask import aligned_host, oracle_unmask_regions
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True, params=[0, 1], ids=["plain", "pipe"])
+@pytest.fixture(autouse=True, params=[0, 1, 2], ids=["plain", "pipe", "early"])
 def utf8_pipe(request):
-    """every test runs on both forms of k_unmask_sorted_utf8 (plain and software-pipelined)"""
+    """every test runs on every form of k_unmask_sorted_utf8 (plain, software-pipelined,
+    loads before the owner lookup)"""
     from flashws_amd import lib
     old = lib().fws_internal_set_sorted_utf8_pipe(request.param)
     yield request.param
@@ -125,9 +126,9 @@ def test_sorted_utf8_c5_shape(ctx, cuda):
     assert np.array_equal(ok2.cpu().numpy(), ok)
 
 
-@pytest.mark.parametrize("pipe", [0, 1])
+@pytest.mark.parametrize("pipe", [0, 1, 2])
 def test_sorted_utf8_both_variants(ctx, cuda, pipe):
-    """The software-pipelined and the plain fused kernel give the same bytes and flags."""
+    """The plain, software-pipelined and early-load fused kernels give the same bytes and flags."""
     from flashws_amd import lib
     old = lib().fws_internal_set_sorted_utf8_pipe(pipe)
     try:

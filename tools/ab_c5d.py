@@ -2,7 +2,9 @@
 """A/B timing of the C5 descriptor-mode passes on one 4 GiB C5 batch, in one
 process (the library variant from FWS_LIB_VARIANT): the plain unmask
 (k_unmask_sorted, the HBM floor of the pass), fws_gpu_unmask_sorted_utf8 in
-its plain form (pipe 0) and its early-load form (pipe 1). HIP events, 20 calls
+its plain form (pipe 0), the software-pipelined form (pipe 1) and the
+early-load form (pipe 2, the default: the unit's loads before the owner
+lookup). HIP events, 20 calls
 per repetition after a warm-up of >= 0.5 s; prints one JSON line per mode."""
 import json
 import os
@@ -35,11 +37,11 @@ def main(calls=20, reps=3):
             lib().fws_internal_set_grid_cap(0)
         return f
     modes = {"plain_unmask": lambda: gpu.unmask_sorted(ctx, w, dd, n),
-             "utf8_pipe0": utf8(0), "utf8_pipe1": utf8(1)}
+             "utf8_pipe0": utf8(0), "utf8_pipe2": utf8(2)}
     for cap in (os.environ.get("AB_CAPS") or "").split(","):
         if cap:
             modes[f"utf8_pipe0_cap{cap}"] = utf8(0, int(cap))
-            modes[f"utf8_pipe1_cap{cap}"] = utf8(1, int(cap))
+            modes[f"utf8_pipe2_cap{cap}"] = utf8(2, int(cap))
     for name in list(modes) + list(modes)[::-1]:
         fn = modes[name]
         t0 = time.perf_counter()
@@ -57,7 +59,7 @@ def main(calls=20, reps=3):
             ms.append(round(e0.elapsed_time(e1) / calls, 4))
         print(json.dumps({"variant": os.environ.get("FWS_LIB_VARIANT", "") or "product", "mode": name,
                           "ms": sorted(ms)[len(ms) // 2], "reps": ms}), flush=True)
-    lib().fws_internal_set_sorted_utf8_pipe(0)
+    lib().fws_internal_set_sorted_utf8_pipe(2)
     # correctness of the product setting on the masked batch
     w.copy_(torch.from_numpy(w5).to(dev))
     gpu.unmask_sorted_utf8(ctx, w, dd, n, ok)

@@ -48,7 +48,7 @@ def main(reps=6):
     torch.cuda.synchronize()
     assert np.array_equal(ok.cpu().numpy(), np.asarray(ok5, dtype=np.uint8)[:n]), "fused utf8 flags differ"
     from flashws_amd import lib
-    for pipe in (1, 0):
+    for pipe in (1, 0, 2):
         old = lib().fws_internal_set_sorted_utf8_pipe(pipe)
         tf = 0.0
         for _ in range(reps):
@@ -58,7 +58,7 @@ def main(reps=6):
             torch.cuda.synchronize()
             tf += e[0].elapsed_time(e[1]) / reps
         lib().fws_internal_set_sorted_utf8_pipe(old)
-        print(json.dumps({"C5_descriptor_fused": {"pipelined": pipe,
+        print(json.dumps({"C5_descriptor_fused": {"form": pipe,
                                                   "GiB_per_s": round(payload / (tf / 1e3) / 2**30, 1),
                                                   "ms_per_step": round(tf, 4)}}))
     print(json.dumps({"C5_descriptor_unmask_utf8": {"GiB_per_s": round(payload / (t / 1e3) / 2**30, 1),

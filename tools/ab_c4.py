@@ -52,7 +52,7 @@ def main():
             e1.record()
             torch.cuda.synchronize()
             times[f].append(e0.elapsed_time(e1) * 1e3 / steps)
-    L.fws_internal_set_gather_one(1)
+    L.fws_internal_set_gather_one(0)                   # the library default (plan + k_gather_fast)
     L.fws_internal_set_gather_flat(1)
     L.fws_internal_set_gather_dpp(2)
     L.fws_internal_set_gather_shape(0, 0)

@@ -182,6 +182,7 @@ public:
             return r;
         });
         listen.SetOnClose([self](Sock &w, uint32_t code, std::string_view reason, void *ud) {
+            if (self->DispatchBeforeClose(w)) return;   // its own CLOSE frame closed it, as on the per-read path
             self->Retire(w);
             self->user_close_(w, code, reason, ud);
         });
@@ -356,6 +357,30 @@ private:
     // removes any socket from the loop then (DeleteDeferred does, at the end of
     // the step; a DeleteFd nested in DeleteFd could move the map entry the outer
     // call still holds).
+    //
+    // The socket can close before a read it already handed over is dispatched:
+    // the TLS socket closes on the peer's close_notify or an SSL error right
+    // after delivering the read (tls_socket.h:507-559), the loop's error branch
+    // on a reset, and a batched read waits for its chunk (or, deferred, for the
+    // next step). The reference decodes that read before the close, so a CLOSE
+    // frame in it reaches on_close with its own code and reason and the
+    // under-socket's close then finds on_close called (w_socket.h:407-414).
+    // The wrapped on_close therefore dispatches such reads first with
+    // has_called_on_close_ cleared; if they called on_close (a CLOSE frame),
+    // that was the connection's on_close and the under-socket's 1006 one is
+    // dropped, else the flag is restored and the close goes on as before.
+    bool DispatchBeforeClose(Sock &w) {
+        auto it = conns_.find(&w.under_socket());
+        if (it == conns_.end() || retiring_ != nullptr || !(it->second.pending || it->second.inflight)) return false;
+        w.*(&A::has_called_on_close_) = false;
+        retiring_ = static_cast<USock *>(&w.under_socket());
+        Flush();
+        retiring_ = nullptr;
+        if (w.*(&A::has_called_on_close_)) return true;   // on_close ran (and retired the connection)
+        w.*(&A::has_called_on_close_) = true;
+        return false;
+    }
+
     void Retire(Sock &w) {
         auto it = conns_.find(&w.under_socket());
         if (it == conns_.end()) return;

@@ -205,7 +205,7 @@ def test_dropin_reference_client_load(cuda, clients, msg_len, tls, batch, chunk,
     assert st["gpu_reads"] > 0 and st["msgs"] == clients * 620
     if not tls:                     # the loop's MemPool read slots, proven by the pool's own records
         assert st["zc_slots"] > 0
-    assert all(c == [1000, b"bye".hex()] for c in st["close_log_hex"][:clients])
+    assert all(c == [1000, b"bye".hex()] for c in st["close_log_hex"][:clients]), st
     if batch:                       # the step's reads went to the GPU together
         assert 0 < st["gpu_batches"] <= st["gpu_reads"]
     if chunk == "flush":            # SetDeferLastChunk(false): no step end leaves a chunk in flight
